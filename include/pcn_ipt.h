@@ -1,0 +1,179 @@
+/*
+ * pcn_ipt.h — C ABI of the MI355X-native pcn-iptables classification datapath.
+ *
+ * This is the drop-in boundary that replaces the reference's kernel layer
+ * (the tail-called eBPF pipeline under src/services/pcn-iptables/src/datapaths/)
+ * and the "Program wrapper + RawTable::set into BPF maps" seam of the control
+ * plane.  Every entry point is extern "C", takes plain
+ * pointers and sizes, never throws, and returns 0 or a negative errno value;
+ * pcn_ipt_last_error() returns a thread-local message for the last failure,
+ * mirroring how the reference handlers turn exceptions into
+ * {kGenericError, strdup(msg)} (api/IptablesApi.cpp:72-74).
+ *
+ * Reference paths below are relative to /root/reference/src/.
+ */
+#ifndef PCN_IPT_H
+#define PCN_IPT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCN_IPT_ABI_VERSION 1
+
+/* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
+enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
+enum { PCN_IPT_INGRESS = 0, PCN_IPT_EGRESS = 1 };
+/* Actions (ActionsInt, services/pcn-iptables/src/defines.h:79). */
+enum { PCN_IPT_DROP = 0, PCN_IPT_ACCEPT = 1 };
+/* Per-field module ids, same numbering as ModulesConstants (defines.h:48-56). */
+enum {
+  PCN_IPT_F_CONNTRACK = 0, PCN_IPT_F_IPSRC = 1, PCN_IPT_F_IPDST = 2, PCN_IPT_F_L4PROTO = 3,
+  PCN_IPT_F_SPORT = 4, PCN_IPT_F_DPORT = 5, PCN_IPT_F_IFACE = 6, PCN_IPT_F_TCPFLAGS = 7,
+  PCN_IPT_NFIELDS = 8
+};
+/* rule_ids[] output codes besides a matched rule id >= 0. */
+#define PCN_IPT_RID_DEFAULT (-1)   /* chain default action taken (default counters bumped) */
+#define PCN_IPT_RID_NOCHAIN (-2)   /* decided before/without a rule chain (parser, ICMP checks, PASS) */
+
+typedef struct pcn_ipt pcn_ipt;
+
+/* Context configuration.  Replaces the per-cube state created by
+ * Iptables::Iptables (services/pcn-iptables/src/Iptables.cpp:21-133). */
+typedef struct {
+  int device;                 /* HIP device ordinal; -1 = control plane only (no GPU) */
+  uint32_t max_counted_rules; /* 0 => 8000   (Iptables_ActionLookup_dp.c:55-56)  */
+  uint32_t max_action_rules;  /* 0 => 10000  (Iptables_ActionLookup_dp.c:36)     */
+  uint32_t max_rules;         /* 0 => 8192   (Iptables.h:173); hard cap 65535    */
+} pcn_ipt_config;
+
+/* One rule as received by the REST surface: ChainRuleJsonObject /
+ * ChainAppendInputJsonObject (datamodel/iptables.yang:221-230, Chain.cpp:139-192).
+ * NULL / negative = field not set. */
+typedef struct {
+  const char *src;       /* "a.b.c.d" or "a.b.c.d/n" */
+  const char *dst;
+  const char *l4proto;   /* "TCP"/"UDP"/"ICMP"/"GRE" (upper or lower case) */
+  const char *tcpflags;  /* e.g. "SYN !ACK" */
+  const char *in_iface;  /* cube port name */
+  const char *out_iface;
+  const char *conntrack; /* "NEW"/"ESTABLISHED"/"RELATED"/"INVALID" */
+  int32_t sport;         /* -1 unset */
+  int32_t dport;
+  int32_t action;        /* -1 unset (=> DROP, ChainRule.cpp:76-82), 0 DROP, 1 ACCEPT */
+} pcn_ipt_rule;
+
+/* A packet batch.  All buffers are caller-owned DEVICE pointers (HBM); the
+ * call is stream-ordered and asynchronous.  Replaces the per-packet entry
+ * handle_rx(ctx, md) (polycubed/src/cube_xdp.cpp:403-449, extiface_xdp.cpp:178-200):
+ * frames[] holds the L2 frames, lens[] is md->packet_len, in_port[] is md->in_port. */
+typedef struct {
+  const uint8_t *frames;     /* frame bytes */
+  uint64_t frames_bytes;     /* size of the frames buffer (reads never go past it) */
+  const uint32_t *offsets;   /* NULL => frame i starts at i*stride */
+  const uint16_t *lens;      /* NULL => every frame is fixed_len bytes */
+  uint32_t stride;
+  uint32_t fixed_len;
+  const uint16_t *in_port;   /* NULL => const_in_port for every frame */
+  uint16_t const_in_port;
+  uint16_t direction;        /* PCN_IPT_INGRESS or PCN_IPT_EGRESS */
+  const uint8_t *ct_status;  /* NULL => status from an empty conntrack table */
+  uint64_t n;                /* number of frames */
+  uint8_t *verdicts;         /* out: 0 DROP (RX_DROP), 1 ACCEPT (RX_OK / pass / redirect) */
+  int32_t *rule_ids;         /* out, nullable: matched rule, or PCN_IPT_RID_* */
+} pcn_ipt_batch;
+
+/* ---- context ---------------------------------------------------------- */
+int pcn_ipt_abi_version(void);
+const char *pcn_ipt_last_error(void);
+int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out);
+void pcn_ipt_destroy(pcn_ipt *ctx);
+
+/* Cube ports: name -> polycube port index used by in/out-iface rules.
+ * Replaces Iptables::interfaceNameToIndex (Iptables.cpp:480-484). */
+int pcn_ipt_add_port(pcn_ipt *ctx, const char *name, uint16_t index);
+
+/* Host IPs that select INPUT (ingress) / OUTPUT (egress).  Replaces the
+ * `localip` BPF hash (Iptables_ChainSelector_dp.c:54) updated by
+ * ChainSelector::updateLocalIps (modules/ChainSelector.cpp:72-133). */
+int pcn_ipt_set_localip(pcn_ipt *ctx, const uint32_t *ips_nbo, size_t n);
+
+/* ---- rule-level control (mirror of the REST chain verbs) -------------- */
+/* Chain::append (Chain.cpp:139-192) */
+int pcn_ipt_chain_append(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule);
+/* Chain::insert (Chain.cpp:194-300); id <= number of rules */
+int pcn_ipt_chain_insert(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rule *rule);
+/* Chain::delRule (Chain.cpp:1039-1064) */
+int pcn_ipt_chain_delete_id(pcn_ipt *ctx, int chain, uint32_t id);
+/* Chain::deletes (Chain.cpp:302-352): delete the first rule equal to *rule */
+int pcn_ipt_chain_delete_match(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule);
+/* Chain::delRuleList (Chain.cpp:1066-1073) */
+int pcn_ipt_chain_flush(pcn_ipt *ctx, int chain);
+/* Chain::setDefault (Chain.cpp:79-127) */
+int pcn_ipt_chain_set_default(pcn_ipt *ctx, int chain, int action);
+/* Iptables `interactive` leaf (iptables.yang:98-104, Iptables.h:181): when 0,
+ * rule edits are staged until pcn_ipt_chain_apply_rules (Chain::applyRules). */
+int pcn_ipt_set_interactive(pcn_ipt *ctx, int interactive);
+int pcn_ipt_chain_apply_rules(pcn_ipt *ctx, int chain);
+int pcn_ipt_chain_nrules(pcn_ipt *ctx, int chain);
+
+/* ---- table-level boundary (what Chain::updateChain pushes) ------------ */
+/* Replace a chain's compiled tables in one step: the per-field {key -> rule
+ * bitvector} maps that Chain::updateChain (Chain.cpp:600-874) would push via
+ * RawTable::set (libs/polycube/src/table.cpp:53-75), plus the action table.
+ * Staged into the inactive slot of a double buffer, then flipped atomically
+ * between batches (Chain.cpp:441-457,924 chainNumber).  Caller-owned, copied. */
+typedef struct {
+  uint32_t n;              /* entries (0 => module absent) */
+  const uint32_t *keys;    /* IP: NBO u32 as the reference stores it; ports: host u16;
+                              iface: port index (0xffff wildcard); proto/flags/ct: value */
+  const uint8_t *plen;     /* IP prefix lengths (NULL for other fields) */
+  const uint64_t *vecs;    /* n * nrw words, 63 rule bits per word (defines.h:168) */
+} pcn_ipt_field_map;
+typedef struct {
+  uint32_t nrules;
+  int default_action;
+  const uint8_t *actions;                /* nrules entries (ActionLookup updateTableValue) */
+  pcn_ipt_field_map maps[PCN_IPT_NFIELDS];
+} pcn_ipt_tables;
+int pcn_ipt_load_chain(pcn_ipt *ctx, int chain, const pcn_ipt_tables *tables);
+/* Export the maps the rule compiler produced for a chain (same layout as
+ * pcn_ipt_field_map, std::map order).  Returns entries, 0 if absent. */
+int pcn_ipt_export_map(pcn_ipt *ctx, int chain, int field, uint32_t *keys, uint8_t *plen,
+                       uint64_t *vecs, uint32_t cap, uint32_t nrw);
+uint32_t pcn_ipt_chain_nrw(pcn_ipt *ctx, int chain);
+
+/* ---- datapath ---------------------------------------------------------- */
+/* Classify a batch (device pointers), stream = hipStream_t (NULL = default). */
+int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *batch, void *stream);
+/* Wait for all work this context queued. */
+int pcn_ipt_synchronize(pcn_ipt *ctx);
+
+/* ---- counters ---------------------------------------------------------- */
+/* Per-rule pkts/bytes (ActionLookup pkts_/bytes_<CHAIN>) and default counters
+ * (pkts_/bytes_default_<CHAIN>).  flush != 0 zeroes the per-rule counters after
+ * reading (read-and-flush, modules/ActionLookup.cpp:78-151).  scope 0 = this
+ * GPU, 1 = summed over the communicator (after pcn_ipt_sync_counters). */
+int pcn_ipt_read_counters(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n,
+                          uint64_t *def_pkts, uint64_t *def_bytes, int flush, int scope);
+/* Accumulated stats like Chain::getStatsList (Chain.cpp:961-976): per-rule
+ * totals kept in the control plane across rule edits + the DEFAULT row. */
+int pcn_ipt_chain_stats(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n,
+                        uint64_t *def_pkts, uint64_t *def_bytes);
+/* Chain::resetCounters (Chain.cpp:354-380) */
+int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ------------------- */
+/* 128-byte ncclUniqueId produced on rank 0 and shared out of band. */
+int pcn_ipt_comm_unique_id(uint8_t out[128]);
+int pcn_ipt_comm_init(pcn_ipt *ctx, int nranks, int rank, const uint8_t uid[128]);
+/* All-gather every rank's per-rule/default counters over RCCL and sum them
+ * into the scope=1 view.  Stream-ordered. */
+int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

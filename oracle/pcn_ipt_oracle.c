@@ -1,0 +1,774 @@
+/*
+ * pcn_ipt_oracle.c — TEST INFRASTRUCTURE ONLY (parity checker, CPU baseline).
+ *
+ * A deliberately literal, scalar C restatement of the reference pcn-iptables
+ * datapath and rule compiler.  Every function cites the reference file:line it
+ * follows (paths relative to src/services/pcn-iptables/src/ unless noted).
+ * It is never linked into the product library.
+ *
+ * Semantics restated:
+ *   rule parsing      ChainRule.cpp:29-83, defines.h:84-114 (IpAddr),
+ *                     libs/polycube/src/utils.cpp:38-50,233-239, Utils.cpp:19-200
+ *   rule compiler     Utils.cpp:223-732 (*FromRulesToMap), Chain.cpp:431-929
+ *   datapath          datapaths/Iptables_{Parser,ChainSelector,ConntrackLabel,
+ *                     IpLookup,L4ProtocolLookup,L4PortLookup,InterfaceLookup,
+ *                     TcpFlagsLookup,ConntrackMatch,BitScan,ActionLookup}_dp.c
+ *   kernel LPM trie   longest prefix wins, MSB-first over the key bytes, an
+ *                     insert with an equal (prefixlen, prefix) replaces the value;
+ *                     1024-entry capacity (Iptables_IpLookup_dp.c:54-55).
+ *                     Linux kernel/bpf/lpm_trie.c is not in /root/reference;
+ *                     this is its published behaviour.
+ * The module order chosen by Chain.cpp:624-849 does not change verdicts or
+ * counters (every module ANDs into one vector; any miss/zero exits to the
+ * default action once), so modules run in the fixed defines.h order here.
+ */
+#define _GNU_SOURCE
+#include "pcn_ipt_oracle.h"
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define NCHAINS 3
+#define REF_MAX_RULES 8192 /* Iptables.h:173 */
+#define NRULES_TO_NELEMS(x) ((x) / 63 + ((x) % 63 != 0 ? 1 : 0)) /* defines.h:168 */
+#define TRIE_MAX 1024     /* Iptables_IpLookup_dp.c:54-55 */
+
+enum { F_CT = 0, F_IPSRC, F_IPDST, F_PROTO, F_SPORT, F_DPORT, F_IFACE, F_FLAGS, NFIELDS };
+enum { RX_OK = 0, RX_DROP = 2 };
+enum { CT_NEW = 0, CT_ESTABLISHED = 1, CT_RELATED = 2, CT_INVALID = 3 };
+
+typedef struct { uint32_t ip; uint8_t netmask; } ipaddr_t; /* defines.h:84-114 */
+
+typedef struct {
+  int src_set, dst_set, proto_set, sport_set, dport_set, flags_set_, in_set, out_set, ct_set;
+  ipaddr_t src, dst;
+  int proto;
+  uint16_t sport, dport;
+  uint8_t fset, fnot;
+  char in_iface[64], out_iface[64];
+  int ct;
+  int action;
+} prule_t;
+
+typedef struct tnode {
+  struct tnode *ch[2];
+  int has;
+  int vec; /* index into chain pool */
+} tnode_t;
+
+typedef struct {      /* one compiled map, as pushed by updateMap */
+  int n;
+  uint32_t *key;      /* map key in push order */
+  uint8_t *plen;
+  int *vec;           /* pool index */
+} omap_t;
+
+typedef struct {
+  int nrules, default_action, nrw, vlen;
+  prule_t *rules;
+  uint64_t *pool; int npool, cappool;
+  int present[NFIELDS];
+  omap_t maps[NFIELDS];
+  /* datapath views */
+  tnode_t *trie[2]; int trie_nodes[2];
+  int proto_tab[256];
+  int sport_tab[65536], dport_tab[65536], iface_tab[65536];
+  int sport_wild, dport_wild, iface_wild; /* pool idx or -1 */
+  int flags_tab[256];
+  int ct_tab[4];
+  uint8_t *actions; /* per rule */
+  /* counters (ActionLookup_dp.c:55-56, Parser_dp.c:47-58) */
+  uint64_t *pkts, *bytes;
+  uint64_t def_pkts, def_bytes;
+} ochain_t;
+
+typedef struct { char name[64]; uint16_t index; } port_t;
+
+struct orc_ctx {
+  ochain_t ch[NCHAINS];
+  port_t ports[1024]; int nports;
+  uint32_t localip[256]; int nlocal;
+  uint32_t max_counted, max_action;
+  uint16_t index64[64];
+  pthread_mutex_t mu;
+};
+
+/* ---------------- rule parsing ---------------- */
+
+/* libs/polycube/src/utils.cpp:38-50 (+ get_ip_from_string :233-239) */
+static int ip_string_to_nbo_uint(const char *s, uint32_t *out) {
+  char buf[128];
+  const char *slash = strchr(s, '/');
+  size_t len = slash ? (size_t)(slash - s) : strlen(s);
+  if (len >= sizeof buf) return -EINVAL;
+  memcpy(buf, s, len); buf[len] = 0;
+  unsigned char a[4]; int last = -1;
+  int rc = sscanf(buf, "%hhu.%hhu.%hhu.%hhu%n", a + 0, a + 1, a + 2, a + 3, &last);
+  if (rc != 4 || (int)len != last) return -EINVAL;
+  *out = (uint32_t)a[3] << 24 | (uint32_t)a[2] << 16 | (uint32_t)a[1] << 8 | (uint32_t)a[0];
+  return 0;
+}
+
+/* defines.h:91-109 IpAddr::fromString (netmask via std::stol into a uint8_t) */
+static int ipaddr_from_string(const char *s, ipaddr_t *o) {
+  const char *slash = strchr(s, '/');
+  uint8_t nm = 32;
+  if (slash) {
+    char *end; errno = 0;
+    long v = strtol(slash + 1, &end, 10);
+    if (end == slash + 1 || errno) return -EINVAL; /* std::stol throws */
+    nm = (uint8_t)v;
+  }
+  if (nm > 32) return -EINVAL;
+  uint32_t ip;
+  if (ip_string_to_nbo_uint(s, &ip)) return -EINVAL;
+  o->ip = ip; o->netmask = nm;
+  return 0;
+}
+
+static int strieq2(const char *a, const char *up, const char *lo) {
+  return strcmp(a, up) == 0 || strcmp(a, lo) == 0;
+}
+
+/* Utils.cpp:45-57 ChainRule::protocolFromStringToInt */
+static int proto_from_string(const char *p, int *out) {
+  if (strieq2(p, "TCP", "tcp")) { *out = 6; return 0; }
+  if (strieq2(p, "UDP", "udp")) { *out = 17; return 0; }
+  if (strieq2(p, "ICMP", "icmp")) { *out = 1; return 0; }
+  if (strieq2(p, "GRE", "gre")) { *out = 47; return 0; }
+  return -EINVAL;
+}
+
+/* erase the first occurrence of pat from s (std::string::erase(find(pat), len)) */
+static int erase_first(char *s, const char *pat) {
+  char *p = strstr(s, pat);
+  if (!p) return 0;
+  size_t l = strlen(pat);
+  memmove(p, p + l, strlen(p + l) + 1);
+  return 1;
+}
+
+/* Utils.cpp:73-140 ChainRule::flagsFromStringToMasks */
+static int flags_from_string(const char *flags, uint8_t *set, uint8_t *notset) {
+  static const char *names[8] = {"FIN", "SYN", "RST", "PSH", "ACK", "URG", "ECE", "CWR"};
+  char buf[256];
+  if (strlen(flags) >= sizeof buf) return -EINVAL;
+  strcpy(buf, flags);
+  uint8_t ns = 0, s = 0;
+  for (int i = 0; i < 8; i++) {
+    char neg[8]; snprintf(neg, sizeof neg, "!%s", names[i]);
+    if (erase_first(buf, neg)) ns |= (uint8_t)(1u << i);
+  }
+  for (int i = 0; i < 8; i++)
+    if (strstr(buf, names[i])) s |= (uint8_t)(1u << i);
+  if (s & ns) return -EINVAL;
+  *set = s; *notset = ns;
+  return 0;
+}
+
+static int ct_from_string(const char *s, int *o) {
+  if (!strcmp(s, "NEW")) *o = CT_NEW;
+  else if (!strcmp(s, "ESTABLISHED")) *o = CT_ESTABLISHED;
+  else if (!strcmp(s, "RELATED")) *o = CT_RELATED;
+  else if (!strcmp(s, "INVALID")) *o = CT_INVALID;
+  else return -EINVAL;
+  return 0;
+}
+
+static int port_index(orc_ctx *c, const char *name, uint16_t *idx) {
+  for (int i = 0; i < c->nports; i++)
+    if (!strcmp(c->ports[i].name, name)) { *idx = c->ports[i].index; return 0; }
+  return -ENOENT; /* Iptables.cpp:480-484 get_port throws */
+}
+
+/* ChainRule.cpp:29-83 ChainRule::update */
+static int parse_rule(orc_ctx *c, const orc_rule *r, prule_t *p) {
+  memset(p, 0, sizeof *p);
+  if (r->conntrack) { if (ct_from_string(r->conntrack, &p->ct)) return -EINVAL; p->ct_set = 1; }
+  if (r->src) { if (ipaddr_from_string(r->src, &p->src)) return -EINVAL; p->src_set = 1; }
+  if (r->dst) { if (ipaddr_from_string(r->dst, &p->dst)) return -EINVAL; p->dst_set = 1; }
+  if (r->sport >= 0) { if (r->sport > 65535) return -EINVAL; p->sport = (uint16_t)r->sport; p->sport_set = 1; }
+  if (r->dport >= 0) { if (r->dport > 65535) return -EINVAL; p->dport = (uint16_t)r->dport; p->dport_set = 1; }
+  if (r->tcpflags) { if (flags_from_string(r->tcpflags, &p->fset, &p->fnot)) return -EINVAL; p->flags_set_ = 1; }
+  if (r->l4proto) { if (proto_from_string(r->l4proto, &p->proto)) return -EINVAL; p->proto_set = 1; }
+  uint16_t dummy;
+  if (r->in_iface) {
+    if (strlen(r->in_iface) >= 64 || port_index(c, r->in_iface, &dummy)) return -EINVAL;
+    strcpy(p->in_iface, r->in_iface); p->in_set = 1;
+  }
+  if (r->out_iface) {
+    if (strlen(r->out_iface) >= 64 || port_index(c, r->out_iface, &dummy)) return -EINVAL;
+    strcpy(p->out_iface, r->out_iface); p->out_set = 1;
+  }
+  if (r->action < 0) p->action = 0;            /* ChainRule.cpp:76-82: unset => DROP */
+  else if (r->action <= 1) p->action = r->action;
+  else return -EINVAL;                         /* Utils.cpp:200-207 (LOG throws) */
+  return 0;
+}
+
+/* ---------------- compiler ---------------- */
+
+static int pool_new(ochain_t *ch) {
+  if (ch->npool == ch->cappool) {
+    int nc = ch->cappool ? ch->cappool * 2 : 64;
+    uint64_t *np = realloc(ch->pool, (size_t)nc * ch->vlen * 8);
+    if (!np) return -1;
+    ch->pool = np; ch->cappool = nc;
+  }
+  memset(ch->pool + (size_t)ch->npool * ch->vlen, 0, (size_t)ch->vlen * 8);
+  return ch->npool++;
+}
+static inline uint64_t *VEC(ochain_t *ch, int i) { return ch->pool + (size_t)i * ch->vlen; }
+/* defines.h:165 SET_BIT on bitVector[id/63], bit id%63 (Utils.cpp:316) */
+static inline void setbit(uint64_t *v, uint32_t id) { v[id / 63] |= (uint64_t)1 << (id % 63); }
+
+static void omap_push(omap_t *m, uint32_t key, uint8_t plen, int vec) {
+  m->key = realloc(m->key, (size_t)(m->n + 1) * 4);
+  m->plen = realloc(m->plen, (size_t)(m->n + 1));
+  m->vec = realloc(m->vec, (size_t)(m->n + 1) * sizeof(int));
+  m->key[m->n] = key; m->plen[m->n] = plen; m->vec[m->n] = vec; m->n++;
+}
+
+static int cmp_ipaddr(const void *a, const void *b) { /* defines.h:110-113 operator< */
+  const ipaddr_t *x = a, *y = b;
+  if (x->ip != y->ip) return x->ip < y->ip ? -1 : 1;
+  return (int)x->netmask - (int)y->netmask;
+}
+static int cmp_u32(const void *a, const void *b) {
+  uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+  return x < y ? -1 : x > y;
+}
+
+/* Utils.cpp:294-318 containment test (with its NBO-as-integer mask quirk) */
+static int ip_contains(ipaddr_t addr, ipaddr_t rule) {
+  uint32_t mask = rule.netmask == 32 ? 0xffffffffu : (((uint32_t)1 << rule.netmask) - 1);
+  return ((addr.ip & mask) == (rule.ip & mask)) && (rule.netmask <= addr.netmask);
+}
+
+/* Utils.cpp:223-375 Chain::ipFromRulesToMap */
+static void compile_ip(ochain_t *ch, int field) {
+  int is_src = field == F_IPSRC;
+  ipaddr_t *keys = malloc(sizeof(ipaddr_t) * (ch->nrules + 1));
+  int nk = 0, ndc = 0;
+  for (int i = 0; i < ch->nrules; i++) {
+    prule_t *r = &ch->rules[i];
+    int set = is_src ? r->src_set : r->dst_set;
+    if (!set) { ndc++; continue; }
+    keys[nk++] = is_src ? r->src : r->dst;
+  }
+  qsort(keys, nk, sizeof(ipaddr_t), cmp_ipaddr);
+  int nu = 0;
+  for (int i = 0; i < nk; i++)
+    if (nu == 0 || cmp_ipaddr(&keys[nu - 1], &keys[i]) != 0) keys[nu++] = keys[i];
+  if (nu != 0 && ndc != 0) { /* :326-374 wildcard 0.0.0.0/0 (insert keeps an existing key) */
+    ipaddr_t w = {0, 0};
+    int found = 0;
+    for (int i = 0; i < nu; i++) if (keys[i].ip == 0 && keys[i].netmask == 0) found = 1;
+    if (!found) {
+      keys[nu++] = w;
+      qsort(keys, nu, sizeof(ipaddr_t), cmp_ipaddr);
+    }
+  }
+  omap_t *m = &ch->maps[field];
+  for (int k = 0; k < nu; k++) {
+    int v = pool_new(ch);
+    for (int i = 0; i < ch->nrules; i++) {
+      prule_t *r = &ch->rules[i];
+      int set = is_src ? r->src_set : r->dst_set;
+      ipaddr_t rip = set ? (is_src ? r->src : r->dst) : (ipaddr_t){0, 0};
+      if (ip_contains(keys[k], rip)) setbit(VEC(ch, v), (uint32_t)i);
+    }
+    omap_push(m, keys[k].ip, keys[k].netmask, v);
+  }
+  ch->present[field] = nu > 0;
+  free(keys);
+}
+
+static inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+/* kernel LPM trie insert, modules/IpLookup.cpp:122-140 updateMap order */
+static int trie_insert(ochain_t *ch, int t, uint32_t ip_nbo, uint8_t plen, int vec) {
+  if (!ch->trie[t]) ch->trie[t] = calloc(1, sizeof(tnode_t));
+  tnode_t *n = ch->trie[t];
+  uint32_t h = bswap32(ip_nbo);
+  for (int b = 0; b < plen; b++) {
+    int bit = (h >> (31 - b)) & 1;
+    if (!n->ch[bit]) n->ch[bit] = calloc(1, sizeof(tnode_t));
+    n = n->ch[bit];
+  }
+  if (!n->has) {
+    if (ch->trie_nodes[t] >= TRIE_MAX) return -ENOSPC;
+    ch->trie_nodes[t]++;
+  }
+  n->has = 1; n->vec = vec;
+  return 0;
+}
+static int trie_lookup(const tnode_t *n, uint32_t ip_nbo) {
+  uint32_t h = bswap32(ip_nbo);
+  int best = -1;
+  for (int b = 0; n; b++) {
+    if (n->has) best = n->vec;
+    if (b == 32) break;
+    n = n->ch[(h >> (31 - b)) & 1];
+  }
+  return best;
+}
+static void trie_free(tnode_t *n) {
+  if (!n) return;
+  trie_free(n->ch[0]); trie_free(n->ch[1]); free(n);
+}
+
+typedef int (*getkey_fn)(orc_ctx *, const prule_t *, int chain, uint32_t *key);
+static int gk_proto(orc_ctx *c, const prule_t *r, int chain, uint32_t *k) {
+  (void)c; (void)chain; if (!r->proto_set) return 0; *k = (uint32_t)r->proto; return 1;
+}
+static int gk_sport(orc_ctx *c, const prule_t *r, int chain, uint32_t *k) {
+  (void)c; (void)chain; if (!r->sport_set) return 0; *k = r->sport; return 1;
+}
+static int gk_dport(orc_ctx *c, const prule_t *r, int chain, uint32_t *k) {
+  (void)c; (void)chain; if (!r->dport_set) return 0; *k = r->dport; return 1;
+}
+/* Utils.cpp:483-501: IN_TYPE for INPUT/FORWARD, OUT_TYPE for OUTPUT (Chain.cpp:611) */
+static int gk_iface(orc_ctx *c, const prule_t *r, int chain, uint32_t *k) {
+  const char *nm = chain == ORC_OUTPUT ? (r->out_set ? r->out_iface : NULL)
+                                        : (r->in_set ? r->in_iface : NULL);
+  uint16_t idx;
+  if (!nm || port_index(c, nm, &idx)) return 0;
+  *k = idx; return 1;
+}
+
+/* Utils.cpp:381-429 / 431-474 / 476-526: keyed bitvector maps with a wildcard key */
+static void compile_keyed(orc_ctx *c, ochain_t *ch, int chain, int field, getkey_fn gk,
+                          uint32_t wildkey) {
+  uint32_t *keys = malloc(sizeof(uint32_t) * (ch->nrules + 1));
+  int nk = 0, ndc = 0;
+  for (int i = 0; i < ch->nrules; i++) {
+    uint32_t k;
+    if (gk(c, &ch->rules[i], chain, &k)) keys[nk++] = k; else ndc++;
+  }
+  qsort(keys, nk, 4, cmp_u32);
+  int nu = 0;
+  for (int i = 0; i < nk; i++) if (nu == 0 || keys[nu - 1] != keys[i]) keys[nu++] = keys[i];
+  if (nu != 0 && ndc != 0) {
+    int found = 0;
+    for (int i = 0; i < nu; i++) if (keys[i] == wildkey) found = 1;
+    if (!found) { keys[nu++] = wildkey; qsort(keys, nu, 4, cmp_u32); }
+  }
+  omap_t *m = &ch->maps[field];
+  for (int k = 0; k < nu; k++) omap_push(m, keys[k], 0, pool_new(ch));
+  for (int i = 0; i < ch->nrules; i++) {
+    uint32_t kk;
+    if (gk(c, &ch->rules[i], chain, &kk)) {
+      for (int k = 0; k < nu; k++) if (keys[k] == kk) setbit(VEC(ch, m->vec[k]), (uint32_t)i);
+    } else if (nu != 0) { /* don't-care rules are in all entries */
+      for (int k = 0; k < nu; k++) setbit(VEC(ch, m->vec[k]), (uint32_t)i);
+    }
+  }
+  ch->present[field] = nu > 0;
+  free(keys);
+}
+
+/* Utils.cpp:680-732 Chain::flagsFromRulesToMap */
+static void compile_flags(ochain_t *ch) {
+  int any = 0;
+  for (int i = 0; i < ch->nrules; i++) if (ch->rules[i].flags_set_) any = 1;
+  if (!any) return;
+  omap_t *m = &ch->maps[F_FLAGS];
+  for (int j = 0; j < 256; j++) omap_push(m, (uint32_t)j, 0, pool_new(ch));
+  for (int i = 0; i < ch->nrules; i++) {
+    prule_t *r = &ch->rules[i];
+    if (!r->flags_set_) {
+      for (int j = 0; j < 256; j++) setbit(VEC(ch, m->vec[j]), (uint32_t)i);
+      continue;
+    }
+    uint8_t fs = r->fset, fn = r->fnot;
+    if (fs == 0) fs = 255; /* :714-717 */
+    for (int j = 0; j < 256; j++) {
+      uint8_t cand = (uint8_t)j; /* possible_flags_combinations_[j] == j */
+      if ((cand & fs) == fs && (cand & fn) == 0) setbit(VEC(ch, m->vec[cand]), (uint32_t)i);
+    }
+  }
+  ch->present[F_FLAGS] = 1;
+}
+
+/* Utils.cpp:642-678 Chain::conntrackFromRulesToMap */
+static void compile_ct(ochain_t *ch) {
+  int any = 0;
+  for (int i = 0; i < ch->nrules; i++) if (ch->rules[i].ct_set) any = 1;
+  if (!any) return;
+  omap_t *m = &ch->maps[F_CT];
+  for (int s = 0; s < 4; s++) {
+    int v = pool_new(ch);
+    for (int i = 0; i < ch->nrules; i++) {
+      prule_t *r = &ch->rules[i];
+      if (!r->ct_set || r->ct == s) setbit(VEC(ch, v), (uint32_t)i);
+    }
+    omap_push(m, (uint32_t)s, 0, v);
+  }
+  ch->present[F_CT] = 1;
+}
+
+static void chain_free(ochain_t *ch) {
+  free(ch->rules); free(ch->pool); free(ch->actions); free(ch->pkts); free(ch->bytes);
+  for (int f = 0; f < NFIELDS; f++) {
+    free(ch->maps[f].key); free(ch->maps[f].plen); free(ch->maps[f].vec);
+  }
+  trie_free(ch->trie[0]); trie_free(ch->trie[1]);
+  memset(ch, 0, sizeof *ch);
+}
+
+/* Chain::updateChain, Chain.cpp:600-874 */
+static int compile_chain(orc_ctx *c, int chain) {
+  ochain_t *ch = &c->ch[chain];
+  int n = ch->nrules;
+  ch->nrw = NRULES_TO_NELEMS(n);
+  int mr = NRULES_TO_NELEMS(REF_MAX_RULES);
+  ch->vlen = ch->nrw > mr ? ch->nrw : mr;
+  compile_ct(ch);
+  compile_ip(ch, F_IPSRC);
+  compile_ip(ch, F_IPDST);
+  compile_keyed(c, ch, chain, F_PROTO, gk_proto, 0);
+  compile_keyed(c, ch, chain, F_SPORT, gk_sport, 0);
+  compile_keyed(c, ch, chain, F_DPORT, gk_dport, 0);
+  compile_keyed(c, ch, chain, F_IFACE, gk_iface, 0xffff);
+  compile_flags(ch);
+  /* datapath views */
+  for (int t = 0; t < 2; t++) {
+    omap_t *m = &ch->maps[t == 0 ? F_IPSRC : F_IPDST];
+    for (int k = 0; k < m->n; k++) {
+      int rc = trie_insert(ch, t, m->key[k], m->plen[k], m->vec[k]);
+      if (rc) return rc;
+    }
+  }
+  for (int i = 0; i < 256; i++) ch->proto_tab[i] = -1;
+  for (int k = 0; k < ch->maps[F_PROTO].n; k++)
+    ch->proto_tab[ch->maps[F_PROTO].key[k] & 0xff] = ch->maps[F_PROTO].vec[k];
+  int *tabs[3] = {ch->sport_tab, ch->dport_tab, ch->iface_tab};
+  int *wild[3] = {&ch->sport_wild, &ch->dport_wild, &ch->iface_wild};
+  int fl[3] = {F_SPORT, F_DPORT, F_IFACE};
+  uint32_t wk[3] = {0, 0, 0xffff};
+  for (int t = 0; t < 3; t++) {
+    for (int i = 0; i < 65536; i++) tabs[t][i] = -1;
+    *wild[t] = -1;
+    omap_t *m = &ch->maps[fl[t]];
+    for (int k = 0; k < m->n; k++) {
+      tabs[t][m->key[k]] = m->vec[k];
+      if (m->key[k] == wk[t]) *wild[t] = m->vec[k]; /* L4PortLookup.cpp:44-56, InterfaceLookup.cpp:44-56 */
+    }
+  }
+  for (int i = 0; i < 256; i++) ch->flags_tab[i] = -1;
+  for (int k = 0; k < ch->maps[F_FLAGS].n; k++) ch->flags_tab[k] = ch->maps[F_FLAGS].vec[k];
+  for (int i = 0; i < 4; i++) ch->ct_tab[i] = -1;
+  for (int k = 0; k < ch->maps[F_CT].n; k++) ch->ct_tab[k] = ch->maps[F_CT].vec[k];
+  ch->actions = calloc((size_t)n + 1, 1);
+  for (int i = 0; i < n; i++) ch->actions[i] = (uint8_t)ch->rules[i].action;
+  return 0;
+}
+
+/* ---------------- public control API ---------------- */
+
+static void build_index64(uint16_t t[64]) {
+  /* BitScan_dp.c:97: idx = ((b ^ (b-1)) * 0x03f79d71b4cb0a89) >> 58; index64[idx] = ctz(b) */
+  for (int p = 0; p < 64; p++) {
+    uint64_t b = (uint64_t)1 << p;
+    int idx = (int)(((b ^ (b - 1)) * 0x03f79d71b4cb0a89ull) >> 58);
+    t[idx] = (uint16_t)p;
+  }
+}
+
+orc_ctx *orc_create(uint32_t max_counted, uint32_t max_action) {
+  orc_ctx *c = calloc(1, sizeof *c);
+  if (!c) return NULL;
+  c->max_counted = max_counted ? max_counted : 8000;  /* ActionLookup_dp.c:55-56 */
+  c->max_action = max_action ? max_action : 10000;    /* ActionLookup_dp.c:36 */
+  build_index64(c->index64);
+  pthread_mutex_init(&c->mu, NULL);
+  for (int i = 0; i < NCHAINS; i++) {
+    c->ch[i].default_action = 1; /* Iptables.cpp:33-38: chains start ACCEPT */
+    c->ch[i].pkts = calloc(c->max_counted, 8);
+    c->ch[i].bytes = calloc(c->max_counted, 8);
+  }
+  return c;
+}
+
+void orc_destroy(orc_ctx *c) {
+  if (!c) return;
+  for (int i = 0; i < NCHAINS; i++) chain_free(&c->ch[i]);
+  free(c);
+}
+
+int orc_add_port(orc_ctx *c, const char *name, uint16_t index) {
+  if (c->nports >= 1024 || strlen(name) >= 64) return -ENOSPC;
+  strcpy(c->ports[c->nports].name, name);
+  c->ports[c->nports].index = index;
+  c->nports++;
+  return 0;
+}
+
+int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n, int def) {
+  if (chain < 0 || chain >= NCHAINS || (def != 0 && def != 1)) return -EINVAL;
+  prule_t *pr = calloc((size_t)n + 1, sizeof(prule_t));
+  for (uint32_t i = 0; i < n; i++)
+    if (parse_rule(c, &rules[i], &pr[i])) { free(pr); return -EINVAL; }
+  ochain_t *ch = &c->ch[chain];
+  uint64_t *pk = ch->pkts, *by = ch->bytes;
+  ch->pkts = ch->bytes = NULL;
+  chain_free(ch);
+  ch->pkts = pk; ch->bytes = by;
+  memset(pk, 0, c->max_counted * 8); memset(by, 0, c->max_counted * 8);
+  ch->rules = pr; ch->nrules = (int)n; ch->default_action = def;
+  return compile_chain(c, chain);
+}
+
+int orc_set_localip(orc_ctx *c, const uint32_t *ips, uint32_t n) {
+  if (n > 256) return -ENOSPC; /* ChainSelector_dp.c:54 hash(256) */
+  memcpy(c->localip, ips, n * 4); c->nlocal = (int)n;
+  return 0;
+}
+
+uint32_t orc_chain_nrw(orc_ctx *c, int chain) { return (uint32_t)c->ch[chain].nrw; }
+
+void orc_index64(uint16_t out[64]) { build_index64(out); }
+
+int orc_export_map(orc_ctx *c, int chain, int field, uint32_t *keys, uint8_t *plen,
+                   uint64_t *vecs, uint32_t cap, uint32_t nrw) {
+  if (chain < 0 || chain >= NCHAINS || field < 0 || field >= NFIELDS) return -EINVAL;
+  ochain_t *ch = &c->ch[chain];
+  omap_t *m = &ch->maps[field];
+  if ((uint32_t)m->n > cap) return -ENOSPC;
+  for (int k = 0; k < m->n; k++) {
+    keys[k] = m->key[k]; plen[k] = m->plen[k];
+    for (uint32_t w = 0; w < nrw; w++)
+      vecs[(size_t)k * nrw + w] = (int)w < ch->vlen ? VEC(ch, m->vec[k])[w] : 0;
+  }
+  return m->n;
+}
+
+int orc_read_counters(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n,
+                      uint64_t *dp, uint64_t *db, int flush) {
+  if (chain < 0 || chain >= NCHAINS) return -EINVAL;
+  ochain_t *ch = &c->ch[chain];
+  for (uint32_t i = 0; i < n; i++) {
+    int ok = i < c->max_counted;
+    if (pkts) pkts[i] = ok ? ch->pkts[i] : 0;
+    if (bytes) bytes[i] = ok ? ch->bytes[i] : 0;
+    if (ok && flush) { ch->pkts[i] = 0; ch->bytes[i] = 0; } /* ActionLookup.cpp:124-151 */
+  }
+  if (dp) *dp = ch->def_pkts;
+  if (db) *db = ch->def_bytes;
+  return 0;
+}
+
+/* ---------------- datapath ---------------- */
+
+typedef struct {        /* per-CPU counters (percpu arrays) */
+  uint64_t *pkts[NCHAINS], *bytes[NCHAINS];
+  uint64_t dpk[NCHAINS], dby[NCHAINS];
+} pcpu_t;
+
+static inline uint16_t be16(const uint8_t *p) { return (uint16_t)(p[0] << 8 | p[1]); }
+static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+
+static int localip_has(const orc_ctx *c, uint32_t ip) {
+  for (int i = 0; i < c->nlocal; i++) if (c->localip[i] == ip) return 1;
+  return 0;
+}
+
+/* ConntrackLabel_dp.c:190-531 with an empty `connections` table (stateless). */
+static int ct_label_empty(int proto, uint8_t flags, int icmp_type) {
+  if (proto == 6) /* TCP_MISS :372-383 */
+    return ((flags & 0x02) && (flags | 0x02) == 0x02) ? CT_NEW : CT_INVALID;
+  if (proto == 17) return CT_NEW;            /* UDP_MISS :428-432 */
+  if (proto == 1) return icmp_type == 8 ? CT_NEW : CT_INVALID;
+  return CT_INVALID;                         /* :562-566 */
+}
+
+/* default action tail: Program.cpp:88-111 (+ default counters from each module) */
+static inline int default_verdict(const ochain_t *ch, pcpu_t *pc, int chain, uint32_t L,
+                                  int32_t *rid) {
+  pc->dpk[chain] += 1; pc->dby[chain] += L;
+  *rid = -1;
+  return ch->default_action == 0 ? RX_DROP : RX_OK;
+}
+
+static int classify_one(const orc_ctx *c, int dir, const uint8_t *f, uint32_t L, uint16_t port,
+                        int ct_in, pcpu_t *pc, int32_t *rid) {
+  *rid = -2;
+  /* Parser_dp.c:94-153 */
+  if (L < 14) return RX_DROP;
+  if (be16(f + 12) != 0x0800) return RX_OK;
+  if (L < 34) return RX_DROP;
+  uint32_t saddr = ld32(f + 26), daddr = ld32(f + 30);
+  int proto = f[23];
+  uint16_t sport = 0, dport = 0;
+  uint8_t flags = 0;
+  if (proto == 6) {
+    if (L < 54) return RX_DROP;
+    memcpy(&sport, f + 34, 2); memcpy(&dport, f + 36, 2);
+    flags = f[47];
+  } else if (proto == 17) {
+    if (L < 42) return RX_DROP;
+    memcpy(&sport, f + 34, 2); memcpy(&dport, f + 36, 2);
+  }
+  /* ports as the NBO u16 the eBPF hash keys hold; the maps store ntohs(port) */
+  sport = (uint16_t)(sport >> 8 | sport << 8);
+  dport = (uint16_t)(dport >> 8 | dport << 8);
+
+  /* ChainSelector_dp.c:131-298 */
+  int chain, pass_labeling = 0;
+  if (dir == ORC_INGRESS) {
+    const ochain_t *in = &c->ch[ORC_INPUT], *fw = &c->ch[ORC_FORWARD];
+    if (in->default_action == 1 && fw->default_action == 1 && in->nrules == 0 &&
+        fw->nrules == 0) { /* _INGRESS_ALLOWLOGIC, modules/ChainSelector.cpp:190-202 */
+      chain = -1; pass_labeling = 1;
+    } else {
+      chain = localip_has(c, daddr) ? ORC_INPUT : ORC_FORWARD;
+    }
+  } else {
+    if (!localip_has(c, saddr)) return RX_OK; /* PASS */
+    chain = ORC_OUTPUT;
+  }
+  if (chain >= 0 && c->ch[chain].nrules == 0) {
+    pc->dpk[chain] += 1; pc->dby[chain] += L;
+    *rid = -1;
+    if (c->ch[chain].default_action == 0) return RX_DROP; /* DROP_NO_LABELING */
+    pass_labeling = 1;
+  }
+  /* ConntrackLabel_dp.c:436-531: ICMP length checks (stateless: empty table) */
+  int icmp_type = -1;
+  if (proto == 1) {
+    if (L < 42) return RX_DROP;
+    icmp_type = f[34];
+    if (icmp_type != 8 && icmp_type != 0 && !(icmp_type >= 13 && icmp_type <= 18)) {
+      if (L < 62) return RX_DROP;
+      if (L < 70) return RX_DROP;
+    }
+  }
+  int ct = ct_in >= 0 ? ct_in : ct_label_empty(proto, flags, icmp_type);
+  if (pass_labeling) return RX_OK; /* ChainForwarder → ConntrackTableUpdate → RX_OK */
+
+  const ochain_t *ch = &c->ch[chain];
+  int nrw = ch->nrw;
+  uint64_t v[1024];
+  uint64_t *vv = nrw <= 1024 ? v : malloc((size_t)nrw * 8);
+  for (int i = 0; i < nrw; i++) vv[i] = 0x7FFFFFFFFFFFFFFFull; /* ChainSelector_dp.c:205-218 */
+  int verdict = -1;
+  for (int fld = 0; fld < NFIELDS && verdict < 0; fld++) {
+    if (!ch->present[fld]) continue;
+    int e = -1;
+    switch (fld) {
+    case F_CT: /* ConntrackMatch_dp.c:90-153 */
+      if (ct < 0 || ct > 3) { verdict = RX_DROP; *rid = -2; continue; }
+      e = ch->ct_tab[ct]; break;
+    case F_IPSRC: e = trie_lookup(ch->trie[0], saddr); break; /* IpLookup_dp.c:98-104 */
+    case F_IPDST: e = trie_lookup(ch->trie[1], daddr); break;
+    case F_PROTO: /* L4ProtocolLookup_dp.c:95-103 */
+      e = ch->proto_tab[proto];
+      if (e < 0) e = ch->proto_tab[0];
+      break;
+    case F_SPORT: case F_DPORT: /* L4PortLookup_dp.c:99-135 */
+      if (proto != 6 && proto != 17) continue;
+      e = fld == F_SPORT ? ch->sport_tab[sport] : ch->dport_tab[dport];
+      if (e < 0) e = fld == F_SPORT ? ch->sport_wild : ch->dport_wild;
+      break;
+    case F_IFACE: /* InterfaceLookup_dp.c:103-135 */
+      e = ch->iface_tab[port];
+      if (e < 0) e = ch->iface_wild;
+      break;
+    case F_FLAGS: /* TcpFlagsLookup_dp.c:93-110 */
+      if (proto != 6) continue;
+      e = ch->flags_tab[flags];
+      break;
+    }
+    if (e < 0) { verdict = default_verdict(ch, pc, chain, L, rid); break; }
+    const uint64_t *ev = ch->pool + (size_t)e * ch->vlen;
+    int allzero = 1;
+    for (int i = 0; i < nrw; i++) { vv[i] &= ev[i]; if (vv[i]) allzero = 0; }
+    if (allzero) verdict = default_verdict(ch, pc, chain, L, rid);
+  }
+  if (verdict < 0) {
+    /* BitScan_dp.c:88-110 */
+    int rule = -1;
+    for (int i = 0; i < nrw; i++) {
+      uint64_t b = vv[i];
+      if (b) {
+        int idx = (int)(((b ^ (b - 1)) * 0x03f79d71b4cb0a89ull) >> 58);
+        rule = c->index64[idx] + i * 63;
+        break;
+      }
+    }
+    if (rule < 0) {
+      verdict = default_verdict(ch, pc, chain, L, rid);
+    } else if ((uint32_t)rule >= c->max_action) { /* ActionLookup_dp.c:90-94 lookup miss */
+      verdict = RX_DROP; *rid = -2;
+    } else {
+      /* ActionLookup_dp.c:96-111 */
+      if ((uint32_t)rule < c->max_counted) { pc->pkts[chain][rule] += 1; pc->bytes[chain][rule] += L; }
+      *rid = rule;
+      verdict = ch->actions[rule] == 0 ? RX_DROP : RX_OK;
+    }
+  }
+  if (vv != v) free(vv);
+  return verdict;
+}
+
+typedef struct {
+  const orc_ctx *c; int dir; const uint8_t *frames; const uint32_t *offsets; const uint16_t *lens;
+  uint32_t stride, fixed_len; const uint16_t *in_port; uint16_t const_port; const uint8_t *ct;
+  uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc;
+} job_t;
+
+static void *run_job(void *arg) {
+  job_t *j = arg;
+  for (uint64_t i = j->lo; i < j->hi; i++) {
+    const uint8_t *f = j->frames + (j->offsets ? j->offsets[i] : i * (uint64_t)j->stride);
+    uint32_t L = j->lens ? j->lens[i] : j->fixed_len;
+    uint16_t port = j->in_port ? j->in_port[i] : j->const_port;
+    int ct = j->ct ? j->ct[i] : -1;
+    int32_t rid;
+    int v = classify_one(j->c, j->dir, f, L, port, ct, &j->pc, &rid);
+    j->verdicts[i] = v == RX_DROP ? 0 : 1;
+    if (j->rule_ids) j->rule_ids[i] = rid;
+  }
+  return NULL;
+}
+
+int orc_classify(orc_ctx *c, int dir, const uint8_t *frames, const uint32_t *offsets,
+                 const uint16_t *lens, uint32_t stride, uint32_t fixed_len,
+                 const uint16_t *in_port, uint16_t const_port, const uint8_t *ct_status,
+                 uint64_t n, uint8_t *verdicts, int32_t *rule_ids, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  job_t *jobs = calloc((size_t)nthreads, sizeof(job_t));
+  pthread_t *th = calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    job_t *j = &jobs[t];
+    *j = (job_t){c, dir, frames, offsets, lens, stride, fixed_len, in_port, const_port, ct_status,
+                 n * t / nthreads, n * (t + 1) / nthreads, verdicts, rule_ids,
+                 {{0}, {0}, {0}, {0}}};
+    for (int k = 0; k < NCHAINS; k++) {
+      j->pc.pkts[k] = calloc(c->max_counted, 8);
+      j->pc.bytes[k] = calloc(c->max_counted, 8);
+    }
+  }
+  for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, run_job, &jobs[t]);
+  run_job(&jobs[0]);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  /* control plane sums per-CPU counters (ActionLookup.cpp:78-96) */
+  for (int t = 0; t < nthreads; t++) {
+    for (int k = 0; k < NCHAINS; k++) {
+      for (uint32_t r = 0; r < c->max_counted; r++) {
+        c->ch[k].pkts[r] += jobs[t].pc.pkts[k][r];
+        c->ch[k].bytes[r] += jobs[t].pc.bytes[k][r];
+      }
+      c->ch[k].def_pkts += jobs[t].pc.dpk[k];
+      c->ch[k].def_bytes += jobs[t].pc.dby[k];
+      free(jobs[t].pc.pkts[k]); free(jobs[t].pc.bytes[k]);
+    }
+  }
+  free(jobs); free(th);
+  return 0;
+}

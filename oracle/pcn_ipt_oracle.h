@@ -1,0 +1,79 @@
+/*
+ * pcn_ipt_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference pcn-iptables classification path, used as
+ * the parity checker for the MI355X datapath.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library.  The product library
+ * (polycube_amd/libpcn_ipt.so) never links or calls it.
+ *
+ * Parity status: pinned by the reference's own integration-test scenarios
+ * (src/services/pcn-iptables/test/local_test*.sh, transcribed into
+ * tests/golden/scenarios.json) and by the reference BitScan index64 known-answer
+ * table (modules/BitScan.cpp:32-49 → tests/golden/index64.json).  The reference
+ * eBPF itself is unbuildable here (no BPF backend in llc, no bcc); see DESIGN.md.
+ */
+#ifndef PCN_IPT_ORACLE_H
+#define PCN_IPT_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Rule as received by the REST surface (ChainRuleJsonObject, iptables.yang:221-230).
+ * NULL string / negative integer = field not set. */
+typedef struct {
+  const char *src;       /* "a.b.c.d" or "a.b.c.d/n" */
+  const char *dst;
+  const char *l4proto;   /* "TCP"/"UDP"/"ICMP"/"GRE" (either case) */
+  const char *tcpflags;  /* e.g. "SYN !ACK" */
+  const char *in_iface;  /* port name */
+  const char *out_iface;
+  const char *conntrack; /* "NEW"/"ESTABLISHED"/"RELATED"/"INVALID" */
+  int32_t sport;         /* -1 unset, else 0..65535 */
+  int32_t dport;
+  int32_t action;        /* -1 unset (=> DROP), 0 DROP, 1 ACCEPT */
+} orc_rule;
+
+typedef struct orc_ctx orc_ctx;
+
+enum { ORC_INPUT = 0, ORC_FORWARD = 1, ORC_OUTPUT = 2 };
+enum { ORC_INGRESS = 0, ORC_EGRESS = 1 };
+
+orc_ctx *orc_create(uint32_t max_counted_rules, uint32_t max_action_rules);
+void orc_destroy(orc_ctx *c);
+int orc_add_port(orc_ctx *c, const char *name, uint16_t index);
+/* Replace a chain's rule list and default action and run the rule compiler
+ * (Chain::updateChain).  Returns 0 or a negative errno. */
+int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n,
+                  int default_action);
+int orc_set_localip(orc_ctx *c, const uint32_t *ips_nbo, uint32_t n);
+/* Classify a batch (host pointers).  offsets==NULL => packet i at i*stride;
+ * lens==NULL => every packet fixed_len bytes; in_port==NULL => const_port;
+ * ct_status==NULL => connection status from an empty conntrack table. */
+int orc_classify(orc_ctx *c, int direction, const uint8_t *frames,
+                 const uint32_t *offsets, const uint16_t *lens, uint32_t stride,
+                 uint32_t fixed_len, const uint16_t *in_port,
+                 uint16_t const_port, const uint8_t *ct_status, uint64_t n,
+                 uint8_t *verdicts, int32_t *rule_ids, int nthreads);
+/* Per-rule counters (read-and-flush when flush != 0) and default counters. */
+int orc_read_counters(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes,
+                      uint32_t n, uint64_t *def_pkts, uint64_t *def_bytes,
+                      int flush);
+/* Export the compiled per-field map of a chain, in the order the reference
+ * pushes it (std::map order / array index).  field: 0 conntrack, 1 ipsrc,
+ * 2 ipdst, 3 l4proto, 4 sport, 5 dport, 6 iface, 7 tcpflags.  keys get the map
+ * key (IP: NBO u32 as stored by the reference), plen the prefix length (IP only),
+ * vecs nrw words per entry.  Returns the number of entries, 0 if the module is
+ * absent, negative on error. */
+int orc_export_map(orc_ctx *c, int chain, int field, uint32_t *keys,
+                   uint8_t *plen, uint64_t *vecs, uint32_t cap, uint32_t nrw);
+uint32_t orc_chain_nrw(orc_ctx *c, int chain);
+/* De Bruijn index table restated from Iptables_BitScan_dp.c:88-110. */
+void orc_index64(uint16_t out[64]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,628 @@
+// pcn_ipt.cpp — context, control plane mirror and C ABI (include/pcn_ipt.h).
+//
+// The control-plane half mirrors the reference's Chain / ChainRule / ChainStats
+// objects (services/pcn-iptables/src/Chain.cpp, ChainRule.cpp, ChainStats.cpp):
+// rule edits, interactive vs staged apply, read-and-flush counter accumulation.
+// The datapath half owns the chain images in HBM (double-buffered per chain),
+// the counters, and launches the HIP classify kernel (classify.hip).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "devchain.h"
+#include "image.hpp"
+#include "pcn_ipt.h"
+#include "ruleset.hpp"
+
+namespace pcn {
+int launch_classify(const LaunchArgs &a, bool fixed, int num_cus, hipStream_t stream);
+int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint64_t count, int nranks,
+                     hipStream_t stream);
+}  // namespace pcn
+
+namespace {
+
+using namespace pcn;
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+constexpr uint32_t kMaxLdsRuleBins = 2048;   // per-workgroup LDS histogram budget (32 KB)
+
+struct ImageSlot {
+  void *dev = nullptr;
+  size_t cap = 0;
+};
+
+struct ChainState {
+  // control plane (Chain)
+  std::vector<Rule> rules;
+  int default_action = PCN_IPT_ACCEPT;        // Iptables.cpp:33-38
+  std::vector<std::pair<uint64_t, uint64_t>> stats;   // ChainStats totals (counters_)
+  ChainTables tables;                          // last applied compile
+  // datapath
+  ImageSlot slot[2];
+  int active = -1;
+  DevChain desc{};                             // descriptor of the active slot
+  unsigned long long *ctr = nullptr;           // [2 + 2*max_counted]
+  unsigned long long *ctr_global = nullptr;    // summed over ranks
+  unsigned long long *gather = nullptr;        // [nranks][2 + 2*max_counted]
+};
+
+}  // namespace
+
+struct pcn_ipt {
+  pcn_ipt_config cfg{};
+  std::mutex mu;
+  PortTable ports;
+  ChainState chains[PCN_IPT_NCHAINS];
+  std::vector<uint32_t> localip;
+  uint32_t *d_localip = nullptr;
+  bool interactive = true;                     // Iptables.h:181
+  bool has_device = false;
+  int num_cus = 256;
+  size_t ctr_words = 0;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+void device_guard(pcn_ipt *ctx) {
+  if (ctx->has_device) hip_check(hipSetDevice(ctx->cfg.device), "hipSetDevice");
+}
+
+uint32_t counted(const pcn_ipt *ctx, uint32_t nrules) {
+  return std::min(nrules, ctx->cfg.max_counted_rules);
+}
+
+// Upload a compiled chain into the inactive slot, then flip (Chain.cpp:441-457,924).
+void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
+  ChainState &cs = ctx->chains[chain];
+  HostImage img = build_image(tables);       // may throw (trie capacity etc.)
+  if (ctx->has_device) {
+    device_guard(ctx);
+    // every batch queued before this call must not see a half-written slot
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    int next = cs.active < 0 ? 0 : 1 - cs.active;
+    ImageSlot &s = cs.slot[next];
+    if (s.cap < img.blob.size()) {
+      if (s.dev) hip_check(hipFree(s.dev), "hipFree");
+      s.dev = nullptr;
+      size_t cap = std::max<size_t>(img.blob.size(), 4096);
+      hip_check(hipMalloc(&s.dev, cap), "hipMalloc(chain image)");
+      s.cap = cap;
+    }
+    hip_check(hipMemcpy(s.dev, img.blob.data(), img.blob.size(), hipMemcpyHostToDevice),
+              "hipMemcpy(chain image)");
+    // a new ActionLookup program starts with zeroed per-rule counters; the
+    // default counters live in shared maps and persist (Iptables_Parser_dp.c:47-58)
+    hip_check(hipMemset(cs.ctr + 2, 0, (ctx->ctr_words - 2) * sizeof(unsigned long long)),
+              "hipMemset(counters)");
+    auto sec = [&](size_t off) -> const uint8_t * {
+      return off == kNoSection ? nullptr : static_cast<const uint8_t *>(s.dev) + off;
+    };
+    DevChain d{};
+    for (int i = 0; i < 2; ++i) {
+      d.ip_l1[i] = reinterpret_cast<const uint32_t *>(sec(img.off_ip_l1[i]));
+      d.ip_blk[i] = reinterpret_cast<const uint32_t *>(sec(img.off_ip_blk[i]));
+    }
+    for (int i = 0; i < 3; ++i) d.key_cls[i] = reinterpret_cast<const uint16_t *>(sec(img.off_key[i]));
+    d.proto_cls = reinterpret_cast<const uint16_t *>(sec(img.off_proto));
+    d.flags_cls = reinterpret_cast<const uint16_t *>(sec(img.off_flags));
+    d.ct_cls = reinterpret_cast<const uint16_t *>(sec(img.off_ct));
+    d.pool = reinterpret_cast<const uint64_t *>(sec(img.off_pool));
+    d.summ = reinterpret_cast<const uint64_t *>(sec(img.off_summ));
+    d.actions = sec(img.off_actions);
+    d.ctr = cs.ctr;
+    d.nrules = img.nrules;
+    d.nrw = img.nrw;
+    d.nsw = img.nsw;
+    d.present = img.present;
+    d.ncounted = counted(ctx, img.nrules);
+    d.max_action = ctx->cfg.max_action_rules;
+    d.default_action = img.default_action;
+    d.lds_base = -1;
+    cs.desc = d;
+    cs.active = next;
+  }
+  cs.tables = std::move(tables);
+}
+
+// ChainStats::fetchCounters for every rule (read-and-flush into host totals),
+// i.e. Chain::getStatsList (Chain.cpp:961-976) without the DEFAULT row.
+void fetch_stats(pcn_ipt *ctx, int chain) {
+  ChainState &cs = ctx->chains[chain];
+  cs.stats.resize(cs.rules.size());
+  if (!ctx->has_device || cs.active < 0) return;
+  device_guard(ctx);
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  uint32_t n = counted(ctx, cs.desc.nrules);
+  std::vector<unsigned long long> buf(2 + 2 * size_t(n));
+  hip_check(hipMemcpy(buf.data(), cs.ctr, buf.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
+  for (uint32_t id = 0; id < n && id < cs.stats.size(); ++id) {
+    cs.stats[id].first += buf[2 + 2 * id];
+    cs.stats[id].second += buf[3 + 2 * id];
+  }
+  hip_check(hipMemset(cs.ctr + 2, 0, 2 * size_t(n) * 8), "hipMemset(counters)");
+}
+
+void update_chain(pcn_ipt *ctx, int chain) {       // Chain::updateChain
+  ChainState &cs = ctx->chains[chain];
+  load_tables(ctx, chain, compile_chain(cs.rules, chain, cs.default_action, ctx->ports));
+}
+
+bool valid_chain(int c) { return c >= 0 && c < PCN_IPT_NCHAINS; }
+
+template <typename F>
+int guarded(pcn_ipt *ctx, F &&f) {
+  if (!ctx) return fail(-EINVAL, "null context");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  try {
+    return f();
+  } catch (const HipError &e) {
+    return fail(-EIO, e.what());
+  } catch (const std::exception &e) {
+    return fail(-EINVAL, e.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pcn_ipt_abi_version(void) { return PCN_IPT_ABI_VERSION; }
+
+const char *pcn_ipt_last_error(void) { return g_last_error.c_str(); }
+
+int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
+  if (!cfg || !out) return fail(-EINVAL, "null argument");
+  *out = nullptr;
+  auto ctx = std::make_unique<pcn_ipt>();
+  ctx->cfg = *cfg;
+  if (!ctx->cfg.max_counted_rules) ctx->cfg.max_counted_rules = 8000;
+  if (!ctx->cfg.max_action_rules) ctx->cfg.max_action_rules = 10000;
+  if (!ctx->cfg.max_rules) ctx->cfg.max_rules = 8192;
+  if (ctx->cfg.max_rules > 65535) return fail(-EINVAL, "max_rules > 65535");
+  ctx->ctr_words = 2 + 2 * size_t(ctx->cfg.max_counted_rules);
+  if (cfg->device >= 0) {
+    try {
+      int ndev = 0;
+      hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+      if (cfg->device >= ndev) return fail(-ENODEV, "no such HIP device");
+      ctx->has_device = true;
+      device_guard(ctx.get());
+      hipDeviceProp_t prop;
+      hip_check(hipGetDeviceProperties(&prop, cfg->device), "hipGetDeviceProperties");
+      ctx->num_cus = prop.multiProcessorCount;
+      hip_check(hipMalloc(&ctx->d_localip, PCN_MAX_LOCALIP * 4), "hipMalloc(localip)");
+      for (auto &cs : ctx->chains) {
+        hip_check(hipMalloc(&cs.ctr, ctx->ctr_words * 8), "hipMalloc(counters)");
+        hip_check(hipMemset(cs.ctr, 0, ctx->ctr_words * 8), "hipMemset(counters)");
+        hip_check(hipMalloc(&cs.ctr_global, ctx->ctr_words * 8), "hipMalloc(counters)");
+        hip_check(hipMemset(cs.ctr_global, 0, ctx->ctr_words * 8), "hipMemset(counters)");
+      }
+      for (int c = 0; c < PCN_IPT_NCHAINS; ++c) update_chain(ctx.get(), c);
+    } catch (const std::exception &e) {
+      return fail(-EIO, e.what());
+    }
+  } else {
+    for (int c = 0; c < PCN_IPT_NCHAINS; ++c) update_chain(ctx.get(), c);
+  }
+  *out = ctx.release();
+  return 0;
+}
+
+void pcn_ipt_destroy(pcn_ipt *ctx) {
+  if (!ctx) return;
+  if (ctx->has_device) {
+    (void)hipSetDevice(ctx->cfg.device);
+    (void)hipDeviceSynchronize();
+    for (auto &cs : ctx->chains) {
+      for (auto &s : cs.slot) if (s.dev) (void)hipFree(s.dev);
+      if (cs.ctr) (void)hipFree(cs.ctr);
+      if (cs.ctr_global) (void)hipFree(cs.ctr_global);
+      if (cs.gather) (void)hipFree(cs.gather);
+    }
+    if (ctx->d_localip) (void)hipFree(ctx->d_localip);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+  }
+  delete ctx;
+}
+
+int pcn_ipt_add_port(pcn_ipt *ctx, const char *name, uint16_t index) {
+  return guarded(ctx, [&] {
+    if (!name || !*name) return fail(-EINVAL, "empty port name");
+    ctx->ports.add(name, index);
+    return 0;
+  });
+}
+
+int pcn_ipt_set_localip(pcn_ipt *ctx, const uint32_t *ips, size_t n) {
+  return guarded(ctx, [&] {
+    if (n > PCN_MAX_LOCALIP) return fail(-ENOSPC, "localip holds at most 256 addresses");
+    std::vector<uint32_t> v(ips, ips + n);
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    if (ctx->has_device) {
+      device_guard(ctx);
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      if (!v.empty())
+        hip_check(hipMemcpy(ctx->d_localip, v.data(), v.size() * 4, hipMemcpyHostToDevice), "hipMemcpy(localip)");
+    }
+    ctx->localip = std::move(v);
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_append(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain) || !rule) return fail(-EINVAL, "bad chain or rule");
+    ChainState &cs = ctx->chains[chain];
+    Rule r = Rule::from_c(*rule, ctx->ports);
+    if (cs.rules.size() >= ctx->cfg.max_rules) return fail(-ENOSPC, "too many rules");
+    fetch_stats(ctx, chain);                          // Chain::addRule -> getStatsList
+    cs.rules.push_back(std::move(r));
+    cs.stats.resize(cs.rules.size());
+    if (ctx->interactive) update_chain(ctx, chain);
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_insert(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rule *rule) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain) || !rule) return fail(-EINVAL, "bad chain or rule");
+    ChainState &cs = ctx->chains[chain];
+    if (id > cs.rules.size()) return fail(-EINVAL, "id not allowed");   // Chain.cpp:238-240
+    Rule r = Rule::from_c(*rule, ctx->ports);
+    if (cs.rules.size() >= ctx->cfg.max_rules) return fail(-ENOSPC, "too many rules");
+    fetch_stats(ctx, chain);
+    cs.rules.insert(cs.rules.begin() + id, std::move(r));
+    cs.stats.insert(cs.stats.begin() + id, {0, 0});
+    if (ctx->interactive) update_chain(ctx, chain);
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_delete_id(pcn_ipt *ctx, int chain, uint32_t id) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    ChainState &cs = ctx->chains[chain];
+    if (id >= cs.rules.size()) return fail(-ENOENT, "There is no rule " + std::to_string(id));
+    fetch_stats(ctx, chain);
+    cs.rules.erase(cs.rules.begin() + id);
+    cs.stats.erase(cs.stats.begin() + id);
+    if (ctx->interactive) update_chain(ctx, chain);
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_delete_match(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain) || !rule) return fail(-EINVAL, "bad chain or rule");
+    ChainState &cs = ctx->chains[chain];
+    Rule r;
+    try {
+      r = Rule::from_c(*rule, ctx->ports);
+    } catch (const std::exception &) {
+      return fail(-EINVAL, "No matching rule to delete");    // Chain.cpp:344-346
+    }
+    for (size_t i = 0; i < cs.rules.size(); ++i) {
+      if (cs.rules[i] == r) {
+        fetch_stats(ctx, chain);
+        cs.rules.erase(cs.rules.begin() + i);
+        cs.stats.erase(cs.stats.begin() + i);
+        if (ctx->interactive) update_chain(ctx, chain);
+        return 0;
+      }
+    }
+    return 0;   // no match: the reference returns without error
+  });
+}
+
+int pcn_ipt_chain_flush(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    ChainState &cs = ctx->chains[chain];
+    cs.rules.clear();
+    cs.stats.clear();
+    if (ctx->interactive) update_chain(ctx, chain);
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_set_default(pcn_ipt *ctx, int chain, int action) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain) || (action != PCN_IPT_DROP && action != PCN_IPT_ACCEPT))
+      return fail(-EINVAL, "bad chain or action");
+    ChainState &cs = ctx->chains[chain];
+    if (cs.default_action == action) return 0;
+    cs.default_action = action;
+    // Chain::setDefault -> reloadChain: the programs are rebuilt from the
+    // current rule list with the new default action.
+    fetch_stats(ctx, chain);
+    update_chain(ctx, chain);
+    return 0;
+  });
+}
+
+int pcn_ipt_set_interactive(pcn_ipt *ctx, int interactive) {
+  return guarded(ctx, [&] {
+    ctx->interactive = interactive != 0;
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_apply_rules(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    fetch_stats(ctx, chain);
+    update_chain(ctx, chain);
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_nrules(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    return static_cast<int>(ctx->chains[chain].rules.size());
+  });
+}
+
+int pcn_ipt_load_chain(pcn_ipt *ctx, int chain, const pcn_ipt_tables *t) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain) || !t) return fail(-EINVAL, "bad chain or tables");
+    if (t->default_action != PCN_IPT_DROP && t->default_action != PCN_IPT_ACCEPT)
+      return fail(-EINVAL, "bad default action");
+    ChainTables ct;
+    ct.nrules = t->nrules;
+    ct.nrw = words_for_rules(t->nrules);
+    ct.default_action = t->default_action;
+    if (t->nrules && !t->actions) return fail(-EINVAL, "actions required");
+    ct.actions.assign(t->actions, t->actions + t->nrules);
+    for (int f = 0; f < PCN_IPT_NFIELDS; ++f) {
+      const pcn_ipt_field_map &m = t->maps[f];
+      if (!m.n) continue;
+      if (!m.keys || !m.vecs) return fail(-EINVAL, "field map without keys/vecs");
+      bool ip = f == PCN_IPT_F_IPSRC || f == PCN_IPT_F_IPDST;
+      if (ip && !m.plen) return fail(-EINVAL, "IP map without prefix lengths");
+      FieldMap &fm = ct.maps[f];
+      for (uint32_t k = 0; k < m.n; ++k) {
+        fm.keys.push_back(m.keys[k]);
+        if (ip) {
+          if (m.plen[k] > 32) return fail(-EINVAL, "prefix length > 32");
+          fm.plen.push_back(m.plen[k]);
+        }
+        fm.vecs.emplace_back(m.vecs + size_t(k) * ct.nrw, m.vecs + size_t(k + 1) * ct.nrw);
+      }
+    }
+    load_tables(ctx, chain, std::move(ct));
+    return 0;
+  });
+}
+
+int pcn_ipt_export_map(pcn_ipt *ctx, int chain, int field, uint32_t *keys, uint8_t *plen, uint64_t *vecs,
+                       uint32_t cap, uint32_t nrw) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain) || field < 0 || field >= PCN_IPT_NFIELDS) return fail(-EINVAL, "bad chain/field");
+    const ChainTables &t = ctx->chains[chain].tables;
+    const FieldMap &m = t.maps[field];
+    if (m.keys.size() > cap) return fail(-ENOSPC, "export buffer too small");
+    for (size_t k = 0; k < m.keys.size(); ++k) {
+      if (keys) keys[k] = m.keys[k];
+      if (plen) plen[k] = m.plen.empty() ? 0 : m.plen[k];
+      if (vecs)
+        for (uint32_t w = 0; w < nrw; ++w) vecs[k * nrw + w] = w < t.nrw ? m.vecs[k][w] : 0;
+    }
+    return static_cast<int>(m.keys.size());
+  });
+}
+
+uint32_t pcn_ipt_chain_nrw(pcn_ipt *ctx, int chain) {
+  if (!ctx || !valid_chain(chain)) return 0;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  return ctx->chains[chain].tables.nrw;
+}
+
+int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
+  return guarded(ctx, [&] {
+    if (!b) return fail(-EINVAL, "null batch");
+    if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
+    if (b->n == 0) return 0;
+    if (!b->frames || !b->verdicts) return fail(-EINVAL, "frames and verdicts are required");
+    if (b->direction != PCN_IPT_INGRESS && b->direction != PCN_IPT_EGRESS) return fail(-EINVAL, "bad direction");
+    device_guard(ctx);
+    LaunchArgs a{};
+    // LDS histogram bins: 3 default bins, then rule bins (FORWARD first).
+    uint32_t base = 3;
+    const int order[3] = {PCN_IPT_FORWARD, PCN_IPT_INPUT, PCN_IPT_OUTPUT};
+    for (int c : order) {
+      ChainState &cs = ctx->chains[c];
+      a.ch[c] = cs.desc;
+      uint32_t nc = cs.desc.ncounted;
+      if (nc && base - 3 + nc <= kMaxLdsRuleBins) { a.ch[c].lds_base = static_cast<int32_t>(base); base += nc; }
+      else a.ch[c].lds_base = -1;
+    }
+    a.nbins = base;
+    a.frames = b->frames;
+    a.frames_bytes = b->frames_bytes;
+    a.offsets = b->offsets;
+    a.lens = b->lens;
+    a.in_port = b->in_port;
+    a.ct_status = b->ct_status;
+    a.verdicts = b->verdicts;
+    a.rule_ids = b->rule_ids;
+    a.localip = ctx->d_localip;
+    a.nlocal = static_cast<uint32_t>(ctx->localip.size());
+    a.n = b->n;
+    a.stride = b->stride;
+    a.fixed_len = b->fixed_len;
+    a.const_in_port = b->const_in_port;
+    a.direction = b->direction;
+    const ChainState &in = ctx->chains[PCN_IPT_INPUT], &fw = ctx->chains[PCN_IPT_FORWARD];
+    a.allow_logic = in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
+                    in.rules.size() == 0 && fw.rules.size() == 0 && in.desc.nrules == 0 &&
+                    fw.desc.nrules == 0;
+    // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
+    bool fixed = !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
+                 (reinterpret_cast<uintptr_t>(b->frames) % 16) == 0 &&
+                 (b->n - 1) * uint64_t(b->stride) + 48 <= b->frames_bytes;
+    if (!b->offsets) {
+      uint64_t last = (b->n - 1) * uint64_t(b->stride);
+      if (last >= b->frames_bytes) return fail(-EINVAL, "frames_bytes smaller than n*stride");
+    }
+    int rc = launch_classify(a, fixed, ctx->num_cus, static_cast<hipStream_t>(stream));
+    if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
+    return 0;
+  });
+}
+
+int pcn_ipt_synchronize(pcn_ipt *ctx) {
+  return guarded(ctx, [&] {
+    if (ctx->has_device) {
+      device_guard(ctx);
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    }
+    return 0;
+  });
+}
+
+int pcn_ipt_read_counters(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n,
+                          uint64_t *def_pkts, uint64_t *def_bytes, int flush, int scope) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    ChainState &cs = ctx->chains[chain];
+    std::vector<unsigned long long> buf(ctx->ctr_words, 0);
+    if (ctx->has_device) {
+      device_guard(ctx);
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      hip_check(hipMemcpy(buf.data(), scope ? cs.ctr_global : cs.ctr, buf.size() * 8, hipMemcpyDeviceToHost),
+                "hipMemcpy(counters)");
+    }
+    uint32_t nc = ctx->cfg.max_counted_rules;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (pkts) pkts[i] = i < nc ? buf[2 + 2 * size_t(i)] : 0;
+      if (bytes) bytes[i] = i < nc ? buf[3 + 2 * size_t(i)] : 0;
+    }
+    if (def_pkts) *def_pkts = buf[0];
+    if (def_bytes) *def_bytes = buf[1];
+    if (flush && ctx->has_device) {
+      hip_check(hipMemset(cs.ctr + 2, 0, (ctx->ctr_words - 2) * 8), "hipMemset(counters)");
+      hip_check(hipMemset(cs.ctr_global + 2, 0, (ctx->ctr_words - 2) * 8), "hipMemset(counters)");
+    }
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_stats(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n,
+                        uint64_t *def_pkts, uint64_t *def_bytes) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    ChainState &cs = ctx->chains[chain];
+    fetch_stats(ctx, chain);
+    for (uint32_t i = 0; i < n; ++i) {
+      if (pkts) pkts[i] = i < cs.stats.size() ? cs.stats[i].first : 0;
+      if (bytes) bytes[i] = i < cs.stats.size() ? cs.stats[i].second : 0;
+    }
+    unsigned long long d[2] = {0, 0};
+    if (ctx->has_device) hip_check(hipMemcpy(d, cs.ctr, 16, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
+    if (def_pkts) *def_pkts = d[0];
+    if (def_bytes) *def_bytes = d[1];
+    return static_cast<int>(cs.stats.size());
+  });
+}
+
+int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    ChainState &cs = ctx->chains[chain];
+    if (ctx->has_device) {
+      device_guard(ctx);
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      hip_check(hipMemset(cs.ctr + 2, 0, (ctx->ctr_words - 2) * 8), "hipMemset(counters)");
+    }
+    cs.stats.assign(cs.rules.size(), {0, 0});     // counters_.clear()
+    return 0;
+  });
+}
+
+int pcn_ipt_comm_unique_id(uint8_t out[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(-EIO, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(out, &id, 128);
+  return 0;
+}
+
+int pcn_ipt_comm_init(pcn_ipt *ctx, int nranks, int rank, const uint8_t uid[128]) {
+  return guarded(ctx, [&] {
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(-EINVAL, "bad rank/nranks");
+    device_guard(ctx);
+    if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    ncclUniqueId id;
+    std::memcpy(&id, uid, 128);
+    ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
+    if (r != ncclSuccess) return fail(-EIO, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    for (auto &cs : ctx->chains) {
+      if (cs.gather) hip_check(hipFree(cs.gather), "hipFree");
+      hip_check(hipMalloc(&cs.gather, ctx->ctr_words * 8 * size_t(nranks)), "hipMalloc(gather)");
+    }
+    return 0;
+  });
+}
+
+int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
+  return guarded(ctx, [&] {
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    device_guard(ctx);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!ctx->comm || ctx->nranks == 1) {
+      for (auto &cs : ctx->chains)
+        hip_check(hipMemcpyAsync(cs.ctr_global, cs.ctr, ctx->ctr_words * 8, hipMemcpyDeviceToDevice, s),
+                  "hipMemcpyAsync(counters)");
+      return 0;
+    }
+    // one all-gather per chain of its live prefix (defaults + counted rules)
+    size_t count[PCN_IPT_NCHAINS];
+    ncclResult_t r = ncclGroupStart();
+    for (int c = 0; c < PCN_IPT_NCHAINS && r == ncclSuccess; ++c) {
+      ChainState &cs = ctx->chains[c];
+      count[c] = 2 + 2 * size_t(cs.desc.ncounted);
+      r = ncclAllGather(cs.ctr, cs.gather, count[c], ncclUint64, ctx->comm, s);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(-EIO, std::string("ncclAllGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
+      ChainState &cs = ctx->chains[c];
+      int rc = launch_sum_ranks(cs.gather, cs.ctr_global, count[c], ctx->nranks, s);
+      if (rc != hipSuccess) return fail(-EIO, "sum_ranks launch failed");
+    }
+    return 0;
+  });
+}
+
+}  // extern "C"

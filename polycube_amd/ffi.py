@@ -1,0 +1,108 @@
+"""ctypes binding of include/pcn_ipt.h (the product C ABI).
+
+Loading fails loudly: there is no Python or CPU fallback for the datapath.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpcn_ipt.so")
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+class Rule(C.Structure):
+    _fields_ = [
+        ("src", C.c_char_p), ("dst", C.c_char_p), ("l4proto", C.c_char_p),
+        ("tcpflags", C.c_char_p), ("in_iface", C.c_char_p), ("out_iface", C.c_char_p),
+        ("conntrack", C.c_char_p), ("sport", C.c_int32), ("dport", C.c_int32),
+        ("action", C.c_int32),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int), ("max_counted_rules", C.c_uint32),
+                ("max_action_rules", C.c_uint32), ("max_rules", C.c_uint32)]
+
+
+class Batch(C.Structure):
+    _fields_ = [
+        ("frames", C.c_void_p), ("frames_bytes", C.c_uint64), ("offsets", C.c_void_p),
+        ("lens", C.c_void_p), ("stride", C.c_uint32), ("fixed_len", C.c_uint32),
+        ("in_port", C.c_void_p), ("const_in_port", C.c_uint16), ("direction", C.c_uint16),
+        ("ct_status", C.c_void_p), ("n", C.c_uint64), ("verdicts", C.c_void_p),
+        ("rule_ids", C.c_void_p),
+    ]
+
+
+class FieldMap(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("keys", C.POINTER(C.c_uint32)),
+                ("plen", C.POINTER(C.c_uint8)), ("vecs", C.POINTER(C.c_uint64))]
+
+
+class Tables(C.Structure):
+    _fields_ = [("nrules", C.c_uint32), ("default_action", C.c_int),
+                ("actions", C.POINTER(C.c_uint8)), ("maps", FieldMap * 8)]
+
+
+# name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
+SIGNATURES = {
+    "pcn_ipt_abi_version": (C.c_int, []),
+    "pcn_ipt_last_error": (C.c_char_p, []),
+    "pcn_ipt_create": (C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    "pcn_ipt_destroy": (None, [C.c_void_p]),
+    "pcn_ipt_add_port": (C.c_int, [C.c_void_p, C.c_char_p, C.c_uint16]),
+    "pcn_ipt_set_localip": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t]),
+    "pcn_ipt_chain_append": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Rule)]),
+    "pcn_ipt_chain_insert": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32, C.POINTER(Rule)]),
+    "pcn_ipt_chain_delete_id": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
+    "pcn_ipt_chain_delete_match": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Rule)]),
+    "pcn_ipt_chain_flush": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_chain_set_default": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "pcn_ipt_set_interactive": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_chain_apply_rules": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_chain_nrules": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_load_chain": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Tables)]),
+    "pcn_ipt_export_map": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.c_uint32,
+                                     C.c_uint32]),
+    "pcn_ipt_chain_nrw": (C.c_uint32, [C.c_void_p, C.c_int]),
+    "pcn_ipt_classify": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p]),
+    "pcn_ipt_synchronize": (C.c_int, [C.c_void_p]),
+    "pcn_ipt_read_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64), C.c_int, C.c_int]),
+    "pcn_ipt_chain_stats": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64)]),
+    "pcn_ipt_chain_reset_counters": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "pcn_ipt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
+    "pcn_ipt_sync_counters": (C.c_int, [C.c_void_p, C.c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libpcn_ipt.so (built by __graft_entry__.build() / `make -C polycube_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LibraryMissing(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch (if already imported) owns the process's HIP runtime; libpcn_ipt.so
+        # binds to the same libamdhip64.so.7 soname, so device pointers are shared.
+        h = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def last_error():
+    msg = lib().pcn_ipt_last_error()
+    return msg.decode() if msg else ""

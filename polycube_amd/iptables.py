@@ -1,0 +1,214 @@
+"""Python host mirroring the pcn-iptables cube API over the C ABI.
+
+Names and error behaviour follow the reference REST surface:
+  Iptables            -> services/pcn-iptables/src/Iptables.cpp (cube, ports, localip)
+  Chain.append/insert -> Chain.cpp:139-300
+  Chain.delete/deletes-> Chain.cpp:302-352, 1039-1064
+  Chain.flush         -> Chain.cpp:1066-1073 (delRuleList)
+  Chain.default       -> Chain.cpp:79-127 (setDefault)
+  Chain.apply_rules   -> Chain.cpp:382-392 (applyRules)
+  Chain.stats         -> Chain.cpp:931-976 (getStats/getStatsList, DEFAULT row last)
+  Chain.reset_counters-> Chain.cpp:354-380
+Invalid input raises IptablesError, like a handler's {kGenericError, msg}.
+"""
+import ctypes as C
+
+from . import ffi
+
+INPUT, FORWARD, OUTPUT = 0, 1, 2
+INGRESS, EGRESS = 0, 1
+DROP, ACCEPT = 0, 1
+_CHAIN_NAMES = {"INPUT": INPUT, "FORWARD": FORWARD, "OUTPUT": OUTPUT}
+_ACTIONS = {"DROP": DROP, "ACCEPT": ACCEPT}
+
+
+class IptablesError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (errno {-code})")
+        self.code = code
+
+
+def _check(rc):
+    if rc < 0:
+        raise IptablesError(rc, ffi.last_error())
+    return rc
+
+
+def _enc(v):
+    return None if v is None else str(v).encode()
+
+
+def make_rule(src=None, dst=None, l4proto=None, sport=None, dport=None, tcpflags=None,
+              in_iface=None, out_iface=None, conntrack=None, action=None):
+    """Build a pcn_ipt_rule from REST-style fields (None = not set)."""
+    if isinstance(action, str):
+        if action.upper() not in _ACTIONS:
+            raise IptablesError(-22, f"Action not supported: {action}")
+        action = _ACTIONS[action.upper()]
+    r = ffi.Rule(_enc(src), _enc(dst), _enc(l4proto), _enc(tcpflags), _enc(in_iface),
+                 _enc(out_iface), _enc(conntrack), -1 if sport is None else int(sport),
+                 -1 if dport is None else int(dport), -1 if action is None else int(action))
+    return r
+
+
+class Chain:
+    def __init__(self, ipt, cid):
+        self._ipt = ipt
+        self.id = cid
+
+    def _h(self):
+        return self._ipt._h
+
+    def append(self, **fields):
+        _check(ffi.lib().pcn_ipt_chain_append(self._h(), self.id, C.byref(make_rule(**fields))))
+
+    def insert(self, id=0, **fields):  # noqa: A002 (REST leaf name)
+        _check(ffi.lib().pcn_ipt_chain_insert(self._h(), self.id, id, C.byref(make_rule(**fields))))
+
+    def delete(self, id):  # noqa: A002
+        _check(ffi.lib().pcn_ipt_chain_delete_id(self._h(), self.id, id))
+
+    def deletes(self, **fields):
+        _check(ffi.lib().pcn_ipt_chain_delete_match(self._h(), self.id, C.byref(make_rule(**fields))))
+
+    def flush(self):
+        _check(ffi.lib().pcn_ipt_chain_flush(self._h(), self.id))
+
+    @property
+    def default(self):
+        return self._ipt._defaults[self.id]
+
+    @default.setter
+    def default(self, action):
+        a = _ACTIONS[action.upper()] if isinstance(action, str) else int(action)
+        _check(ffi.lib().pcn_ipt_chain_set_default(self._h(), self.id, a))
+        self._ipt._defaults[self.id] = a
+
+    def apply_rules(self):
+        _check(ffi.lib().pcn_ipt_chain_apply_rules(self._h(), self.id))
+
+    def __len__(self):
+        return _check(ffi.lib().pcn_ipt_chain_nrules(self._h(), self.id))
+
+    def stats(self):
+        """[(id, pkts, bytes), ...] + [("DEFAULT", pkts, bytes)] (getStatsList)."""
+        n = len(self)
+        pk = (C.c_uint64 * max(n, 1))()
+        by = (C.c_uint64 * max(n, 1))()
+        dp, db = C.c_uint64(), C.c_uint64()
+        _check(ffi.lib().pcn_ipt_chain_stats(self._h(), self.id, pk, by, n, C.byref(dp), C.byref(db)))
+        return [(i, pk[i], by[i]) for i in range(n)] + [("DEFAULT", dp.value, db.value)]
+
+    def reset_counters(self):
+        _check(ffi.lib().pcn_ipt_chain_reset_counters(self._h(), self.id))
+
+    def read_counters(self, n, flush=False, scope=0):
+        """Raw datapath counters: (pkts[n], bytes[n], def_pkts, def_bytes)."""
+        pk = (C.c_uint64 * max(n, 1))()
+        by = (C.c_uint64 * max(n, 1))()
+        dp, db = C.c_uint64(), C.c_uint64()
+        _check(ffi.lib().pcn_ipt_read_counters(self._h(), self.id, pk, by, n, C.byref(dp),
+                                               C.byref(db), int(flush), int(scope)))
+        return list(pk[:n]), list(by[:n]), dp.value, db.value
+
+    def export_map(self, field, cap=70000):
+        nrw = ffi.lib().pcn_ipt_chain_nrw(self._h(), self.id)
+        keys = (C.c_uint32 * cap)()
+        plen = (C.c_uint8 * cap)()
+        vecs = (C.c_uint64 * (cap * max(nrw, 1)))()
+        n = _check(ffi.lib().pcn_ipt_export_map(self._h(), self.id, field, keys, plen, vecs, cap, nrw))
+        return ([keys[i] for i in range(n)], [plen[i] for i in range(n)],
+                [list(vecs[i * nrw:(i + 1) * nrw]) for i in range(n)], nrw)
+
+
+class Iptables:
+    """One pcn-iptables cube bound to one GPU (device=-1: control plane only)."""
+
+    def __init__(self, device=0, max_counted_rules=0, max_action_rules=0, max_rules=0):
+        cfg = ffi.Config(device, max_counted_rules, max_action_rules, max_rules)
+        h = C.c_void_p()
+        _check(ffi.lib().pcn_ipt_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.device = device
+        self._defaults = [ACCEPT, ACCEPT, ACCEPT]
+        self.chains = {name: Chain(self, cid) for name, cid in _CHAIN_NAMES.items()}
+
+    def chain(self, name):
+        return self.chains[name.upper()] if isinstance(name, str) else Chain(self, name)
+
+    def close(self):
+        if self._h:
+            ffi.lib().pcn_ipt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_port(self, name, index):
+        _check(ffi.lib().pcn_ipt_add_port(self._h, name.encode(), index))
+
+    def set_localip(self, ips_nbo):
+        arr = (C.c_uint32 * max(len(ips_nbo), 1))(*ips_nbo)
+        _check(ffi.lib().pcn_ipt_set_localip(self._h, arr, len(ips_nbo)))
+
+    @property
+    def interactive(self):
+        return self._interactive if hasattr(self, "_interactive") else True
+
+    @interactive.setter
+    def interactive(self, v):
+        _check(ffi.lib().pcn_ipt_set_interactive(self._h, int(bool(v))))
+        self._interactive = bool(v)
+
+    def load_chain(self, chain, tables):
+        _check(ffi.lib().pcn_ipt_load_chain(self._h, chain, C.byref(tables)))
+
+    # ---- datapath (device pointers; torch tensors accepted for convenience) ----
+    def classify_ptrs(self, frames, frames_bytes, n, verdicts, rule_ids=None, offsets=None,
+                      lens=None, stride=64, fixed_len=64, in_port=None, const_in_port=1,
+                      direction=INGRESS, ct_status=None, stream=None):
+        b = ffi.Batch(frames, frames_bytes, offsets, lens, stride, fixed_len, in_port, const_in_port,
+                      direction, ct_status, n, verdicts, rule_ids)
+        _check(ffi.lib().pcn_ipt_classify(self._h, C.byref(b), stream))
+
+    def classify(self, frames, n=None, verdicts=None, rule_ids=None, offsets=None, lens=None,
+                 stride=64, fixed_len=64, in_port=None, const_in_port=1, direction=INGRESS,
+                 ct_status=None, stream=None):
+        """Classify device-resident frames (torch uint8 tensor on cuda).  Returns
+        (verdicts, rule_ids) tensors; the call is asynchronous on `stream`."""
+        import torch
+        if n is None:
+            n = offsets.numel() if offsets is not None else frames.numel() // stride
+        dev = frames.device
+        if verdicts is None:
+            verdicts = torch.empty(n, dtype=torch.uint8, device=dev)
+        if rule_ids is None:
+            rule_ids = torch.empty(n, dtype=torch.int32, device=dev)
+
+        def p(t):
+            return None if t is None else t.data_ptr()
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        self.classify_ptrs(frames.data_ptr(), frames.numel(), n, verdicts.data_ptr(),
+                           p(rule_ids) if rule_ids is not False else None, p(offsets), p(lens),
+                           stride, fixed_len, p(in_port), const_in_port, direction, p(ct_status), s)
+        return verdicts, rule_ids
+
+    def synchronize(self):
+        _check(ffi.lib().pcn_ipt_synchronize(self._h))
+
+    # ---- multi-GPU counters over RCCL ----
+    @staticmethod
+    def comm_unique_id():
+        buf = (C.c_uint8 * 128)()
+        _check(ffi.lib().pcn_ipt_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (C.c_uint8 * 128)(*uid)
+        _check(ffi.lib().pcn_ipt_comm_init(self._h, nranks, rank, buf))
+
+    def sync_counters(self, stream=None):
+        _check(ffi.lib().pcn_ipt_sync_counters(self._h, stream))

@@ -1,0 +1,168 @@
+"""Shared test helpers: scenario replay on the oracle and on the GPU datapath."""
+import json
+import os
+
+import numpy as np
+
+from polycube_amd import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CHAINS = {"INPUT": 0, "FORWARD": 1, "OUTPUT": 2}
+DIRS = {"ingress": 0, "egress": 1}
+
+
+def load_scenarios():
+    with open(os.path.join(GOLDEN, "scenarios.json")) as fh:
+        return json.load(fh)
+
+
+def ip_host(s):
+    a, b, c, d = (int(x) for x in s.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def ip_nbo(s):
+    return synth.ip_nbo(ip_host(s))
+
+
+def probe_frames(packets, stride=128):
+    """Frames (n*stride bytes), lens, in_port, ct (or None) for probe packet dicts."""
+    n = len(packets)
+    src = np.array([ip_host(p["src"]) for p in packets], np.uint32)
+    dst = np.array([ip_host(p["dst"]) for p in packets], np.uint32)
+    proto = np.array([p["proto"] for p in packets], np.int32)
+    sport = np.array([p["sport"] for p in packets], np.int32)
+    dport = np.array([p["dport"] for p in packets], np.int32)
+    flags = np.array([p["flags"] for p in packets], np.int32)
+    icmp = np.array([p.get("icmp_type", 0) for p in packets], np.int32)
+    f = synth.build_frames(src, dst, proto, sport, dport, flags, frame_len=stride, icmp_type=icmp)
+    lens = np.array([p["len"] for p in packets], np.uint16)
+    ports = np.array([p["port"] for p in packets], np.uint16)
+    ct = None
+    if all("ct" in p for p in packets):
+        ct = np.array([p["ct"] for p in packets], np.uint8)
+    return f.reshape(-1), lens, ports, ct
+
+
+def norm_rule(r):
+    r = dict(r)
+    r["action"] = str(r.get("action", "DROP")).upper()
+    if "l4proto" in r:
+        r["l4proto"] = r["l4proto"].upper()
+    return r
+
+
+class OracleCube:
+    """Mirror of the reference Chain rule-list semantics driving the CPU oracle."""
+
+    def __init__(self, oracle, ports, localip):
+        self.o = oracle
+        for name, idx in ports.items():
+            self.o.add_port(name, idx)
+        self.o.set_localip([ip_nbo(s) for s in localip])
+        self.rules = {c: [] for c in CHAINS}
+        self.default = {c: "ACCEPT" for c in CHAINS}
+        self.interactive = True
+        for c in CHAINS:
+            self._apply(c)
+
+    def _apply(self, c):
+        self.o.set_chain(CHAINS[c], self.rules[c], self.default[c])
+
+    def op(self, op):
+        kind = op[0]
+        if kind == "interactive":
+            self.interactive = bool(op[1])
+            return
+        c = op[1]
+        if kind == "append":
+            self.rules[c].append(op[2])
+        elif kind == "insert":
+            self.rules[c].insert(op[2], op[3])
+        elif kind == "delete":
+            self.rules[c].pop(op[2])
+        elif kind == "deletes":
+            want = norm_rule(op[2])
+            for i, r in enumerate(self.rules[c]):
+                if norm_rule(r) == want:
+                    self.rules[c].pop(i)
+                    break
+        elif kind == "flush":
+            self.rules[c] = []
+        elif kind == "default":
+            self.default[c] = op[2]
+            self._apply(c)
+            return
+        elif kind == "apply":
+            self._apply(c)
+            return
+        else:
+            raise ValueError(kind)
+        if self.interactive:
+            self._apply(c)
+
+    def probe(self, packets):
+        out = []
+        for d, dcode in DIRS.items():
+            sel = [p for p in packets if p["dir"] == d]
+            if not sel:
+                continue
+            f, lens, ports, ct = probe_frames(sel)
+            v, r = self.o.classify(f, n=len(sel), lens=lens, stride=128, in_port=ports, direction=dcode,
+                                   ct_status=ct)
+            out.extend(int(x) for x in v)
+        return out
+
+
+class GpuCube:
+    """The same scenario ops through the product C ABI (polycube_amd.Iptables)."""
+
+    def __init__(self, ipt, ports, localip):
+        import torch
+        self.torch = torch
+        self.ipt = ipt
+        for name, idx in ports.items():
+            ipt.add_port(name, idx)
+        ipt.set_localip([ip_nbo(s) for s in localip])
+
+    def op(self, op):
+        kind = op[0]
+        if kind == "interactive":
+            self.ipt.interactive = bool(op[1])
+            return
+        ch = self.ipt.chain(op[1])
+        if kind == "append":
+            ch.append(**op[2])
+        elif kind == "insert":
+            ch.insert(op[2], **op[3])
+        elif kind == "delete":
+            ch.delete(op[2])
+        elif kind == "deletes":
+            ch.deletes(**op[2])
+        elif kind == "flush":
+            ch.flush()
+        elif kind == "default":
+            ch.default = op[2]
+        elif kind == "apply":
+            ch.apply_rules()
+        else:
+            raise ValueError(kind)
+
+    def probe(self, packets):
+        torch = self.torch
+        out = []
+        for d, dcode in DIRS.items():
+            sel = [p for p in packets if p["dir"] == d]
+            if not sel:
+                continue
+            f, lens, ports, ct = probe_frames(sel)
+            dev = torch.device("cuda", self.ipt.device)
+            tf = torch.from_numpy(f).to(dev)
+            tl = torch.from_numpy(lens.astype(np.int16)).to(dev)
+            tp = torch.from_numpy(ports.astype(np.int16)).to(dev)
+            tc = None if ct is None else torch.from_numpy(ct).to(dev)
+            v, _ = self.ipt.classify(tf, n=len(sel), lens=tl, stride=128, in_port=tp, direction=dcode,
+                                     ct_status=tc)
+            torch.cuda.synchronize()
+            out.extend(int(x) for x in v.cpu().numpy())
+        return out

@@ -1,0 +1,56 @@
+"""The C-ABI library loads and exports every symbol include/pcn_ipt.h declares (CPU only)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from polycube_amd import ffi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "pcn_ipt.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(pcn_ipt_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_the_boundary():
+    names = header_functions()
+    for must in ("pcn_ipt_create", "pcn_ipt_load_chain", "pcn_ipt_classify", "pcn_ipt_read_counters",
+                 "pcn_ipt_set_localip", "pcn_ipt_sync_counters"):
+        assert must in names
+
+
+def test_library_exports_every_header_symbol():
+    lib = ffi.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", ffi.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (pcn_ipt_\w+)", out))
+    for name in header_functions():
+        assert name in exported, name
+        assert getattr(lib, name) is not None
+    assert set(header_functions()) == set(ffi.SIGNATURES), "ffi.SIGNATURES out of sync with the header"
+
+
+def test_abi_version():
+    assert ffi.lib().pcn_ipt_abi_version() == 1
+
+
+def test_classify_fails_loudly_without_device():
+    from polycube_amd import Iptables, IptablesError
+    ipt = Iptables(device=-1)
+    with pytest.raises(IptablesError) as e:
+        ipt.classify_ptrs(frames=1, frames_bytes=64, n=1, verdicts=1)
+    assert e.value.code == -19  # -ENODEV: no CPU fallback exists
+    ipt.close()
+
+
+def test_null_context_is_an_error():
+    assert ffi.lib().pcn_ipt_chain_flush(None, 0) < 0
+    assert b"null" in ffi.lib().pcn_ipt_last_error()
+    cfg = ffi.Config(-1, 0, 0, 70000)
+    h = C.c_void_p()
+    assert ffi.lib().pcn_ipt_create(C.byref(cfg), C.byref(h)) < 0
