@@ -1,0 +1,218 @@
+"""Headline benchmark: device-resident pcn-iptables classification on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): a 1,000-rule FORWARD
+chain (synth.config_rules(3), default DROP) over 2^24 synthetic 64-byte IPv4
+frames per GPU, 50/50 TCP/UDP, half built to hit a rule and half uniform random.
+One step = one classify pass over the resident batch (verdicts + per-rule and
+default counters); with N > 1 GPUs each rank owns its own 2^24-frame shard
+(weak scaling) and every step ends with the RCCL all-gather of the per-rule
+counters over xGMI (pcn_ipt_sync_counters).  Frames are in HBM before the timed
+region starts; the PCIe-inclusive rate is reported separately under "e2e".
+
+Run: python bench.py [--gpus N --steps K --warmup W]  (N > 1 under torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpkt/s device-resident classify @64B, 1k-rule chain, 1 GPU; %HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_PKT = 64             # algorithmic bytes: the 64-byte frame slot
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def gen_frames(n, rs, seed, chunk=1 << 22):
+    from polycube_amd import synth
+    out = np.empty((n, 64), np.uint8)
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        cols = synth.make_headers(rs, m, seed + s // chunk)
+        out[s:s + m] = synth.build_frames(*cols, frame_len=64)
+    return out.reshape(-1)
+
+
+def cpu_baseline(rules, frames, n, threads, min_seconds=8.0):
+    """The oracle (scalar C restatement of the reference eBPF algorithm) on the host cores."""
+    from oracle.ffi import Oracle
+    o = Oracle()
+    o.set_chain(1, rules, "DROP")
+    done, t0 = 0, time.perf_counter()
+    while True:
+        o.classify(frames, n=n, nthreads=threads)
+        done += n
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    return done / el / 1e6, done, el
+
+
+def parity_sample(o_rules, frames, v_dev, r_dev, k=1 << 16):
+    from oracle.ffi import Oracle
+    o = Oracle()
+    o.set_chain(1, o_rules, "DROP")
+    v, r = o.classify(frames[:k * 64], n=k, nthreads=4)
+    return bool(np.array_equal(v, v_dev[:k]) and np.array_equal(r, r_dev[:k]))
+
+
+def e2e_rate(ipt, frames_host, n, torch, chunk=1 << 21, nstreams=3, reps=2):
+    """Pinned host frames -> hipMemcpyAsync H2D -> classify -> D2H verdicts, pipelined."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = torch.from_numpy(frames_host[: n * 64]).pin_memory()
+    vout = torch.empty(n, dtype=torch.uint8).pin_memory()
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    dbuf = [torch.empty(chunk * 64, dtype=torch.uint8, device=dev) for _ in range(nstreams)]
+    vbuf = [torch.empty(chunk, dtype=torch.uint8, device=dev) for _ in range(nstreams)]
+    torch.cuda.synchronize()
+    best = 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for i, s in enumerate(range(0, n, chunk)):
+            m = min(chunk, n - s)
+            k = i % nstreams
+            st = streams[k]
+            with torch.cuda.stream(st):
+                dbuf[k][: m * 64].copy_(src[s * 64:(s + m) * 64], non_blocking=True)
+                ipt.classify(dbuf[k], n=m, verdicts=vbuf[k], rule_ids=False, stream=st.cuda_stream)
+                vout[s:s + m].copy_(vbuf[k][:m], non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, n / (time.perf_counter() - t0) / 1e6)
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--log2n", type=int, default=24, help="frames per GPU = 2^log2n")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe end-to-end leg")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from polycube_amd import Iptables, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    n = 1 << args.log2n
+    rs = synth.config_rules(3)
+    rules = rs.rules()
+    ipt = Iptables(device=local)
+    ipt.interactive = False
+    fw = ipt.chain("FORWARD")
+    for r in rules:
+        fw.append(**r)
+    fw.default = "DROP"
+    fw.apply_rules()
+    if world > 1:
+        uid = [Iptables.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ipt.comm_init(world, rank, uid[0])
+
+    t = time.perf_counter()
+    frames_host = gen_frames(n, rs, synth.CONFIG_SEEDS[3] + 7919 * rank)
+    log(f"[rank {rank}] generated {n} frames in {time.perf_counter() - t:.1f}s")
+    frames = torch.from_numpy(frames_host).to(dev)
+    verdicts = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    s_ptr = stream.cuda_stream
+
+    def step():
+        ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=False, stream=s_ptr)
+        if world > 1:
+            ipt.sync_counters(s_ptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=False, stream=s_ptr)
+        ev[k][1].record(stream)
+        if world > 1:
+            ipt.sync_counters(s_ptr)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        tt = torch.tensor([elapsed])
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    value = n * world * args.steps / elapsed / 1e6
+    achieved = BYTES_PER_PKT * n / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as fh:
+            pm = json.load(fh)
+        if pm.get("frames") == n:
+            traffic = pm.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        # one untimed pass with rule ids for the parity sample
+        rid = torch.empty(n, dtype=torch.int32, device=dev)
+        fw.read_counters(len(rules), flush=True)
+        ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=rid, stream=s_ptr)
+        torch.cuda.synchronize()
+        ok = parity_sample(rules, frames_host, verdicts[: 1 << 16].cpu().numpy(), rid[: 1 << 16].cpu().numpy())
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded synth.config_rules(3) + make_headers; no captured traffic)",
+            "config": {"workload": "config3: 1k-rule FORWARD chain, 64B IPv4 50/50 TCP/UDP frames resident in HBM",
+                       "rules": len(rules), "frames_per_gpu": n, "frame_bytes": 64,
+                       "parallelism": f"dp{world} (packet-index shards, RCCL counter all-gather)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "classify_kernel<true>", "kernel_ms": round(kern_ms, 4),
+                         "bytes_per_unit": BYTES_PER_PKT, "units_per_launch": n},
+            "parity_sample_vs_oracle": ok,
+        }
+        if world == 1 and not args.no_cpu:
+            threads = min(16, os.cpu_count() or 1)
+            sample = 1 << 22
+            v1, done1, el1 = cpu_baseline(rules, frames_host, sample, 1, min_seconds=3.0)
+            vT, doneT, elT = cpu_baseline(rules, frames_host, n, threads, min_seconds=6.0)
+            line["cpu_baseline"] = {
+                "value": round(vT, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+                "sample": f"{doneT} frames ({doneT // n} passes over the same 2^{args.log2n} batch) in {elT:.1f}s",
+                "single_core": {"value": round(v1, 2), "sample": f"{done1} frames of the batch in {el1:.1f}s"}}
+        if world == 1 and not args.no_e2e:
+            line["e2e"] = {"value": round(e2e_rate(ipt, frames_host, n, torch), 2), "unit": "Mpkt/s",
+                           "what": "pinned host frames -> H2D -> classify -> D2H verdicts, 3 streams, 2^21-frame chunks"}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ipt.close()
+
+
+if __name__ == "__main__":
+    main()
