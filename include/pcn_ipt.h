@@ -144,6 +144,23 @@ int pcn_ipt_load_chain(pcn_ipt *ctx, int chain, const pcn_ipt_tables *tables);
 int pcn_ipt_export_map(pcn_ipt *ctx, int chain, int field, uint32_t *keys, uint8_t *plen,
                        uint64_t *vecs, uint32_t cap, uint32_t nrw);
 uint32_t pcn_ipt_chain_nrw(pcn_ipt *ctx, int chain);
+/* Shape of a chain's compiled device image (diagnostics / capacity planning). */
+typedef struct {
+  uint32_t nrules;       /* rules in the chain */
+  uint32_t nrw;          /* 63-bit words per vector after the type-group permutation */
+  uint32_t nsw;          /* 64-bit summary words per vector */
+  uint32_t nvec;         /* distinct vectors (classes) across all fields */
+  uint32_t ngroups;      /* rule type groups */
+  uint32_t present;      /* bit f set: field module f present */
+  uint32_t table_bytes;  /* LDS-staged table image size */
+  uint64_t part_bytes;   /* partial vector words (part of the table image) */
+} pcn_ipt_chain_info;
+int pcn_ipt_chain_get_info(pcn_ipt *ctx, int chain, pcn_ipt_chain_info *out);
+/* Copy a chain's table image bytes and its scalar descriptor words (layout
+ * offsets, nrw, nsw, present, all_cls) for offline inspection.  Returns the
+ * image size; copies nothing when cap is too small. */
+int pcn_ipt_chain_get_image(pcn_ipt *ctx, int chain, uint8_t *buf, uint32_t cap, uint32_t *desc,
+                            uint32_t desc_cap);
 
 /* ---- datapath ---------------------------------------------------------- */
 /* Classify a batch (device pointers), stream = hipStream_t (NULL = default). */

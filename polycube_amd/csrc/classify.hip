@@ -1,20 +1,22 @@
 // classify.hip — the MI355X (gfx950) batch classifier for pcn-iptables.
 //
-// One lane per packet.  Each lane reads the 48-byte header window of its frame,
-// runs the reference's Parser / ChainSelector / ConntrackLabel checks
+// One lane per packet.  Each lane reads the 48-byte header window of its frame
+// and runs the reference's Parser / ChainSelector / ConntrackLabel checks
 // (Iptables_Parser_dp.c:94-153, Iptables_ChainSelector_dp.c:131-298,
-// Iptables_ConntrackLabel_dp.c:436-531), maps every present field to a class id
-// through the chain image (devchain.h), then finds the lowest rule whose bit
-// survives the AND of all field vectors (the IpLookup/L4*/InterfaceLookup/
-// TcpFlagsLookup/ConntrackMatch ANDs + BitScan + ActionLookup of
-// Iptables_*_dp.c).  Instead of ANDing every word of every vector, the lane
-// ANDs the per-vector word summaries first and only visits candidate words in
-// ascending order: the first non-zero word of the full AND is the same word,
-// so the rule id is identical.  Integer work only; no MFMA.
+// Iptables_ConntrackLabel_dp.c:436-531).  It then maps every present field to
+// a class through the chain's table image (devchain.h) — staged in LDS by each
+// workgroup — and ANDs the class summaries.  Only words whose summary bit
+// survives are fetched from the HBM vector pool, and only for fields whose
+// word is not FULL.  The lowest set bit of a word is its lowest rule id (the
+// permutation keeps ids ascending inside a word), so the matched rule is the
+// minimum over the non-zero candidate words — the same rule the reference's
+// per-field ANDs + BitScan pick (Iptables_{IpLookup,L4ProtocolLookup,
+// L4PortLookup,InterfaceLookup,TcpFlagsLookup,ConntrackMatch,BitScan,
+// ActionLookup}_dp.c).  Integer work only; no MFMA.
 //
-// Per-rule and default pkts/bytes counters are accumulated in an LDS histogram
-// per workgroup (u64 LDS atomics; default bins are wave-aggregated with a
-// ballot) and flushed once per workgroup with global u64 atomics.
+// Per-rule and default pkts/bytes counters go to an LDS histogram per
+// workgroup (u64 LDS atomics; default bins wave-aggregated with a ballot) that
+// is flushed once per workgroup with global u64 atomics.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -22,17 +24,47 @@
 #include "devchain.h"
 #include "pcn_ipt.h"
 
+extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
+
+// Measurement-only ablation builds (tools/ablate.py; never the product .so):
+// 1 parse only, 2 + field lookups, 3 + summary AND, 4 full minus counters.
+#ifndef PCN_ABLATE
+#define PCN_ABLATE 0
+#endif
+
 namespace pcn {
 
 namespace {
 
-constexpr int kBlock = 256;
+constexpr int kBlock = 512;
+constexpr uint32_t kHashMul = 0x9E3779B1u;
+constexpr uint32_t kNoRule = 0xFFFFFFFFu;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t bswap16u(uint32_t x) { return ((x & 0xff) << 8) | ((x >> 8) & 0xff); }
 
+// Table image accessor: LDS-staged (LDS=true) or read from HBM/L2.
+template <bool LDS>
+struct Tab {
+  const uint8_t *g;
+  uint32_t base;
+  __device__ __forceinline__ uint32_t u32(uint32_t off) const {
+    return LDS ? *reinterpret_cast<const uint32_t *>(pcn_smem + base + off)
+               : *reinterpret_cast<const uint32_t *>(g + off);
+  }
+  __device__ __forceinline__ uint32_t u16(uint32_t off) const {
+    return LDS ? *reinterpret_cast<const uint16_t *>(pcn_smem + base + off)
+               : *reinterpret_cast<const uint16_t *>(g + off);
+  }
+  __device__ __forceinline__ uint64_t u64(uint32_t off) const {
+    return LDS ? *reinterpret_cast<const uint64_t *>(pcn_smem + base + off)
+               : *reinterpret_cast<const uint64_t *>(g + off);
+  }
+};
+
 // 48-byte header window as 12 little-endian dwords.
 struct Hdr { uint32_t w[12]; };
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void load_fixed(const uint8_t *frame, Hdr &h) {
   const u32x4 *p = reinterpret_cast<const u32x4 *>(frame);
@@ -60,6 +92,18 @@ __device__ __forceinline__ void load_generic(const uint8_t *frames, uint64_t fra
   for (int k = 0; k < 12; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 }
 
+template <bool FIXED>
+__device__ __forceinline__ void load_header(const LaunchArgs &a, uint64_t i, Hdr &h, uint32_t &L) {
+  if (FIXED) {
+    load_fixed(a.frames + i * a.stride, h);
+    L = a.fixed_len;
+  } else {
+    uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
+    load_generic(a.frames, a.frames_bytes, off, h);
+    L = a.lens ? a.lens[i] : a.fixed_len;
+  }
+}
+
 __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
   uint32_t lo = 0, hi = a.nlocal;
   while (lo < hi) {
@@ -71,13 +115,31 @@ __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
   return false;
 }
 
-__device__ __forceinline__ uint32_t lpm(const uint32_t *l1, const uint32_t *blk, uint32_t h) {
-  uint32_t e = l1[h >> 16];
-  if (e & PCN_IP_PTR) {
-    e = blk[((e & ~PCN_IP_PTR) << 8) | ((h >> 8) & 0xff)];
-    if (e & PCN_IP_PTR) e = blk[((e & ~PCN_IP_PTR) << 8) | (h & 0xff)];
+// Kernel-LPM answer for a host-order address: bucket index on the top 12 bits,
+// then a binary search among the few boundaries inside the bucket.
+template <bool LDS>
+__device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t bnd, uint32_t cls,
+                                             uint32_t h) {
+  uint32_t b = h >> (32 - PCN_IP_BUCKET_BITS);
+  uint32_t lo = t.u16(bkt + 2 * b);
+  uint32_t hi = t.u16(bkt + 2 * b + 2);
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (t.u32(bnd + 4 * mid) <= h) lo = mid + 1; else hi = mid;
   }
-  return e;
+  return t.u16(cls + 2 * lo);
+}
+
+template <bool LDS>
+__device__ __forceinline__ uint32_t key_class(const Tab<LDS> &t, uint32_t tab, uint32_t mask, uint32_t wild,
+                                              uint32_t key) {
+  uint32_t h = (key * kHashMul) >> __builtin_clz(mask);
+  while (true) {
+    uint32_t e = t.u32(tab + 4 * h);
+    if (e == PCN_HASH_EMPTY) return wild;
+    if ((e >> 16) == key) return e & 0xffff;
+    h = (h + 1) & mask;
+  }
 }
 
 struct Parsed {
@@ -86,102 +148,141 @@ struct Parsed {
   uint32_t ct;                 // conntrack status 0..3 (or >3: invalid input)
 };
 
-// Rule-chain stage for lanes of one chain (ch is wave-uniform).
-// Returns verdict; sets rid (>=0 rule, -1 default, -2 no-chain drop).
-__device__ __forceinline__ uint32_t run_chain(const DevChain &ch, const Parsed &p, uint32_t port,
-                                              int32_t &rid) {
-  uint32_t cls[8];
-  uint32_t nf = 0;
-  bool miss = false;
+// Rule-chain stage (ch is wave-uniform).  Returns the verdict and sets rid
+// (>= 0 matched rule, -1 default action, -2 decided without the chain).
+// Every field has a fixed slot; absent or skipped fields hold the all-ones
+// class, so the eight summary loads issue back to back without branches.
+template <bool LDS>
+__device__ __forceinline__ uint32_t run_chain(const DevChain &ch, const Parsed &p, uint32_t port, int32_t &rid) {
+  const Tab<LDS> t{ch.image, ch.lds_image};
+  const TableLayout &lay = ch.lay;
   const uint32_t present = ch.present;
+  const uint32_t all = ch.all_cls;
+  uint32_t cls[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) cls[f] = all;
   if (present & (1u << PCN_IPT_F_CONNTRACK)) {
     if (p.ct > 3) { rid = PCN_IPT_RID_NOCHAIN; return PCN_IPT_DROP; }   // array miss => RX_DROP
-    uint32_t c = ch.ct_cls[p.ct];
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
+    cls[0] = t.u16(lay.ct + 2 * p.ct);
   }
-  if (present & (1u << PCN_IPT_F_IPSRC)) {
-    uint32_t c = lpm(ch.ip_l1[0], ch.ip_blk[0], __builtin_bswap32(p.saddr));
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
+  if (present & (1u << PCN_IPT_F_IPSRC))
+    cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
+  if (present & (1u << PCN_IPT_F_IPDST))
+    cls[2] = ip_class(t, lay.ip_bkt[1], lay.ip_bnd[1], lay.ip_cls[1], __builtin_bswap32(p.daddr));
+  if (present & (1u << PCN_IPT_F_L4PROTO)) cls[3] = t.u16(lay.proto + 2 * p.proto);
+  const bool l4 = p.proto == 6 || p.proto == 17;                    // L4PortLookup_dp.c:99-103
+  if (present & (1u << PCN_IPT_F_SPORT)) {
+    uint32_t c = key_class(t, lay.hash[0], lay.hash_mask[0], lay.hash_wild[0], p.sport);
+    cls[4] = l4 ? c : all;
   }
-  if (present & (1u << PCN_IPT_F_IPDST)) {
-    uint32_t c = lpm(ch.ip_l1[1], ch.ip_blk[1], __builtin_bswap32(p.daddr));
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
+  if (present & (1u << PCN_IPT_F_DPORT)) {
+    uint32_t c = key_class(t, lay.hash[1], lay.hash_mask[1], lay.hash_wild[1], p.dport);
+    cls[5] = l4 ? c : all;
   }
-  if (present & (1u << PCN_IPT_F_L4PROTO)) {
-    uint32_t c = ch.proto_cls[p.proto];
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
+  if (present & (1u << PCN_IPT_F_IFACE))
+    cls[6] = key_class(t, lay.hash[2], lay.hash_mask[2], lay.hash_wild[2], port);
+  if (present & (1u << PCN_IPT_F_TCPFLAGS)) {                      // TcpFlagsLookup_dp.c:93-97
+    uint32_t c = t.u16(lay.flags + 2 * p.flags);
+    cls[7] = p.proto == 6 ? c : all;
   }
-  const bool l4 = p.proto == 6 || p.proto == 17;   // L4PortLookup_dp.c:99-103
-  if ((present & (1u << PCN_IPT_F_SPORT)) && l4) {
-    uint32_t c = ch.key_cls[0][p.sport];
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
-  }
-  if ((present & (1u << PCN_IPT_F_DPORT)) && l4) {
-    uint32_t c = ch.key_cls[1][p.dport];
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
-  }
-  if (present & (1u << PCN_IPT_F_IFACE)) {
-    uint32_t c = ch.key_cls[2][port];
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
-  }
-  if ((present & (1u << PCN_IPT_F_TCPFLAGS)) && p.proto == 6) {   // TcpFlagsLookup_dp.c:93-97
-    uint32_t c = ch.flags_cls[p.flags];
-    miss |= c == PCN_CLS_MISS; cls[nf] = c; nf += c != PCN_CLS_MISS;
-  }
+  bool miss = false;
+#pragma unroll
+  for (int f = 0; f < 8; ++f) miss |= cls[f] == PCN_CLS_MISS;
   if (miss) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(ch.default_action); }
+  if (PCN_ABLATE == 2) {   // keep the lookups alive: the verdict depends on them
+    uint32_t x = 0;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) x ^= cls[f];
+    rid = PCN_IPT_RID_DEFAULT;
+    return x & 1;
+  }
 
   const uint32_t nrw = ch.nrw, nsw = ch.nsw;
-  int32_t rule = -1;
-  for (uint32_t k = 0; k < nsw && rule < 0; ++k) {
+  uint32_t best = kNoRule;   // (orig id << 1 | action), minimum over candidate words
+  uint64_t mseen = 0;        // PCN_ABLATE == 3 only
+  for (uint32_t k = 0; k < nsw; ++k) {
     uint32_t live = nrw - k * 64;
     uint64_t m = live >= 64 ? ~0ull : ((1ull << live) - 1);
+    uint64_t s[8];
 #pragma unroll
-    for (int f = 0; f < 8; ++f)
-      if (f < static_cast<int>(nf)) m &= ch.summ[cls[f] * nsw + k];
+    for (int f = 0; f < 8; ++f) s[f] = t.u64(lay.summ + 8 * (cls[f] * nsw + k));
+#pragma unroll
+    for (int f = 0; f < 8; ++f) m &= s[f];
+    if (PCN_ABLATE == 3) { mseen |= m; continue; }
+    if (!m) continue;
+    uint64_t fm[8];
+    uint32_t pb[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      const uint32_t rec = cls[f] * nsw + k;
+      fm[f] = t.u64(lay.full + 8 * rec);
+      pb[f] = t.u32(lay.pbase + 4 * rec);
+      s[f] &= ~fm[f];                 // s[f] now marks the partial words
+    }
     while (m) {
-      uint32_t w = k * 64 + static_cast<uint32_t>(__builtin_ctzll(m));
-      uint64_t acc = 0x7FFFFFFFFFFFFFFFull;   // ChainSelector_dp.c:205-218 init
+      const uint32_t bit = static_cast<uint32_t>(__builtin_ctzll(m));
+      m &= m - 1;
+      const uint32_t w = k * 64 + bit;
+      const uint64_t below = (1ull << bit) - 1;
+      uint64_t v[8];
 #pragma unroll
       for (int f = 0; f < 8; ++f)
-        if (f < static_cast<int>(nf)) acc &= ch.pool[cls[f] * nrw + w];
-      if (acc) { rule = static_cast<int32_t>(w * 63 + __builtin_ctzll(acc)); break; }
-      m &= m - 1;
+        v[f] = ((fm[f] >> bit) & 1)
+                   ? ~0ull
+                   : t.u64(lay.part + 8 * (pb[f] + static_cast<uint32_t>(__builtin_popcountll(s[f] & below))));
+      uint64_t acc = ~0ull;
+#pragma unroll
+      for (int f = 0; f < 8; ++f) acc &= v[f];
+      if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
+        uint32_t e = t.u16(lay.perm + 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
+        best = e < best ? e : best;
+      }
     }
   }
-  if (rule < 0) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(ch.default_action); }
-  if (static_cast<uint32_t>(rule) >= ch.max_action) { rid = PCN_IPT_RID_NOCHAIN; return PCN_IPT_DROP; }
-  rid = rule;
-  return ch.actions[rule] ? PCN_IPT_ACCEPT : PCN_IPT_DROP;
+  if (PCN_ABLATE == 3) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(mseen & 1); }
+  if (best == kNoRule) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(ch.default_action); }
+  uint32_t rule = best >> 1;
+  if (rule >= ch.max_action) { rid = PCN_IPT_RID_NOCHAIN; return PCN_IPT_DROP; }
+  rid = static_cast<int32_t>(rule);
+  return (best & 1) ? PCN_IPT_ACCEPT : PCN_IPT_DROP;
 }
 
-template <bool FIXED>
+template <bool FIXED, bool LDS, int CH>
 __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
-  extern __shared__ unsigned long long bins[];   // [nbins][2]: pkts, bytes
+  unsigned long long *bins = reinterpret_cast<unsigned long long *>(pcn_smem + a.bins_offset);
+  // stage every chain's table image in LDS and zero the counter histogram
+  if (LDS) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const DevChain &ch = a.ch[c];
+      if (!ch.nrules) continue;
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(ch.image);
+      u32x4 *dst = reinterpret_cast<u32x4 *>(pcn_smem + ch.lds_image);
+      for (uint32_t k = threadIdx.x; k < ch.lay.bytes / 16; k += blockDim.x) dst[k] = src[k];
+    }
+  }
   for (uint32_t b = threadIdx.x; b < 2 * a.nbins; b += blockDim.x) bins[b] = 0;
   __syncthreads();
 
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t n_round = (a.n + step - 1) / step * step;   // uniform trip count per wave
+  // software pipeline: the next frame's header is in flight while this one is classified
+  Hdr nh;
+  uint32_t nL = 0;
+  if (first < a.n) load_header<FIXED>(a, first, nh, nL);
   for (uint64_t i = first; i < n_round; i += step) {
     const bool valid = i < a.n;
+    const Hdr h = nh;
+    const uint32_t L = nL;
+    if (i + step < a.n) load_header<FIXED>(a, i + step, nh, nL);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
     int32_t cchain = -1;    // chain whose counters this packet bumps
-    uint32_t L = 0;
     int32_t chain = -1;     // chain whose rules must run (-1: decided already)
     Parsed p{};
     uint32_t port = 0;
     if (valid) {
-      Hdr h;
-      if (FIXED) {
-        load_fixed(a.frames + i * a.stride, h);
-        L = a.fixed_len;
-      } else {
-        uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
-        load_generic(a.frames, a.frames_bytes, off, h);
-        L = a.lens ? a.lens[i] : a.fixed_len;
-      }
       port = a.in_port ? a.in_port[i] : a.const_in_port;
       // ---- Parser_dp.c:94-153 ----
       bool done = true;
@@ -212,9 +313,9 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
           if (a.nlocal && localip_has(a, p.saddr)) chain = PCN_IPT_OUTPUT;
           else { verdict = PCN_IPT_ACCEPT; done = true; }   // egress PASS
         }
-        if (!done && chain >= 0 && a.ch[chain].nrules == 0) {
+        if (!done && chain >= 0 && ((a.empty_mask >> chain) & 1)) {
           cchain = chain; rid = PCN_IPT_RID_DEFAULT;       // default counters
-          if (a.ch[chain].default_action == PCN_IPT_DROP) { verdict = PCN_IPT_DROP; done = true; }
+          if ((a.drop_mask >> chain) & 1) { verdict = PCN_IPT_DROP; done = true; }
           pass = true;
           chain = -1;
         }
@@ -242,15 +343,24 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
         if (done) chain = -1;
       }
     }
-    // ---- rule chains: one wave-uniform chain at a time ----
-    while (true) {
-      uint64_t pending = __ballot(chain >= 0);
-      if (!pending) break;
-      int32_t c = __builtin_amdgcn_readfirstlane(__shfl(chain, __builtin_ctzll(pending)));
-      if (chain == c) {
-        verdict = run_chain(a.ch[c], p, port, rid);
-        cchain = c;
-        chain = -1;
+    // ---- rule chains ----
+    // CH < 3: only chain CH can reach the rule stage in this launch (the host
+    // picks the variant), so its descriptor is a constant-index kernarg load
+    // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
+    if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
+    if (CH < 3) {
+      if (chain >= 0) {
+        verdict = run_chain<LDS>(a.ch[CH < 3 ? CH : 0], p, port, rid);
+        cchain = chain;
+      }
+    } else {
+      if (__ballot(chain == PCN_IPT_FORWARD) && chain == PCN_IPT_FORWARD) {
+        verdict = run_chain<LDS>(a.ch[PCN_IPT_FORWARD], p, port, rid);
+        cchain = PCN_IPT_FORWARD;
+      }
+      if (__ballot(chain == PCN_IPT_INPUT) && chain == PCN_IPT_INPUT) {
+        verdict = run_chain<LDS>(a.ch[PCN_IPT_INPUT], p, port, rid);
+        cchain = PCN_IPT_INPUT;
       }
     }
     if (valid) {
@@ -258,24 +368,32 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
       if (a.rule_ids) a.rule_ids[i] = rid;
     }
     // ---- counters ----
-    // default bins: wave-aggregated per chain
-    for (int c = 0; c < 3; ++c) {
-      bool mine = valid && cchain == c && rid == PCN_IPT_RID_DEFAULT;
-      uint64_t m = __ballot(mine);
-      if (!m) continue;
-      uint32_t bytes = mine ? L : 0u;
+    if (PCN_ABLATE == 4) continue;
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) bytes += __shfl_xor(bytes, o);
-      if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&bins[2 * c], static_cast<unsigned long long>(__builtin_popcountll(m)));
-        atomicAdd(&bins[2 * c + 1], static_cast<unsigned long long>(bytes));
+    for (int c = 0; c < 3; ++c) {
+      // default bins: wave-aggregated per chain
+      const bool mine = valid && cchain == c && rid == PCN_IPT_RID_DEFAULT;
+      const uint64_t m = __ballot(mine);
+      if (m) {
+        unsigned long long bytes;
+        if (FIXED) {
+          bytes = static_cast<unsigned long long>(__builtin_popcountll(m)) * a.fixed_len;
+        } else {
+          uint32_t x = mine ? L : 0u;
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+          bytes = x;
+        }
+        if ((threadIdx.x & 63) == 0) {
+          atomicAdd(&bins[2 * c], static_cast<unsigned long long>(__builtin_popcountll(m)));
+          atomicAdd(&bins[2 * c + 1], bytes);
+        }
       }
-    }
-    if (valid && cchain >= 0 && rid >= 0) {
-      const DevChain &ch = a.ch[cchain];
-      if (static_cast<uint32_t>(rid) < ch.ncounted) {
-        if (ch.lds_base >= 0) {
-          uint32_t b = static_cast<uint32_t>(ch.lds_base) + static_cast<uint32_t>(rid);
+      // per-rule bins
+      const DevChain &ch = a.ch[c];
+      if (valid && cchain == c && rid >= 0 && static_cast<uint32_t>(rid) < ch.ncounted) {
+        if (ch.lds_bins >= 0) {
+          uint32_t b = static_cast<uint32_t>(ch.lds_bins) + static_cast<uint32_t>(rid);
           atomicAdd(&bins[2 * b], 1ull);
           atomicAdd(&bins[2 * b + 1], static_cast<unsigned long long>(L));
         } else {
@@ -290,37 +408,52 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   for (uint32_t b = threadIdx.x; b < a.nbins; b += blockDim.x) {
     unsigned long long pk = bins[2 * b], by = bins[2 * b + 1];
     if (!pk) continue;
-    unsigned long long *dst;
+    unsigned long long *dst = nullptr;
     if (b < 3) {
       dst = a.ch[b].ctr;
     } else {
-      int c = 0;
-      for (; c < 3; ++c) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
         const DevChain &ch = a.ch[c];
-        if (ch.lds_base >= 0 && b >= static_cast<uint32_t>(ch.lds_base) &&
-            b < static_cast<uint32_t>(ch.lds_base) + ch.ncounted) break;
+        if (ch.lds_bins >= 0 && b >= static_cast<uint32_t>(ch.lds_bins) &&
+            b < static_cast<uint32_t>(ch.lds_bins) + ch.ncounted)
+          dst = ch.ctr + 2 + 2 * (b - static_cast<uint32_t>(ch.lds_bins));
       }
-      if (c == 3) continue;
-      dst = a.ch[c].ctr + 2 + 2 * (b - static_cast<uint32_t>(a.ch[c].lds_base));
+      if (!dst) continue;
     }
     atomicAdd(dst, pk);
     atomicAdd(dst + 1, by);
   }
 }
 
+template <bool FIXED, bool LDS>
+void launch_variant(const LaunchArgs &a, int ch, unsigned grid, size_t lds, hipStream_t stream) {
+  switch (ch) {
+    case 0: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 0>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+    case 1: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 1>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+    case 2: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 2>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+    default: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 3>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+  }
+}
+
 }  // namespace
 
-// Host-side launcher (called from pcn_ipt.cpp).  Returns a hipError_t value.
-int launch_classify(const LaunchArgs &a, bool fixed, int num_cus, hipStream_t stream) {
+// Host-side launcher (called from pcn_ipt.cpp).  `ch` is the only chain that can
+// reach the rule stage (0..2) or 3 for INPUT+FORWARD.  Returns a hipError_t.
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
+  const size_t lds = a.bins_offset + static_cast<size_t>(a.nbins) * 16;
+  const bool in_lds = a.lds_images_bytes > 0;
+  size_t per_cu = lds ? (160 * 1024) / lds : 4;
+  if (per_cu > 4) per_cu = 4;
+  if (per_cu < 1) per_cu = 1;
   const uint64_t want = (a.n + kBlock - 1) / kBlock;
-  const uint64_t cap = static_cast<uint64_t>(num_cus) * 8;
+  const uint64_t cap = static_cast<uint64_t>(num_cus) * per_cu;
   const unsigned grid = static_cast<unsigned>(want < cap ? want : cap);
-  const size_t lds = static_cast<size_t>(a.nbins) * 2 * sizeof(unsigned long long);
-  if (fixed)
-    hipLaunchKernelGGL(classify_kernel<true>, dim3(grid), dim3(kBlock), lds, stream, a);
-  else
-    hipLaunchKernelGGL(classify_kernel<false>, dim3(grid), dim3(kBlock), lds, stream, a);
+  if (fixed && in_lds) launch_variant<true, true>(a, ch, grid, lds, stream);
+  else if (fixed) launch_variant<true, false>(a, ch, grid, lds, stream);
+  else if (in_lds) launch_variant<false, true>(a, ch, grid, lds, stream);
+  else launch_variant<false, false>(a, ch, grid, lds, stream);
   return static_cast<int>(hipGetLastError());
 }
 

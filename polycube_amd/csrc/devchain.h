@@ -3,40 +3,67 @@
 //
 // The reference keeps one BPF map per field module (LPM trie / hash / array of
 // 1,048-byte bitvectors, Iptables_*Lookup_dp.c) and walks them with ~12 tail
-// calls per packet.  Here a chain is one contiguous HBM blob:
-//   * IP fields: DIR-16-8-8 tables (u32 entries) giving the kernel-LPM answer
-//     for any /32 key (longest prefix, same-prefix last-writer-wins);
-//   * port / interface fields: direct 65,536-entry u16 class tables with the
-//     wildcard fallback (key 0 / 0xffff) already folded in;
-//   * proto / tcp-flags / conntrack: 256/256/4-entry u16 class tables;
-//   * a deduplicated bitvector pool [nvec][nrw] (63 rule bits per word) plus a
-//     per-vector summary [nvec][nsw] (bit w set iff word w != 0).
-// A class id of PCN_CLS_MISS means "lookup miss with no wildcard" => default.
+// calls per packet.  Here a chain is one compact TABLE IMAGE (tens of KB at
+// 1k rules) that each workgroup copies into LDS, so the per-packet path makes
+// no dependent HBM/L2 access at all:
+//   - IP src/dst: the kernel-LPM answer as sorted interval boundaries plus a
+//     4096-bucket index on the top 12 address bits;
+//   - sport/dport/iface: open-addressing hashes {key -> class} with the
+//     wildcard class (key 0 / 0xffff) as the miss fallback;
+//   - proto/tcpflags/conntrack: 256/256/4-entry class tables;
+//   - per class and 64-word block: SUMM (bit w: word w of the class vector
+//     != 0), FULL (bit w: word w holds all of its rules) and PBASE, the start
+//     of the class's PARTIAL words (neither zero nor full) in PART, stored in
+//     word order (a partial word's index = PBASE + popcount(partial bits below));
+//   - PERM: bit position -> (original rule id << 1 | action).
+// Images too large for LDS are read from HBM through the same accessors.
+//
+// Rule bits are permuted so rules that constrain the same set of fields share
+// words ("type groups"); a field a word's rules do not constrain has that word
+// FULL, and a field they do constrain has a sparse summary, which is what makes
+// the summary AND selective.  Inside a word, bits are in ascending rule id, so
+// the lowest set bit of a word is its lowest-numbered matching rule and the
+// packet's rule is the minimum over its non-zero candidate words.
 #pragma once
 #include <cstdint>
 
 #define PCN_CLS_MISS 0xFFFFu
-#define PCN_IP_PTR 0x80000000u
 #define PCN_MAX_LOCALIP 256
+#define PCN_IP_BUCKET_BITS 12
+#define PCN_HASH_EMPTY 0xFFFFFFFFu
 
 namespace pcn {
 
+// Byte offsets inside a table image (all 16-byte aligned).
+struct TableLayout {
+  uint32_t bytes;
+  uint32_t ip_bkt[2];      // u32[4097]: first boundary index per bucket (+ sentinel)
+  uint32_t ip_bnd[2];      // u32[m]: interval boundaries (host-order addresses)
+  uint32_t ip_cls[2];      // u16[m+1]: class of each interval
+  uint32_t hash[3];        // u32[size]: (key << 16) | class  (sport, dport, iface)
+  uint32_t hash_mask[3];   // size - 1
+  uint32_t hash_wild[3];   // class used when the key is absent (PCN_CLS_MISS: none)
+  uint32_t proto, flags, ct;   // u16[256], u16[256], u16[4]
+  uint32_t summ, full;     // u64[nvec][nsw]
+  uint32_t pbase;          // u32[nvec][nsw]: first PART index of the class's block
+  uint32_t part;           // u64[]: partial words
+  uint32_t perm;           // u16[nrw * 63]
+};
+
 struct DevChain {
-  const uint32_t *ip_l1[2];      // [0]=src [1]=dst: 65536 entries, index = host-order ip >> 16
-  const uint32_t *ip_blk[2];     // 256-entry blocks for /17../32
-  const uint16_t *key_cls[3];    // [0]=sport [1]=dport [2]=iface, 65536 entries each
-  const uint16_t *proto_cls;     // 256
-  const uint16_t *flags_cls;     // 256
-  const uint16_t *ct_cls;        // 4
-  const uint64_t *pool;          // [nvec][nrw]
-  const uint64_t *summ;          // [nvec][nsw]
-  const uint8_t *actions;        // [nrules] 0 DROP / 1 ACCEPT
+  TableLayout lay;
+  const uint8_t *image;          // table image in HBM (copied to LDS when it fits)
   unsigned long long *ctr;       // [2 + 2*ncounted]: def_pkts, def_bytes, pkts0, bytes0, ...
-  uint32_t nrules, nrw, nsw, present;
+  uint32_t nrules, nrw, nsw, present, nvec;
+  uint32_t all_cls;              // class of the all-ones vector (fields absent or skipped)
   uint32_t ncounted, max_action;
   int32_t default_action;
-  int32_t lds_base;              // first LDS bin of this chain's rules; -1 => global atomics
+  uint32_t lds_image;            // byte offset of this chain's image in LDS
+  int32_t lds_bins;              // first LDS counter bin of this chain's rules; -1 => global atomics
 };
+
+// LDS layout of a classify workgroup: [chain images][counter bins]
+constexpr uint32_t kLdsDescBytes = 0;
 
 struct LaunchArgs {
   DevChain ch[3];
@@ -52,10 +79,14 @@ struct LaunchArgs {
   uint64_t n;
   uint32_t stride, fixed_len;
   uint32_t nlocal;
-  uint32_t nbins;                // LDS bins (3 default bins + rule bins)
+  uint32_t nbins;                // LDS counter bins (3 default bins + rule bins)
+  uint32_t bins_offset;          // byte offset of the counter bins in LDS
+  uint32_t lds_images_bytes;     // bytes of chain images staged in LDS after the descriptors (0: from HBM)
   uint16_t const_in_port;
   uint16_t direction;
   uint32_t allow_logic;          // _INGRESS_ALLOWLOGIC (modules/ChainSelector.cpp:190-202)
+  uint32_t empty_mask;           // bit c: chain c has no rules (ChainSelector default path)
+  uint32_t drop_mask;            // bit c: chain c's default action is DROP
 };
 
 }  // namespace pcn

@@ -1,98 +1,121 @@
-// image.cpp — chain tables -> HBM chain image (see devchain.h for the layout).
+// image.cpp — chain tables -> chain image (see devchain.h for the layout).
 #include "image.hpp"
 
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <numeric>
 #include <stdexcept>
 #include <string>
-
-#include "devchain.h"
 
 namespace pcn {
 namespace {
 
-constexpr size_t kAlign = 256;
+constexpr size_t kAlign = 16;
 constexpr uint32_t kTrieCapacity = 1024;   // Iptables_IpLookup_dp.c:54-55
+constexpr size_t kGroupAlignMin = 8;       // type groups this large start on a fresh word
+constexpr uint32_t kHashMul = 0x9E3779B1u;
 
-// Vector dedup across all fields of a chain: identical bitvectors share one
-// pool slot (and one summary).
-class VecPool {
- public:
-  explicit VecPool(uint32_t nrw) : nrw_(nrw) {}
-  uint16_t intern(const BitVec &v) {
-    BitVec key(v.begin(), v.begin() + nrw_);
-    auto it = ids_.find(key);
-    if (it != ids_.end()) return it->second;
-    if (vecs_.size() >= PCN_CLS_MISS) throw std::runtime_error("too many distinct rule bitvectors");
-    uint16_t id = static_cast<uint16_t>(vecs_.size());
-    ids_.emplace(key, id);
-    vecs_.push_back(std::move(key));
-    return id;
-  }
-  const std::vector<BitVec> &vecs() const { return vecs_; }
- private:
-  uint32_t nrw_;
-  std::map<BitVec, uint16_t> ids_;
-  std::vector<BitVec> vecs_;
-};
+inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
+inline uint32_t prefix_mask(uint8_t len) { return len == 0 ? 0u : ~uint32_t(0) << (32 - len); }
+inline bool test_bit(const BitVec &v, uint32_t id) { return (v[id / kBitsPerWord] >> (id % kBitsPerWord)) & 1; }
 
 struct Blob {
   std::vector<uint8_t> bytes;
   template <typename T>
-  size_t add(const std::vector<T> &v) {
+  uint32_t add(const std::vector<T> &v) {
     size_t off = (bytes.size() + kAlign - 1) / kAlign * kAlign;
-    bytes.resize(off + v.size() * sizeof(T));
+    bytes.resize(off + std::max<size_t>(v.size() * sizeof(T), kAlign));
     if (!v.empty()) std::memcpy(bytes.data() + off, v.data(), v.size() * sizeof(T));
-    return off;
+    return static_cast<uint32_t>(off);
   }
 };
 
-inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
-inline uint32_t prefix_mask(uint8_t len) { return len == 0 ? 0u : ~uint32_t(0) << (32 - len); }
+// Rule -> bit position permutation.  Rules are ordered by the set of fields
+// they constrain (their "type"), larger type groups start on a fresh 63-bit
+// word, and each word lists its rules in ascending id.
+struct Permutation {
+  uint32_t nrw = 0;
+  std::vector<uint32_t> pos;        // rule id -> bit position
+  std::vector<uint16_t> perm;       // bit position -> id << 1 | action (PCN pad: 0xFFFF)
+  std::vector<uint64_t> valid;      // per word: bits holding a rule
+  uint32_t ngroups = 0;
+};
 
-// DIR-16-8-8 expansion.  Prefixes are painted shortest first, so a longer
-// prefix always overwrites the shorter ones it nests in (= longest match).
-struct DirTable {
-  std::vector<uint32_t> l1 = std::vector<uint32_t>(65536, PCN_CLS_MISS);
-  std::vector<uint32_t> blk;
+Permutation make_permutation(const ChainTables &t, const std::vector<std::vector<const BitVec *>> &field_vecs) {
+  const uint32_t n = t.nrules;
+  std::vector<uint32_t> type(n, 0);
+  for (int f = 0; f < PCN_IPT_NFIELDS; ++f) {
+    const auto &vs = field_vecs[f];
+    if (vs.empty()) continue;
+    BitVec all(t.nrw, ~uint64_t(0));
+    for (const BitVec *v : vs)
+      for (uint32_t w = 0; w < t.nrw; ++w) all[w] &= (*v)[w];
+    for (uint32_t r = 0; r < n; ++r)
+      if (!test_bit(all, r)) type[r] |= 1u << f;   // r is not a wildcard in field f
+  }
+  std::vector<uint32_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return type[a] < type[b]; });
+  std::map<uint32_t, size_t> group_size;
+  for (uint32_t r = 0; r < n; ++r) group_size[type[r]]++;
+  std::vector<std::vector<uint32_t>> words;
+  uint32_t cur_type = ~0u;
+  for (uint32_t r : order) {
+    bool fresh = words.empty() || words.back().size() == kBitsPerWord;
+    if (type[r] != cur_type) {
+      cur_type = type[r];
+      if (group_size[cur_type] >= kGroupAlignMin) fresh = true;
+    }
+    if (fresh && !(words.size() && words.back().empty())) words.emplace_back();
+    words.back().push_back(r);
+  }
+  Permutation p;
+  p.ngroups = static_cast<uint32_t>(group_size.size());
+  p.nrw = static_cast<uint32_t>(words.size());
+  p.pos.assign(n, 0);
+  p.perm.assign(size_t(p.nrw) * kBitsPerWord, 0xFFFF);
+  p.valid.assign(p.nrw, 0);
+  for (uint32_t w = 0; w < p.nrw; ++w) {
+    std::sort(words[w].begin(), words[w].end());
+    for (uint32_t j = 0; j < words[w].size(); ++j) {
+      uint32_t r = words[w][j];
+      uint32_t bit = w * kBitsPerWord + j;
+      p.pos[r] = bit;
+      p.perm[bit] = static_cast<uint16_t>((r << 1) | (t.actions[r] ? 1u : 0u));
+      p.valid[w] |= uint64_t(1) << j;
+    }
+  }
+  return p;
+}
 
-  uint32_t push_block(uint32_t fill) {
-    uint32_t id = static_cast<uint32_t>(blk.size() / 256);
-    blk.insert(blk.end(), 256, fill);
+class VecPool {
+ public:
+  VecPool(const Permutation &p, uint32_t n) : p_(p), n_(n) {}
+  uint16_t intern(const BitVec &orig) {
+    BitVec v(p_.nrw, 0);
+    for (uint32_t w = 0; w * kBitsPerWord < n_ && w < orig.size(); ++w) {
+      uint64_t bits = orig[w];
+      while (bits) {
+        uint32_t r = w * kBitsPerWord + static_cast<uint32_t>(__builtin_ctzll(bits));
+        bits &= bits - 1;
+        if (r < n_) { uint32_t q = p_.pos[r]; v[q / kBitsPerWord] |= uint64_t(1) << (q % kBitsPerWord); }
+      }
+    }
+    auto it = ids_.find(v);
+    if (it != ids_.end()) return it->second;
+    if (vecs_.size() >= PCN_CLS_MISS) throw std::runtime_error("too many distinct rule bitvectors");
+    uint16_t id = static_cast<uint16_t>(vecs_.size());
+    ids_.emplace(v, id);
+    vecs_.push_back(std::move(v));
     return id;
   }
-  // Turn a leaf slot into a pointer to a fresh block filled with the leaf;
-  // returns the block id.  (Slots are addressed by index: push_block may
-  // reallocate `blk`.)
-  uint32_t descend_l1(uint32_t s) {
-    if (!(l1[s] & PCN_IP_PTR)) l1[s] = PCN_IP_PTR | push_block(l1[s]);
-    return l1[s] & ~PCN_IP_PTR;
-  }
-  uint32_t descend_blk(size_t at) {
-    if (!(blk[at] & PCN_IP_PTR)) {
-      uint32_t id = push_block(blk[at]);
-      blk[at] = PCN_IP_PTR | id;
-    }
-    return blk[at] & ~PCN_IP_PTR;
-  }
-  void paint(uint32_t prefix, uint8_t len, uint32_t cls) {
-    if (len <= 16) {
-      uint32_t first = prefix >> 16, count = 1u << (16 - len);
-      for (uint32_t s = first; s < first + count; ++s) l1[s] = cls;
-      return;
-    }
-    uint32_t b2 = descend_l1(prefix >> 16);
-    uint32_t mid = (prefix >> 8) & 0xff;
-    if (len <= 24) {
-      uint32_t count = 1u << (24 - len);
-      for (uint32_t j = mid; j < mid + count; ++j) blk[b2 * 256 + j] = cls;
-      return;
-    }
-    uint32_t b3 = descend_blk(size_t(b2) * 256 + mid);
-    uint32_t lo = prefix & 0xff, count = 1u << (32 - len);
-    for (uint32_t k = lo; k < lo + count; ++k) blk[b3 * 256 + k] = cls;
-  }
+  const std::vector<BitVec> &vecs() const { return vecs_; }
+ private:
+  const Permutation &p_;
+  uint32_t n_;
+  std::map<BitVec, uint16_t> ids_;
+  std::vector<BitVec> vecs_;
 };
 
 }  // namespace
@@ -112,81 +135,163 @@ std::vector<LpmEntry> lpm_entries(const FieldMap &m) {
   return out;   // sorted by (len, prefix): shortest first
 }
 
+Intervals lpm_intervals(const FieldMap &m) {
+  std::vector<LpmEntry> es = lpm_entries(m);
+  std::vector<uint64_t> pts{0};
+  for (const LpmEntry &e : es) {
+    uint64_t lo = e.prefix, hi = uint64_t(e.prefix) + (uint64_t(1) << (32 - e.len));
+    pts.push_back(lo);
+    if (hi <= 0xFFFFFFFFull) pts.push_back(hi);
+  }
+  std::sort(pts.begin(), pts.end());
+  pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+  Intervals iv;
+  for (uint64_t s : pts) {
+    // longest prefix covering s (entries are sorted by length: keep the last hit)
+    int32_t cls = -1;
+    for (const LpmEntry &e : es)
+      if ((uint32_t(s) & prefix_mask(e.len)) == e.prefix) cls = static_cast<int32_t>(e.vec);
+    if (!iv.cls.empty() && iv.cls.back() == cls) continue;
+    if (s != 0) iv.bnd.push_back(static_cast<uint32_t>(s));
+    iv.cls.push_back(cls);
+  }
+  return iv;
+}
+
 HostImage build_image(const ChainTables &t) {
   HostImage img;
   img.nrules = t.nrules;
-  img.nrw = t.nrw;
-  img.nsw = (t.nrw + 63) / 64;
   img.default_action = t.default_action;
   Blob blob;
-  VecPool pool(t.nrw);
-  if (t.nrules > 0) {
-    for (int f = 0; f < PCN_IPT_NFIELDS; ++f)
-      if (t.maps[f].present()) img.present |= 1u << f;
+  TableLayout &lay = img.lay;
+  std::memset(&lay, 0, sizeof lay);
+  for (int i = 0; i < 3; ++i) lay.hash_wild[i] = PCN_CLS_MISS;
 
-    for (int side = 0; side < 2; ++side) {
-      const FieldMap &m = t.maps[side == 0 ? PCN_IPT_F_IPSRC : PCN_IPT_F_IPDST];
-      if (!m.present()) continue;
-      DirTable dir;
-      for (const LpmEntry &e : lpm_entries(m)) dir.paint(e.prefix, e.len, pool.intern(m.vecs[e.vec]));
-      img.off_ip_l1[side] = blob.add(dir.l1);
-      if (dir.blk.empty()) dir.blk.assign(256, PCN_CLS_MISS);
-      img.off_ip_blk[side] = blob.add(dir.blk);
-    }
-    // ports (L4PortLookup.cpp:44-56 wildcard key 0) and interfaces
-    // (InterfaceLookup.cpp:44-56 wildcard key 0xffff): the miss fallback is folded in.
-    const int key_fields[3] = {PCN_IPT_F_SPORT, PCN_IPT_F_DPORT, PCN_IPT_F_IFACE};
-    const uint32_t wild[3] = {0, 0, 0xffff};
-    for (int i = 0; i < 3; ++i) {
-      const FieldMap &m = t.maps[key_fields[i]];
-      if (!m.present()) continue;
-      std::vector<uint16_t> tab(65536, PCN_CLS_MISS);
-      for (size_t k = 0; k < m.keys.size(); ++k)
-        if (m.keys[k] == wild[i]) std::fill(tab.begin(), tab.end(), pool.intern(m.vecs[k]));
-      for (size_t k = 0; k < m.keys.size(); ++k) tab[m.keys[k] & 0xffff] = pool.intern(m.vecs[k]);
-      img.off_key[i] = blob.add(tab);
-    }
-    // L4ProtocolLookup_dp.c:95-103: a miss retries with key 0 (the wildcard).
-    if (t.maps[PCN_IPT_F_L4PROTO].present()) {
-      const FieldMap &m = t.maps[PCN_IPT_F_L4PROTO];
-      std::vector<uint16_t> tab(256, PCN_CLS_MISS);
-      for (size_t k = 0; k < m.keys.size(); ++k)
-        if (m.keys[k] == 0) std::fill(tab.begin(), tab.end(), pool.intern(m.vecs[k]));
-      for (size_t k = 0; k < m.keys.size(); ++k) tab[m.keys[k] & 0xff] = pool.intern(m.vecs[k]);
-      img.off_proto = blob.add(tab);
-    }
-    if (t.maps[PCN_IPT_F_TCPFLAGS].present()) {
-      const FieldMap &m = t.maps[PCN_IPT_F_TCPFLAGS];
-      std::vector<uint16_t> tab(256, PCN_CLS_MISS);
-      for (size_t k = 0; k < m.keys.size(); ++k) tab[m.keys[k] & 0xff] = pool.intern(m.vecs[k]);
-      img.off_flags = blob.add(tab);
-    }
-    if (t.maps[PCN_IPT_F_CONNTRACK].present()) {
-      const FieldMap &m = t.maps[PCN_IPT_F_CONNTRACK];
-      std::vector<uint16_t> tab(4, PCN_CLS_MISS);
-      for (size_t k = 0; k < m.keys.size() && k < 4; ++k) tab[m.keys[k] & 3] = pool.intern(m.vecs[k]);
-      img.off_ct = blob.add(tab);
-    }
-    const auto &vecs = pool.vecs();
-    img.nvec = static_cast<uint32_t>(vecs.size());
-    std::vector<uint64_t> flat, summ;
-    flat.reserve(size_t(img.nvec) * t.nrw);
-    summ.assign(size_t(img.nvec) * img.nsw, 0);
-    for (uint32_t v = 0; v < img.nvec; ++v) {
-      for (uint32_t w = 0; w < t.nrw; ++w) {
-        flat.push_back(vecs[v][w]);
-        if (vecs[v][w]) summ[size_t(v) * img.nsw + w / 64] |= uint64_t(1) << (w % 64);
-      }
-    }
-    if (flat.empty()) flat.push_back(0);
-    if (summ.empty()) summ.push_back(0);
-    img.off_pool = blob.add(flat);
-    img.off_summ = blob.add(summ);
+  if (t.nrules == 0) {
+    img.nrw = img.nsw = 0;
+    blob.add(std::vector<uint32_t>(4, 0));
+    lay.bytes = static_cast<uint32_t>(blob.bytes.size());
+    img.tables = std::move(blob.bytes);
+    return img;
   }
-  std::vector<uint8_t> actions(t.actions);
-  if (actions.empty()) actions.push_back(0);
-  img.off_actions = blob.add(actions);
-  img.blob = std::move(blob.bytes);
+  for (int f = 0; f < PCN_IPT_NFIELDS; ++f)
+    if (t.maps[f].present()) img.present |= 1u << f;
+
+  // vectors visible to the datapath, per field (IP: after the trie collapse)
+  std::vector<LpmEntry> lpm[2];
+  std::vector<std::vector<const BitVec *>> field_vecs(PCN_IPT_NFIELDS);
+  for (int f = 0; f < PCN_IPT_NFIELDS; ++f) {
+    const FieldMap &m = t.maps[f];
+    if (!m.present()) continue;
+    if (f == PCN_IPT_F_IPSRC || f == PCN_IPT_F_IPDST) {
+      auto &es = lpm[f - PCN_IPT_F_IPSRC];
+      es = lpm_entries(m);
+      for (const LpmEntry &e : es) field_vecs[f].push_back(&m.vecs[e.vec]);
+    } else {
+      for (const BitVec &v : m.vecs) field_vecs[f].push_back(&v);
+    }
+  }
+  Permutation perm = make_permutation(t, field_vecs);
+  img.nrw = perm.nrw;
+  img.nsw = (perm.nrw + 63) / 64;
+  img.ngroups = perm.ngroups;
+  VecPool pool(perm, t.nrules);
+
+  // IP fields: interval tables
+  for (int side = 0; side < 2; ++side) {
+    const FieldMap &m = t.maps[PCN_IPT_F_IPSRC + side];
+    if (!m.present()) continue;
+    Intervals iv = lpm_intervals(m);
+    std::vector<uint16_t> cls;
+    for (int32_t c : iv.cls) cls.push_back(c < 0 ? PCN_CLS_MISS : pool.intern(m.vecs[c]));
+    std::vector<uint16_t> bkt(4097 + 7, 0);   // u16 first-boundary index per bucket
+    if (iv.bnd.size() > 0xFFFF) throw std::runtime_error("too many LPM intervals");
+    for (uint32_t b = 0; b <= 4096; ++b) {
+      uint64_t start = uint64_t(b) << (32 - PCN_IP_BUCKET_BITS);
+      bkt[b] = static_cast<uint16_t>(std::lower_bound(iv.bnd.begin(), iv.bnd.end(), start) - iv.bnd.begin());
+    }
+    lay.ip_bkt[side] = blob.add(bkt);
+    lay.ip_bnd[side] = blob.add(iv.bnd);
+    lay.ip_cls[side] = blob.add(cls);
+  }
+  // sport / dport / iface: hash of explicit keys; wildcard key (0 / 0 / 0xffff)
+  // becomes the miss class (L4PortLookup.cpp:44-56, InterfaceLookup.cpp:44-56)
+  const int key_fields[3] = {PCN_IPT_F_SPORT, PCN_IPT_F_DPORT, PCN_IPT_F_IFACE};
+  const uint32_t wild[3] = {0, 0, 0xffff};
+  for (int i = 0; i < 3; ++i) {
+    const FieldMap &m = t.maps[key_fields[i]];
+    if (!m.present()) continue;
+    size_t nk = 0;
+    for (size_t k = 0; k < m.keys.size(); ++k) {
+      if (m.keys[k] == wild[i]) lay.hash_wild[i] = pool.intern(m.vecs[k]);
+      else ++nk;
+    }
+    uint32_t size = 16;
+    while (size < 2 * nk) size <<= 1;
+    const uint32_t shift = static_cast<uint32_t>(__builtin_clz(size - 1));
+    std::vector<uint32_t> tab(size, PCN_HASH_EMPTY);
+    for (size_t k = 0; k < m.keys.size(); ++k) {
+      if (m.keys[k] == wild[i]) continue;
+      uint32_t key = m.keys[k] & 0xffff;
+      uint32_t h = (key * kHashMul) >> shift;
+      while (tab[h] != PCN_HASH_EMPTY) h = (h + 1) & (size - 1);
+      tab[h] = (key << 16) | pool.intern(m.vecs[k]);
+    }
+    lay.hash[i] = blob.add(tab);
+    lay.hash_mask[i] = size - 1;
+  }
+  // L4ProtocolLookup_dp.c:95-103: a miss retries with key 0 (the wildcard).
+  if (t.maps[PCN_IPT_F_L4PROTO].present()) {
+    const FieldMap &m = t.maps[PCN_IPT_F_L4PROTO];
+    std::vector<uint16_t> tab(256, PCN_CLS_MISS);
+    for (size_t k = 0; k < m.keys.size(); ++k)
+      if (m.keys[k] == 0) std::fill(tab.begin(), tab.end(), pool.intern(m.vecs[k]));
+    for (size_t k = 0; k < m.keys.size(); ++k) tab[m.keys[k] & 0xff] = pool.intern(m.vecs[k]);
+    lay.proto = blob.add(tab);
+  }
+  if (t.maps[PCN_IPT_F_TCPFLAGS].present()) {
+    const FieldMap &m = t.maps[PCN_IPT_F_TCPFLAGS];
+    std::vector<uint16_t> tab(256, PCN_CLS_MISS);
+    for (size_t k = 0; k < m.keys.size(); ++k) tab[m.keys[k] & 0xff] = pool.intern(m.vecs[k]);
+    lay.flags = blob.add(tab);
+  }
+  if (t.maps[PCN_IPT_F_CONNTRACK].present()) {
+    const FieldMap &m = t.maps[PCN_IPT_F_CONNTRACK];
+    std::vector<uint16_t> tab(8, PCN_CLS_MISS);
+    for (size_t k = 0; k < m.keys.size() && k < 4; ++k) tab[m.keys[k] & 3] = pool.intern(m.vecs[k]);
+    lay.ct = blob.add(tab);
+  }
+  // the all-ones class: slots of fields a packet skips (or the chain lacks)
+  BitVec ones(t.nrw, 0);
+  for (uint32_t r = 0; r < t.nrules; ++r) ones[r / kBitsPerWord] |= uint64_t(1) << (r % kBitsPerWord);
+  img.all_cls = pool.intern(ones);
+  // Per class and 64-word block: SUMM (bit w: word w != 0), FULL (bit w: word w
+  // holds every rule of its word) and the PART array of the remaining
+  // "partial" words, stored in word order from PBASE (rank = popcount below w).
+  const auto &vecs = pool.vecs();
+  img.nvec = static_cast<uint32_t>(vecs.size());
+  const size_t nrec = size_t(img.nvec) * img.nsw;
+  std::vector<uint64_t> summ(nrec, 0), full(nrec, 0), part;
+  std::vector<uint32_t> pbase(nrec, 0);
+  for (uint32_t v = 0; v < img.nvec; ++v) {
+    for (uint32_t w = 0; w < img.nrw; ++w) {
+      const size_t rec = size_t(v) * img.nsw + w / 64;
+      if (w % 64 == 0) pbase[rec] = static_cast<uint32_t>(part.size());
+      const uint64_t x = vecs[v][w];
+      if (x) summ[rec] |= uint64_t(1) << (w % 64);
+      if (x == perm.valid[w]) full[rec] |= uint64_t(1) << (w % 64);
+      else if (x) part.push_back(x);
+    }
+  }
+  img.part_words = static_cast<uint32_t>(part.size());
+  lay.summ = blob.add(summ);
+  lay.full = blob.add(full);
+  lay.pbase = blob.add(pbase);
+  lay.part = blob.add(part);
+  lay.perm = blob.add(perm.perm);
+  lay.bytes = static_cast<uint32_t>((blob.bytes.size() + kAlign - 1) / kAlign * kAlign);
+  blob.bytes.resize(lay.bytes);
+  img.tables = std::move(blob.bytes);
   return img;
 }
 

@@ -22,7 +22,7 @@
 #include "ruleset.hpp"
 
 namespace pcn {
-int launch_classify(const LaunchArgs &a, bool fixed, int num_cus, hipStream_t stream);
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStream_t stream);
 int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint64_t count, int nranks,
                      hipStream_t stream);
 }  // namespace pcn
@@ -46,12 +46,27 @@ void hip_check(hipError_t e, const char *what) {
   if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-constexpr uint32_t kMaxLdsRuleBins = 2048;   // per-workgroup LDS histogram budget (32 KB)
+#ifndef PCN_DEBUG_MAX_RULE_BINS
+#define PCN_DEBUG_MAX_RULE_BINS 2048
+#endif
+#ifndef PCN_DEBUG_LDS_BUDGET
+#define PCN_DEBUG_LDS_BUDGET (160 * 1024)
+#endif
+constexpr uint32_t kMaxLdsRuleBins = PCN_DEBUG_MAX_RULE_BINS;   // per-workgroup LDS histogram budget (32 KB)
+constexpr uint32_t kLdsBudget = PCN_DEBUG_LDS_BUDGET;  // gfx950 LDS per CU (one workgroup may take it all)
 
 struct ImageSlot {
-  void *dev = nullptr;
-  size_t cap = 0;
+  void *tables = nullptr;
+  size_t tables_cap = 0;
 };
+
+void ensure(void *&buf, size_t &cap, size_t need) {
+  if (cap >= need && buf) return;
+  if (buf) hip_check(hipFree(buf), "hipFree");
+  buf = nullptr;
+  cap = std::max<size_t>(need, 4096);
+  hip_check(hipMalloc(&buf, cap), "hipMalloc(chain image)");
+}
 
 struct ChainState {
   // control plane (Chain)
@@ -59,6 +74,9 @@ struct ChainState {
   int default_action = PCN_IPT_ACCEPT;        // Iptables.cpp:33-38
   std::vector<std::pair<uint64_t, uint64_t>> stats;   // ChainStats totals (counters_)
   ChainTables tables;                          // last applied compile
+  pcn_ipt_chain_info info{};                   // shape of the last built image
+  std::vector<uint8_t> image_copy;             // host copy of the last built table image
+  std::vector<uint32_t> desc_words;            // TableLayout words + nrw, nsw, present, all_cls
   // datapath
   ImageSlot slot[2];
   int active = -1;
@@ -99,49 +117,40 @@ uint32_t counted(const pcn_ipt *ctx, uint32_t nrules) {
 void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
   ChainState &cs = ctx->chains[chain];
   HostImage img = build_image(tables);       // may throw (trie capacity etc.)
+  cs.image_copy = img.tables;
+  cs.desc_words.assign(reinterpret_cast<const uint32_t *>(&img.lay),
+                       reinterpret_cast<const uint32_t *>(&img.lay) + sizeof(TableLayout) / 4);
+  cs.desc_words.insert(cs.desc_words.end(), {img.nrw, img.nsw, img.present, img.all_cls});
+  cs.info = pcn_ipt_chain_info{img.nrules, img.nrw, img.nsw, img.nvec, img.ngroups, img.present,
+                               img.lay.bytes, static_cast<uint64_t>(img.part_words) * 8};
   if (ctx->has_device) {
     device_guard(ctx);
     // every batch queued before this call must not see a half-written slot
     hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     int next = cs.active < 0 ? 0 : 1 - cs.active;
     ImageSlot &s = cs.slot[next];
-    if (s.cap < img.blob.size()) {
-      if (s.dev) hip_check(hipFree(s.dev), "hipFree");
-      s.dev = nullptr;
-      size_t cap = std::max<size_t>(img.blob.size(), 4096);
-      hip_check(hipMalloc(&s.dev, cap), "hipMalloc(chain image)");
-      s.cap = cap;
-    }
-    hip_check(hipMemcpy(s.dev, img.blob.data(), img.blob.size(), hipMemcpyHostToDevice),
-              "hipMemcpy(chain image)");
+    ensure(s.tables, s.tables_cap, img.tables.size());
+    hip_check(hipMemcpy(s.tables, img.tables.data(), img.tables.size(), hipMemcpyHostToDevice),
+              "hipMemcpy(chain tables)");
     // a new ActionLookup program starts with zeroed per-rule counters; the
     // default counters live in shared maps and persist (Iptables_Parser_dp.c:47-58)
     hip_check(hipMemset(cs.ctr + 2, 0, (ctx->ctr_words - 2) * sizeof(unsigned long long)),
               "hipMemset(counters)");
-    auto sec = [&](size_t off) -> const uint8_t * {
-      return off == kNoSection ? nullptr : static_cast<const uint8_t *>(s.dev) + off;
-    };
     DevChain d{};
-    for (int i = 0; i < 2; ++i) {
-      d.ip_l1[i] = reinterpret_cast<const uint32_t *>(sec(img.off_ip_l1[i]));
-      d.ip_blk[i] = reinterpret_cast<const uint32_t *>(sec(img.off_ip_blk[i]));
-    }
-    for (int i = 0; i < 3; ++i) d.key_cls[i] = reinterpret_cast<const uint16_t *>(sec(img.off_key[i]));
-    d.proto_cls = reinterpret_cast<const uint16_t *>(sec(img.off_proto));
-    d.flags_cls = reinterpret_cast<const uint16_t *>(sec(img.off_flags));
-    d.ct_cls = reinterpret_cast<const uint16_t *>(sec(img.off_ct));
-    d.pool = reinterpret_cast<const uint64_t *>(sec(img.off_pool));
-    d.summ = reinterpret_cast<const uint64_t *>(sec(img.off_summ));
-    d.actions = sec(img.off_actions);
+    d.lay = img.lay;
+    d.image = static_cast<const uint8_t *>(s.tables);
     d.ctr = cs.ctr;
     d.nrules = img.nrules;
     d.nrw = img.nrw;
     d.nsw = img.nsw;
     d.present = img.present;
+    d.nvec = img.nvec;
+    d.all_cls = img.all_cls;
     d.ncounted = counted(ctx, img.nrules);
     d.max_action = ctx->cfg.max_action_rules;
     d.default_action = img.default_action;
-    d.lds_base = -1;
+    d.lds_image = 0;
+    d.lds_bins = -1;
     cs.desc = d;
     cs.active = next;
   }
@@ -202,7 +211,7 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
   if (!ctx->cfg.max_counted_rules) ctx->cfg.max_counted_rules = 8000;
   if (!ctx->cfg.max_action_rules) ctx->cfg.max_action_rules = 10000;
   if (!ctx->cfg.max_rules) ctx->cfg.max_rules = 8192;
-  if (ctx->cfg.max_rules > 65535) return fail(-EINVAL, "max_rules > 65535");
+  if (ctx->cfg.max_rules > 32767) return fail(-EINVAL, "max_rules > 32767");
   ctx->ctr_words = 2 + 2 * size_t(ctx->cfg.max_counted_rules);
   if (cfg->device >= 0) {
     try {
@@ -238,7 +247,9 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     (void)hipSetDevice(ctx->cfg.device);
     (void)hipDeviceSynchronize();
     for (auto &cs : ctx->chains) {
-      for (auto &s : cs.slot) if (s.dev) (void)hipFree(s.dev);
+      for (auto &s : cs.slot) {
+        if (s.tables) (void)hipFree(s.tables);
+      }
       if (cs.ctr) (void)hipFree(cs.ctr);
       if (cs.ctr_global) (void)hipFree(cs.ctr_global);
       if (cs.gather) (void)hipFree(cs.gather);
@@ -452,17 +463,30 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     if (b->direction != PCN_IPT_INGRESS && b->direction != PCN_IPT_EGRESS) return fail(-EINVAL, "bad direction");
     device_guard(ctx);
     LaunchArgs a{};
-    // LDS histogram bins: 3 default bins, then rule bins (FORWARD first).
+    // LDS: the table images of every chain with rules (when they fit), then the
+    // counter histogram: 3 default bins + rule bins (FORWARD first).
+    uint32_t img_bytes = 0;
+    for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
+      a.ch[c] = ctx->chains[c].desc;
+      if (a.ch[c].nrules) { a.ch[c].lds_image = kLdsDescBytes + img_bytes; img_bytes += a.ch[c].lay.bytes; }
+      else a.empty_mask |= 1u << c;
+      if (a.ch[c].default_action == PCN_IPT_DROP) a.drop_mask |= 1u << c;
+    }
     uint32_t base = 3;
     const int order[3] = {PCN_IPT_FORWARD, PCN_IPT_INPUT, PCN_IPT_OUTPUT};
     for (int c : order) {
-      ChainState &cs = ctx->chains[c];
-      a.ch[c] = cs.desc;
-      uint32_t nc = cs.desc.ncounted;
-      if (nc && base - 3 + nc <= kMaxLdsRuleBins) { a.ch[c].lds_base = static_cast<int32_t>(base); base += nc; }
-      else a.ch[c].lds_base = -1;
+      uint32_t nc = a.ch[c].ncounted;
+      if (nc && base - 3 + nc <= kMaxLdsRuleBins) { a.ch[c].lds_bins = static_cast<int32_t>(base); base += nc; }
+      else a.ch[c].lds_bins = -1;
     }
     a.nbins = base;
+    if (kLdsDescBytes + img_bytes + a.nbins * 16 <= kLdsBudget) {
+      a.lds_images_bytes = img_bytes;
+      a.bins_offset = kLdsDescBytes + img_bytes;
+    } else {
+      a.lds_images_bytes = 0;
+      a.bins_offset = kLdsDescBytes;
+    }
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
     a.offsets = b->offsets;
@@ -490,9 +514,38 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       uint64_t last = (b->n - 1) * uint64_t(b->stride);
       if (last >= b->frames_bytes) return fail(-EINVAL, "frames_bytes smaller than n*stride");
     }
-    int rc = launch_classify(a, fixed, ctx->num_cus, static_cast<hipStream_t>(stream));
+    // which chains can reach the rule stage (ChainSelector_dp.c:157-168, 243-260)
+    const bool has_local = !ctx->localip.empty();
+    const bool reach_fw = b->direction == PCN_IPT_INGRESS && !a.allow_logic && a.ch[PCN_IPT_FORWARD].nrules;
+    const bool reach_in = b->direction == PCN_IPT_INGRESS && !a.allow_logic && has_local && a.ch[PCN_IPT_INPUT].nrules;
+    const bool reach_out = b->direction == PCN_IPT_EGRESS && has_local && a.ch[PCN_IPT_OUTPUT].nrules;
+    int ch = PCN_IPT_FORWARD;
+    if (reach_fw && reach_in) ch = 3;
+    else if (reach_in) ch = PCN_IPT_INPUT;
+    else if (reach_out) ch = PCN_IPT_OUTPUT;
+    int rc = launch_classify(a, fixed, ch, ctx->num_cus, static_cast<hipStream_t>(stream));
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
     return 0;
+  });
+}
+
+int pcn_ipt_chain_get_info(pcn_ipt *ctx, int chain, pcn_ipt_chain_info *out) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain) || !out) return fail(-EINVAL, "bad chain or output");
+    *out = ctx->chains[chain].info;
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_get_image(pcn_ipt *ctx, int chain, uint8_t *buf, uint32_t cap, uint32_t *desc,
+                            uint32_t desc_cap) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    const ChainState &cs = ctx->chains[chain];
+    if (buf && cap >= cs.image_copy.size()) std::memcpy(buf, cs.image_copy.data(), cs.image_copy.size());
+    if (desc && desc_cap >= cs.desc_words.size())
+      std::memcpy(desc, cs.desc_words.data(), cs.desc_words.size() * 4);
+    return static_cast<int>(cs.image_copy.size());
   });
 }
 

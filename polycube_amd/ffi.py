@@ -47,6 +47,12 @@ class Tables(C.Structure):
                 ("actions", C.POINTER(C.c_uint8)), ("maps", FieldMap * 8)]
 
 
+class ChainInfo(C.Structure):
+    _fields_ = [("nrules", C.c_uint32), ("nrw", C.c_uint32), ("nsw", C.c_uint32), ("nvec", C.c_uint32),
+                ("ngroups", C.c_uint32), ("present", C.c_uint32), ("table_bytes", C.c_uint32),
+                ("part_bytes", C.c_uint64)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
@@ -69,6 +75,9 @@ SIGNATURES = {
                                      C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.c_uint32,
                                      C.c_uint32]),
     "pcn_ipt_chain_nrw": (C.c_uint32, [C.c_void_p, C.c_int]),
+    "pcn_ipt_chain_get_info": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ChainInfo)]),
+    "pcn_ipt_chain_get_image": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint8), C.c_uint32,
+                                          C.POINTER(C.c_uint32), C.c_uint32]),
     "pcn_ipt_classify": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p]),
     "pcn_ipt_synchronize": (C.c_int, [C.c_void_p]),
     "pcn_ipt_read_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),

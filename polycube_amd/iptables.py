@@ -111,6 +111,12 @@ class Chain:
                                                C.byref(db), int(flush), int(scope)))
         return list(pk[:n]), list(by[:n]), dp.value, db.value
 
+    def info(self):
+        """Shape of the compiled device image (pcn_ipt_chain_get_info)."""
+        out = ffi.ChainInfo()
+        _check(ffi.lib().pcn_ipt_chain_get_info(self._h(), self.id, C.byref(out)))
+        return {k: getattr(out, k) for k, _ in ffi.ChainInfo._fields_}
+
     def export_map(self, field, cap=70000):
         nrw = ffi.lib().pcn_ipt_chain_nrw(self._h(), self.id)
         keys = (C.c_uint32 * cap)()

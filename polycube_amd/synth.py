@@ -131,7 +131,7 @@ def config_rules(cfg, seed=None):
     if cfg == 3:
         return make_rules(1000, seed)
     if cfg == 5:
-        return make_rules(10000, seed, pool_size=1000)
+        return make_rules(10000, seed, pool_size=480)
     raise ValueError(cfg)
 
 

@@ -1,0 +1,134 @@
+"""Scalar CPU model of the kernel's chain stage over an exported table image.
+
+TEST INFRASTRUCTURE ONLY: it reads the bytes libpcn_ipt.so builds for the GPU
+(pcn_ipt_chain_get_image) and walks them exactly as classify.hip's run_chain
+does, so the image builder can be checked against the oracle without a GPU.
+It is never part of the product path."""
+import ctypes as C
+import struct
+
+import numpy as np
+
+from polycube_amd import ffi
+
+LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_bnd0", "ip_bnd1", "ip_cls0", "ip_cls1", "hash0", "hash1",
+          "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "proto", "flags", "ct", "summ",
+          "full", "pbase", "part", "perm"]
+MISS = 0xFFFF
+EMPTY = 0xFFFFFFFF
+
+
+class ImageModel:
+    def __init__(self, chain):
+        lib = ffi.lib()
+        n = lib.pcn_ipt_chain_get_image(chain._h(), chain.id, None, 0, None, 0)
+        buf = (C.c_uint8 * max(n, 1))()
+        desc = (C.c_uint32 * 64)()
+        assert lib.pcn_ipt_chain_get_image(chain._h(), chain.id, buf, n, desc, 64) == n
+        self.img = bytes(buf)[:n]
+        d = list(desc)
+        self.lay = dict(zip(LAYOUT, d[:len(LAYOUT)]))
+        self.nrw, self.nsw, self.present, self.all = d[len(LAYOUT):len(LAYOUT) + 4]
+
+    def u16(self, off):
+        return struct.unpack_from("<H", self.img, off)[0]
+
+    def u32(self, off):
+        return struct.unpack_from("<I", self.img, off)[0]
+
+    def u64(self, off):
+        return struct.unpack_from("<Q", self.img, off)[0]
+
+    def ip_class(self, side, h):
+        L = self.lay
+        b = h >> 20
+        lo, hi = self.u16(L[f"ip_bkt{side}"] + 2 * b), self.u16(L[f"ip_bkt{side}"] + 2 * b + 2)
+        while lo < hi:
+            mid = (lo + hi) >> 1
+            if self.u32(L[f"ip_bnd{side}"] + 4 * mid) <= h:
+                lo = mid + 1
+            else:
+                hi = mid
+        return self.u16(L[f"ip_cls{side}"] + 2 * lo)
+
+    def key_class(self, i, key):
+        L = self.lay
+        mask = L[f"mask{i}"]
+        shift = 32 - mask.bit_length()
+        h = ((key * 0x9E3779B1) & 0xFFFFFFFF) >> shift
+        while True:
+            e = self.u32(L[f"hash{i}"] + 4 * h)
+            if e == EMPTY:
+                return L[f"wild{i}"]
+            if e >> 16 == key:
+                return e & 0xFFFF
+            h = (h + 1) & mask
+
+    def run(self, saddr_h, daddr_h, proto, sport, dport, flags, port=1, ct=0):
+        """-> (rule id or -1 for default, action bit or None)."""
+        L, p = self.lay, self.present
+        cls = [self.all] * 8
+        if p & 1:
+            cls[0] = self.u16(L["ct"] + 2 * ct)
+        if p & 2:
+            cls[1] = self.ip_class(0, saddr_h)
+        if p & 4:
+            cls[2] = self.ip_class(1, daddr_h)
+        if p & 8:
+            cls[3] = self.u16(L["proto"] + 2 * proto)
+        l4 = proto in (6, 17)
+        if p & 16:
+            c = self.key_class(0, sport)
+            cls[4] = c if l4 else self.all
+        if p & 32:
+            c = self.key_class(1, dport)
+            cls[5] = c if l4 else self.all
+        if p & 64:
+            cls[6] = self.key_class(2, port)
+        if p & 128:
+            c = self.u16(L["flags"] + 2 * flags)
+            cls[7] = c if proto == 6 else self.all
+        if MISS in cls:
+            return -1, None
+        best = None
+        for k in range(self.nsw):
+            live = self.nrw - 64 * k
+            m = (1 << 64) - 1 if live >= 64 else (1 << live) - 1
+            recs = [c * self.nsw + k for c in cls]
+            for r in recs:
+                m &= self.u64(L["summ"] + 8 * r)
+            while m:
+                bit = (m & -m).bit_length() - 1
+                m &= m - 1
+                acc = (1 << 64) - 1
+                for r in recs:
+                    fm = self.u64(L["full"] + 8 * r)
+                    if fm >> bit & 1:
+                        continue
+                    part = self.u64(L["summ"] + 8 * r) & ~fm
+                    rank = bin(part & ((1 << bit) - 1)).count("1")
+                    acc &= self.u64(L["part"] + 8 * (self.u32(L["pbase"] + 4 * r) + rank))
+                if acc:
+                    low = (acc & -acc).bit_length() - 1
+                    e = self.u16(L["perm"] + 2 * ((64 * k + bit) * 63 + low))
+                    best = e if best is None else min(best, e)
+        if best is None:
+            return -1, None
+        return best >> 1, best & 1
+
+
+def model_classify(model, frames, n, stride=64):
+    """Rule ids for well-formed IPv4 TCP/UDP frames (fields at fixed offsets)."""
+    f = np.asarray(frames, np.uint8).reshape(n, stride)
+    out = np.empty(n, np.int32)
+    for i in range(n):
+        row = f[i]
+        s = int.from_bytes(bytes(row[26:30]), "big")
+        d = int.from_bytes(bytes(row[30:34]), "big")
+        proto = int(row[23])
+        sp = int.from_bytes(bytes(row[34:36]), "big")
+        dp = int.from_bytes(bytes(row[36:38]), "big")
+        fl = int(row[47]) if proto == 6 else 0
+        ct = (0 if (fl & 2 and (fl | 2) == 2) else 3) if proto == 6 else 0
+        out[i] = model.run(s, d, proto, sp, dp, fl, 1, ct)[0]
+    return out

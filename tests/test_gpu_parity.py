@@ -153,7 +153,7 @@ def test_fuzz_parity(dev, seed):
 def test_imix_config5_parity(dev):
     """10k rules (extended limits), IMIX 64/576/1500 with VLAN/IPv6 mixed in (variable offsets)."""
     rs = synth.config_rules(5)
-    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, max_rules=65535, max_counted_rules=10000,
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, max_rules=16384, max_counted_rules=10000,
                        max_action_rules=10000)
     n = 1 << 17
     buf, offsets, lens = synth.imix_frames(rs, n, 5)

@@ -1,0 +1,77 @@
+"""Kernel-time ablation of the classify datapath (measurement tool, GPU box).
+
+Runs config 3 (1k rules, 2^24 64-byte frames) through the product library and
+through the PCN_ABLATE builds (polycube_amd/build/libpcn_ipt_ablate{1..4}.so:
+1 parse only, 2 + field lookups, 3 + summary AND, 4 full minus counters), for
+traffic that is all-default (hit 0), the bench mix (hit 0.5) and all-hit (1).
+Each variant runs in its own process (one library per process)."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib, hit, log2n, iters, cfg):
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+    from polycube_amd import ffi
+    if lib:
+        ffi.LIB_PATH = lib
+    from polycube_amd import Iptables, synth
+    rs = synth.config_rules(cfg)
+    ipt = Iptables(device=0)
+    ipt.interactive = False
+    fw = ipt.chain("FORWARD")
+    for r in rs.rules():
+        fw.append(**r)
+    fw.default = "DROP"
+    fw.apply_rules()
+    n = 1 << log2n
+    cols = synth.make_headers(rs, n, synth.CONFIG_SEEDS[3], hit_frac=hit,
+                              protos=(6, 17) if cfg == 3 else (17,))
+    frames = torch.from_numpy(synth.build_frames(*cols).reshape(-1)).cuda()
+    v = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for _ in range(3):
+        ipt.classify(frames, n=n, verdicts=v, rule_ids=False)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for a, b in evs:
+        a.record()
+        ipt.classify(frames, n=n, verdicts=v, rule_ids=False)
+        b.record()
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    print(json.dumps({"lib": os.path.basename(lib or "product"), "hit": hit, "ms": ms,
+                      "gpkt_s": n / ms / 1e6, "frac": 64 * n / (ms * 1e-3) / 8e12}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--child", action="store_true")
+    ap.add_argument("--lib", default="")
+    ap.add_argument("--hit", type=float, default=0.5)
+    ap.add_argument("--log2n", type=int, default=24)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cfg", type=int, default=3)
+    ap.add_argument("--variants", default="product,1,2,3,4")
+    ap.add_argument("--hits", default="0,0.5,1")
+    a = ap.parse_args()
+    if a.child:
+        child(a.lib, a.hit, a.log2n, a.iters, a.cfg)
+        return
+    for var in a.variants.split(","):
+        lib = "" if var == "product" else os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_ablate{var}.so")
+        for hit in a.hits.split(","):
+            r = subprocess.run([sys.executable, __file__, "--child", "--lib", lib, "--hit", hit, "--log2n",
+                                str(a.log2n), "--iters", str(a.iters), "--cfg", str(a.cfg)],
+                               capture_output=True, text=True, timeout=300)
+            out = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            print(out[-1] if out else f"{var} hit={hit} FAILED rc={r.returncode}: {r.stderr[-400:]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
