@@ -153,7 +153,7 @@ typedef struct {
   uint32_t ngroups;      /* rule type groups */
   uint32_t present;      /* bit f set: field module f present */
   uint32_t table_bytes;  /* LDS-staged table image size */
-  uint64_t part_bytes;   /* partial vector words (part of the table image) */
+  uint64_t part_bytes;   /* partial-word indices + distinct partial words (in the image) */
 } pcn_ipt_chain_info;
 int pcn_ipt_chain_get_info(pcn_ipt *ctx, int chain, pcn_ipt_chain_info *out);
 /* Copy a chain's table image bytes and its scalar descriptor words (layout

@@ -31,12 +31,16 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #ifndef PCN_ABLATE
 #define PCN_ABLATE 0
 #endif
+// Tuning switches (tools/ablate.py builds experiment variants with -D...).
+#ifndef PCN_BLOCK
+#define PCN_BLOCK 512
+#endif
 
 namespace pcn {
 
 namespace {
 
-constexpr int kBlock = 512;
+constexpr int kBlock = PCN_BLOCK;
 constexpr uint32_t kHashMul = 0x9E3779B1u;
 constexpr uint32_t kNoRule = 0xFFFFFFFFu;
 
@@ -118,11 +122,12 @@ __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
 // Kernel-LPM answer for a host-order address: bucket index on the top 12 bits,
 // then a binary search among the few boundaries inside the bucket.
 template <bool LDS>
-__device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t bnd, uint32_t cls,
-                                             uint32_t h) {
-  uint32_t b = h >> (32 - PCN_IP_BUCKET_BITS);
-  uint32_t lo = t.u16(bkt + 2 * b);
-  uint32_t hi = t.u16(bkt + 2 * b + 2);
+__device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t shift, uint32_t bnd,
+                                             uint32_t cls, uint32_t h) {
+  const uint32_t e = t.u32(bkt + 4 * (h >> shift));
+  if (e & PCN_IP_LEAF) return e & 0xFFFFu;   // no boundary inside this bucket
+  uint32_t lo = e & 0xFFFFu;
+  uint32_t hi = lo + (e >> 16);
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
     if (t.u32(bnd + 4 * mid) <= h) lo = mid + 1; else hi = mid;
@@ -166,9 +171,9 @@ __device__ __forceinline__ uint32_t run_chain(const DevChain &ch, const Parsed &
     cls[0] = t.u16(lay.ct + 2 * p.ct);
   }
   if (present & (1u << PCN_IPT_F_IPSRC))
-    cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
+    cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_shift[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
   if (present & (1u << PCN_IPT_F_IPDST))
-    cls[2] = ip_class(t, lay.ip_bkt[1], lay.ip_bnd[1], lay.ip_cls[1], __builtin_bswap32(p.daddr));
+    cls[2] = ip_class(t, lay.ip_bkt[1], lay.ip_shift[1], lay.ip_bnd[1], lay.ip_cls[1], __builtin_bswap32(p.daddr));
   if (present & (1u << PCN_IPT_F_L4PROTO)) cls[3] = t.u16(lay.proto + 2 * p.proto);
   const bool l4 = p.proto == 6 || p.proto == 17;                    // L4PortLookup_dp.c:99-103
   if (present & (1u << PCN_IPT_F_SPORT)) {
@@ -222,18 +227,24 @@ __device__ __forceinline__ uint32_t run_chain(const DevChain &ch, const Parsed &
     while (m) {
       const uint32_t bit = static_cast<uint32_t>(__builtin_ctzll(m));
       m &= m - 1;
-      const uint32_t w = k * 64 + bit;
       const uint64_t below = (1ull << bit) - 1;
-      uint64_t v[8];
+      // Straight-line on purpose: every field's index read, then every pool
+      // read, issue back to back (two LDS round trips per word).  A FULL field
+      // reads the zero cell, i.e. POOL[0], the all-ones word.
+      uint32_t q[8];
 #pragma unroll
-      for (int f = 0; f < 8; ++f)
-        v[f] = ((fm[f] >> bit) & 1)
-                   ? ~0ull
-                   : t.u64(lay.part + 8 * (pb[f] + static_cast<uint32_t>(__builtin_popcountll(s[f] & below))));
+      for (int f = 0; f < 8; ++f) {
+        const uint32_t j = pb[f] + static_cast<uint32_t>(__builtin_popcountll(s[f] & below));
+        const bool wide = !LDS && lay.part_wide;
+        const uint32_t part_mask = static_cast<uint32_t>((fm[f] >> bit) & 1) - 1u;   // ~0: partial
+        const uint32_t at = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
+        q[f] = wide ? t.u32(at) : t.u16(at);
+      }
       uint64_t acc = ~0ull;
 #pragma unroll
-      for (int f = 0; f < 8; ++f) acc &= v[f];
+      for (int f = 0; f < 8; ++f) acc &= t.u64(lay.pool + 8 * q[f]);
       if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
+        const uint32_t w = k * 64 + bit;
         uint32_t e = t.u16(lay.perm + 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
         best = e < best ? e : best;
       }
@@ -444,8 +455,9 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStr
   if (a.n == 0) return hipSuccess;
   const size_t lds = a.bins_offset + static_cast<size_t>(a.nbins) * 16;
   const bool in_lds = a.lds_images_bytes > 0;
-  size_t per_cu = lds ? (160 * 1024) / lds : 4;
-  if (per_cu > 4) per_cu = 4;
+  const size_t max_per_cu = 2048 / kBlock;   // 32 waves per CU
+  size_t per_cu = lds ? (160 * 1024) / lds : max_per_cu;
+  if (per_cu > max_per_cu) per_cu = max_per_cu;
   if (per_cu < 1) per_cu = 1;
   const uint64_t want = (a.n + kBlock - 1) / kBlock;
   const uint64_t cap = static_cast<uint64_t>(num_cus) * per_cu;

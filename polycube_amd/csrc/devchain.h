@@ -7,7 +7,8 @@
 // 1k rules) that each workgroup copies into LDS, so the per-packet path makes
 // no dependent HBM/L2 access at all:
 //   - IP src/dst: the kernel-LPM answer as sorted interval boundaries plus a
-//     4096-bucket index on the top 12 address bits;
+//     bucket index on the top address bits (2^4..2^12 buckets, sized to the
+//     boundary count; a bucket no boundary falls into holds its class);
 //   - sport/dport/iface: open-addressing hashes {key -> class} with the
 //     wildcard class (key 0 / 0xffff) as the miss fallback;
 //   - proto/tcpflags/conntrack: 256/256/4-entry class tables;
@@ -15,6 +16,8 @@
 //     != 0), FULL (bit w: word w holds all of its rules) and PBASE, the start
 //     of the class's PARTIAL words (neither zero nor full) in PART, stored in
 //     word order (a partial word's index = PBASE + popcount(partial bits below));
+//     PART holds u16 (u32 when PART_WIDE) indices into POOL, the distinct
+//     partial words (at 1k rules ~10x fewer than partial words);
 //   - PERM: bit position -> (original rule id << 1 | action).
 // Images too large for LDS are read from HBM through the same accessors.
 //
@@ -29,7 +32,8 @@
 
 #define PCN_CLS_MISS 0xFFFFu
 #define PCN_MAX_LOCALIP 256
-#define PCN_IP_BUCKET_BITS 12
+#define PCN_IP_BUCKET_BITS_MAX 12
+#define PCN_IP_LEAF 0x80000000u
 #define PCN_HASH_EMPTY 0xFFFFFFFFu
 
 namespace pcn {
@@ -37,7 +41,8 @@ namespace pcn {
 // Byte offsets inside a table image (all 16-byte aligned).
 struct TableLayout {
   uint32_t bytes;
-  uint32_t ip_bkt[2];      // u32[4097]: first boundary index per bucket (+ sentinel)
+  uint32_t ip_bkt[2];      // u32[1 << (32 - ip_shift)]: LEAF|class, or (count << 16) | first boundary
+  uint32_t ip_shift[2];    // bucket = address >> ip_shift
   uint32_t ip_bnd[2];      // u32[m]: interval boundaries (host-order addresses)
   uint32_t ip_cls[2];      // u16[m+1]: class of each interval
   uint32_t hash[3];        // u32[size]: (key << 16) | class  (sport, dport, iface)
@@ -46,7 +51,10 @@ struct TableLayout {
   uint32_t proto, flags, ct;   // u16[256], u16[256], u16[4]
   uint32_t summ, full;     // u64[nvec][nsw]
   uint32_t pbase;          // u32[nvec][nsw]: first PART index of the class's block
-  uint32_t part;           // u64[]: partial words
+  uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
+  uint32_t part_wide;
+  uint32_t pool;           // u64[]: distinct partial words; POOL[0] is all-ones
+  uint32_t zero;           // 16 zero bytes (the PART cell a FULL field reads: index 0)
   uint32_t perm;           // u16[nrw * 63]
 };
 

@@ -13,7 +13,7 @@ namespace {
 
 constexpr size_t kAlign = 16;
 constexpr uint32_t kTrieCapacity = 1024;   // Iptables_IpLookup_dp.c:54-55
-constexpr size_t kGroupAlignMin = 8;       // type groups this large start on a fresh word
+constexpr size_t kGroupAlignMin = 8;       // densest packing: smaller type groups share words
 constexpr uint32_t kHashMul = 0x9E3779B1u;
 
 inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
@@ -59,17 +59,31 @@ Permutation make_permutation(const ChainTables &t, const std::vector<std::vector
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return type[a] < type[b]; });
   std::map<uint32_t, size_t> group_size;
   for (uint32_t r = 0; r < n; ++r) group_size[type[r]]++;
-  std::vector<std::vector<uint32_t>> words;
-  uint32_t cur_type = ~0u;
-  for (uint32_t r : order) {
-    bool fresh = words.empty() || words.back().size() == kBitsPerWord;
-    if (type[r] != cur_type) {
-      cur_type = type[r];
-      if (group_size[cur_type] >= kGroupAlignMin) fresh = true;
+  // Pack type groups into words.  A word mixing types can pass every field's
+  // summary with no rule matching (rule A wild in src, rule B wild in dst...),
+  // so each group gets words of its own unless that costs an extra 64-word
+  // summary block; then groups smaller than `min_own` share words.
+  auto pack = [&](size_t min_own) {
+    std::vector<std::vector<uint32_t>> ws;
+    uint32_t cur_type = ~0u;
+    for (uint32_t r : order) {
+      bool fresh = ws.empty() || ws.back().size() == kBitsPerWord;
+      if (type[r] != cur_type) {
+        cur_type = type[r];
+        if (group_size[cur_type] >= min_own) fresh = true;
+      }
+      if (fresh) ws.emplace_back();
+      ws.back().push_back(r);
     }
-    if (fresh && !(words.size() && words.back().empty())) words.emplace_back();
-    words.back().push_back(r);
+    return ws;
+  };
+  std::vector<std::vector<uint32_t>> words = pack(kGroupAlignMin);
+  const size_t blocks = (words.size() + 63) / 64;
+  for (size_t min_own : {size_t(1), size_t(2), size_t(4)}) {
+    auto ws = pack(min_own);
+    if ((ws.size() + 63) / 64 <= blocks) { words = std::move(ws); break; }
   }
+  for (auto &w : words) std::sort(w.begin(), w.end());
   Permutation p;
   p.ngroups = static_cast<uint32_t>(group_size.size());
   p.nrw = static_cast<uint32_t>(words.size());
@@ -77,7 +91,6 @@ Permutation make_permutation(const ChainTables &t, const std::vector<std::vector
   p.perm.assign(size_t(p.nrw) * kBitsPerWord, 0xFFFF);
   p.valid.assign(p.nrw, 0);
   for (uint32_t w = 0; w < p.nrw; ++w) {
-    std::sort(words[w].begin(), words[w].end());
     for (uint32_t j = 0; j < words[w].size(); ++j) {
       uint32_t r = words[w][j];
       uint32_t bit = w * kBitsPerWord + j;
@@ -204,12 +217,24 @@ HostImage build_image(const ChainTables &t) {
     Intervals iv = lpm_intervals(m);
     std::vector<uint16_t> cls;
     for (int32_t c : iv.cls) cls.push_back(c < 0 ? PCN_CLS_MISS : pool.intern(m.vecs[c]));
-    std::vector<uint16_t> bkt(4097 + 7, 0);   // u16 first-boundary index per bucket
-    if (iv.bnd.size() > 0xFFFF) throw std::runtime_error("too many LPM intervals");
-    for (uint32_t b = 0; b <= 4096; ++b) {
-      uint64_t start = uint64_t(b) << (32 - PCN_IP_BUCKET_BITS);
-      bkt[b] = static_cast<uint16_t>(std::lower_bound(iv.bnd.begin(), iv.bnd.end(), start) - iv.bnd.begin());
+    // bucket entry: PCN_IP_LEAF | class when no boundary falls inside the
+    // bucket (one LDS read answers), else (count << 16) | first boundary index.
+    // About two buckets per boundary: 2^4 .. 2^12 buckets.
+    if (iv.bnd.size() > 0x7FFF) throw std::runtime_error("too many LPM intervals");
+    uint32_t bits = 4;
+    while (bits < PCN_IP_BUCKET_BITS_MAX && (size_t(1) << bits) < 2 * iv.bnd.size()) ++bits;
+    const uint32_t nb = 1u << bits;
+    std::vector<uint32_t> first(nb + 1);
+    for (uint32_t b = 0; b <= nb; ++b) {
+      uint64_t start = uint64_t(b) << (32 - bits);
+      first[b] = static_cast<uint32_t>(std::lower_bound(iv.bnd.begin(), iv.bnd.end(), start) - iv.bnd.begin());
     }
+    std::vector<uint32_t> bkt(nb);
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint32_t lo = first[b], count = first[b + 1] - lo;
+      bkt[b] = count == 0 ? (PCN_IP_LEAF | cls[lo]) : ((count << 16) | lo);
+    }
+    lay.ip_shift[side] = 32 - bits;
     lay.ip_bkt[side] = blob.add(bkt);
     lay.ip_bnd[side] = blob.add(iv.bnd);
     lay.ip_cls[side] = blob.add(cls);
@@ -227,7 +252,7 @@ HostImage build_image(const ChainTables &t) {
       else ++nk;
     }
     uint32_t size = 16;
-    while (size < 2 * nk) size <<= 1;
+    while (size < 4 * nk) size <<= 1;   // load <= 1/4: nearly always one probe
     const uint32_t shift = static_cast<uint32_t>(__builtin_clz(size - 1));
     std::vector<uint32_t> tab(size, PCN_HASH_EMPTY);
     for (size_t k = 0; k < m.keys.size(); ++k) {
@@ -271,8 +296,9 @@ HostImage build_image(const ChainTables &t) {
   const auto &vecs = pool.vecs();
   img.nvec = static_cast<uint32_t>(vecs.size());
   const size_t nrec = size_t(img.nvec) * img.nsw;
-  std::vector<uint64_t> summ(nrec, 0), full(nrec, 0), part;
-  std::vector<uint32_t> pbase(nrec, 0);
+  std::vector<uint64_t> summ(nrec, 0), full(nrec, 0), words{~uint64_t(0)};
+  std::vector<uint32_t> pbase(nrec, 0), part;
+  std::map<uint64_t, uint32_t> word_id{{~uint64_t(0), 0}};
   for (uint32_t v = 0; v < img.nvec; ++v) {
     for (uint32_t w = 0; w < img.nrw; ++w) {
       const size_t rec = size_t(v) * img.nsw + w / 64;
@@ -280,14 +306,24 @@ HostImage build_image(const ChainTables &t) {
       const uint64_t x = vecs[v][w];
       if (x) summ[rec] |= uint64_t(1) << (w % 64);
       if (x == perm.valid[w]) full[rec] |= uint64_t(1) << (w % 64);
-      else if (x) part.push_back(x);
+      else if (x) {
+        auto it = word_id.emplace(x, static_cast<uint32_t>(words.size())).first;
+        if (it->second == words.size()) words.push_back(x);
+        part.push_back(it->second);
+      }
     }
   }
   img.part_words = static_cast<uint32_t>(part.size());
   lay.summ = blob.add(summ);
   lay.full = blob.add(full);
   lay.pbase = blob.add(pbase);
-  lay.part = blob.add(part);
+  lay.part_wide = words.size() > 0xFFFF;
+  if (lay.part_wide) lay.part = blob.add(part);
+  else lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
+  lay.pool = blob.add(words);
+  lay.zero = blob.add(std::vector<uint32_t>(4, 0));
+  img.pool_words = static_cast<uint32_t>(words.size());
+  img.part_bytes = part.size() * (lay.part_wide ? 4 : 2) + words.size() * 8;
   lay.perm = blob.add(perm.perm);
   lay.bytes = static_cast<uint32_t>((blob.bytes.size() + kAlign - 1) / kAlign * kAlign);
   blob.bytes.resize(lay.bytes);

@@ -14,7 +14,9 @@ struct HostImage {
   std::vector<uint8_t> tables;   // table image (TableLayout offsets)
   TableLayout lay{};
   uint32_t nrules = 0, nrw = 0, nsw = 0, present = 0, nvec = 0, ngroups = 0, all_cls = 0;
-  uint32_t part_words = 0;       // partial (neither zero nor full) vector words stored
+  uint32_t part_words = 0;       // partial (neither zero nor full) vector words
+  uint32_t pool_words = 0;       // distinct partial words stored
+  uint64_t part_bytes = 0;       // PART indices + POOL bytes
   int default_action = 1;
 };
 

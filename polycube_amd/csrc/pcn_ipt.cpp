@@ -122,7 +122,7 @@ void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
                        reinterpret_cast<const uint32_t *>(&img.lay) + sizeof(TableLayout) / 4);
   cs.desc_words.insert(cs.desc_words.end(), {img.nrw, img.nsw, img.present, img.all_cls});
   cs.info = pcn_ipt_chain_info{img.nrules, img.nrw, img.nsw, img.nvec, img.ngroups, img.present,
-                               img.lay.bytes, static_cast<uint64_t>(img.part_words) * 8};
+                               img.lay.bytes, img.part_bytes};
   if (ctx->has_device) {
     device_guard(ctx);
     // every batch queued before this call must not see a half-written slot

@@ -11,9 +11,9 @@ import numpy as np
 
 from polycube_amd import ffi
 
-LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_bnd0", "ip_bnd1", "ip_cls0", "ip_cls1", "hash0", "hash1",
-          "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "proto", "flags", "ct", "summ",
-          "full", "pbase", "part", "perm"]
+LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_shift0", "ip_shift1", "ip_bnd0", "ip_bnd1", "ip_cls0", "ip_cls1",
+          "hash0", "hash1", "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "proto", "flags", "ct",
+          "summ", "full", "pbase", "part", "part_wide", "pool", "zero", "perm"]
 MISS = 0xFFFF
 EMPTY = 0xFFFFFFFF
 
@@ -41,8 +41,11 @@ class ImageModel:
 
     def ip_class(self, side, h):
         L = self.lay
-        b = h >> 20
-        lo, hi = self.u16(L[f"ip_bkt{side}"] + 2 * b), self.u16(L[f"ip_bkt{side}"] + 2 * b + 2)
+        e = self.u32(L[f"ip_bkt{side}"] + 4 * (h >> L[f"ip_shift{side}"]))
+        if e & 0x80000000:
+            return e & 0xFFFF
+        lo = e & 0xFFFF
+        hi = lo + (e >> 16)
         while lo < hi:
             mid = (lo + hi) >> 1
             if self.u32(L[f"ip_bnd{side}"] + 4 * mid) <= h:
@@ -107,7 +110,9 @@ class ImageModel:
                         continue
                     part = self.u64(L["summ"] + 8 * r) & ~fm
                     rank = bin(part & ((1 << bit) - 1)).count("1")
-                    acc &= self.u64(L["part"] + 8 * (self.u32(L["pbase"] + 4 * r) + rank))
+                    j = self.u32(L["pbase"] + 4 * r) + rank
+                    q = self.u32(L["part"] + 4 * j) if L["part_wide"] else self.u16(L["part"] + 2 * j)
+                    acc &= self.u64(L["pool"] + 8 * q)
                 if acc:
                     low = (acc & -acc).bit_length() - 1
                     e = self.u16(L["perm"] + 2 * ((64 * k + bit) * 63 + low))

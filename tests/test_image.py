@@ -1,0 +1,96 @@
+"""The chain image the GPU kernel walks (intervals, hashes, summaries, partial
+words, permutation) answers exactly like the oracle — checked on the CPU by
+walking the exported bytes with tests/image_model.py (no GPU needed)."""
+import numpy as np
+import pytest
+
+from oracle.ffi import Oracle
+from polycube_amd import FORWARD, Iptables
+from polycube_amd import synth
+from image_model import ImageModel, model_classify
+from rulegen import PORTS, quirky_rules
+
+
+def build(rules, default="DROP"):
+    o = Oracle()
+    ipt = Iptables(device=-1)
+    for name, idx in PORTS.items():
+        o.add_port(name, idx)
+        ipt.add_port(name, idx)
+    o.set_chain(FORWARD, rules, default)
+    ipt.interactive = False
+    ch = ipt.chain(FORWARD)
+    for r in rules:
+        ch.append(**r)
+    ch.apply_rules()
+    return o, ipt, ch
+
+
+def check(rules, frames, n):
+    o, ipt, ch = build(rules)
+    model = ImageModel(ch)
+    _, rid = o.classify(frames, n=n, stride=64)
+    got = model_classify(model, frames, n)
+    bad = np.nonzero(got != rid)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[0]}: model {got[bad[0]]} oracle {rid[bad[0]]}"
+    return ch
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 1500), (2, 1500), (3, 1500)])
+def test_image_configs(cfg, n):
+    rs = synth.config_rules(cfg)
+    frames = synth.config_frames(cfg, n, rs)
+    check(rs.rules(), frames, n)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_image_random_rulesets(seed):
+    rs = synth.make_rules(150 + 200 * seed, seed + 100)
+    cols = synth.make_headers(rs, 1000, seed + 7, hit_frac=0.7)
+    frames = synth.build_frames(*cols, frame_len=64)
+    check(rs.rules(), frames, 1000)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_image_quirky_rules(seed):
+    # quirky rules (negations, masks with host bits, ports 0, same-prefix
+    # overwrite) under well-formed TCP/UDP probes that hit them
+    rules = [r for r in quirky_rules(60 + 40 * seed, seed) if "in_iface" not in r and "out_iface" not in r]
+    rng = np.random.default_rng(seed)
+    n = 800
+    src = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    for i, r in enumerate(rules[: n // 2]):
+        if "src" in r:
+            src[2 * i] = synth_host(r["src"])
+        if "dst" in r:
+            dst[2 * i] = synth_host(r["dst"])
+    proto = rng.choice([6, 17], n).astype(np.int32)
+    sport = rng.choice([0, 53, 80, 443, 8080, 1234], n).astype(np.int32)
+    dport = rng.choice([0, 53, 80, 443, 8080, 1234], n).astype(np.int32)
+    flags = rng.choice([0x02, 0x12, 0x10, 0x01, 0x04, 0x3F], n).astype(np.int32)
+    frames = synth.build_frames(src, dst, proto, sport, dport, flags, frame_len=64)
+    check(rules, frames, n)
+
+
+def synth_host(s):
+    a, b, c, d = (int(x) & 0xFF for x in s.split("/")[0].split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def test_ip_buckets_agree_with_a_full_interval_search():
+    rs = synth.config_rules(3)
+    _, _, ch = build(rs.rules())
+    m = ImageModel(ch)
+    bkt, bnd_off, cls_off = m.lay["ip_bkt1"], m.lay["ip_bnd1"], m.lay["ip_cls1"]
+    ent = np.frombuffer(m.img, np.uint32, 1 << (32 - m.lay["ip_shift1"]), bkt)
+    nb = max(int(e >> 16) + int(e & 0xFFFF) for e in ent if not e & 0x80000000)
+    bnd = np.frombuffer(m.img, np.uint32, nb, bnd_off)
+    assert (np.diff(bnd.astype(np.int64)) > 0).all()
+    assert (ent & 0x80000000).sum() > ent.size // 2   # most buckets answer with one read
+    rng = np.random.default_rng(5)
+    probes = np.concatenate([rng.integers(0, 1 << 32, 3000, dtype=np.uint64),
+                             bnd.astype(np.uint64), bnd.astype(np.uint64) - 1]).astype(np.uint32)
+    for h in probes:
+        want = m.u16(cls_off + 2 * int(np.searchsorted(bnd, h, side="right")))
+        assert m.ip_class(1, int(h)) == want

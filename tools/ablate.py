@@ -64,7 +64,12 @@ def main():
         child(a.lib, a.hit, a.log2n, a.iters, a.cfg)
         return
     for var in a.variants.split(","):
-        lib = "" if var == "product" else os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_ablate{var}.so")
+        if var == "product":
+            lib = ""
+        elif var.startswith("exp_"):
+            lib = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_{var}.so")
+        else:
+            lib = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_ablate{var}.so")
         for hit in a.hits.split(","):
             r = subprocess.run([sys.executable, __file__, "--child", "--lib", lib, "--hit", hit, "--log2n",
                                 str(a.log2n), "--iters", str(a.iters), "--cfg", str(a.cfg)],
