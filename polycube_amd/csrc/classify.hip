@@ -275,6 +275,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   for (uint32_t b = threadIdx.x; b < 2 * a.nbins; b += blockDim.x) bins[b] = 0;
   __syncthreads();
 
+  const uint32_t const_port = a.const_in_port;
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t n_round = (a.n + step - 1) / step * step;   // uniform trip count per wave
@@ -294,7 +295,10 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     Parsed p{};
     uint32_t port = 0;
     if (valid) {
-      port = a.in_port ? a.in_port[i] : a.const_in_port;
+      // (a select between a register and a load: `in_port ? in_port[i] :
+      // a.const_in_port` compiles to a flat load from the kernarg segment,
+      // which counts in lgkmcnt and stalls every later LDS wait)
+      port = a.in_port ? static_cast<uint32_t>(a.in_port[i]) : const_port;
       // ---- Parser_dp.c:94-153 ----
       bool done = true;
       if (L < 14) verdict = PCN_IPT_DROP;
@@ -400,7 +404,8 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
           atomicAdd(&bins[2 * c + 1], bytes);
         }
       }
-      // per-rule bins
+      // per-rule bins: only chains that run rules in this variant
+      if (CH < 3 ? c != CH : c == PCN_IPT_OUTPUT) continue;
       const DevChain &ch = a.ch[c];
       if (valid && cchain == c && rid >= 0 && static_cast<uint32_t>(rid) < ch.ncounted) {
         if (ch.lds_bins >= 0) {
