@@ -46,7 +46,7 @@ typedef struct {
   int device;                 /* HIP device ordinal; -1 = control plane only (no GPU) */
   uint32_t max_counted_rules; /* 0 => 8000   (Iptables_ActionLookup_dp.c:55-56)  */
   uint32_t max_action_rules;  /* 0 => 10000  (Iptables_ActionLookup_dp.c:36)     */
-  uint32_t max_rules;         /* 0 => 8192   (Iptables.h:173); hard cap 65535    */
+  uint32_t max_rules;         /* 0 => 8192   (Iptables.h:173); hard cap 32767    */
 } pcn_ipt_config;
 
 /* One rule as received by the REST surface: ChainRuleJsonObject /
