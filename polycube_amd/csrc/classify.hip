@@ -32,9 +32,6 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #define PCN_ABLATE 0
 #endif
 // Tuning switches (tools/ablate.py builds experiment variants with -D...).
-#ifndef PCN_BLOCK
-#define PCN_BLOCK 512
-#endif
 
 namespace pcn {
 
@@ -100,7 +97,6 @@ template <bool FIXED>
 __device__ __forceinline__ void load_header(const LaunchArgs &a, uint64_t i, Hdr &h, uint32_t &L) {
   if (FIXED) {
     load_fixed(a.frames + i * a.stride, h);
-    L = a.fixed_len;
   } else {
     uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
     load_generic(a.frames, a.frames_bytes, off, h);
@@ -108,11 +104,14 @@ __device__ __forceinline__ void load_header(const LaunchArgs &a, uint64_t i, Hdr
   }
 }
 
+// localip is staged in LDS (sorted NBO u32), so the search makes no global
+// load inside the loop.
 __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
+  const uint32_t *tab = reinterpret_cast<const uint32_t *>(pcn_smem + a.lds_localip);
   uint32_t lo = 0, hi = a.nlocal;
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
-    uint32_t v = a.localip[mid];
+    uint32_t v = tab[mid];
     if (v == ip) return true;
     if (v < ip) lo = mid + 1; else hi = mid;
   }
@@ -153,21 +152,22 @@ struct Parsed {
   uint32_t ct;                 // conntrack status 0..3 (or >3: invalid input)
 };
 
-// Rule-chain stage (ch is wave-uniform).  Returns the verdict and sets rid
-// (>= 0 matched rule, -1 default action, -2 decided without the chain).
-// Every field has a fixed slot; absent or skipped fields hold the all-ones
-// class, so the eight summary loads issue back to back without branches.
+// ---- rule-chain stage, part 1 (per lane) ----
+// Maps every field to its class.  Returns true when the packet needs the
+// candidate stage; otherwise the verdict is decided here (a field without a
+// class takes the default action, a bad conntrack label drops).  Every field
+// has a fixed slot; absent or skipped fields hold the all-ones class.
 template <bool LDS>
-__device__ __forceinline__ uint32_t run_chain(const DevChain &ch, const Parsed &p, uint32_t port, int32_t &rid) {
+__device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &p, uint32_t port, uint32_t cls[8],
+                                              uint32_t &verdict, int32_t &rid) {
   const Tab<LDS> t{ch.image, ch.lds_image};
   const TableLayout &lay = ch.lay;
   const uint32_t present = ch.present;
   const uint32_t all = ch.all_cls;
-  uint32_t cls[8];
 #pragma unroll
   for (int f = 0; f < 8; ++f) cls[f] = all;
   if (present & (1u << PCN_IPT_F_CONNTRACK)) {
-    if (p.ct > 3) { rid = PCN_IPT_RID_NOCHAIN; return PCN_IPT_DROP; }   // array miss => RX_DROP
+    if (p.ct > 3) { rid = PCN_IPT_RID_NOCHAIN; verdict = PCN_IPT_DROP; return false; }   // array miss => RX_DROP
     cls[0] = t.u16(lay.ct + 2 * p.ct);
   }
   if (present & (1u << PCN_IPT_F_IPSRC))
@@ -193,74 +193,148 @@ __device__ __forceinline__ uint32_t run_chain(const DevChain &ch, const Parsed &
   bool miss = false;
 #pragma unroll
   for (int f = 0; f < 8; ++f) miss |= cls[f] == PCN_CLS_MISS;
-  if (miss) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(ch.default_action); }
+  if (miss) { rid = PCN_IPT_RID_DEFAULT; verdict = static_cast<uint32_t>(ch.default_action); return false; }
   if (PCN_ABLATE == 2) {   // keep the lookups alive: the verdict depends on them
     uint32_t x = 0;
 #pragma unroll
     for (int f = 0; f < 8; ++f) x ^= cls[f];
     rid = PCN_IPT_RID_DEFAULT;
-    return x & 1;
+    verdict = x & 1;
+    return false;
   }
+  return true;
+}
 
+// Per-wave LDS scratch of the candidate stage.
+struct WaveScratch {
+  uint32_t cls[64][4];   // each lane's eight u16 classes
+  uint32_t item[64];     // (owner lane << 8) | candidate bit
+  uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
+};
+static_assert(sizeof(WaveScratch) == PCN_WAVE_SCRATCH_BYTES, "host sizes the scratch");
+
+// ---- rule-chain stage, part 2 (whole wave, converged) ----
+// Lanes with `active` AND their class summaries into a candidate-word mask.
+// The (lane, word) candidate pairs of the whole wave are then dealt out one
+// per lane, 64 at a time, so a lane with many candidates does not hold the
+// wave hostage: each worker re-reads its owner's class records, ANDs the
+// partial words of its one word and folds the matched entry into the
+// owner's slot with an LDS atomic min.  Returns the owner's best entry.
+template <bool LDS>
+__device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[8],
+                                                     WaveScratch *ws) {
+  const uint32_t lane = __lane_id();
+  if (__ballot(active) == 0) return kNoRule;
+  const Tab<LDS> t{ch.image, ch.lds_image};
+  const TableLayout &lay = ch.lay;
   const uint32_t nrw = ch.nrw, nsw = ch.nsw;
-  uint32_t best = kNoRule;   // (orig id << 1 | action), minimum over candidate words
-  uint64_t mseen = 0;        // PCN_ABLATE == 3 only
+  ws->best[lane] = kNoRule;
+  ws->cls[lane][0] = cls[0] | (cls[1] << 16);
+  ws->cls[lane][1] = cls[2] | (cls[3] << 16);
+  ws->cls[lane][2] = cls[4] | (cls[5] << 16);
+  ws->cls[lane][3] = cls[6] | (cls[7] << 16);
+  uint64_t mseen = 0;   // PCN_ABLATE == 3 only
   for (uint32_t k = 0; k < nsw; ++k) {
-    uint32_t live = nrw - k * 64;
-    uint64_t m = live >= 64 ? ~0ull : ((1ull << live) - 1);
-    uint64_t s[8];
+    const uint32_t live = nrw - k * 64;
+    uint64_t m = 0;
+    if (active) {
+      m = live >= 64 ? ~0ull : ((1ull << live) - 1);
+      uint64_t sm[8];
 #pragma unroll
-    for (int f = 0; f < 8; ++f) s[f] = t.u64(lay.summ + 8 * (cls[f] * nsw + k));
+          for (int f = 0; f < 8; ++f) sm[f] = t.u64(lay.sf + 16 * (cls[f] * nsw + k));
 #pragma unroll
-    for (int f = 0; f < 8; ++f) m &= s[f];
-    if (PCN_ABLATE == 3) { mseen |= m; continue; }
-    if (!m) continue;
-    uint64_t fm[8];
-    uint32_t pb[8];
-#pragma unroll
-    for (int f = 0; f < 8; ++f) {
-      const uint32_t rec = cls[f] * nsw + k;
-      fm[f] = t.u64(lay.full + 8 * rec);
-      pb[f] = t.u32(lay.pbase + 4 * rec);
-      s[f] &= ~fm[f];                 // s[f] now marks the partial words
+      for (int f = 0; f < 8; ++f) m &= sm[f];
     }
-    while (m) {
-      const uint32_t bit = static_cast<uint32_t>(__builtin_ctzll(m));
-      m &= m - 1;
-      const uint64_t below = (1ull << bit) - 1;
-      // Straight-line on purpose: every field's index read, then every pool
-      // read, issue back to back (two LDS round trips per word).  A FULL field
-      // reads the zero cell, i.e. POOL[0], the all-ones word.
-      uint32_t q[8];
+    if (PCN_ABLATE == 3) { mseen |= m; continue; }
+    // exclusive prefix of the per-lane candidate counts (bit-sliced ballots)
+    const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(m));
+    uint32_t pos = 0, total = 0;
 #pragma unroll
-      for (int f = 0; f < 8; ++f) {
-        const uint32_t j = pb[f] + static_cast<uint32_t>(__builtin_popcountll(s[f] & below));
-        const bool wide = !LDS && lay.part_wide;
-        const uint32_t part_mask = static_cast<uint32_t>((fm[f] >> bit) & 1) - 1u;   // ~0: partial
-        const uint32_t at = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
-        q[f] = wide ? t.u32(at) : t.u16(at);
+    for (int b = 0; b < 7; ++b) {
+      const uint64_t bm = __ballot((c >> b) & 1);
+      pos += static_cast<uint32_t>(__builtin_popcountll(bm & ((1ull << lane) - 1))) << b;
+      total += static_cast<uint32_t>(__builtin_popcountll(bm)) << b;
+    }
+    for (uint32_t done = 0; done < total; done += 64) {
+      // deal: each owner writes its candidates that fall in [done, done + 64)
+      while (m && pos < done + 64) {
+        ws->item[pos - done] = (lane << 8) | static_cast<uint32_t>(__builtin_ctzll(m));
+        m &= m - 1;
+        ++pos;
       }
-      uint64_t acc = ~0ull;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < total - done) {
+        const uint32_t it = ws->item[lane];
+        const uint32_t owner = it >> 8, bit = it & 63;
+        const uint64_t below = (1ull << bit) - 1;
+        const uint32_t r0 = ws->cls[owner][0], r1 = ws->cls[owner][1], r2 = ws->cls[owner][2],
+                       r3 = ws->cls[owner][3];
+        const uint32_t oc[8] = {r0 & 0xffff, r0 >> 16, r1 & 0xffff, r1 >> 16,
+                                r2 & 0xffff, r2 >> 16, r3 & 0xffff, r3 >> 16};
+        // At a candidate word every field's summary bit is set, so a field is
+        // PARTIAL there iff its FULL bit is clear.  Straight-line on purpose:
+        // every index read, then every pool read, issue back to back.  A FULL
+        // field reads the zero cell, i.e. POOL[0], the all-ones word.
+        uint32_t q[8];
 #pragma unroll
-      for (int f = 0; f < 8; ++f) acc &= t.u64(lay.pool + 8 * q[f]);
-      if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
-        const uint32_t w = k * 64 + bit;
-        uint32_t e = t.u16(lay.perm + 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
-        best = e < best ? e : best;
+        for (int f = 0; f < 8; ++f) {
+          const uint32_t rec = oc[f] * nsw + k;
+          const u32x4 r = LDS ? *reinterpret_cast<const u32x4 *>(pcn_smem + ch.lds_image + lay.sf + 16 * rec)
+                              : *reinterpret_cast<const u32x4 *>(ch.image + lay.sf + 16 * rec);
+          const uint64_t pm = (static_cast<uint64_t>(r.y) << 32 | r.x) & ~(static_cast<uint64_t>(r.w) << 32 | r.z);
+          const uint32_t j = t.u32(lay.pbase + 4 * rec) + static_cast<uint32_t>(__builtin_popcountll(pm & below));
+          const bool wide = !LDS && lay.part_wide;
+          const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
+          const uint32_t at = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
+          q[f] = wide ? t.u32(at) : t.u16(at);
+        }
+        uint64_t acc = ~0ull;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) acc &= t.u64(lay.pool + 8 * q[f]);
+        if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
+          const uint32_t w = k * 64 + bit;
+          const uint32_t e = t.u16(lay.perm + 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
+          atomicMin(&ws->best[owner], e);
+        }
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
-  if (PCN_ABLATE == 3) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(mseen & 1); }
+  if (PCN_ABLATE == 3) return mseen ? 0u : kNoRule;
+  return ws->best[lane];
+}
+
+// ---- rule-chain stage, part 3 (per lane) ----
+__device__ __forceinline__ uint32_t chain_finish(const DevChain &ch, uint32_t best, int32_t &rid) {
   if (best == kNoRule) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(ch.default_action); }
-  uint32_t rule = best >> 1;
+  const uint32_t rule = best >> 1;
   if (rule >= ch.max_action) { rid = PCN_IPT_RID_NOCHAIN; return PCN_IPT_DROP; }
   rid = static_cast<int32_t>(rule);
   return (best & 1) ? PCN_IPT_ACCEPT : PCN_IPT_DROP;
 }
 
+// One chain through the three parts; `mine` = lanes whose packet runs it.
+// Called with the wave converged.
+template <bool LDS>
+__device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const Parsed &p, uint32_t port,
+                                          WaveScratch *ws, uint32_t &verdict, int32_t &rid) {
+  uint32_t cls[8];
+  bool need = false;
+  if (mine) need = chain_classes<LDS>(ch, p, port, cls, verdict, rid);
+  const uint32_t best = chain_candidates<LDS>(ch, need, cls, ws);
+  if (need) verdict = chain_finish(ch, best, rid);
+}
+
 template <bool FIXED, bool LDS, int CH>
 __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
-  unsigned long long *bins = reinterpret_cast<unsigned long long *>(pcn_smem + a.bins_offset);
+  // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
+  // frames per workgroup so neither can wrap; the flush widens to u64)
+  uint32_t *bins = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);
+  WaveScratch *ws = reinterpret_cast<WaveScratch *>(pcn_smem + a.lds_scratch) + (threadIdx.x >> 6);
   // stage every chain's table image in LDS and zero the counter histogram
   if (LDS) {
 #pragma unroll
@@ -273,6 +347,8 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     }
   }
   for (uint32_t b = threadIdx.x; b < 2 * a.nbins; b += blockDim.x) bins[b] = 0;
+  for (uint32_t k = threadIdx.x; k < a.nlocal; k += blockDim.x)
+    reinterpret_cast<uint32_t *>(pcn_smem + a.lds_localip)[k] = a.localip[k];
   __syncthreads();
 
   const uint32_t const_port = a.const_in_port;
@@ -280,14 +356,33 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   const uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t n_round = (a.n + step - 1) / step * step;   // uniform trip count per wave
   // software pipeline: the next frame's header is in flight while this one is classified
+  // The prefetch is unconditional (the index is clamped to the last frame):
+  // a conditional load merges into a phi the compiler can only resolve with
+  // an immediate s_waitcnt vmcnt(0), which serialises load and compute.
+  const uint64_t last = a.n - 1;
+  // in_port / ct_status ride along with the header: when the batch has none
+  // the host points them at a zero cell with a zero index mask, so the loads
+  // stay unconditional too.
   Hdr nh;
-  uint32_t nL = 0;
-  if (first < a.n) load_header<FIXED>(a, first, nh, nL);
+  uint32_t nL = a.fixed_len, nport, nct;
+  auto prefetch = [&](uint64_t j) {
+    load_header<FIXED>(a, j, nh, nL);
+    nport = a.in_port[j & a.in_port_mask];
+    nct = a.ct_status[j & a.ct_mask];
+  };
+  prefetch(first < a.n ? first : last);
   for (uint64_t i = first; i < n_round; i += step) {
     const bool valid = i < a.n;
+    // Pin every prefetched dword (used or not) until here, so no register the
+    // load writes is recycled mid-iteration (a WAW hazard costs a vmcnt wait).
+#pragma unroll
+    for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(nh.w[k]));
+    asm volatile("" : "+v"(nport), "+v"(nct));
     const Hdr h = nh;
-    const uint32_t L = nL;
-    if (i + step < a.n) load_header<FIXED>(a, i + step, nh, nL);
+    const uint32_t L = FIXED ? a.fixed_len : nL;
+    const uint32_t cur_port = nport, cur_ct = nct;
+    const uint64_t next = i + step;
+    prefetch(next < a.n ? next : last);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
     int32_t cchain = -1;    // chain whose counters this packet bumps
@@ -295,10 +390,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     Parsed p{};
     uint32_t port = 0;
     if (valid) {
-      // (a select between a register and a load: `in_port ? in_port[i] :
-      // a.const_in_port` compiles to a flat load from the kernarg segment,
-      // which counts in lgkmcnt and stalls every later LDS wait)
-      port = a.in_port ? static_cast<uint32_t>(a.in_port[i]) : const_port;
+      port = a.has_in_port ? cur_port : const_port;
       // ---- Parser_dp.c:94-153 ----
       bool done = true;
       if (L < 14) verdict = PCN_IPT_DROP;
@@ -344,8 +436,8 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
           }
         }
         if (!done) {
-          if (a.ct_status) {
-            p.ct = a.ct_status[i];
+          if (a.has_ct) {
+            p.ct = cur_ct;
           } else if (p.proto == 6) {      // empty-table labels, ConntrackLabel_dp.c:372-383
             p.ct = (p.flags & 0x02) && ((p.flags | 0x02) == 0x02) ? 0u : 3u;
           } else if (p.proto == 17) {
@@ -364,18 +456,16 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
     if (CH < 3) {
-      if (chain >= 0) {
-        verdict = run_chain<LDS>(a.ch[CH < 3 ? CH : 0], p, port, rid);
-        cchain = chain;
-      }
+      run_chain<LDS>(a.ch[CH < 3 ? CH : 0], chain >= 0, p, port, ws, verdict, rid);
+      if (chain >= 0) cchain = chain;
     } else {
-      if (__ballot(chain == PCN_IPT_FORWARD) && chain == PCN_IPT_FORWARD) {
-        verdict = run_chain<LDS>(a.ch[PCN_IPT_FORWARD], p, port, rid);
-        cchain = PCN_IPT_FORWARD;
+      if (__ballot(chain == PCN_IPT_FORWARD)) {
+        run_chain<LDS>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, verdict, rid);
+        if (chain == PCN_IPT_FORWARD) cchain = PCN_IPT_FORWARD;
       }
-      if (__ballot(chain == PCN_IPT_INPUT) && chain == PCN_IPT_INPUT) {
-        verdict = run_chain<LDS>(a.ch[PCN_IPT_INPUT], p, port, rid);
-        cchain = PCN_IPT_INPUT;
+      if (__ballot(chain == PCN_IPT_INPUT)) {
+        run_chain<LDS>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, verdict, rid);
+        if (chain == PCN_IPT_INPUT) cchain = PCN_IPT_INPUT;
       }
     }
     if (valid) {
@@ -390,9 +480,9 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
       const bool mine = valid && cchain == c && rid == PCN_IPT_RID_DEFAULT;
       const uint64_t m = __ballot(mine);
       if (m) {
-        unsigned long long bytes;
+        uint32_t bytes;
         if (FIXED) {
-          bytes = static_cast<unsigned long long>(__builtin_popcountll(m)) * a.fixed_len;
+          bytes = static_cast<uint32_t>(__builtin_popcountll(m)) * a.fixed_len;
         } else {
           uint32_t x = mine ? L : 0u;
 #pragma unroll
@@ -400,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
           bytes = x;
         }
         if ((threadIdx.x & 63) == 0) {
-          atomicAdd(&bins[2 * c], static_cast<unsigned long long>(__builtin_popcountll(m)));
+          atomicAdd(&bins[2 * c], static_cast<uint32_t>(__builtin_popcountll(m)));
           atomicAdd(&bins[2 * c + 1], bytes);
         }
       }
@@ -410,8 +500,8 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
       if (valid && cchain == c && rid >= 0 && static_cast<uint32_t>(rid) < ch.ncounted) {
         if (ch.lds_bins >= 0) {
           uint32_t b = static_cast<uint32_t>(ch.lds_bins) + static_cast<uint32_t>(rid);
-          atomicAdd(&bins[2 * b], 1ull);
-          atomicAdd(&bins[2 * b + 1], static_cast<unsigned long long>(L));
+          atomicAdd(&bins[2 * b], 1u);
+          if (!FIXED) atomicAdd(&bins[2 * b + 1], L);   // fixed length: bytes = pkts * len at flush
         } else {
           atomicAdd(&ch.ctr[2 + 2 * rid], 1ull);
           atomicAdd(&ch.ctr[3 + 2 * rid], static_cast<unsigned long long>(L));
@@ -422,7 +512,8 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   __syncthreads();
   // ---- flush the workgroup histogram ----
   for (uint32_t b = threadIdx.x; b < a.nbins; b += blockDim.x) {
-    unsigned long long pk = bins[2 * b], by = bins[2 * b + 1];
+    const unsigned long long pk = bins[2 * b];
+    const unsigned long long by = (FIXED && b >= 3) ? pk * a.fixed_len : bins[2 * b + 1];
     if (!pk) continue;
     unsigned long long *dst = nullptr;
     if (b < 3) {
@@ -458,7 +549,7 @@ void launch_variant(const LaunchArgs &a, int ch, unsigned grid, size_t lds, hipS
 // reach the rule stage (0..2) or 3 for INPUT+FORWARD.  Returns a hipError_t.
 int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
-  const size_t lds = a.bins_offset + static_cast<size_t>(a.nbins) * 16;
+  const size_t lds = a.lds_bytes;
   const bool in_lds = a.lds_images_bytes > 0;
   const size_t max_per_cu = 2048 / kBlock;   // 32 waves per CU
   size_t per_cu = lds ? (160 * 1024) / lds : max_per_cu;
@@ -467,11 +558,31 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStr
   const uint64_t want = (a.n + kBlock - 1) / kBlock;
   const uint64_t cap = static_cast<uint64_t>(num_cus) * per_cu;
   const unsigned grid = static_cast<unsigned>(want < cap ? want : cap);
-  if (fixed && in_lds) launch_variant<true, true>(a, ch, grid, lds, stream);
-  else if (fixed) launch_variant<true, false>(a, ch, grid, lds, stream);
-  else if (in_lds) launch_variant<false, true>(a, ch, grid, lds, stream);
-  else launch_variant<false, false>(a, ch, grid, lds, stream);
-  return static_cast<int>(hipGetLastError());
+  // u32 histogram bins: at most 2^32-1 bytes per workgroup per launch, so a
+  // batch whose workgroups could exceed that is split into launches.
+  const uint64_t max_len = a.lens ? 65535u : (a.fixed_len ? a.fixed_len : 1u);
+  const uint64_t per_block = 0xFFFFFFFFull / max_len;
+  const uint64_t chunk = per_block * grid;
+  for (uint64_t base = 0; base < a.n; base += chunk) {
+    LaunchArgs c = a;
+    c.n = a.n - base < chunk ? a.n - base : chunk;
+    if (base) {
+      if (!a.offsets) { c.frames = a.frames + base * a.stride; c.frames_bytes = a.frames_bytes - base * a.stride; }
+      else c.offsets = a.offsets + base;
+      if (a.lens) c.lens = a.lens + base;
+      if (a.has_in_port) c.in_port = a.in_port + base;
+      if (a.has_ct) c.ct_status = a.ct_status + base;
+      c.verdicts = a.verdicts + base;
+      if (a.rule_ids) c.rule_ids = a.rule_ids + base;
+    }
+    if (fixed && in_lds) launch_variant<true, true>(c, ch, grid, lds, stream);
+    else if (fixed) launch_variant<true, false>(c, ch, grid, lds, stream);
+    else if (in_lds) launch_variant<false, true>(c, ch, grid, lds, stream);
+    else launch_variant<false, false>(c, ch, grid, lds, stream);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return hipSuccess;
 }
 
 // Sum `nranks` gathered counter blocks into `out` (u64 element-wise).

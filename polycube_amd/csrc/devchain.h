@@ -35,6 +35,10 @@
 #define PCN_IP_BUCKET_BITS_MAX 12
 #define PCN_IP_LEAF 0x80000000u
 #define PCN_HASH_EMPTY 0xFFFFFFFFu
+#ifndef PCN_BLOCK
+#define PCN_BLOCK 512               // classify workgroup size (threads)
+#endif
+#define PCN_WAVE_SCRATCH_BYTES 1536 // per-wave LDS scratch of the candidate stage
 
 namespace pcn {
 
@@ -49,7 +53,7 @@ struct TableLayout {
   uint32_t hash_mask[3];   // size - 1
   uint32_t hash_wild[3];   // class used when the key is absent (PCN_CLS_MISS: none)
   uint32_t proto, flags, ct;   // u16[256], u16[256], u16[4]
-  uint32_t summ, full;     // u64[nvec][nsw]
+  uint32_t sf;             // u64x2[nvec][nsw]: {SUMM, FULL}
   uint32_t pbase;          // u32[nvec][nsw]: first PART index of the class's block
   uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
   uint32_t part_wide;
@@ -70,7 +74,7 @@ struct DevChain {
   int32_t lds_bins;              // first LDS counter bin of this chain's rules; -1 => global atomics
 };
 
-// LDS layout of a classify workgroup: [chain images][counter bins]
+// LDS layout of a classify workgroup: [chain images][counter bins (u32 x2)][localip][wave scratch]
 constexpr uint32_t kLdsDescBytes = 0;
 
 struct LaunchArgs {
@@ -79,8 +83,10 @@ struct LaunchArgs {
   uint64_t frames_bytes;
   const uint32_t *offsets;
   const uint16_t *lens;
-  const uint16_t *in_port;
-  const uint8_t *ct_status;
+  const uint16_t *in_port;        // never null: a zero cell (mask 0) when the batch has none
+  const uint8_t *ct_status;       // likewise
+  uint64_t in_port_mask, ct_mask; // index masks: ~0 (per-frame arrays) or 0 (zero cell)
+  uint32_t has_in_port, has_ct;
   uint8_t *verdicts;
   int32_t *rule_ids;
   const uint32_t *localip;       // sorted NBO u32
@@ -89,7 +95,10 @@ struct LaunchArgs {
   uint32_t nlocal;
   uint32_t nbins;                // LDS counter bins (3 default bins + rule bins)
   uint32_t bins_offset;          // byte offset of the counter bins in LDS
-  uint32_t lds_images_bytes;     // bytes of chain images staged in LDS after the descriptors (0: from HBM)
+  uint32_t lds_images_bytes;     // bytes of chain images staged in LDS (0: read from HBM)
+  uint32_t lds_localip;          // byte offset of the staged localip table in LDS
+  uint32_t lds_scratch;          // byte offset of the per-wave candidate scratch in LDS
+  uint32_t lds_bytes;            // dynamic LDS per workgroup
   uint16_t const_in_port;
   uint16_t direction;
   uint32_t allow_logic;          // _INGRESS_ALLOWLOGIC (modules/ChainSelector.cpp:190-202)

@@ -296,7 +296,7 @@ HostImage build_image(const ChainTables &t) {
   const auto &vecs = pool.vecs();
   img.nvec = static_cast<uint32_t>(vecs.size());
   const size_t nrec = size_t(img.nvec) * img.nsw;
-  std::vector<uint64_t> summ(nrec, 0), full(nrec, 0), words{~uint64_t(0)};
+  std::vector<uint64_t> sf(2 * nrec, 0), words{~uint64_t(0)};   // {SUMM, FULL} per record
   std::vector<uint32_t> pbase(nrec, 0), part;
   std::map<uint64_t, uint32_t> word_id{{~uint64_t(0), 0}};
   for (uint32_t v = 0; v < img.nvec; ++v) {
@@ -304,8 +304,8 @@ HostImage build_image(const ChainTables &t) {
       const size_t rec = size_t(v) * img.nsw + w / 64;
       if (w % 64 == 0) pbase[rec] = static_cast<uint32_t>(part.size());
       const uint64_t x = vecs[v][w];
-      if (x) summ[rec] |= uint64_t(1) << (w % 64);
-      if (x == perm.valid[w]) full[rec] |= uint64_t(1) << (w % 64);
+      if (x) sf[2 * rec] |= uint64_t(1) << (w % 64);
+      if (x == perm.valid[w]) sf[2 * rec + 1] |= uint64_t(1) << (w % 64);
       else if (x) {
         auto it = word_id.emplace(x, static_cast<uint32_t>(words.size())).first;
         if (it->second == words.size()) words.push_back(x);
@@ -314,8 +314,7 @@ HostImage build_image(const ChainTables &t) {
     }
   }
   img.part_words = static_cast<uint32_t>(part.size());
-  lay.summ = blob.add(summ);
-  lay.full = blob.add(full);
+  lay.sf = blob.add(sf);
   lay.pbase = blob.add(pbase);
   lay.part_wide = words.size() > 0xFFFF;
   if (lay.part_wide) lay.part = blob.add(part);

@@ -52,7 +52,7 @@ void hip_check(hipError_t e, const char *what) {
 #ifndef PCN_DEBUG_LDS_BUDGET
 #define PCN_DEBUG_LDS_BUDGET (160 * 1024)
 #endif
-constexpr uint32_t kMaxLdsRuleBins = PCN_DEBUG_MAX_RULE_BINS;   // per-workgroup LDS histogram budget (32 KB)
+constexpr uint32_t kMaxLdsRuleBins = PCN_DEBUG_MAX_RULE_BINS;   // per-workgroup LDS histogram budget (16 KB of u32 pairs)
 constexpr uint32_t kLdsBudget = PCN_DEBUG_LDS_BUDGET;  // gfx950 LDS per CU (one workgroup may take it all)
 
 struct ImageSlot {
@@ -95,6 +95,7 @@ struct pcn_ipt {
   ChainState chains[PCN_IPT_NCHAINS];
   std::vector<uint32_t> localip;
   uint32_t *d_localip = nullptr;
+  uint8_t *d_zero = nullptr;                   // 64 zero bytes: stand-in in_port / ct_status
   bool interactive = true;                     // Iptables.h:181
   bool has_device = false;
   int num_cus = 256;
@@ -224,6 +225,8 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
       hip_check(hipGetDeviceProperties(&prop, cfg->device), "hipGetDeviceProperties");
       ctx->num_cus = prop.multiProcessorCount;
       hip_check(hipMalloc(&ctx->d_localip, PCN_MAX_LOCALIP * 4), "hipMalloc(localip)");
+      hip_check(hipMalloc(&ctx->d_zero, 64), "hipMalloc(zero cell)");
+      hip_check(hipMemset(ctx->d_zero, 0, 64), "hipMemset(zero cell)");
       for (auto &cs : ctx->chains) {
         hip_check(hipMalloc(&cs.ctr, ctx->ctr_words * 8), "hipMalloc(counters)");
         hip_check(hipMemset(cs.ctr, 0, ctx->ctr_words * 8), "hipMemset(counters)");
@@ -255,6 +258,7 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
       if (cs.gather) (void)hipFree(cs.gather);
     }
     if (ctx->d_localip) (void)hipFree(ctx->d_localip);
+    if (ctx->d_zero) (void)hipFree(ctx->d_zero);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
   }
   delete ctx;
@@ -480,23 +484,32 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       else a.ch[c].lds_bins = -1;
     }
     a.nbins = base;
-    if (kLdsDescBytes + img_bytes + a.nbins * 16 <= kLdsBudget) {
+    a.nlocal = static_cast<uint32_t>(ctx->localip.size());
+    const uint32_t tail = (a.nbins * 8 + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
+                          (PCN_BLOCK / 64) * PCN_WAVE_SCRATCH_BYTES;   // bins + localip + scratch
+    if (kLdsDescBytes + img_bytes + tail <= kLdsBudget) {
       a.lds_images_bytes = img_bytes;
       a.bins_offset = kLdsDescBytes + img_bytes;
     } else {
       a.lds_images_bytes = 0;
       a.bins_offset = kLdsDescBytes;
     }
+    a.lds_localip = a.bins_offset + (a.nbins * 8 + 15) / 16 * 16;
+    a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
+    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * PCN_WAVE_SCRATCH_BYTES;
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
     a.offsets = b->offsets;
     a.lens = b->lens;
-    a.in_port = b->in_port;
-    a.ct_status = b->ct_status;
+    a.has_in_port = b->in_port != nullptr;
+    a.has_ct = b->ct_status != nullptr;
+    a.in_port = a.has_in_port ? b->in_port : reinterpret_cast<const uint16_t *>(ctx->d_zero);
+    a.ct_status = a.has_ct ? b->ct_status : ctx->d_zero;
+    a.in_port_mask = a.has_in_port ? ~uint64_t(0) : 0;
+    a.ct_mask = a.has_ct ? ~uint64_t(0) : 0;
     a.verdicts = b->verdicts;
     a.rule_ids = b->rule_ids;
     a.localip = ctx->d_localip;
-    a.nlocal = static_cast<uint32_t>(ctx->localip.size());
     a.n = b->n;
     a.stride = b->stride;
     a.fixed_len = b->fixed_len;

@@ -13,7 +13,7 @@ from polycube_amd import ffi
 
 LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_shift0", "ip_shift1", "ip_bnd0", "ip_bnd1", "ip_cls0", "ip_cls1",
           "hash0", "hash1", "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "proto", "flags", "ct",
-          "summ", "full", "pbase", "part", "part_wide", "pool", "zero", "perm"]
+          "sf", "pbase", "part", "part_wide", "pool", "zero", "perm"]
 MISS = 0xFFFF
 EMPTY = 0xFFFFFFFF
 
@@ -99,16 +99,16 @@ class ImageModel:
             m = (1 << 64) - 1 if live >= 64 else (1 << live) - 1
             recs = [c * self.nsw + k for c in cls]
             for r in recs:
-                m &= self.u64(L["summ"] + 8 * r)
+                m &= self.u64(L["sf"] + 16 * r)
             while m:
                 bit = (m & -m).bit_length() - 1
                 m &= m - 1
                 acc = (1 << 64) - 1
                 for r in recs:
-                    fm = self.u64(L["full"] + 8 * r)
+                    fm = self.u64(L["sf"] + 16 * r + 8)
                     if fm >> bit & 1:
                         continue
-                    part = self.u64(L["summ"] + 8 * r) & ~fm
+                    part = self.u64(L["sf"] + 16 * r) & ~fm
                     rank = bin(part & ((1 << bit) - 1)).count("1")
                     j = self.u32(L["pbase"] + 4 * r) + rank
                     q = self.u32(L["part"] + 4 * j) if L["part_wide"] else self.u16(L["part"] + 2 * j)

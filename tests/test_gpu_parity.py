@@ -246,3 +246,42 @@ def test_rccl_single_rank_counter_sync(dev):
     torch.cuda.synchronize()
     fw = ipt.chain("FORWARD")
     assert fw.read_counters(128, scope=1) == fw.read_counters(128, scope=0)
+
+
+def test_u32_bins_split_launch_counts_exactly(dev):
+    """2^26 jumbo-length frames (lens 65535) all hitting one rule: the per-
+    workgroup u32 byte bins would wrap, so the launch is split; every counter
+    must still come out exact (n pkts, n * 65535 bytes)."""
+    rules = [{"dst": "10.1.0.0/16", "l4proto": "UDP", "dport": 53, "action": "ACCEPT"},
+             {"src": "192.0.2.0/24", "action": "DROP"}]
+    o, ipt = make_pair({1: rules}, {1: "DROP"})
+    one = synth.build_frames(np.array([0xC0000201], np.uint32), np.array([0x0A010203], np.uint32),
+                             np.array([17]), np.array([4000]), np.array([53]), np.array([0]),
+                             frame_len=64).reshape(-1)
+    n = 1 << 26
+    frames = torch.from_numpy(one).to(dev)
+    offsets = torch.zeros(n, dtype=torch.int32, device=dev)
+    lens = torch.full((n,), -1, dtype=torch.int16, device=dev)      # 65535 as u16
+    v, r = ipt.classify(frames, n=n, offsets=offsets, lens=lens)
+    torch.cuda.synchronize()
+    assert int((r == 0).sum()) == n and int((v == 1).sum()) == n
+    pk, by, dp, db = ipt.chain("FORWARD").read_counters(2)
+    assert pk == [n, 0] and by == [n * 65535, 0] and dp == 0 and db == 0
+    del offsets, lens, v, r
+
+
+def test_localip_input_output_from_lds(dev):
+    """INPUT/OUTPUT selection by a 200-address localip set staged in LDS."""
+    rs = synth.config_rules(2)
+    rules = rs.rules()
+    rng = np.random.default_rng(11)
+    n = 1 << 16
+    frames = synth.config_frames(2, n, rs).reshape(n, 64)
+    dsts = frames[:, 30:34].copy().view(">u4").reshape(-1)
+    local = sorted({int(synth.ip_nbo(int(x))) for x in rng.choice(dsts, 200, replace=False)})
+    o, ipt = make_pair({0: rules[:64], 1: rules[64:], 2: rules[::2]}, {0: "DROP", 1: "ACCEPT", 2: "DROP"},
+                       localip=local)
+    for direction in (0, 1):
+        v_o, r_o, v_g, r_g = run_both(o, ipt, dev, frames.reshape(-1), n, direction=direction)
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_counters(o, ipt)
