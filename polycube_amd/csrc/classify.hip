@@ -31,6 +31,9 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #ifndef PCN_ABLATE
 #define PCN_ABLATE 0
 #endif
+#ifndef PCN_PREFETCH
+#define PCN_PREFETCH 1   // frames per lane in flight ahead of the one being classified
+#endif
 // Tuning switches (tools/ablate.py builds experiment variants with -D...).
 
 namespace pcn {
@@ -58,6 +61,10 @@ struct Tab {
     return LDS ? *reinterpret_cast<const uint16_t *>(pcn_smem + base + off)
                : *reinterpret_cast<const uint16_t *>(g + off);
   }
+  __device__ __forceinline__ uint32_t u8(uint32_t off) const {
+    return LDS ? *reinterpret_cast<const uint8_t *>(pcn_smem + base + off)
+               : *reinterpret_cast<const uint8_t *>(g + off);
+  }
   __device__ __forceinline__ uint64_t u64(uint32_t off) const {
     return LDS ? *reinterpret_cast<const uint64_t *>(pcn_smem + base + off)
                : *reinterpret_cast<const uint64_t *>(g + off);
@@ -67,12 +74,15 @@ struct Tab {
 // 48-byte header window as 12 little-endian dwords.
 struct Hdr { uint32_t w[12]; };
 
+// Fixed-stride frame: bytes 12..47 (ethertype .. TCP flags); the MAC
+// addresses (w0..w2) are never read.
 __device__ __forceinline__ void load_fixed(const uint8_t *frame, Hdr &h) {
   const u32x4 *p = reinterpret_cast<const u32x4 *>(frame);
-  u32x4 a = __builtin_nontemporal_load(p + 0);
+  const uint32_t w3 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(frame) + 3);
   u32x4 b = __builtin_nontemporal_load(p + 1);
   u32x4 c = __builtin_nontemporal_load(p + 2);
-  h.w[0] = a.x; h.w[1] = a.y; h.w[2] = a.z; h.w[3] = a.w;
+  h.w[0] = h.w[1] = h.w[2] = 0;
+  h.w[3] = w3;
   h.w[4] = b.x; h.w[5] = b.y; h.w[6] = b.z; h.w[7] = b.w;
   h.w[8] = c.x; h.w[9] = c.y; h.w[10] = c.z; h.w[11] = c.w;
 }
@@ -118,32 +128,34 @@ __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
   return false;
 }
 
-// Kernel-LPM answer for a host-order address: bucket index on the top 12 bits,
-// then a binary search among the few boundaries inside the bucket.
+// Kernel-LPM answer for a host-order address: the bucket on the top address
+// bits gives the boundaries inside it, then a branchless upper-bound search
+// of `steps` (wave-uniform) probes finds the interval.
 template <bool LDS>
-__device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t shift, uint32_t bnd,
-                                             uint32_t cls, uint32_t h) {
+__device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t shift, uint32_t steps,
+                                             uint32_t bnd, uint32_t cls, uint32_t h) {
   const uint32_t e = t.u32(bkt + 4 * (h >> shift));
-  if (e & PCN_IP_LEAF) return e & 0xFFFFu;   // no boundary inside this bucket
   uint32_t lo = e & 0xFFFFu;
-  uint32_t hi = lo + (e >> 16);
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (t.u32(bnd + 4 * mid) <= h) lo = mid + 1; else hi = mid;
+  const uint32_t end = lo + (e >> 16);
+  for (uint32_t k = steps; k-- > 0;) {
+    const uint32_t probe = lo + (1u << k);          // candidate: bnd[lo .. probe) all <= h
+    const uint32_t idx = (probe <= end ? probe : lo + 1) - 1;
+    const bool ok = probe <= end && t.u32(bnd + 4 * idx) <= h;
+    lo = ok ? probe : lo;
   }
   return t.u16(cls + 2 * lo);
 }
 
+// Port / iface hash: the key is in its home slot or the next one (the image
+// builder guarantees it), so two adjacent reads decide without a loop.
 template <bool LDS>
 __device__ __forceinline__ uint32_t key_class(const Tab<LDS> &t, uint32_t tab, uint32_t mask, uint32_t wild,
                                               uint32_t key) {
-  uint32_t h = (key * kHashMul) >> __builtin_clz(mask);
-  while (true) {
-    uint32_t e = t.u32(tab + 4 * h);
-    if (e == PCN_HASH_EMPTY) return wild;
-    if ((e >> 16) == key) return e & 0xffff;
-    h = (h + 1) & mask;
-  }
+  const uint32_t h = (key * kHashMul) >> __builtin_clz(mask);
+  const uint32_t e0 = t.u32(tab + 4 * h), e1 = t.u32(tab + 4 * h + 4);
+  const bool m0 = e0 != PCN_HASH_EMPTY && (e0 >> 16) == key;
+  const bool m1 = e1 != PCN_HASH_EMPTY && (e1 >> 16) == key;
+  return m0 ? (e0 & 0xffff) : (m1 ? (e1 & 0xffff) : wild);
 }
 
 struct Parsed {
@@ -153,51 +165,56 @@ struct Parsed {
 };
 
 // ---- rule-chain stage, part 1 (per lane) ----
-// Maps every field to its class.  Returns true when the packet needs the
-// candidate stage; otherwise the verdict is decided here (a field without a
-// class takes the default action, a bad conntrack label drops).  Every field
-// has a fixed slot; absent or skipped fields hold the all-ones class.
-template <bool LDS>
-__device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &p, uint32_t port, uint32_t cls[8],
+// Maps the packet to its NS slot classes: 0 = META (proto x tcpflags x
+// conntrack, and iface when the chain merged it), 1/2 = IP src/dst, 3/4 =
+// sport/dport, 5 = iface (NS == 6 only).  Returns true when the packet needs
+// the candidate stage; otherwise the verdict is decided here (a field without
+// an entry takes the default action, a bad conntrack label drops).  Absent or
+// skipped fields contribute the all-ones vector.
+template <bool LDS, int NS>
+__device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &p, uint32_t port, uint32_t cls[NS],
                                               uint32_t &verdict, int32_t &rid) {
   const Tab<LDS> t{ch.image, ch.lds_image};
   const TableLayout &lay = ch.lay;
   const uint32_t present = ch.present;
   const uint32_t all = ch.all_cls;
 #pragma unroll
-  for (int f = 0; f < 8; ++f) cls[f] = all;
+  for (int f = 1; f < NS; ++f) cls[f] = all;
+  uint32_t pi = 0, fi = 0, ci = 0, ii = 0;
   if (present & (1u << PCN_IPT_F_CONNTRACK)) {
     if (p.ct > 3) { rid = PCN_IPT_RID_NOCHAIN; verdict = PCN_IPT_DROP; return false; }   // array miss => RX_DROP
-    cls[0] = t.u16(lay.ct + 2 * p.ct);
+    ci = t.u8(lay.ct_idx + p.ct);
   }
+  if (present & (1u << PCN_IPT_F_L4PROTO)) pi = t.u8(lay.proto_idx + p.proto);
+  if (present & (1u << PCN_IPT_F_TCPFLAGS))                        // TcpFlagsLookup_dp.c:93-97
+    fi = p.proto == 6 ? t.u16(lay.flags_idx + 2 * p.flags) : lay.flags_skip;
+  if (present & (1u << PCN_IPT_F_IFACE)) {
+    const uint32_t x = key_class(t, lay.hash[2], lay.hash_mask[2], lay.hash_wild[2], port);
+    if (NS == 6 && !lay.iface_merged) cls[NS - 1] = x;
+    else ii = x;
+  }
+  cls[0] = t.u16(lay.meta + 2 * (((pi * lay.meta_nf + fi) * lay.meta_nc + ci) * lay.meta_ni + ii));
   if (present & (1u << PCN_IPT_F_IPSRC))
-    cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_shift[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
+    cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_shift[0], lay.ip_steps[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
   if (present & (1u << PCN_IPT_F_IPDST))
-    cls[2] = ip_class(t, lay.ip_bkt[1], lay.ip_shift[1], lay.ip_bnd[1], lay.ip_cls[1], __builtin_bswap32(p.daddr));
-  if (present & (1u << PCN_IPT_F_L4PROTO)) cls[3] = t.u16(lay.proto + 2 * p.proto);
+    cls[2] = ip_class(t, lay.ip_bkt[1], lay.ip_shift[1], lay.ip_steps[1], lay.ip_bnd[1], lay.ip_cls[1], __builtin_bswap32(p.daddr));
   const bool l4 = p.proto == 6 || p.proto == 17;                    // L4PortLookup_dp.c:99-103
   if (present & (1u << PCN_IPT_F_SPORT)) {
     uint32_t c = key_class(t, lay.hash[0], lay.hash_mask[0], lay.hash_wild[0], p.sport);
-    cls[4] = l4 ? c : all;
+    cls[3] = l4 ? c : all;
   }
   if (present & (1u << PCN_IPT_F_DPORT)) {
     uint32_t c = key_class(t, lay.hash[1], lay.hash_mask[1], lay.hash_wild[1], p.dport);
-    cls[5] = l4 ? c : all;
-  }
-  if (present & (1u << PCN_IPT_F_IFACE))
-    cls[6] = key_class(t, lay.hash[2], lay.hash_mask[2], lay.hash_wild[2], port);
-  if (present & (1u << PCN_IPT_F_TCPFLAGS)) {                      // TcpFlagsLookup_dp.c:93-97
-    uint32_t c = t.u16(lay.flags + 2 * p.flags);
-    cls[7] = p.proto == 6 ? c : all;
+    cls[4] = l4 ? c : all;
   }
   bool miss = false;
 #pragma unroll
-  for (int f = 0; f < 8; ++f) miss |= cls[f] == PCN_CLS_MISS;
+  for (int f = 0; f < NS; ++f) miss |= cls[f] == PCN_CLS_MISS;
   if (miss) { rid = PCN_IPT_RID_DEFAULT; verdict = static_cast<uint32_t>(ch.default_action); return false; }
   if (PCN_ABLATE == 2) {   // keep the lookups alive: the verdict depends on them
     uint32_t x = 0;
 #pragma unroll
-    for (int f = 0; f < 8; ++f) x ^= cls[f];
+    for (int f = 0; f < NS; ++f) x ^= cls[f];
     rid = PCN_IPT_RID_DEFAULT;
     verdict = x & 1;
     return false;
@@ -220,40 +237,45 @@ static_assert(sizeof(WaveScratch) == PCN_WAVE_SCRATCH_BYTES, "host sizes the scr
 // wave hostage: each worker re-reads its owner's class records, ANDs the
 // partial words of its one word and folds the matched entry into the
 // owner's slot with an LDS atomic min.  Returns the owner's best entry.
-template <bool LDS>
-__device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[8],
+template <bool LDS, int NS>
+__device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[NS],
                                                      WaveScratch *ws) {
   const uint32_t lane = __lane_id();
   if (__ballot(active) == 0) return kNoRule;
   const Tab<LDS> t{ch.image, ch.lds_image};
   const TableLayout &lay = ch.lay;
   const uint32_t nrw = ch.nrw, nsw = ch.nsw;
-  ws->best[lane] = kNoRule;
-  ws->cls[lane][0] = cls[0] | (cls[1] << 16);
-  ws->cls[lane][1] = cls[2] | (cls[3] << 16);
-  ws->cls[lane][2] = cls[4] | (cls[5] << 16);
-  ws->cls[lane][3] = cls[6] | (cls[7] << 16);
+  bool staged = false;  // class rows / best slots written (only once some lane has a candidate)
   uint64_t mseen = 0;   // PCN_ABLATE == 3 only
   for (uint32_t k = 0; k < nsw; ++k) {
     const uint32_t live = nrw - k * 64;
     uint64_t m = 0;
     if (active) {
       m = live >= 64 ? ~0ull : ((1ull << live) - 1);
-      uint64_t sm[8];
+      uint64_t sm[NS];
 #pragma unroll
-          for (int f = 0; f < 8; ++f) sm[f] = t.u64(lay.sf + 16 * (cls[f] * nsw + k));
+      for (int f = 0; f < NS; ++f) sm[f] = t.u64(lay.sf + 16 * (cls[f] * nsw + k));
 #pragma unroll
-      for (int f = 0; f < 8; ++f) m &= sm[f];
+      for (int f = 0; f < NS; ++f) m &= sm[f];
     }
     if (PCN_ABLATE == 3) { mseen |= m; continue; }
-    // exclusive prefix of the per-lane candidate counts (bit-sliced ballots)
+    // exclusive prefix of the per-lane candidate counts (bit-sliced ballots,
+    // as many slices as the largest count needs)
     const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(m));
     uint32_t pos = 0, total = 0;
-#pragma unroll
-    for (int b = 0; b < 7; ++b) {
+    for (uint32_t b = 0; b < 7; ++b) {
       const uint64_t bm = __ballot((c >> b) & 1);
       pos += static_cast<uint32_t>(__builtin_popcountll(bm & ((1ull << lane) - 1))) << b;
       total += static_cast<uint32_t>(__builtin_popcountll(bm)) << b;
+      if (__ballot(c >> (b + 1)) == 0) break;
+    }
+    if (total == 0) continue;
+    if (!staged) {
+      staged = true;
+      ws->best[lane] = kNoRule;
+#pragma unroll
+      for (int f = 0; f < NS; f += 2)
+        ws->cls[lane][f / 2] = cls[f] | ((f + 1 < NS ? cls[f + 1] : 0u) << 16);
     }
     for (uint32_t done = 0; done < total; done += 64) {
       // deal: each owner writes its candidates that fall in [done, done + 64)
@@ -269,17 +291,16 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
         const uint32_t it = ws->item[lane];
         const uint32_t owner = it >> 8, bit = it & 63;
         const uint64_t below = (1ull << bit) - 1;
-        const uint32_t r0 = ws->cls[owner][0], r1 = ws->cls[owner][1], r2 = ws->cls[owner][2],
-                       r3 = ws->cls[owner][3];
-        const uint32_t oc[8] = {r0 & 0xffff, r0 >> 16, r1 & 0xffff, r1 >> 16,
-                                r2 & 0xffff, r2 >> 16, r3 & 0xffff, r3 >> 16};
+        uint32_t oc[NS];
+#pragma unroll
+        for (int f = 0; f < NS; ++f) oc[f] = (ws->cls[owner][f / 2] >> (16 * (f & 1))) & 0xffff;
         // At a candidate word every field's summary bit is set, so a field is
         // PARTIAL there iff its FULL bit is clear.  Straight-line on purpose:
         // every index read, then every pool read, issue back to back.  A FULL
         // field reads the zero cell, i.e. POOL[0], the all-ones word.
-        uint32_t q[8];
+        uint32_t q[NS];
 #pragma unroll
-        for (int f = 0; f < 8; ++f) {
+        for (int f = 0; f < NS; ++f) {
           const uint32_t rec = oc[f] * nsw + k;
           const u32x4 r = LDS ? *reinterpret_cast<const u32x4 *>(pcn_smem + ch.lds_image + lay.sf + 16 * rec)
                               : *reinterpret_cast<const u32x4 *>(ch.image + lay.sf + 16 * rec);
@@ -292,7 +313,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
         }
         uint64_t acc = ~0ull;
 #pragma unroll
-        for (int f = 0; f < 8; ++f) acc &= t.u64(lay.pool + 8 * q[f]);
+        for (int f = 0; f < NS; ++f) acc &= t.u64(lay.pool + 8 * q[f]);
         if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
           const uint32_t w = k * 64 + bit;
           const uint32_t e = t.u16(lay.perm + 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
@@ -305,7 +326,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     }
   }
   if (PCN_ABLATE == 3) return mseen ? 0u : kNoRule;
-  return ws->best[lane];
+  return staged ? ws->best[lane] : kNoRule;
 }
 
 // ---- rule-chain stage, part 3 (per lane) ----
@@ -319,17 +340,17 @@ __device__ __forceinline__ uint32_t chain_finish(const DevChain &ch, uint32_t be
 
 // One chain through the three parts; `mine` = lanes whose packet runs it.
 // Called with the wave converged.
-template <bool LDS>
+template <bool LDS, int NS>
 __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const Parsed &p, uint32_t port,
                                           WaveScratch *ws, uint32_t &verdict, int32_t &rid) {
-  uint32_t cls[8];
+  uint32_t cls[NS];
   bool need = false;
-  if (mine) need = chain_classes<LDS>(ch, p, port, cls, verdict, rid);
-  const uint32_t best = chain_candidates<LDS>(ch, need, cls, ws);
+  if (mine) need = chain_classes<LDS, NS>(ch, p, port, cls, verdict, rid);
+  const uint32_t best = chain_candidates<LDS, NS>(ch, need, cls, ws);
   if (need) verdict = chain_finish(ch, best, rid);
 }
 
-template <bool FIXED, bool LDS, int CH>
+template <bool FIXED, bool LDS, int CH, int NS>
 __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
   // frames per workgroup so neither can wrap; the flush widens to u64)
@@ -362,27 +383,78 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   const uint64_t last = a.n - 1;
   // in_port / ct_status ride along with the header: when the batch has none
   // the host points them at a zero cell with a zero index mask, so the loads
-  // stay unconditional too.
-  Hdr nh;
-  uint32_t nL = a.fixed_len, nport, nct;
-  auto prefetch = [&](uint64_t j) {
-    load_header<FIXED>(a, j, nh, nL);
-    nport = a.in_port[j & a.in_port_mask];
-    nct = a.ct_status[j & a.ct_mask];
+  // stay unconditional too.  PCN_PREFETCH frames per lane are in flight.
+  // Fixed-stride frames are fetched coalesced: a wave's 64 frames are 192
+  // 16-byte chunks (bytes 0..47 of each frame), chunk t = 64q + lane is loaded
+  // by instruction q of that lane, and the chunks are transposed through a
+  // 3 KB per-wave LDS buffer into one header per lane.  Each instruction then
+  // touches ~11 cache lines instead of 32.
+  struct Stage {
+    Hdr h;          // generic path
+    u32x4 c[3];     // fixed path: this lane's three chunks
+    uint32_t L, port, ct;
   };
-  prefetch(first < a.n ? first : last);
-  for (uint64_t i = first; i < n_round; i += step) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t cf[3], co[3];   // fixed path: frame within the wave's group, byte offset of the chunk
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint32_t t = 64 * q + lane;
+    cf[q] = t / 3;
+    co[q] = 16 * (t - 3 * cf[q]);
+  }
+  u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_hdr) + (threadIdx.x >> 6) * 192;
+  Stage st[PCN_PREFETCH];
+  auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
+    if (FIXED) {
+      const uint64_t group = j - lane;           // wave-uniform
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        uint64_t f = group + cf[q];
+        f = f < a.n ? f : last;
+        x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]));
+      }
+    } else {
+      x.L = a.fixed_len;
+      load_header<FIXED>(a, j < a.n ? j : last, x.h, x.L);
+    }
+    const uint64_t jc = j < a.n ? j : last;
+    x.port = a.in_port[jc & a.in_port_mask];
+    x.ct = a.ct_status[jc & a.ct_mask];
+  };
+#pragma unroll
+  for (int d = 0; d < PCN_PREFETCH; ++d) prefetch(st[d], first + d * step);
+  // Stage d always holds the frames i with (i - first) / step == d (mod
+  // PCN_PREFETCH): the loop is unrolled PCN_PREFETCH times so no stage is
+  // ever copied (a register move of an in-flight load waits for it).
+  auto process = [&](const uint64_t i, Stage &cur) {
     const bool valid = i < a.n;
     // Pin every prefetched dword (used or not) until here, so no register the
     // load writes is recycled mid-iteration (a WAW hazard costs a vmcnt wait).
+    Hdr h;
+    if (FIXED) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(nh.w[k]));
-    asm volatile("" : "+v"(nport), "+v"(nct));
-    const Hdr h = nh;
-    const uint32_t L = FIXED ? a.fixed_len : nL;
-    const uint32_t cur_port = nport, cur_ct = nct;
-    const uint64_t next = i + step;
-    prefetch(next < a.n ? next : last);
+      for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
+#pragma unroll
+      for (int q = 0; q < 3; ++q) hbuf[64 * q + lane] = cur.c[q];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const u32x4 c0 = hbuf[3 * lane], c1 = hbuf[3 * lane + 1], c2 = hbuf[3 * lane + 2];
+      h.w[0] = c0.x; h.w[1] = c0.y; h.w[2] = c0.z; h.w[3] = c0.w;
+      h.w[4] = c1.x; h.w[5] = c1.y; h.w[6] = c1.z; h.w[7] = c1.w;
+      h.w[8] = c2.x; h.w[9] = c2.y; h.w[10] = c2.z; h.w[11] = c2.w;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(cur.h.w[k]));
+      h = cur.h;
+    }
+    asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
+    const uint32_t L = FIXED ? a.fixed_len : cur.L;
+    const uint32_t cur_port = cur.port, cur_ct = cur.ct;
+    prefetch(cur, i + PCN_PREFETCH * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
     int32_t cchain = -1;    // chain whose counters this packet bumps
@@ -456,15 +528,15 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
     if (CH < 3) {
-      run_chain<LDS>(a.ch[CH < 3 ? CH : 0], chain >= 0, p, port, ws, verdict, rid);
+      run_chain<LDS, NS>(a.ch[CH < 3 ? CH : 0], chain >= 0, p, port, ws, verdict, rid);
       if (chain >= 0) cchain = chain;
     } else {
       if (__ballot(chain == PCN_IPT_FORWARD)) {
-        run_chain<LDS>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, verdict, rid);
+        run_chain<LDS, NS>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, verdict, rid);
         if (chain == PCN_IPT_FORWARD) cchain = PCN_IPT_FORWARD;
       }
       if (__ballot(chain == PCN_IPT_INPUT)) {
-        run_chain<LDS>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, verdict, rid);
+        run_chain<LDS, NS>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, verdict, rid);
         if (chain == PCN_IPT_INPUT) cchain = PCN_IPT_INPUT;
       }
     }
@@ -473,9 +545,10 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
       if (a.rule_ids) a.rule_ids[i] = rid;
     }
     // ---- counters ----
-    if (PCN_ABLATE == 4) continue;
+    if (PCN_ABLATE == 4) return;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
+      if (!((a.count_mask >> c) & 1)) continue;   // chain unreachable in this launch
       // default bins: wave-aggregated per chain
       const bool mine = valid && cchain == c && rid == PCN_IPT_RID_DEFAULT;
       const uint64_t m = __ballot(mine);
@@ -508,6 +581,11 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
         }
       }
     }
+  };
+  for (uint64_t i = first; i < n_round; i += PCN_PREFETCH * step) {
+#pragma unroll
+    for (int d = 0; d < PCN_PREFETCH; ++d)
+      if (d == 0 || i + d * step < n_round) process(i + d * step, st[d]);
   }
   __syncthreads();
   // ---- flush the workgroup histogram ----
@@ -533,21 +611,27 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   }
 }
 
-template <bool FIXED, bool LDS>
+template <bool FIXED, bool LDS, int NS>
 void launch_variant(const LaunchArgs &a, int ch, unsigned grid, size_t lds, hipStream_t stream) {
   switch (ch) {
-    case 0: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 0>), dim3(grid), dim3(kBlock), lds, stream, a); break;
-    case 1: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 1>), dim3(grid), dim3(kBlock), lds, stream, a); break;
-    case 2: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 2>), dim3(grid), dim3(kBlock), lds, stream, a); break;
-    default: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 3>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+    case 0: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 0, NS>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+    case 1: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 1, NS>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+    case 2: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 2, NS>), dim3(grid), dim3(kBlock), lds, stream, a); break;
+    default: hipLaunchKernelGGL((classify_kernel<FIXED, LDS, 3, NS>), dim3(grid), dim3(kBlock), lds, stream, a); break;
   }
+}
+
+template <bool FIXED, bool LDS>
+void launch_ns(const LaunchArgs &a, int ch, int ns, unsigned grid, size_t lds, hipStream_t stream) {
+  if (ns == 5) launch_variant<FIXED, LDS, 5>(a, ch, grid, lds, stream);
+  else launch_variant<FIXED, LDS, 6>(a, ch, grid, lds, stream);
 }
 
 }  // namespace
 
 // Host-side launcher (called from pcn_ipt.cpp).  `ch` is the only chain that can
 // reach the rule stage (0..2) or 3 for INPUT+FORWARD.  Returns a hipError_t.
-int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStream_t stream) {
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   const size_t lds = a.lds_bytes;
   const bool in_lds = a.lds_images_bytes > 0;
@@ -561,7 +645,8 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStr
   // u32 histogram bins: at most 2^32-1 bytes per workgroup per launch, so a
   // batch whose workgroups could exceed that is split into launches.
   const uint64_t max_len = a.lens ? 65535u : (a.fixed_len ? a.fixed_len : 1u);
-  const uint64_t per_block = 0xFFFFFFFFull / max_len;
+  // (a workgroup takes whole kBlock-frame rows of the grid stride)
+  const uint64_t per_block = 0xFFFFFFFFull / max_len / kBlock * kBlock;
   const uint64_t chunk = per_block * grid;
   for (uint64_t base = 0; base < a.n; base += chunk) {
     LaunchArgs c = a;
@@ -575,10 +660,10 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStr
       c.verdicts = a.verdicts + base;
       if (a.rule_ids) c.rule_ids = a.rule_ids + base;
     }
-    if (fixed && in_lds) launch_variant<true, true>(c, ch, grid, lds, stream);
-    else if (fixed) launch_variant<true, false>(c, ch, grid, lds, stream);
-    else if (in_lds) launch_variant<false, true>(c, ch, grid, lds, stream);
-    else launch_variant<false, false>(c, ch, grid, lds, stream);
+    if (fixed && in_lds) launch_ns<true, true>(c, ch, ns, grid, lds, stream);
+    else if (fixed) launch_ns<true, false>(c, ch, ns, grid, lds, stream);
+    else if (in_lds) launch_ns<false, true>(c, ch, ns, grid, lds, stream);
+    else launch_ns<false, false>(c, ch, ns, grid, lds, stream);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
   }

@@ -7,11 +7,13 @@
 // 1k rules) that each workgroup copies into LDS, so the per-packet path makes
 // no dependent HBM/L2 access at all:
 //   - IP src/dst: the kernel-LPM answer as sorted interval boundaries plus a
-//     bucket index on the top address bits (2^4..2^12 buckets, sized to the
-//     boundary count; a bucket no boundary falls into holds its class);
+//     bucket index on the top address bits (2^4..2^12 buckets, sized so a
+//     bucket holds few boundaries) searched in a fixed number of steps;
 //   - sport/dport/iface: open-addressing hashes {key -> class} with the
 //     wildcard class (key 0 / 0xffff) as the miss fallback;
-//   - proto/tcpflags/conntrack: 256/256/4-entry class tables;
+//   - proto/tcpflags/conntrack (and iface while small) share one META slot:
+//     each maps its value to a small index and a 4-D table holds the class of
+//     the AND of their vectors;
 //   - per class and 64-word block: SUMM (bit w: word w of the class vector
 //     != 0), FULL (bit w: word w holds all of its rules) and PBASE, the start
 //     of the class's PARTIAL words (neither zero nor full) in PART, stored in
@@ -33,26 +35,32 @@
 #define PCN_CLS_MISS 0xFFFFu
 #define PCN_MAX_LOCALIP 256
 #define PCN_IP_BUCKET_BITS_MAX 12
-#define PCN_IP_LEAF 0x80000000u
 #define PCN_HASH_EMPTY 0xFFFFFFFFu
 #ifndef PCN_BLOCK
-#define PCN_BLOCK 512               // classify workgroup size (threads)
+#define PCN_BLOCK 1024              // classify workgroup size (threads): one per CU
 #endif
 #define PCN_WAVE_SCRATCH_BYTES 1536 // per-wave LDS scratch of the candidate stage
+#define PCN_WAVE_HDR_BYTES 3072     // per-wave LDS header transpose buffer (64 frames x 48 B)
 
 namespace pcn {
 
 // Byte offsets inside a table image (all 16-byte aligned).
 struct TableLayout {
   uint32_t bytes;
-  uint32_t ip_bkt[2];      // u32[1 << (32 - ip_shift)]: LEAF|class, or (count << 16) | first boundary
+  uint32_t ip_bkt[2];      // u32[1 << (32 - ip_shift)]: (count << 16) | first boundary in the bucket
   uint32_t ip_shift[2];    // bucket = address >> ip_shift
+  uint32_t ip_steps[2];    // branchless search steps: every bucket holds < 2^steps boundaries
   uint32_t ip_bnd[2];      // u32[m]: interval boundaries (host-order addresses)
   uint32_t ip_cls[2];      // u16[m+1]: class of each interval
-  uint32_t hash[3];        // u32[size]: (key << 16) | class  (sport, dport, iface)
+  uint32_t hash[3];        // u32[size + 1]: (key << 16) | class (sport, dport, iface); every key
+                           // sits in its home slot or the next; slot size mirrors slot 0
   uint32_t hash_mask[3];   // size - 1
   uint32_t hash_wild[3];   // class used when the key is absent (PCN_CLS_MISS: none)
-  uint32_t proto, flags, ct;   // u16[256], u16[256], u16[4]
+  uint32_t proto_idx, flags_idx, ct_idx;   // u8[256], u16[256], u8[4]: value -> meta index
+  uint32_t flags_skip;     // flags index of a non-TCP packet (the module is skipped)
+  uint32_t meta;           // u16[np][nf][nc][ni]: class of the meta slot
+  uint32_t meta_nf, meta_nc, meta_ni;
+  uint32_t iface_merged;   // iface hash holds meta indices (else classes, own slot)
   uint32_t sf;             // u64x2[nvec][nsw]: {SUMM, FULL}
   uint32_t pbase;          // u32[nvec][nsw]: first PART index of the class's block
   uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
@@ -74,7 +82,7 @@ struct DevChain {
   int32_t lds_bins;              // first LDS counter bin of this chain's rules; -1 => global atomics
 };
 
-// LDS layout of a classify workgroup: [chain images][counter bins (u32 x2)][localip][wave scratch]
+// LDS layout of a classify workgroup: [chain images][counter bins (u32 x2)][localip][wave scratch][header buffers]
 constexpr uint32_t kLdsDescBytes = 0;
 
 struct LaunchArgs {
@@ -98,12 +106,14 @@ struct LaunchArgs {
   uint32_t lds_images_bytes;     // bytes of chain images staged in LDS (0: read from HBM)
   uint32_t lds_localip;          // byte offset of the staged localip table in LDS
   uint32_t lds_scratch;          // byte offset of the per-wave candidate scratch in LDS
+  uint32_t lds_hdr;              // byte offset of the per-wave header transpose buffers
   uint32_t lds_bytes;            // dynamic LDS per workgroup
   uint16_t const_in_port;
   uint16_t direction;
   uint32_t allow_logic;          // _INGRESS_ALLOWLOGIC (modules/ChainSelector.cpp:190-202)
   uint32_t empty_mask;           // bit c: chain c has no rules (ChainSelector default path)
   uint32_t drop_mask;            // bit c: chain c's default action is DROP
+  uint32_t count_mask;           // bit c: packets of this launch can select chain c
 };
 
 }  // namespace pcn

@@ -15,6 +15,7 @@ constexpr size_t kAlign = 16;
 constexpr uint32_t kTrieCapacity = 1024;   // Iptables_IpLookup_dp.c:54-55
 constexpr size_t kGroupAlignMin = 8;       // densest packing: smaller type groups share words
 constexpr uint32_t kHashMul = 0x9E3779B1u;
+constexpr size_t kMetaMaxEntries = 8192;   // iface joins the meta slot while the table stays this small
 
 inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
 inline uint32_t prefix_mask(uint8_t len) { return len == 0 ? 0u : ~uint32_t(0) << (32 - len); }
@@ -217,79 +218,167 @@ HostImage build_image(const ChainTables &t) {
     Intervals iv = lpm_intervals(m);
     std::vector<uint16_t> cls;
     for (int32_t c : iv.cls) cls.push_back(c < 0 ? PCN_CLS_MISS : pool.intern(m.vecs[c]));
-    // bucket entry: PCN_IP_LEAF | class when no boundary falls inside the
-    // bucket (one LDS read answers), else (count << 16) | first boundary index.
-    // About two buckets per boundary: 2^4 .. 2^12 buckets.
+    // Bucket entry (count << 16) | first: the boundaries inside the bucket
+    // are bnd[first, first + count).  The kernel runs a branchless upper-bound
+    // search of ip_steps[side] steps (a wave-uniform trip count), so the bucket
+    // count is the smallest 2^4..2^12 keeping every bucket at <= 3 boundaries
+    // (2 steps), else <= 7 (3 steps), else 2^12.
     if (iv.bnd.size() > 0x7FFF) throw std::runtime_error("too many LPM intervals");
-    uint32_t bits = 4;
-    while (bits < PCN_IP_BUCKET_BITS_MAX && (size_t(1) << bits) < 2 * iv.bnd.size()) ++bits;
+    auto first_of = [&](uint32_t bits) {
+      const uint32_t nb = 1u << bits;
+      std::vector<uint32_t> first(nb + 1);
+      for (uint32_t b = 0; b <= nb; ++b) {
+        uint64_t start = uint64_t(b) << (32 - bits);
+        first[b] = static_cast<uint32_t>(std::lower_bound(iv.bnd.begin(), iv.bnd.end(), start) - iv.bnd.begin());
+      }
+      return first;
+    };
+    auto max_count = [](const std::vector<uint32_t> &first) {
+      uint32_t mc = 0;
+      for (size_t b = 0; b + 1 < first.size(); ++b) mc = std::max(mc, first[b + 1] - first[b]);
+      return mc;
+    };
+    uint32_t bits = 0;
+    for (uint32_t limit : {3u, 7u}) {
+      for (uint32_t b = 4; b <= PCN_IP_BUCKET_BITS_MAX && !bits; ++b)
+        if (max_count(first_of(b)) <= limit) bits = b;
+      if (bits) break;
+    }
+    if (!bits) bits = PCN_IP_BUCKET_BITS_MAX;
+    const std::vector<uint32_t> first = first_of(bits);
+    uint32_t steps = 0;
+    while ((1u << steps) - 1 < max_count(first)) ++steps;
     const uint32_t nb = 1u << bits;
-    std::vector<uint32_t> first(nb + 1);
-    for (uint32_t b = 0; b <= nb; ++b) {
-      uint64_t start = uint64_t(b) << (32 - bits);
-      first[b] = static_cast<uint32_t>(std::lower_bound(iv.bnd.begin(), iv.bnd.end(), start) - iv.bnd.begin());
-    }
     std::vector<uint32_t> bkt(nb);
-    for (uint32_t b = 0; b < nb; ++b) {
-      const uint32_t lo = first[b], count = first[b + 1] - lo;
-      bkt[b] = count == 0 ? (PCN_IP_LEAF | cls[lo]) : ((count << 16) | lo);
-    }
+    for (uint32_t b = 0; b < nb; ++b) bkt[b] = ((first[b + 1] - first[b]) << 16) | first[b];
     lay.ip_shift[side] = 32 - bits;
+    lay.ip_steps[side] = steps;
     lay.ip_bkt[side] = blob.add(bkt);
     lay.ip_bnd[side] = blob.add(iv.bnd);
     lay.ip_cls[side] = blob.add(cls);
   }
+  // the all-ones vector: fields a packet skips (or the chain lacks)
+  BitVec ones(t.nrw, 0);
+  for (uint32_t r = 0; r < t.nrules; ++r) ones[r / kBitsPerWord] |= uint64_t(1) << (r % kBitsPerWord);
+  img.all_cls = pool.intern(ones);
+
+  // ---- the meta slot: proto x tcpflags x conntrack (x iface) ----
+  // Each of these fields maps a packet value to a small index into its list
+  // of distinct vectors (nullptr = no entry: the packet takes the default
+  // action); the meta table holds the class of the AND of the four.
+  struct Small {
+    std::vector<const BitVec *> vecs;
+    uint32_t index(const BitVec *v) {
+      for (size_t k = 0; k < vecs.size(); ++k)
+        if (vecs[k] == v || (v && vecs[k] && *vecs[k] == *v)) return static_cast<uint32_t>(k);
+      vecs.push_back(v);
+      return static_cast<uint32_t>(vecs.size() - 1);
+    }
+  };
+  Small P, F, Cn, I;
+  std::vector<uint8_t> pidx(256, 0), cidx(4, 0);
+  std::vector<uint16_t> fidx(256, 0);   // up to 256 distinct flag vectors + the skip entry
+  // L4ProtocolLookup_dp.c:95-103: a miss retries with key 0 (the wildcard).
+  if (t.maps[PCN_IPT_F_L4PROTO].present()) {
+    const FieldMap &m = t.maps[PCN_IPT_F_L4PROTO];
+    std::vector<const BitVec *> by(256, nullptr);
+    for (size_t k = 0; k < m.keys.size(); ++k)
+      if (m.keys[k] == 0) std::fill(by.begin(), by.end(), &m.vecs[k]);
+    for (size_t k = 0; k < m.keys.size(); ++k) by[m.keys[k] & 0xff] = &m.vecs[k];
+    for (int v = 0; v < 256; ++v) pidx[v] = static_cast<uint8_t>(P.index(by[v]));
+  } else {
+    P.index(&ones);
+  }
+  // TcpFlagsLookup_dp.c:93-97: skipped (all rules pass) unless the packet is TCP
+  if (t.maps[PCN_IPT_F_TCPFLAGS].present()) {
+    const FieldMap &m = t.maps[PCN_IPT_F_TCPFLAGS];
+    std::vector<const BitVec *> by(256, nullptr);
+    for (size_t k = 0; k < m.keys.size(); ++k) by[m.keys[k] & 0xff] = &m.vecs[k];
+    for (int v = 0; v < 256; ++v) fidx[v] = static_cast<uint16_t>(F.index(by[v]));
+  }
+  lay.flags_skip = F.index(&ones);
+  if (t.maps[PCN_IPT_F_CONNTRACK].present()) {
+    const FieldMap &m = t.maps[PCN_IPT_F_CONNTRACK];
+    std::vector<const BitVec *> by(4, nullptr);
+    for (size_t k = 0; k < m.keys.size(); ++k)
+      if (m.keys[k] < 4) by[m.keys[k]] = &m.vecs[k];
+    for (int v = 0; v < 4; ++v) cidx[v] = static_cast<uint8_t>(Cn.index(by[v]));
+  } else {
+    Cn.index(&ones);
+  }
+  if (P.vecs.size() > 256 || Cn.vecs.size() > 256) throw std::runtime_error("meta index overflow");
+
   // sport / dport / iface: hash of explicit keys; wildcard key (0 / 0 / 0xffff)
-  // becomes the miss class (L4PortLookup.cpp:44-56, InterfaceLookup.cpp:44-56)
+  // becomes the miss value (L4PortLookup.cpp:44-56, InterfaceLookup.cpp:44-56).
+  // Port hashes hold classes; the iface hash holds an index into I when iface
+  // joins the meta slot, else a class (its own slot).
+  const size_t meta3 = P.vecs.size() * F.vecs.size() * Cn.vecs.size();
+  const FieldMap &im = t.maps[PCN_IPT_F_IFACE];
+  if (im.present()) {
+    for (size_t k = 0; k < im.keys.size(); ++k) I.index(&im.vecs[k]);
+    I.index(nullptr);
+  }
+  lay.iface_merged = !im.present() || meta3 * I.vecs.size() <= kMetaMaxEntries;
+  if (!im.present()) I.index(&ones);
   const int key_fields[3] = {PCN_IPT_F_SPORT, PCN_IPT_F_DPORT, PCN_IPT_F_IFACE};
   const uint32_t wild[3] = {0, 0, 0xffff};
   for (int i = 0; i < 3; ++i) {
     const FieldMap &m = t.maps[key_fields[i]];
     if (!m.present()) continue;
+    const bool to_index = i == 2 && lay.iface_merged;
+    auto value = [&](const BitVec *v) -> uint32_t {
+      if (to_index) return I.index(v);
+      return v ? pool.intern(*v) : PCN_CLS_MISS;
+    };
+    lay.hash_wild[i] = value(nullptr);
     size_t nk = 0;
     for (size_t k = 0; k < m.keys.size(); ++k) {
-      if (m.keys[k] == wild[i]) lay.hash_wild[i] = pool.intern(m.vecs[k]);
+      if (m.keys[k] == wild[i]) lay.hash_wild[i] = value(&m.vecs[k]);
       else ++nk;
     }
-    uint32_t size = 16;
-    while (size < 4 * nk) size <<= 1;   // load <= 1/4: nearly always one probe
-    const uint32_t shift = static_cast<uint32_t>(__builtin_clz(size - 1));
-    std::vector<uint32_t> tab(size, PCN_HASH_EMPTY);
-    for (size_t k = 0; k < m.keys.size(); ++k) {
-      if (m.keys[k] == wild[i]) continue;
-      uint32_t key = m.keys[k] & 0xffff;
-      uint32_t h = (key * kHashMul) >> shift;
-      while (tab[h] != PCN_HASH_EMPTY) h = (h + 1) & (size - 1);
-      tab[h] = (key << 16) | pool.intern(m.vecs[k]);
+    // load <= 1/4 and every key within two probes of its home slot (the
+    // kernel reads slots h and h+1 and never loops); slot `size` mirrors slot 0
+    std::vector<uint32_t> tab;
+    for (uint32_t size = 16;; size <<= 1) {
+      if (size < 4 * nk) continue;
+      const uint32_t shift = static_cast<uint32_t>(__builtin_clz(size - 1));
+      tab.assign(size + 1, PCN_HASH_EMPTY);
+      bool ok = true;
+      for (size_t k = 0; k < m.keys.size() && ok; ++k) {
+        if (m.keys[k] == wild[i]) continue;
+        uint32_t key = m.keys[k] & 0xffff;
+        uint32_t h = (key * kHashMul) >> shift;
+        if (tab[h] != PCN_HASH_EMPTY) h = (h + 1) & (size - 1);
+        if (tab[h] != PCN_HASH_EMPTY) { ok = false; break; }
+        tab[h] = (key << 16) | value(&m.vecs[k]);
+      }
+      if (!ok) continue;
+      tab[size] = tab[0];
+      lay.hash_mask[i] = size - 1;
+      break;
     }
     lay.hash[i] = blob.add(tab);
-    lay.hash_mask[i] = size - 1;
   }
-  // L4ProtocolLookup_dp.c:95-103: a miss retries with key 0 (the wildcard).
-  if (t.maps[PCN_IPT_F_L4PROTO].present()) {
-    const FieldMap &m = t.maps[PCN_IPT_F_L4PROTO];
-    std::vector<uint16_t> tab(256, PCN_CLS_MISS);
-    for (size_t k = 0; k < m.keys.size(); ++k)
-      if (m.keys[k] == 0) std::fill(tab.begin(), tab.end(), pool.intern(m.vecs[k]));
-    for (size_t k = 0; k < m.keys.size(); ++k) tab[m.keys[k] & 0xff] = pool.intern(m.vecs[k]);
-    lay.proto = blob.add(tab);
-  }
-  if (t.maps[PCN_IPT_F_TCPFLAGS].present()) {
-    const FieldMap &m = t.maps[PCN_IPT_F_TCPFLAGS];
-    std::vector<uint16_t> tab(256, PCN_CLS_MISS);
-    for (size_t k = 0; k < m.keys.size(); ++k) tab[m.keys[k] & 0xff] = pool.intern(m.vecs[k]);
-    lay.flags = blob.add(tab);
-  }
-  if (t.maps[PCN_IPT_F_CONNTRACK].present()) {
-    const FieldMap &m = t.maps[PCN_IPT_F_CONNTRACK];
-    std::vector<uint16_t> tab(8, PCN_CLS_MISS);
-    for (size_t k = 0; k < m.keys.size() && k < 4; ++k) tab[m.keys[k] & 3] = pool.intern(m.vecs[k]);
-    lay.ct = blob.add(tab);
-  }
-  // the all-ones class: slots of fields a packet skips (or the chain lacks)
-  BitVec ones(t.nrw, 0);
-  for (uint32_t r = 0; r < t.nrules; ++r) ones[r / kBitsPerWord] |= uint64_t(1) << (r % kBitsPerWord);
-  img.all_cls = pool.intern(ones);
+  if (!lay.iface_merged) { I.vecs.clear(); I.index(&ones); }
+  lay.meta_nf = static_cast<uint32_t>(F.vecs.size());
+  lay.meta_nc = static_cast<uint32_t>(Cn.vecs.size());
+  lay.meta_ni = static_cast<uint32_t>(I.vecs.size());
+  std::vector<uint16_t> meta;
+  meta.reserve(meta3 * I.vecs.size());
+  for (const BitVec *pv : P.vecs)
+    for (const BitVec *fv : F.vecs)
+      for (const BitVec *cv : Cn.vecs)
+        for (const BitVec *iv : I.vecs) {
+          if (!pv || !fv || !cv || !iv) { meta.push_back(PCN_CLS_MISS); continue; }
+          BitVec v(t.nrw);
+          for (uint32_t w = 0; w < t.nrw; ++w) v[w] = (*pv)[w] & (*fv)[w] & (*cv)[w] & (*iv)[w];
+          meta.push_back(pool.intern(v));
+        }
+  lay.proto_idx = blob.add(pidx);
+  lay.flags_idx = blob.add(fidx);
+  lay.ct_idx = blob.add(cidx);
+  lay.meta = blob.add(meta);
+  img.meta_entries = static_cast<uint32_t>(meta.size());
   // Per class and 64-word block: SUMM (bit w: word w != 0), FULL (bit w: word w
   // holds every rule of its word) and the PART array of the remaining
   // "partial" words, stored in word order from PBASE (rank = popcount below w).

@@ -17,6 +17,7 @@ struct HostImage {
   uint32_t part_words = 0;       // partial (neither zero nor full) vector words
   uint32_t pool_words = 0;       // distinct partial words stored
   uint64_t part_bytes = 0;       // PART indices + POOL bytes
+  uint32_t meta_entries = 0;     // proto x flags x conntrack (x iface) table size
   int default_action = 1;
 };
 

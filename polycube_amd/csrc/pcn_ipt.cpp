@@ -22,7 +22,7 @@
 #include "ruleset.hpp"
 
 namespace pcn {
-int launch_classify(const LaunchArgs &a, bool fixed, int ch, int num_cus, hipStream_t stream);
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, hipStream_t stream);
 int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint64_t count, int nranks,
                      hipStream_t stream);
 }  // namespace pcn
@@ -486,7 +486,7 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     a.nbins = base;
     a.nlocal = static_cast<uint32_t>(ctx->localip.size());
     const uint32_t tail = (a.nbins * 8 + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * PCN_WAVE_SCRATCH_BYTES;   // bins + localip + scratch
+                          (PCN_BLOCK / 64) * (PCN_WAVE_SCRATCH_BYTES + PCN_WAVE_HDR_BYTES);
     if (kLdsDescBytes + img_bytes + tail <= kLdsBudget) {
       a.lds_images_bytes = img_bytes;
       a.bins_offset = kLdsDescBytes + img_bytes;
@@ -496,7 +496,8 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     }
     a.lds_localip = a.bins_offset + (a.nbins * 8 + 15) / 16 * 16;
     a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
-    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * PCN_WAVE_SCRATCH_BYTES;
+    a.lds_hdr = a.lds_scratch + (PCN_BLOCK / 64) * PCN_WAVE_SCRATCH_BYTES;
+    a.lds_bytes = a.lds_hdr + (PCN_BLOCK / 64) * PCN_WAVE_HDR_BYTES;
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
     a.offsets = b->offsets;
@@ -532,11 +533,22 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     const bool reach_fw = b->direction == PCN_IPT_INGRESS && !a.allow_logic && a.ch[PCN_IPT_FORWARD].nrules;
     const bool reach_in = b->direction == PCN_IPT_INGRESS && !a.allow_logic && has_local && a.ch[PCN_IPT_INPUT].nrules;
     const bool reach_out = b->direction == PCN_IPT_EGRESS && has_local && a.ch[PCN_IPT_OUTPUT].nrules;
+    // chains a packet of this launch can select (ChainSelector_dp.c:157-168, 243-260)
+    a.count_mask = b->direction == PCN_IPT_INGRESS
+                       ? (1u << PCN_IPT_FORWARD) | (has_local ? 1u << PCN_IPT_INPUT : 0u)
+                       : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
     int ch = PCN_IPT_FORWARD;
     if (reach_fw && reach_in) ch = 3;
     else if (reach_in) ch = PCN_IPT_INPUT;
     else if (reach_out) ch = PCN_IPT_OUTPUT;
-    int rc = launch_classify(a, fixed, ch, ctx->num_cus, static_cast<hipStream_t>(stream));
+    // slot count: 5 unless a chain that runs rules keeps iface in its own slot
+    int ns = 5;
+    for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
+      const bool runs = (c == PCN_IPT_FORWARD && reach_fw) || (c == PCN_IPT_INPUT && reach_in) ||
+                        (c == PCN_IPT_OUTPUT && reach_out);
+      if (runs && a.ch[c].nrules && !a.ch[c].lay.iface_merged) ns = 6;
+    }
+    int rc = launch_classify(a, fixed, ch, ns, ctx->num_cus, static_cast<hipStream_t>(stream));
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
     return 0;
   });
