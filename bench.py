@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--log2n", type=int, default=24, help="frames per GPU = 2^log2n")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe end-to-end leg")
+    ap.add_argument("--jit", type=int, default=1,
+                    help="chain programs: 1 compiled before the first launch (default), 0 background, -1 off")
     args = ap.parse_args()
 
     import torch
@@ -115,7 +117,7 @@ def main():
     n = 1 << args.log2n
     rs = synth.config_rules(3)
     rules = rs.rules()
-    ipt = Iptables(device=local)
+    ipt = Iptables(device=local, jit=args.jit)
     ipt.interactive = False
     fw = ipt.chain("FORWARD")
     for r in rules:
@@ -174,6 +176,9 @@ def main():
         if pm.get("frames") == n:
             traffic = pm.get("hbm_bytes_per_launch")
 
+    jit_info = ipt.jit_info()
+    kernel = ("pcn_classify_jit (chain program, config-3 layout baked in)" if jit_info["launches_jit"] > args.warmup
+              else "classify_kernel<true, true, 1, 5> (generic)")
     if rank == 0:
         # one untimed pass with rule ids for the parity sample
         rid = torch.empty(n, dtype=torch.int32, device=dev)
@@ -191,7 +196,7 @@ def main():
                        "parallelism": f"dp{world} (packet-index shards, RCCL counter all-gather)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "classify_kernel<true>", "kernel_ms": round(kern_ms, 4),
+                         "kernel": kernel, "kernel_ms": round(kern_ms, 4),
                          "bytes_per_unit": BYTES_PER_PKT, "units_per_launch": n},
             "parity_sample_vs_oracle": ok,
         }

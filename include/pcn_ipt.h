@@ -14,14 +14,18 @@
  */
 #ifndef PCN_IPT_H
 #define PCN_IPT_H
+#ifdef __HIPCC_RTC__
+#include <cstdint>   /* the chain-program compile (hiprtc, jit.cpp) has no C headers */
+#else
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 1
+#define PCN_IPT_ABI_VERSION 2
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -47,6 +51,14 @@ typedef struct {
   uint32_t max_counted_rules; /* 0 => 8000   (Iptables_ActionLookup_dp.c:55-56)  */
   uint32_t max_action_rules;  /* 0 => 10000  (Iptables_ActionLookup_dp.c:36)     */
   uint32_t max_rules;         /* 0 => 8192   (Iptables.h:173); hard cap 32767    */
+  /* Chain programs: the classify kernel recompiled (hiprtc) with the running
+   * chain's table layout as constants, like the reference recompiles each
+   * datapath module with substituted macros on every chain update
+   * (modules/Program.cpp:23-119).  0 = compile in the background on the first
+   * launch of a new shape and use it once ready (default); 1 = that first
+   * launch waits for the compile; -1 = off (generic kernel only).  Verdicts,
+   * rule ids and counters are identical either way. */
+  int jit;
 } pcn_ipt_config;
 
 /* One rule as received by the REST surface: ChainRuleJsonObject /
@@ -167,6 +179,21 @@ int pcn_ipt_chain_get_image(pcn_ipt *ctx, int chain, uint8_t *buf, uint32_t cap,
 int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *batch, void *stream);
 /* Wait for all work this context queued. */
 int pcn_ipt_synchronize(pcn_ipt *ctx);
+
+/* Launch/compile statistics of the chain programs (see pcn_ipt_config.jit). */
+typedef struct {
+  uint64_t launches_generic;  /* classify launches that ran the generic kernel */
+  uint64_t launches_jit;      /* ... that ran a chain program                  */
+  uint32_t programs_ready;    /* chain programs compiled                       */
+  uint32_t programs_failed;   /* compiles or module loads that failed          */
+} pcn_ipt_jit_info;
+int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out);
+/* Compile the chain program of `chain` for its usual launch shape (fixed
+ * 64-byte stride, ingress/egress alone, image in LDS) now and wait for it —
+ * the blocking compile the reference does in Chain::updateChain.  Needs no
+ * device (works with device = -1).  On failure the compiler log is in
+ * pcn_ipt_last_error(). */
+int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain);
 
 /* ---- counters ---------------------------------------------------------- */
 /* Per-rule pkts/bytes (ActionLookup pkts_/bytes_<CHAIN>) and default counters

@@ -17,12 +17,17 @@
 // Per-rule and default pkts/bytes counters go to an LDS histogram per
 // workgroup (u64 LDS atomics; default bins wave-aggregated with a ballot) that
 // is flushed once per workgroup with global u64 atomics.
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 
 #include <cstdint>
 
 #include "devchain.h"
 #include "pcn_ipt.h"
+#ifdef PCN_JIT
+#include "pcn_jit_spec.h"   // generated per chain image by jit.cpp (PCN_JIT_CHAIN, PCN_JIT_FIXED, ...)
+#endif
 
 extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 
@@ -350,8 +355,30 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
   if (need) verdict = chain_finish(ch, best, rid);
 }
 
-template <bool FIXED, bool LDS, int CH, int NS>
-__global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
+// The chain program's constants.  A JIT build (jit.cpp, the analogue of the
+// reference's per-chain datapath compile with macro-substituted table sizes,
+// modules/Program.cpp:23-119) bakes the running chain's layout, word counts
+// and field set into the code as immediates; only its pointers stay kernargs.
+#ifdef PCN_JIT
+constexpr DevChain kJitChain = PCN_JIT_CHAIN;
+#else
+constexpr DevChain kJitChain{};
+#endif
+template <bool JIT, int CH>
+__device__ __forceinline__ DevChain chain_desc(const LaunchArgs &a) {
+  if constexpr (JIT) {
+    DevChain c = kJitChain;
+    c.image = a.ch[CH].image;
+    c.ctr = a.ch[CH].ctr;
+    return c;
+  } else {
+    return a.ch[CH < 3 ? CH : 0];
+  }
+}
+
+template <bool FIXED, bool LDS, int CH, int NS, bool JIT>
+__device__ __forceinline__ void classify_body(const LaunchArgs &a) {
+  const DevChain run_ch = chain_desc<JIT, CH>(a);   // the chain that runs rules (CH < 3)
   // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
   // frames per workgroup so neither can wrap; the flush widens to u64)
   uint32_t *bins = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);
@@ -360,7 +387,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
   if (LDS) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const DevChain &ch = a.ch[c];
+      const DevChain &ch = c == CH ? run_ch : a.ch[c];
       if (!ch.nrules) continue;
       const u32x4 *src = reinterpret_cast<const u32x4 *>(ch.image);
       u32x4 *dst = reinterpret_cast<u32x4 *>(pcn_smem + ch.lds_image);
@@ -528,7 +555,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
     if (CH < 3) {
-      run_chain<LDS, NS>(a.ch[CH < 3 ? CH : 0], chain >= 0, p, port, ws, verdict, rid);
+      run_chain<LDS, NS>(run_ch, chain >= 0, p, port, ws, verdict, rid);
       if (chain >= 0) cchain = chain;
     } else {
       if (__ballot(chain == PCN_IPT_FORWARD)) {
@@ -569,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
       }
       // per-rule bins: only chains that run rules in this variant
       if (CH < 3 ? c != CH : c == PCN_IPT_OUTPUT) continue;
-      const DevChain &ch = a.ch[c];
+      const DevChain &ch = CH < 3 ? run_ch : a.ch[c];
       if (valid && cchain == c && rid >= 0 && static_cast<uint32_t>(rid) < ch.ncounted) {
         if (ch.lds_bins >= 0) {
           uint32_t b = static_cast<uint32_t>(ch.lds_bins) + static_cast<uint32_t>(rid);
@@ -599,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     } else {
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const DevChain &ch = a.ch[c];
+        const DevChain &ch = c == CH ? run_ch : a.ch[c];
         if (ch.lds_bins >= 0 && b >= static_cast<uint32_t>(ch.lds_bins) &&
             b < static_cast<uint32_t>(ch.lds_bins) + ch.ncounted)
           dst = ch.ctr + 2 + 2 * (b - static_cast<uint32_t>(ch.lds_bins));
@@ -610,6 +637,21 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
     atomicAdd(dst + 1, by);
   }
 }
+
+template <bool FIXED, bool LDS, int CH, int NS>
+__global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
+  classify_body<FIXED, LDS, CH, NS, false>(a);
+}
+
+}  // namespace
+
+#ifdef PCN_JIT
+// The one kernel of a JIT chain program (looked up by name after hiprtc).
+extern "C" __global__ __launch_bounds__(kBlock) void pcn_classify_jit(const LaunchArgs a) {
+  classify_body<PCN_JIT_FIXED, PCN_JIT_LDS, PCN_JIT_CH, PCN_JIT_NS, true>(a);
+}
+#else
+namespace {
 
 template <bool FIXED, bool LDS, int NS>
 void launch_variant(const LaunchArgs &a, int ch, unsigned grid, size_t lds, hipStream_t stream) {
@@ -630,8 +672,10 @@ void launch_ns(const LaunchArgs &a, int ch, int ns, unsigned grid, size_t lds, h
 }  // namespace
 
 // Host-side launcher (called from pcn_ipt.cpp).  `ch` is the only chain that can
-// reach the rule stage (0..2) or 3 for INPUT+FORWARD.  Returns a hipError_t.
-int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, hipStream_t stream) {
+// reach the rule stage (0..2) or 3 for INPUT+FORWARD.  `jit` (a hipFunction_t
+// or null) is the chain program compiled for exactly this launch shape
+// (jit.cpp); null runs the generic variant.  Returns a hipError_t.
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   const size_t lds = a.lds_bytes;
   const bool in_lds = a.lds_images_bytes > 0;
@@ -660,6 +704,14 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
       c.verdicts = a.verdicts + base;
       if (a.rule_ids) c.rule_ids = a.rule_ids + base;
     }
+    if (jit) {
+      size_t sz = sizeof(LaunchArgs);
+      void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &c, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+      const hipError_t e = hipModuleLaunchKernel(static_cast<hipFunction_t>(jit), grid, 1, 1, kBlock, 1, 1,
+                                                 static_cast<unsigned>(lds), stream, nullptr, extra);
+      if (e != hipSuccess) return static_cast<int>(e);
+      continue;
+    }
     if (fixed && in_lds) launch_ns<true, true>(c, ch, ns, grid, lds, stream);
     else if (fixed) launch_ns<true, false>(c, ch, ns, grid, lds, stream);
     else if (in_lds) launch_ns<false, true>(c, ch, ns, grid, lds, stream);
@@ -687,5 +739,6 @@ int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint
   hipLaunchKernelGGL(sum_ranks_kernel, dim3(grid), dim3(256), 0, stream, in, out, count, nranks);
   return static_cast<int>(hipGetLastError());
 }
+#endif  // PCN_JIT
 
 }  // namespace pcn

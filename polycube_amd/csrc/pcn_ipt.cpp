@@ -18,11 +18,12 @@
 
 #include "devchain.h"
 #include "image.hpp"
+#include "jit.hpp"
 #include "pcn_ipt.h"
 #include "ruleset.hpp"
 
 namespace pcn {
-int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, hipStream_t stream);
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream);
 int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint64_t count, int nranks,
                      hipStream_t stream);
 }  // namespace pcn
@@ -84,6 +85,10 @@ struct ChainState {
   unsigned long long *ctr = nullptr;           // [2 + 2*max_counted]
   unsigned long long *ctr_global = nullptr;    // summed over ranks
   unsigned long long *gather = nullptr;        // [nranks][2 + 2*max_counted]
+  // chain program of the last launch shape (jit.hpp): descriptor + shape it was made for
+  DevChain jit_desc{};
+  JitShape jit_shape{};
+  std::string jit_spec;
 };
 
 }  // namespace
@@ -102,6 +107,8 @@ struct pcn_ipt {
   size_t ctr_words = 0;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  JitCache jit;                                // chain programs (per launch shape)
+  uint64_t launches_generic = 0, launches_jit = 0;
 };
 
 namespace {
@@ -213,6 +220,7 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
   if (!ctx->cfg.max_action_rules) ctx->cfg.max_action_rules = 10000;
   if (!ctx->cfg.max_rules) ctx->cfg.max_rules = 8192;
   if (ctx->cfg.max_rules > 32767) return fail(-EINVAL, "max_rules > 32767");
+  if (ctx->cfg.jit < -1 || ctx->cfg.jit > 1) return fail(-EINVAL, "jit must be -1, 0 or 1");
   ctx->ctr_words = 2 + 2 * size_t(ctx->cfg.max_counted_rules);
   if (cfg->device >= 0) {
     try {
@@ -467,17 +475,39 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     if (b->direction != PCN_IPT_INGRESS && b->direction != PCN_IPT_EGRESS) return fail(-EINVAL, "bad direction");
     device_guard(ctx);
     LaunchArgs a{};
-    // LDS: the table images of every chain with rules (when they fit), then the
-    // counter histogram: 3 default bins + rule bins (FORWARD first).
-    uint32_t img_bytes = 0;
     for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
       a.ch[c] = ctx->chains[c].desc;
-      if (a.ch[c].nrules) { a.ch[c].lds_image = kLdsDescBytes + img_bytes; img_bytes += a.ch[c].lay.bytes; }
-      else a.empty_mask |= 1u << c;
+      if (!a.ch[c].nrules) a.empty_mask |= 1u << c;
       if (a.ch[c].default_action == PCN_IPT_DROP) a.drop_mask |= 1u << c;
     }
+    const ChainState &in = ctx->chains[PCN_IPT_INPUT], &fw = ctx->chains[PCN_IPT_FORWARD];
+    a.allow_logic = in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
+                    in.rules.size() == 0 && fw.rules.size() == 0 && in.desc.nrules == 0 &&
+                    fw.desc.nrules == 0;
+    // which chains can reach the rule stage (ChainSelector_dp.c:157-168, 243-260)
+    const bool has_local = !ctx->localip.empty();
+    const bool reach_fw = b->direction == PCN_IPT_INGRESS && !a.allow_logic && a.ch[PCN_IPT_FORWARD].nrules;
+    const bool reach_in = b->direction == PCN_IPT_INGRESS && !a.allow_logic && has_local && a.ch[PCN_IPT_INPUT].nrules;
+    const bool reach_out = b->direction == PCN_IPT_EGRESS && has_local && a.ch[PCN_IPT_OUTPUT].nrules;
+    int ch = PCN_IPT_FORWARD;
+    if (reach_fw && reach_in) ch = 3;
+    else if (reach_in) ch = PCN_IPT_INPUT;
+    else if (reach_out) ch = PCN_IPT_OUTPUT;
+    // LDS: the table images of every chain with rules (when they fit; the chain
+    // that runs rules first, at offset 0), then the counter histogram: 3
+    // default bins + rule bins (that chain first, then FORWARD, INPUT, OUTPUT).
+    int order[3] = {PCN_IPT_FORWARD, PCN_IPT_INPUT, PCN_IPT_OUTPUT};
+    if (ch < 3) {
+      int k = 1;
+      order[0] = ch;
+      for (int c : {PCN_IPT_FORWARD, PCN_IPT_INPUT, PCN_IPT_OUTPUT})
+        if (c != ch) order[k++] = c;
+    }
+    uint32_t img_bytes = 0;
+    for (int c : order) {
+      if (a.ch[c].nrules) { a.ch[c].lds_image = kLdsDescBytes + img_bytes; img_bytes += a.ch[c].lay.bytes; }
+    }
     uint32_t base = 3;
-    const int order[3] = {PCN_IPT_FORWARD, PCN_IPT_INPUT, PCN_IPT_OUTPUT};
     for (int c : order) {
       uint32_t nc = a.ch[c].ncounted;
       if (nc && base - 3 + nc <= kMaxLdsRuleBins) { a.ch[c].lds_bins = static_cast<int32_t>(base); base += nc; }
@@ -516,10 +546,6 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     a.fixed_len = b->fixed_len;
     a.const_in_port = b->const_in_port;
     a.direction = b->direction;
-    const ChainState &in = ctx->chains[PCN_IPT_INPUT], &fw = ctx->chains[PCN_IPT_FORWARD];
-    a.allow_logic = in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
-                    in.rules.size() == 0 && fw.rules.size() == 0 && in.desc.nrules == 0 &&
-                    fw.desc.nrules == 0;
     // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
     bool fixed = !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
                  (reinterpret_cast<uintptr_t>(b->frames) % 16) == 0 &&
@@ -528,19 +554,10 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       uint64_t last = (b->n - 1) * uint64_t(b->stride);
       if (last >= b->frames_bytes) return fail(-EINVAL, "frames_bytes smaller than n*stride");
     }
-    // which chains can reach the rule stage (ChainSelector_dp.c:157-168, 243-260)
-    const bool has_local = !ctx->localip.empty();
-    const bool reach_fw = b->direction == PCN_IPT_INGRESS && !a.allow_logic && a.ch[PCN_IPT_FORWARD].nrules;
-    const bool reach_in = b->direction == PCN_IPT_INGRESS && !a.allow_logic && has_local && a.ch[PCN_IPT_INPUT].nrules;
-    const bool reach_out = b->direction == PCN_IPT_EGRESS && has_local && a.ch[PCN_IPT_OUTPUT].nrules;
     // chains a packet of this launch can select (ChainSelector_dp.c:157-168, 243-260)
     a.count_mask = b->direction == PCN_IPT_INGRESS
                        ? (1u << PCN_IPT_FORWARD) | (has_local ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
-    int ch = PCN_IPT_FORWARD;
-    if (reach_fw && reach_in) ch = 3;
-    else if (reach_in) ch = PCN_IPT_INPUT;
-    else if (reach_out) ch = PCN_IPT_OUTPUT;
     // slot count: 5 unless a chain that runs rules keeps iface in its own slot
     int ns = 5;
     for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
@@ -548,8 +565,76 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
                         (c == PCN_IPT_OUTPUT && reach_out);
       if (runs && a.ch[c].nrules && !a.ch[c].lay.iface_merged) ns = 6;
     }
-    int rc = launch_classify(a, fixed, ch, ns, ctx->num_cus, static_cast<hipStream_t>(stream));
+    // chain program for this launch shape (jit.hpp), when enabled and ready
+    void *fn = nullptr;
+    if (ch < 3 && (reach_fw || reach_in || reach_out) && ctx->cfg.jit >= 0) {
+      ChainState &cs = ctx->chains[ch];
+      JitShape shape;
+      shape.fixed = fixed;
+      shape.lds = a.lds_images_bytes > 0;
+      shape.ch = ch;
+      shape.ns = ns;
+      DevChain key = a.ch[ch];
+      key.image = nullptr;
+      key.ctr = nullptr;
+      if (cs.jit_spec.empty() || std::memcmp(&key, &cs.jit_desc, sizeof(DevChain)) != 0 ||
+          shape.fixed != cs.jit_shape.fixed ||
+          shape.lds != cs.jit_shape.lds || shape.ch != cs.jit_shape.ch || shape.ns != cs.jit_shape.ns) {
+        cs.jit_desc = key;
+        cs.jit_shape = shape;
+        cs.jit_spec = jit_spec(key, shape);
+      }
+      ctx->jit.request(cs.jit_spec, ctx->cfg.jit == 1);
+      fn = ctx->jit.function(cs.jit_spec, ctx->cfg.device);
+    }
+    ++(fn ? ctx->launches_jit : ctx->launches_generic);
+    int rc = launch_classify(a, fixed, ch, ns, ctx->num_cus, fn, static_cast<hipStream_t>(stream));
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
+    return 0;
+  });
+}
+
+int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out) {
+  return guarded(ctx, [&] {
+    if (!out) return fail(-EINVAL, "null output");
+    out->launches_generic = ctx->launches_generic;
+    out->launches_jit = ctx->launches_jit;
+    out->programs_ready = static_cast<uint32_t>(ctx->jit.compiled());
+    out->programs_failed = static_cast<uint32_t>(ctx->jit.failed());
+    return 0;
+  });
+}
+
+int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    const ChainState &cs = ctx->chains[chain];
+    if (cs.info.nrules == 0) return fail(-ENOENT, "chain has no rules");
+    // the descriptor classify builds when this chain alone runs rules
+    DevChain d{};
+    std::memcpy(&d.lay, cs.desc_words.data(), sizeof(TableLayout));
+    d.nrules = cs.info.nrules;
+    d.nrw = cs.info.nrw;
+    d.nsw = cs.info.nsw;
+    d.present = cs.info.present;
+    d.nvec = cs.info.nvec;
+    d.all_cls = cs.desc_words[sizeof(TableLayout) / 4 + 3];
+    d.ncounted = counted(ctx, cs.info.nrules);
+    d.max_action = ctx->cfg.max_action_rules;
+    d.default_action = cs.default_action;
+    d.lds_image = kLdsDescBytes;
+    d.lds_bins = d.ncounted <= kMaxLdsRuleBins ? 3 : -1;
+    const uint32_t nbins = 3 + (d.lds_bins >= 0 ? d.ncounted : 0);
+    const uint32_t tail = (nbins * 8 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
+                          (PCN_BLOCK / 64) * (PCN_WAVE_SCRATCH_BYTES + PCN_WAVE_HDR_BYTES);
+    JitShape shape;
+    shape.fixed = true;
+    shape.lds = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget;
+    shape.ch = chain;
+    shape.ns = d.lay.iface_merged ? 5 : 6;
+    const std::string spec = jit_spec(d, shape);
+    ctx->jit.request(spec, true);
+    if (!ctx->jit.ready(spec)) return fail(-EIO, "chain program compile failed: " + ctx->jit.last_log());
     return 0;
   });
 }

@@ -24,7 +24,7 @@ class Rule(C.Structure):
 
 class Config(C.Structure):
     _fields_ = [("device", C.c_int), ("max_counted_rules", C.c_uint32),
-                ("max_action_rules", C.c_uint32), ("max_rules", C.c_uint32)]
+                ("max_action_rules", C.c_uint32), ("max_rules", C.c_uint32), ("jit", C.c_int)]
 
 
 class Batch(C.Structure):
@@ -45,6 +45,11 @@ class FieldMap(C.Structure):
 class Tables(C.Structure):
     _fields_ = [("nrules", C.c_uint32), ("default_action", C.c_int),
                 ("actions", C.POINTER(C.c_uint8)), ("maps", FieldMap * 8)]
+
+
+class JitInfo(C.Structure):
+    _fields_ = [("launches_generic", C.c_uint64), ("launches_jit", C.c_uint64),
+                ("programs_ready", C.c_uint32), ("programs_failed", C.c_uint32)]
 
 
 class ChainInfo(C.Structure):
@@ -80,6 +85,8 @@ SIGNATURES = {
                                           C.POINTER(C.c_uint32), C.c_uint32]),
     "pcn_ipt_classify": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p]),
     "pcn_ipt_synchronize": (C.c_int, [C.c_void_p]),
+    "pcn_ipt_get_jit_info": (C.c_int, [C.c_void_p, C.POINTER(JitInfo)]),
+    "pcn_ipt_chain_program_compile": (C.c_int, [C.c_void_p, C.c_int]),
     "pcn_ipt_read_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.c_int, C.c_int]),

@@ -117,6 +117,10 @@ class Chain:
         _check(ffi.lib().pcn_ipt_chain_get_info(self._h(), self.id, C.byref(out)))
         return {k: getattr(out, k) for k, _ in ffi.ChainInfo._fields_}
 
+    def compile_program(self):
+        """Compile this chain's chain program now (pcn_ipt_chain_program_compile)."""
+        _check(ffi.lib().pcn_ipt_chain_program_compile(self._h(), self.id))
+
     def export_map(self, field, cap=70000):
         nrw = ffi.lib().pcn_ipt_chain_nrw(self._h(), self.id)
         keys = (C.c_uint32 * cap)()
@@ -130,8 +134,10 @@ class Chain:
 class Iptables:
     """One pcn-iptables cube bound to one GPU (device=-1: control plane only)."""
 
-    def __init__(self, device=0, max_counted_rules=0, max_action_rules=0, max_rules=0):
-        cfg = ffi.Config(device, max_counted_rules, max_action_rules, max_rules)
+    def __init__(self, device=0, max_counted_rules=0, max_action_rules=0, max_rules=0, jit=0):
+        """jit: 0 chain programs compiled in the background, 1 compiled before the
+        first launch of a new shape, -1 generic kernel only (pcn_ipt_config.jit)."""
+        cfg = ffi.Config(device, max_counted_rules, max_action_rules, max_rules, jit)
         h = C.c_void_p()
         _check(ffi.lib().pcn_ipt_create(C.byref(cfg), C.byref(h)))
         self._h = h
@@ -201,6 +207,12 @@ class Iptables:
                            p(rule_ids) if rule_ids is not False else None, p(offsets), p(lens),
                            stride, fixed_len, p(in_port), const_in_port, direction, p(ct_status), s)
         return verdicts, rule_ids
+
+    def jit_info(self):
+        """Chain-program statistics (pcn_ipt_get_jit_info)."""
+        out = ffi.JitInfo()
+        _check(ffi.lib().pcn_ipt_get_jit_info(self._h, C.byref(out)))
+        return {k: getattr(out, k) for k, _ in ffi.JitInfo._fields_}
 
     def synchronize(self):
         _check(ffi.lib().pcn_ipt_synchronize(self._h))

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert ffi.lib().pcn_ipt_abi_version() == 1
+    assert ffi.lib().pcn_ipt_abi_version() == 2
 
 
 def test_classify_fails_loudly_without_device():
@@ -45,6 +45,21 @@ def test_classify_fails_loudly_without_device():
     with pytest.raises(IptablesError) as e:
         ipt.classify_ptrs(frames=1, frames_bytes=64, n=1, verdicts=1)
     assert e.value.code == -19  # -ENODEV: no CPU fallback exists
+    ipt.close()
+
+
+def test_chain_program_compiles_without_a_device():
+    """The hiprtc chain-program compile (jit.cpp) of classify.hip for config 3's chain."""
+    from polycube_amd import Iptables, synth
+    ipt = Iptables(device=-1)
+    ipt.interactive = False
+    fw = ipt.chain("FORWARD")
+    for r in synth.config_rules(3).rules():
+        fw.append(**r)
+    fw.default = "DROP"
+    fw.apply_rules()
+    fw.compile_program()
+    assert ipt.jit_info()["programs_ready"] == 1
     ipt.close()
 
 

@@ -88,10 +88,22 @@ def assert_counters(o, ipt, chains=(0, 1, 2), n=None):
 SCEN = load_scenarios()
 
 
+JIT = pytest.mark.parametrize("jit", [-1, 1], ids=["generic", "chainprog"])
+
+
+def assert_jit_used(ipt, jit):
+    info = ipt.jit_info()
+    if jit == 1:
+        assert info["launches_jit"] > 0 and info["programs_failed"] == 0, info
+    else:
+        assert info["launches_jit"] == 0, info
+
+
+@JIT
 @pytest.mark.parametrize("sc", SCEN["scenarios"], ids=[s["name"] for s in SCEN["scenarios"]])
-def test_reference_scenarios_on_gpu(dev, sc):
+def test_reference_scenarios_on_gpu(dev, sc, jit):
     from polycube_amd import Iptables
-    cube = GpuCube(Iptables(device=0), SCEN["ports"], SCEN["localip"])
+    cube = GpuCube(Iptables(device=0, jit=jit), SCEN["ports"], SCEN["localip"])
     for k, st in enumerate(sc["steps"]):
         for op in st["ops"]:
             cube.op(op)
@@ -106,17 +118,20 @@ def test_reference_scenarios_on_gpu(dev, sc):
             assert stats[c["rule"]][1] == c["pkts"]
 
 
+@JIT
 @pytest.mark.parametrize("cfg,n", [(1, 1 << 16), (2, 1 << 20), (3, 1 << 20)])
-def test_config_parity(dev, cfg, n):
+def test_config_parity(dev, cfg, n, jit):
     rs = synth.config_rules(cfg)
-    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"})
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=jit)
     frames = synth.config_frames(cfg, n, rs).reshape(-1)
     assert_same(*run_both(o, ipt, dev, frames, n))
     assert_counters(o, ipt)
+    assert_jit_used(ipt, jit)
 
 
+@JIT
 @pytest.mark.parametrize("seed", range(6))
-def test_fuzz_parity(dev, seed):
+def test_fuzz_parity(dev, seed, jit):
     """Quirky rules in all three chains, short/odd frames, random ports/ct, both directions."""
     rng = np.random.default_rng(seed)
     rules = {c: quirky_rules(int(rng.integers(0, 150)), seed * 10 + c) for c in (0, 1, 2)}
@@ -128,7 +143,7 @@ def test_fuzz_parity(dev, seed):
     if seed == 0:
         defaults[0] = defaults[1] = "ACCEPT"
     localip = [ip_nbo(f"10.0.{k}.{k}") for k in range(0, 40)] + [ip_nbo("8.8.8.8")]
-    o, ipt = make_pair(rules, defaults, localip)
+    o, ipt = make_pair(rules, defaults, localip, jit=jit)
     n = 1 << 16
     rs = synth.make_rules(64, seed, protos=(6, 17, 1))
     frames, lens = synth.fuzz_frames(n, seed, rs, stride=96)
@@ -150,25 +165,29 @@ def test_fuzz_parity(dev, seed):
     assert_counters(o, ipt)
 
 
-def test_imix_config5_parity(dev):
+@JIT
+def test_imix_config5_parity(dev, jit):
     """10k rules (extended limits), IMIX 64/576/1500 with VLAN/IPv6 mixed in (variable offsets)."""
     rs = synth.config_rules(5)
     o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, max_rules=16384, max_counted_rules=10000,
-                       max_action_rules=10000)
+                       max_action_rules=10000, jit=jit)
     n = 1 << 17
     buf, offsets, lens = synth.imix_frames(rs, n, 5)
     assert_same(*run_both(o, ipt, dev, buf, n, offsets=offsets, lens=lens))
     assert_counters(o, ipt, n=10000)
+    assert_jit_used(ipt, jit)
 
 
 def test_full_size_headline_config3(dev):
-    """Config 3 at its bench size (2^24 frames): bit-exact verdicts, rule ids and counters."""
+    """Config 3 at its bench size (2^24 frames), through the chain program the
+    bench runs: bit-exact verdicts, rule ids and counters."""
     rs = synth.config_rules(3)
-    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"})
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
     n = 1 << 24
     frames = synth.config_frames(3, n, rs).reshape(-1)
     assert_same(*run_both(o, ipt, dev, frames, n))
     assert_counters(o, ipt)
+    assert_jit_used(ipt, 1)
 
 
 def test_table_level_boundary(dev):

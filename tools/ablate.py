@@ -14,7 +14,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib, hit, log2n, iters, cfg):
+def child(lib, hit, log2n, iters, cfg, jit):
     sys.path.insert(0, ROOT)
     import numpy as np
     import torch
@@ -23,7 +23,7 @@ def child(lib, hit, log2n, iters, cfg):
         ffi.LIB_PATH = lib
     from polycube_amd import Iptables, synth
     rs = synth.config_rules(cfg)
-    ipt = Iptables(device=0)
+    ipt = Iptables(device=0, jit=jit)
     ipt.interactive = False
     fw = ipt.chain("FORWARD")
     for r in rs.rules():
@@ -45,7 +45,8 @@ def child(lib, hit, log2n, iters, cfg):
         b.record()
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
-    print(json.dumps({"lib": os.path.basename(lib or "product"), "hit": hit, "ms": ms,
+    print(json.dumps({"lib": os.path.basename(lib or "product"), "jit": ipt.jit_info()["launches_jit"] > 0,
+                      "hit": hit, "ms": ms,
                       "gpkt_s": n / ms / 1e6, "frac": 64 * n / (ms * 1e-3) / 8e12}))
 
 
@@ -57,14 +58,18 @@ def main():
     ap.add_argument("--log2n", type=int, default=24)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cfg", type=int, default=3)
-    ap.add_argument("--variants", default="product,1,2,3,4")
+    ap.add_argument("--jit", type=int, default=-1)
+    ap.add_argument("--variants", default="jit,product,1,2,3,4")
     ap.add_argument("--hits", default="0,0.5,1")
     a = ap.parse_args()
     if a.child:
-        child(a.lib, a.hit, a.log2n, a.iters, a.cfg)
+        child(a.lib, a.hit, a.log2n, a.iters, a.cfg, a.jit)
         return
     for var in a.variants.split(","):
-        if var == "product":
+        jit = -1
+        if var == "jit":     # the product library's chain program (ablation builds run generic)
+            lib, jit = "", 1
+        elif var == "product":
             lib = ""
         elif var.startswith("exp_"):
             lib = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_{var}.so")
@@ -72,7 +77,7 @@ def main():
             lib = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_ablate{var}.so")
         for hit in a.hits.split(","):
             r = subprocess.run([sys.executable, __file__, "--child", "--lib", lib, "--hit", hit, "--log2n",
-                                str(a.log2n), "--iters", str(a.iters), "--cfg", str(a.cfg)],
+                                str(a.log2n), "--iters", str(a.iters), "--cfg", str(a.cfg), "--jit", str(jit)],
                                capture_output=True, text=True, timeout=300)
             out = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
             print(out[-1] if out else f"{var} hit={hit} FAILED rc={r.returncode}: {r.stderr[-400:]}", flush=True)

@@ -14,7 +14,7 @@ rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 if fatal $rc; then exit $rc; fi
 
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  echo "== pytest -m gpu"; timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+  echo "== pytest -m gpu"; timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_tests.log
   if fatal $rc; then exit $rc; fi
 fi
