@@ -301,9 +301,10 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
         for (int f = 0; f < NS; ++f) oc[f] = (ws->cls[owner][f / 2] >> (16 * (f & 1))) & 0xffff;
         // At a candidate word every field's summary bit is set, so a field is
         // PARTIAL there iff its FULL bit is clear.  Straight-line on purpose:
-        // every index read, then every pool read, issue back to back.  A FULL
-        // field reads the zero cell, i.e. POOL[0], the all-ones word.
-        uint32_t q[NS];
+        // every index read, then every word read, issue back to back.  A FULL
+        // field reads POOL[0], the all-ones word (indexed PART: through the
+        // zero cell, index 0).
+        uint32_t at[NS];   // LDS/image offset of each field's u64 word
 #pragma unroll
         for (int f = 0; f < NS; ++f) {
           const uint32_t rec = oc[f] * nsw + k;
@@ -311,14 +312,18 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
                               : *reinterpret_cast<const u32x4 *>(ch.image + lay.sf + 16 * rec);
           const uint64_t pm = (static_cast<uint64_t>(r.y) << 32 | r.x) & ~(static_cast<uint64_t>(r.w) << 32 | r.z);
           const uint32_t j = t.u32(lay.pbase + 4 * rec) + static_cast<uint32_t>(__builtin_popcountll(pm & below));
-          const bool wide = !LDS && lay.part_wide;
           const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
-          const uint32_t at = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
-          q[f] = wide ? t.u32(at) : t.u16(at);
+          if (lay.part_direct) {
+            at[f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));
+          } else {
+            const bool wide = !LDS && lay.part_wide;
+            const uint32_t ia = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
+            at[f] = lay.pool + 8 * (wide ? t.u32(ia) : t.u16(ia));
+          }
         }
         uint64_t acc = ~0ull;
 #pragma unroll
-        for (int f = 0; f < NS; ++f) acc &= t.u64(lay.pool + 8 * q[f]);
+        for (int f = 0; f < NS; ++f) acc &= t.u64(at[f]);
         if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
           const uint32_t w = k * 64 + bit;
           const uint32_t e = t.u16(lay.perm + 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));

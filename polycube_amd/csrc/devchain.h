@@ -18,8 +18,9 @@
 //     != 0), FULL (bit w: word w holds all of its rules) and PBASE, the start
 //     of the class's PARTIAL words (neither zero nor full) in PART, stored in
 //     word order (a partial word's index = PBASE + popcount(partial bits below));
-//     PART holds u16 (u32 when PART_WIDE) indices into POOL, the distinct
-//     partial words (at 1k rules ~10x fewer than partial words);
+//     PART holds the partial words themselves (PART_DIRECT, while the image
+//     stays small enough for LDS) or u16 (u32 when PART_WIDE) indices into
+//     POOL, the distinct partial words (at 1k rules ~7x fewer);
 //   - PERM: bit position -> (original rule id << 1 | action).
 // Images too large for LDS are read from HBM through the same accessors.
 //
@@ -65,6 +66,7 @@ struct TableLayout {
   uint32_t pbase;          // u32[nvec][nsw]: first PART index of the class's block
   uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
   uint32_t part_wide;
+  uint32_t part_direct;    // PART holds the partial words themselves (u64), not POOL indices
   uint32_t pool;           // u64[]: distinct partial words; POOL[0] is all-ones
   uint32_t zero;           // 16 zero bytes (the PART cell a FULL field reads: index 0)
   uint32_t perm;           // u16[nrw * 63]

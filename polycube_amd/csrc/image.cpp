@@ -16,6 +16,7 @@ constexpr uint32_t kTrieCapacity = 1024;   // Iptables_IpLookup_dp.c:54-55
 constexpr size_t kGroupAlignMin = 8;       // densest packing: smaller type groups share words
 constexpr uint32_t kHashMul = 0x9E3779B1u;
 constexpr size_t kMetaMaxEntries = 8192;   // iface joins the meta slot while the table stays this small
+constexpr size_t kDirectMaxBytes = 72 * 1024;   // images up to this size store partial words directly
 
 inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
 inline uint32_t prefix_mask(uint8_t len) { return len == 0 ? 0u : ~uint32_t(0) << (32 - len); }
@@ -405,13 +406,25 @@ HostImage build_image(const ChainTables &t) {
   img.part_words = static_cast<uint32_t>(part.size());
   lay.sf = blob.add(sf);
   lay.pbase = blob.add(pbase);
-  lay.part_wide = words.size() > 0xFFFF;
-  if (lay.part_wide) lay.part = blob.add(part);
-  else lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
+  // Partial words stored directly (one dependent LDS read less per field in
+  // the candidate stage) while the whole image stays within kDirectMaxBytes.
+  const size_t direct_bytes = blob.bytes.size() + part.size() * 8 + perm.perm.size() * 2 + 4 * kAlign;
+  lay.part_direct = direct_bytes <= kDirectMaxBytes;
+  lay.part_wide = !lay.part_direct && words.size() > 0xFFFF;
+  if (lay.part_direct) {
+    std::vector<uint64_t> direct(part.size());
+    for (size_t k = 0; k < part.size(); ++k) direct[k] = words[part[k]];
+    lay.part = blob.add(direct);
+    words.resize(1);   // POOL[0] = all-ones: what a FULL field reads
+  } else if (lay.part_wide) {
+    lay.part = blob.add(part);
+  } else {
+    lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
+  }
   lay.pool = blob.add(words);
   lay.zero = blob.add(std::vector<uint32_t>(4, 0));
   img.pool_words = static_cast<uint32_t>(words.size());
-  img.part_bytes = part.size() * (lay.part_wide ? 4 : 2) + words.size() * 8;
+  img.part_bytes = part.size() * (lay.part_direct ? 8 : lay.part_wide ? 4 : 2) + words.size() * 8;
   lay.perm = blob.add(perm.perm);
   lay.bytes = static_cast<uint32_t>((blob.bytes.size() + kAlign - 1) / kAlign * kAlign);
   blob.bytes.resize(lay.bytes);

@@ -14,7 +14,7 @@ from polycube_amd import ffi
 LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_shift0", "ip_shift1", "ip_steps0", "ip_steps1", "ip_bnd0", "ip_bnd1", "ip_cls0", "ip_cls1",
           "hash0", "hash1", "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "proto_idx",
           "flags_idx", "ct_idx", "flags_skip", "meta", "meta_nf", "meta_nc", "meta_ni", "iface_merged",
-          "sf", "pbase", "part", "part_wide", "pool", "zero", "perm"]
+          "sf", "pbase", "part", "part_wide", "part_direct", "pool", "zero", "perm"]
 MISS = 0xFFFF
 EMPTY = 0xFFFFFFFF
 
@@ -115,6 +115,9 @@ class ImageModel:
                     part = self.u64(L["sf"] + 16 * r) & ~fm
                     rank = bin(part & ((1 << bit) - 1)).count("1")
                     j = self.u32(L["pbase"] + 4 * r) + rank
+                    if L["part_direct"]:
+                        acc &= self.u64(L["part"] + 8 * j)
+                        continue
                     q = self.u32(L["part"] + 4 * j) if L["part_wide"] else self.u16(L["part"] + 2 * j)
                     acc &= self.u64(L["pool"] + 8 * q)
                 if acc:

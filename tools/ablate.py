@@ -46,6 +46,7 @@ def child(lib, hit, log2n, iters, cfg, jit):
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
     print(json.dumps({"lib": os.path.basename(lib or "product"), "jit": ipt.jit_info()["launches_jit"] > 0,
+                      "defs": os.environ.get("PCN_IPT_JIT_DEFS", ""),
                       "hit": hit, "ms": ms,
                       "gpkt_s": n / ms / 1e6, "frac": 64 * n / (ms * 1e-3) / 8e12}))
 
@@ -67,8 +68,12 @@ def main():
         return
     for var in a.variants.split(","):
         jit = -1
-        if var == "jit":     # the product library's chain program (ablation builds run generic)
+        env = dict(os.environ)
+        if var == "jit":     # the product library's chain program
             lib, jit = "", 1
+        elif var.startswith("jit"):   # jitN: chain program built with -DPCN_ABLATE=N
+            lib, jit = "", 1
+            env["PCN_IPT_JIT_DEFS"] = f"-DPCN_ABLATE={var[3:]}"
         elif var == "product":
             lib = ""
         elif var.startswith("exp_"):
@@ -78,7 +83,7 @@ def main():
         for hit in a.hits.split(","):
             r = subprocess.run([sys.executable, __file__, "--child", "--lib", lib, "--hit", hit, "--log2n",
                                 str(a.log2n), "--iters", str(a.iters), "--cfg", str(a.cfg), "--jit", str(jit)],
-                               capture_output=True, text=True, timeout=300)
+                               capture_output=True, text=True, timeout=300, env=env)
             out = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
             print(out[-1] if out else f"{var} hit={hit} FAILED rc={r.returncode}: {r.stderr[-400:]}", flush=True)
 

@@ -15,7 +15,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def collect(tag_dir, kernel="classify_kernel"):
+def collect(tag_dir, kernel="classify"):
     out = {}
     for path in sorted(glob.glob(os.path.join(tag_dir, "p*", "*counter_collection.csv"))):
         per = defaultdict(lambda: defaultdict(float))
