@@ -36,6 +36,9 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #ifndef PCN_ABLATE
 #define PCN_ABLATE 0
 #endif
+#ifndef PCN_HDR_LDS
+#define PCN_HDR_LDS 1    // fixed stride: 1 coalesced chunks transposed through LDS, 0 per-lane strided loads
+#endif
 #ifndef PCN_PREFETCH
 #define PCN_PREFETCH 1   // frames per lane in flight ahead of the one being classified
 #endif
@@ -135,11 +138,23 @@ __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
 
 // Kernel-LPM answer for a host-order address: the bucket on the top address
 // bits gives the boundaries inside it, then a branchless upper-bound search
-// of `steps` (wave-uniform) probes finds the interval.
+// of `steps` (wave-uniform; unrolled in a chain program) probes finds the
+// interval.
+// Window mode (win != 0): the bucket's <= win boundaries are read at once
+// and counted; boundaries past the bucket (the next buckets', or the
+// 0xFFFFFFFF padding) exceed every address in it, except that the padding
+// equals h == 0xFFFFFFFF, where all real ones are below h too -- hence min.
 template <bool LDS>
 __device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t shift, uint32_t steps,
-                                             uint32_t bnd, uint32_t cls, uint32_t h) {
+                                             uint32_t win, uint32_t bnd, uint32_t cls, uint32_t h) {
   const uint32_t e = t.u32(bkt + 4 * (h >> shift));
+  if (win) {
+    const uint32_t first = e & 0xFFFFu;
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < win; ++k) n += t.u32(bnd + 4 * (first + k)) <= h ? 1u : 0u;
+    const uint32_t count = e >> 16;
+    return t.u16(cls + 2 * (first + (n < count ? n : count)));
+  }
   uint32_t lo = e & 0xFFFFu;
   const uint32_t end = lo + (e >> 16);
   for (uint32_t k = steps; k-- > 0;) {
@@ -171,11 +186,12 @@ struct Parsed {
 
 // ---- rule-chain stage, part 1 (per lane) ----
 // Maps the packet to its NS slot classes: 0 = META (proto x tcpflags x
-// conntrack, and iface when the chain merged it), 1/2 = IP src/dst, 3/4 =
-// sport/dport, 5 = iface (NS == 6 only).  Returns true when the packet needs
-// the candidate stage; otherwise the verdict is decided here (a field without
-// an entry takes the default action, a bad conntrack label drops).  Absent or
-// skipped fields contribute the all-ones vector.
+// conntrack, plus the key fields the chain joined to it), 1/2 = IP src/dst,
+// then the key fields (sport, dport, iface) that keep their own slot
+// (lay.key_slot).  Returns true when the packet needs the candidate stage;
+// otherwise the verdict is decided here (a field without an entry takes the
+// default action, a bad conntrack label drops).  Absent or skipped fields
+// contribute the all-ones vector.
 template <bool LDS, int NS>
 __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &p, uint32_t port, uint32_t cls[NS],
                                               uint32_t &verdict, int32_t &rid) {
@@ -185,33 +201,35 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
   const uint32_t all = ch.all_cls;
 #pragma unroll
   for (int f = 1; f < NS; ++f) cls[f] = all;
-  uint32_t pi = 0, fi = 0, ci = 0, ii = 0;
+  uint32_t mi = 0;   // meta index
   if (present & (1u << PCN_IPT_F_CONNTRACK)) {
     if (p.ct > 3) { rid = PCN_IPT_RID_NOCHAIN; verdict = PCN_IPT_DROP; return false; }   // array miss => RX_DROP
-    ci = t.u8(lay.ct_idx + p.ct);
+    mi += t.u8(lay.ct_idx + p.ct) * lay.meta_stride[2];
   }
-  if (present & (1u << PCN_IPT_F_L4PROTO)) pi = t.u8(lay.proto_idx + p.proto);
+  if (present & (1u << PCN_IPT_F_L4PROTO)) mi += t.u8(lay.proto_idx + p.proto) * lay.meta_stride[0];
   if (present & (1u << PCN_IPT_F_TCPFLAGS))                        // TcpFlagsLookup_dp.c:93-97
-    fi = p.proto == 6 ? t.u16(lay.flags_idx + 2 * p.flags) : lay.flags_skip;
-  if (present & (1u << PCN_IPT_F_IFACE)) {
-    const uint32_t x = key_class(t, lay.hash[2], lay.hash_mask[2], lay.hash_wild[2], port);
-    if (NS == 6 && !lay.iface_merged) cls[NS - 1] = x;
-    else ii = x;
-  }
-  cls[0] = t.u16(lay.meta + 2 * (((pi * lay.meta_nf + fi) * lay.meta_nc + ci) * lay.meta_ni + ii));
-  if (present & (1u << PCN_IPT_F_IPSRC))
-    cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_shift[0], lay.ip_steps[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
-  if (present & (1u << PCN_IPT_F_IPDST))
-    cls[2] = ip_class(t, lay.ip_bkt[1], lay.ip_shift[1], lay.ip_steps[1], lay.ip_bnd[1], lay.ip_cls[1], __builtin_bswap32(p.daddr));
+    mi += (p.proto == 6 ? t.u16(lay.flags_idx + 2 * p.flags) : lay.flags_skip) * lay.meta_stride[1];
   const bool l4 = p.proto == 6 || p.proto == 17;                    // L4PortLookup_dp.c:99-103
-  if (present & (1u << PCN_IPT_F_SPORT)) {
-    uint32_t c = key_class(t, lay.hash[0], lay.hash_mask[0], lay.hash_wild[0], p.sport);
-    cls[3] = l4 ? c : all;
+  const int key_field[3] = {PCN_IPT_F_SPORT, PCN_IPT_F_DPORT, PCN_IPT_F_IFACE};
+  const uint32_t key[3] = {p.sport, p.dport, port};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (!(present & (1u << key_field[i]))) continue;
+    uint32_t x = key_class(t, lay.hash[i], lay.hash_mask[i], lay.hash_wild[i], key[i]);
+    if (i < 2) x = l4 ? x : lay.key_skip[i];
+    const uint32_t slot = lay.key_slot[i];
+    if (slot == 0) {
+      mi += x * lay.meta_stride[3 + i];
+    } else {
+#pragma unroll
+      for (int f = 3; f < NS; ++f) cls[f] = slot == static_cast<uint32_t>(f) ? x : cls[f];
+    }
   }
-  if (present & (1u << PCN_IPT_F_DPORT)) {
-    uint32_t c = key_class(t, lay.hash[1], lay.hash_mask[1], lay.hash_wild[1], p.dport);
-    cls[4] = l4 ? c : all;
-  }
+  cls[0] = t.u16(lay.meta + 2 * mi);
+  if (present & (1u << PCN_IPT_F_IPSRC))
+    cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_shift[0], lay.ip_steps[0], lay.ip_win[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
+  if (present & (1u << PCN_IPT_F_IPDST))
+    cls[2] = ip_class(t, lay.ip_bkt[1], lay.ip_shift[1], lay.ip_steps[1], lay.ip_win[1], lay.ip_bnd[1], lay.ip_cls[1], __builtin_bswap32(p.daddr));
   bool miss = false;
 #pragma unroll
   for (int f = 0; f < NS; ++f) miss |= cls[f] == PCN_CLS_MISS;
@@ -227,13 +245,17 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
   return true;
 }
 
-// Per-wave LDS scratch of the candidate stage.
+// Per-wave LDS scratch of the candidate stage.  It shares the wave's LDS
+// region with the header transpose buffer (used earlier in the iteration).
+#ifndef PCN_ITEM_CLS
+#define PCN_ITEM_CLS 1   // 1: candidates carry their owner's classes; 0: owners stage class rows
+#endif
 struct WaveScratch {
-  uint32_t cls[64][4];   // each lane's eight u16 classes
-  uint32_t item[64];     // (owner lane << 8) | candidate bit
+  u32x4 item[64];        // (owner lane << 8 | candidate bit, the owner's classes as u16 pairs)
   uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
+  u32x4 cls[64];         // PCN_ITEM_CLS == 0: each owner's classes
 };
-static_assert(sizeof(WaveScratch) == PCN_WAVE_SCRATCH_BYTES, "host sizes the scratch");
+static_assert(sizeof(WaveScratch) <= PCN_WAVE_LDS_BYTES, "scratch fits the per-wave region");
 
 // ---- rule-chain stage, part 2 (whole wave, converged) ----
 // Lanes with `active` AND their class summaries into a candidate-word mask.
@@ -275,17 +297,26 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       if (__ballot(c >> (b + 1)) == 0) break;
     }
     if (total == 0) continue;
+    u32x4 mine;   // this lane's classes ride along with each of its candidates
+    {
+      uint32_t pk[3] = {0u, 0u, 0u};
+#pragma unroll
+      for (int f = 0; f < NS; ++f) pk[f / 2] |= cls[f] << (16 * (f & 1));
+      mine.y = pk[0];
+      mine.z = pk[1];
+      mine.w = pk[2];
+    }
     if (!staged) {
       staged = true;
       ws->best[lane] = kNoRule;
-#pragma unroll
-      for (int f = 0; f < NS; f += 2)
-        ws->cls[lane][f / 2] = cls[f] | ((f + 1 < NS ? cls[f + 1] : 0u) << 16);
+      if (!PCN_ITEM_CLS) ws->cls[lane] = mine;
     }
     for (uint32_t done = 0; done < total; done += 64) {
       // deal: each owner writes its candidates that fall in [done, done + 64)
       while (m && pos < done + 64) {
-        ws->item[pos - done] = (lane << 8) | static_cast<uint32_t>(__builtin_ctzll(m));
+        mine.x = (lane << 8) | static_cast<uint32_t>(__builtin_ctzll(m));
+        if (PCN_ITEM_CLS) ws->item[pos - done] = mine;
+        else reinterpret_cast<uint32_t *>(ws->item)[pos - done] = mine.x;
         m &= m - 1;
         ++pos;
       }
@@ -293,12 +324,20 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (lane < total - done) {
-        const uint32_t it = ws->item[lane];
-        const uint32_t owner = it >> 8, bit = it & 63;
+        u32x4 it;
+        if (PCN_ITEM_CLS) {
+          it = ws->item[lane];
+        } else {
+          const uint32_t x = reinterpret_cast<const uint32_t *>(ws->item)[lane];
+          it = ws->cls[x >> 8];
+          it.x = x;
+        }
+        const uint32_t owner = it.x >> 8, bit = it.x & 63;
         const uint64_t below = (1ull << bit) - 1;
+        const uint32_t packed[3] = {it.y, it.z, it.w};
         uint32_t oc[NS];
 #pragma unroll
-        for (int f = 0; f < NS; ++f) oc[f] = (ws->cls[owner][f / 2] >> (16 * (f & 1))) & 0xffff;
+        for (int f = 0; f < NS; ++f) oc[f] = (packed[f / 2] >> (16 * (f & 1))) & 0xffff;
         // At a candidate word every field's summary bit is set, so a field is
         // PARTIAL there iff its FULL bit is clear.  Straight-line on purpose:
         // every index read, then every word read, issue back to back.  A FULL
@@ -387,7 +426,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
   // frames per workgroup so neither can wrap; the flush widens to u64)
   uint32_t *bins = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);
-  WaveScratch *ws = reinterpret_cast<WaveScratch *>(pcn_smem + a.lds_scratch) + (threadIdx.x >> 6);
+  WaveScratch *ws = reinterpret_cast<WaveScratch *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * PCN_WAVE_LDS_BYTES);
   // stage every chain's table image in LDS and zero the counter histogram
   if (LDS) {
 #pragma unroll
@@ -427,17 +466,17 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     uint32_t L, port, ct;
   };
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t cf[3], co[3];   // fixed path: frame within the wave's group, byte offset of the chunk
+  uint32_t cf[3], co[3];   // (the transpose buffer is the wave's LDS region, shared with WaveScratch)   // fixed path: frame within the wave's group, byte offset of the chunk
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const uint32_t t = 64 * q + lane;
     cf[q] = t / 3;
     co[q] = 16 * (t - 3 * cf[q]);
   }
-  u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_hdr) + (threadIdx.x >> 6) * 192;
+  u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch) + (threadIdx.x >> 6) * (PCN_WAVE_LDS_BYTES / 16);
   Stage st[PCN_PREFETCH];
   auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
-    if (FIXED) {
+    if (FIXED && PCN_HDR_LDS) {
       const uint64_t group = j - lane;           // wave-uniform
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
@@ -445,6 +484,11 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         f = f < a.n ? f : last;
         x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]));
       }
+    } else if (FIXED) {
+      const uint64_t f = j < a.n ? j : last;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride) + q);
     } else {
       x.L = a.fixed_len;
       load_header<FIXED>(a, j < a.n ? j : last, x.h, x.L);
@@ -463,9 +507,17 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // Pin every prefetched dword (used or not) until here, so no register the
     // load writes is recycled mid-iteration (a WAW hazard costs a vmcnt wait).
     Hdr h;
-    if (FIXED) {
+    if (FIXED && !PCN_HDR_LDS) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        h.w[4 * q] = cur.c[q].x; h.w[4 * q + 1] = cur.c[q].y; h.w[4 * q + 2] = cur.c[q].z; h.w[4 * q + 3] = cur.c[q].w;
+      }
+    } else if (FIXED) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
+      asm volatile("" ::: "memory");   // the region held the last iteration's WaveScratch
 #pragma unroll
       for (int q = 0; q < 3; ++q) hbuf[64 * q + lane] = cur.c[q];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -668,10 +720,11 @@ void launch_variant(const LaunchArgs &a, int ch, unsigned grid, size_t lds, hipS
   }
 }
 
+// The generic kernel always runs six slots (unused ones hold the all-ones
+// class); a chain program runs exactly the chain's lay.nslots.
 template <bool FIXED, bool LDS>
-void launch_ns(const LaunchArgs &a, int ch, int ns, unsigned grid, size_t lds, hipStream_t stream) {
-  if (ns == 5) launch_variant<FIXED, LDS, 5>(a, ch, grid, lds, stream);
-  else launch_variant<FIXED, LDS, 6>(a, ch, grid, lds, stream);
+void launch_ns(const LaunchArgs &a, int ch, int, unsigned grid, size_t lds, hipStream_t stream) {
+  launch_variant<FIXED, LDS, 6>(a, ch, grid, lds, stream);
 }
 
 }  // namespace

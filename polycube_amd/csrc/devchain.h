@@ -8,12 +8,14 @@
 // no dependent HBM/L2 access at all:
 //   - IP src/dst: the kernel-LPM answer as sorted interval boundaries plus a
 //     bucket index on the top address bits (2^4..2^12 buckets, sized so a
-//     bucket holds few boundaries) searched in a fixed number of steps;
+//     bucket holds few boundaries) searched in a fixed number of steps (a
+//     window read of the whole bucket was measured 8% slower: the kernel is
+//     bound by LDS traffic more than by dependent-read latency);
 //   - sport/dport/iface: open-addressing hashes {key -> class} with the
 //     wildcard class (key 0 / 0xffff) as the miss fallback;
-//   - proto/tcpflags/conntrack (and iface while small) share one META slot:
-//     each maps its value to a small index and a 4-D table holds the class of
-//     the AND of their vectors;
+//   - proto/tcpflags/conntrack (and sport/dport/iface while small) share one
+//     META slot: each maps its value to a small index and a table holds the
+//     class of the AND of their vectors;
 //   - per class and 64-word block: SUMM (bit w: word w of the class vector
 //     != 0), FULL (bit w: word w holds all of its rules) and PBASE, the start
 //     of the class's PARTIAL words (neither zero nor full) in PART, stored in
@@ -40,8 +42,8 @@
 #ifndef PCN_BLOCK
 #define PCN_BLOCK 1024              // classify workgroup size (threads): one per CU
 #endif
-#define PCN_WAVE_SCRATCH_BYTES 1536 // per-wave LDS scratch of the candidate stage
-#define PCN_WAVE_HDR_BYTES 3072     // per-wave LDS header transpose buffer (64 frames x 48 B)
+#define PCN_WAVE_LDS_BYTES 3072     // per-wave LDS region: header transpose buffer (64 frames x 48 B),
+                                    // reused as the candidate-stage scratch
 
 namespace pcn {
 
@@ -51,17 +53,22 @@ struct TableLayout {
   uint32_t ip_bkt[2];      // u32[1 << (32 - ip_shift)]: (count << 16) | first boundary in the bucket
   uint32_t ip_shift[2];    // bucket = address >> ip_shift
   uint32_t ip_steps[2];    // branchless search steps: every bucket holds < 2^steps boundaries
+  uint32_t ip_win[2];      // != 0: no search; every bucket holds <= ip_win boundaries and a lookup
+                           // reads all ip_win of them at once (bnd is padded with 0xFFFFFFFF)
   uint32_t ip_bnd[2];      // u32[m]: interval boundaries (host-order addresses)
   uint32_t ip_cls[2];      // u16[m+1]: class of each interval
-  uint32_t hash[3];        // u32[size + 1]: (key << 16) | class (sport, dport, iface); every key
-                           // sits in its home slot or the next; slot size mirrors slot 0
+  uint32_t hash[3];        // u32[size + 1]: (key << 16) | value (sport, dport, iface); every key
+                           // sits in its home slot or the next; slot size mirrors slot 0.  The
+                           // value is a meta index (field joined to meta) or a class (own slot)
   uint32_t hash_mask[3];   // size - 1
-  uint32_t hash_wild[3];   // class used when the key is absent (PCN_CLS_MISS: none)
+  uint32_t hash_wild[3];   // value used when the key is absent (PCN_CLS_MISS: none, own slot)
+  uint32_t key_skip[2];    // sport/dport value of a non-TCP/UDP packet (the module is skipped)
+  uint32_t key_slot[3];    // sport/dport/iface: own slot (3..5), or 0 (joined to meta / absent)
+  uint32_t nslots;         // 3 + key fields with an own slot
   uint32_t proto_idx, flags_idx, ct_idx;   // u8[256], u16[256], u8[4]: value -> meta index
   uint32_t flags_skip;     // flags index of a non-TCP packet (the module is skipped)
-  uint32_t meta;           // u16[np][nf][nc][ni]: class of the meta slot
-  uint32_t meta_nf, meta_nc, meta_ni;
-  uint32_t iface_merged;   // iface hash holds meta indices (else classes, own slot)
+  uint32_t meta;           // u16[]: class of the meta slot at sum(index_f * meta_stride[f])
+  uint32_t meta_stride[6]; // proto, flags, ct, sport, dport, iface (0: not a meta field)
   uint32_t sf;             // u64x2[nvec][nsw]: {SUMM, FULL}
   uint32_t pbase;          // u32[nvec][nsw]: first PART index of the class's block
   uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
@@ -84,7 +91,7 @@ struct DevChain {
   int32_t lds_bins;              // first LDS counter bin of this chain's rules; -1 => global atomics
 };
 
-// LDS layout of a classify workgroup: [chain images][counter bins (u32 x2)][localip][wave scratch][header buffers]
+// LDS layout of a classify workgroup: [chain images][counter bins (u32 x2)][localip][per-wave regions]
 constexpr uint32_t kLdsDescBytes = 0;
 
 struct LaunchArgs {
@@ -107,8 +114,7 @@ struct LaunchArgs {
   uint32_t bins_offset;          // byte offset of the counter bins in LDS
   uint32_t lds_images_bytes;     // bytes of chain images staged in LDS (0: read from HBM)
   uint32_t lds_localip;          // byte offset of the staged localip table in LDS
-  uint32_t lds_scratch;          // byte offset of the per-wave candidate scratch in LDS
-  uint32_t lds_hdr;              // byte offset of the per-wave header transpose buffers
+  uint32_t lds_scratch;          // byte offset of the per-wave regions (header transpose / candidate scratch)
   uint32_t lds_bytes;            // dynamic LDS per workgroup
   uint16_t const_in_port;
   uint16_t direction;

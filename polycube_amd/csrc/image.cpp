@@ -5,6 +5,7 @@
 #include <cstring>
 #include <map>
 #include <numeric>
+#include <set>
 #include <stdexcept>
 #include <string>
 
@@ -15,8 +16,10 @@ constexpr size_t kAlign = 16;
 constexpr uint32_t kTrieCapacity = 1024;   // Iptables_IpLookup_dp.c:54-55
 constexpr size_t kGroupAlignMin = 8;       // densest packing: smaller type groups share words
 constexpr uint32_t kHashMul = 0x9E3779B1u;
-constexpr size_t kMetaMaxEntries = 8192;   // iface joins the meta slot while the table stays this small
-constexpr size_t kDirectMaxBytes = 72 * 1024;   // images up to this size store partial words directly
+constexpr size_t kMetaMaxEntries = 8192;   // key fields join the meta slot while its table stays this small
+constexpr size_t kMetaMaxClasses = 1024;   // ... and holds at most this many distinct vectors
+constexpr size_t kDirectMaxBytes = 96 * 1024;
+constexpr uint32_t kIpWindowMax = 4;           // IP buckets read whole up to this many boundaries   // images up to this size store partial words directly
 
 inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
 inline uint32_t prefix_mask(uint8_t len) { return len == 0 ? 0u : ~uint32_t(0) << (32 - len); }
@@ -173,7 +176,12 @@ Intervals lpm_intervals(const FieldMap &m) {
   return iv;
 }
 
-HostImage build_image(const ChainTables &t) {
+namespace {
+
+// One image; key field i joins the meta slot when bit i of `join` is set and
+// the meta table stays within kMetaMaxEntries entries / kMetaMaxClasses
+// distinct vectors.
+HostImage build_image_with(const ChainTables &t, uint32_t join) {
   HostImage img;
   img.nrules = t.nrules;
   img.default_action = t.default_action;
@@ -239,21 +247,36 @@ HostImage build_image(const ChainTables &t) {
       for (size_t b = 0; b + 1 < first.size(); ++b) mc = std::max(mc, first[b + 1] - first[b]);
       return mc;
     };
-    uint32_t bits = 0;
-    for (uint32_t limit : {3u, 7u}) {
-      for (uint32_t b = 4; b <= PCN_IP_BUCKET_BITS_MAX && !bits; ++b)
-        if (max_count(first_of(b)) <= limit) bits = b;
-      if (bits) break;
+    // Window mode first: when some 2^4..2^12 buckets keep every bucket at <=
+    // kIpWindowMax boundaries, the kernel reads them all at once and counts
+    // (one dependent read instead of a search).  A prefix's two boundaries
+    // usually share a bucket, so this is the common case.
+    uint32_t bits = 0, win = 0;
+    for (uint32_t b = 4; b <= PCN_IP_BUCKET_BITS_MAX && !bits; ++b)
+      if (max_count(first_of(b)) <= kIpWindowMax) bits = b;
+    if (bits) {
+      win = std::max(1u, max_count(first_of(bits)));
+    } else {
+      for (uint32_t limit : {3u, 7u}) {
+        for (uint32_t b = 4; b <= PCN_IP_BUCKET_BITS_MAX && !bits; ++b)
+          if (max_count(first_of(b)) <= limit) bits = b;
+        if (bits) break;
+      }
     }
     if (!bits) bits = PCN_IP_BUCKET_BITS_MAX;
     const std::vector<uint32_t> first = first_of(bits);
     uint32_t steps = 0;
     while ((1u << steps) - 1 < max_count(first)) ++steps;
+    if (win) {   // padding: window reads past the last boundary see values no address exceeds
+      steps = 0;
+      iv.bnd.insert(iv.bnd.end(), win, 0xFFFFFFFFu);
+    }
     const uint32_t nb = 1u << bits;
     std::vector<uint32_t> bkt(nb);
     for (uint32_t b = 0; b < nb; ++b) bkt[b] = ((first[b + 1] - first[b]) << 16) | first[b];
     lay.ip_shift[side] = 32 - bits;
     lay.ip_steps[side] = steps;
+    lay.ip_win[side] = win;
     lay.ip_bkt[side] = blob.add(bkt);
     lay.ip_bnd[side] = blob.add(iv.bnd);
     lay.ip_cls[side] = blob.add(cls);
@@ -263,10 +286,15 @@ HostImage build_image(const ChainTables &t) {
   for (uint32_t r = 0; r < t.nrules; ++r) ones[r / kBitsPerWord] |= uint64_t(1) << (r % kBitsPerWord);
   img.all_cls = pool.intern(ones);
 
-  // ---- the meta slot: proto x tcpflags x conntrack (x iface) ----
-  // Each of these fields maps a packet value to a small index into its list
-  // of distinct vectors (nullptr = no entry: the packet takes the default
-  // action); the meta table holds the class of the AND of the four.
+  // ---- the meta slot ----
+  // proto, tcpflags and conntrack always, and each of sport / dport / iface
+  // while the table stays small: every such field maps its packet value to an
+  // index into its list of distinct vectors (nullptr = no entry: the packet
+  // takes the default action), and the meta table holds the class of their
+  // AND.  Fewer slots mean fewer summary and partial-word reads per packet,
+  // and the summary of an AND is tighter than the AND of summaries.  A key
+  // field that does not join keeps a slot of its own and its hash holds
+  // classes.
   struct Small {
     std::vector<const BitVec *> vecs;
     uint32_t index(const BitVec *v) {
@@ -276,7 +304,7 @@ HostImage build_image(const ChainTables &t) {
       return static_cast<uint32_t>(vecs.size() - 1);
     }
   };
-  Small P, F, Cn, I;
+  Small P, F, Cn;
   std::vector<uint8_t> pidx(256, 0), cidx(4, 0);
   std::vector<uint16_t> fidx(256, 0);   // up to 256 distinct flag vectors + the skip entry
   // L4ProtocolLookup_dp.c:95-103: a miss retries with key 0 (the wildcard).
@@ -309,34 +337,84 @@ HostImage build_image(const ChainTables &t) {
   }
   if (P.vecs.size() > 256 || Cn.vecs.size() > 256) throw std::runtime_error("meta index overflow");
 
-  // sport / dport / iface: hash of explicit keys; wildcard key (0 / 0 / 0xffff)
-  // becomes the miss value (L4PortLookup.cpp:44-56, InterfaceLookup.cpp:44-56).
-  // Port hashes hold classes; the iface hash holds an index into I when iface
-  // joins the meta slot, else a class (its own slot).
-  const size_t meta3 = P.vecs.size() * F.vecs.size() * Cn.vecs.size();
-  const FieldMap &im = t.maps[PCN_IPT_F_IFACE];
-  if (im.present()) {
-    for (size_t k = 0; k < im.keys.size(); ++k) I.index(&im.vecs[k]);
-    I.index(nullptr);
-  }
-  lay.iface_merged = !im.present() || meta3 * I.vecs.size() <= kMetaMaxEntries;
-  if (!im.present()) I.index(&ones);
+  // sport / dport / iface: hash of explicit keys; the wildcard key (0 / 0 /
+  // 0xffff) becomes the miss value (L4PortLookup.cpp:44-56,
+  // InterfaceLookup.cpp:44-56); ports are skipped for non-TCP/UDP packets
+  // (L4PortLookup_dp.c:99-103).
   const int key_fields[3] = {PCN_IPT_F_SPORT, PCN_IPT_F_DPORT, PCN_IPT_F_IFACE};
   const uint32_t wild[3] = {0, 0, 0xffff};
+  Small K[3];
+  const BitVec *miss_vec[3] = {nullptr, nullptr, nullptr};
+  bool key_present[3] = {false, false, false};
   for (int i = 0; i < 3; ++i) {
     const FieldMap &m = t.maps[key_fields[i]];
     if (!m.present()) continue;
-    const bool to_index = i == 2 && lay.iface_merged;
+    key_present[i] = true;
+    for (size_t k = 0; k < m.keys.size(); ++k) {
+      if (m.keys[k] == wild[i]) miss_vec[i] = &m.vecs[k];
+      else K[i].index(&m.vecs[k]);
+    }
+    K[i].index(miss_vec[i]);
+    if (i < 2) K[i].index(&ones);
+  }
+  bool merged[3] = {false, false, false};
+  auto meta_dims = [&](const bool mg[3]) {
+    std::vector<const std::vector<const BitVec *> *> dims{&P.vecs, &F.vecs, &Cn.vecs};
+    for (int i = 0; i < 3; ++i)
+      if (mg[i]) dims.push_back(&K[i].vecs);
+    return dims;
+  };
+  auto for_each_entry = [&](const std::vector<const std::vector<const BitVec *> *> &dims, auto &&fn) {
+    std::vector<size_t> at(dims.size(), 0);
+    BitVec v(t.nrw);
+    for (;;) {
+      bool miss = false;
+      for (size_t d = 0; d < dims.size(); ++d) miss |= (*dims[d])[at[d]] == nullptr;
+      if (miss) {
+        fn(nullptr);
+      } else {
+        for (uint32_t w = 0; w < t.nrw; ++w) {
+          uint64_t x = ~uint64_t(0);
+          for (size_t d = 0; d < dims.size(); ++d) x &= (*(*dims[d])[at[d]])[w];
+          v[w] = x;
+        }
+        fn(&v);
+      }
+      size_t d = dims.size();
+      while (d-- > 0) {            // row-major: the last dimension varies fastest
+        if (++at[d] < dims[d]->size()) break;
+        at[d] = 0;
+      }
+      if (d == size_t(-1)) break;
+    }
+  };
+  for (int i = 0; i < 3; ++i) {
+    if (!key_present[i] || !((join >> i) & 1)) continue;
+    bool mg[3] = {merged[0], merged[1], merged[2]};
+    mg[i] = true;
+    const auto dims = meta_dims(mg);
+    size_t entries = 1;
+    for (auto *d : dims) entries *= d->size();
+    if (entries > kMetaMaxEntries) continue;
+    std::set<BitVec> distinct;
+    for_each_entry(dims, [&](const BitVec *v) { if (v) distinct.insert(*v); });
+    if (distinct.size() <= kMetaMaxClasses) merged[i] = true;
+  }
+  // slots: 0 meta, 1 src, 2 dst, then key fields that keep their own slot
+  lay.nslots = 3;
+  for (int i = 0; i < 3; ++i) lay.key_slot[i] = (key_present[i] && !merged[i]) ? lay.nslots++ : 0;
+  for (int i = 0; i < 3; ++i) {
+    const FieldMap &m = t.maps[key_fields[i]];
+    if (!key_present[i]) continue;
     auto value = [&](const BitVec *v) -> uint32_t {
-      if (to_index) return I.index(v);
+      if (merged[i]) return K[i].index(v);
       return v ? pool.intern(*v) : PCN_CLS_MISS;
     };
-    lay.hash_wild[i] = value(nullptr);
+    lay.hash_wild[i] = value(miss_vec[i]);
+    if (i < 2) lay.key_skip[i] = merged[i] ? K[i].index(&ones) : img.all_cls;
     size_t nk = 0;
-    for (size_t k = 0; k < m.keys.size(); ++k) {
-      if (m.keys[k] == wild[i]) lay.hash_wild[i] = value(&m.vecs[k]);
-      else ++nk;
-    }
+    for (size_t k = 0; k < m.keys.size(); ++k)
+      if (m.keys[k] != wild[i]) ++nk;
     // load <= 1/4 and every key within two probes of its home slot (the
     // kernel reads slots h and h+1 and never loops); slot `size` mirrors slot 0
     std::vector<uint32_t> tab;
@@ -360,26 +438,28 @@ HostImage build_image(const ChainTables &t) {
     }
     lay.hash[i] = blob.add(tab);
   }
-  if (!lay.iface_merged) { I.vecs.clear(); I.index(&ones); }
-  lay.meta_nf = static_cast<uint32_t>(F.vecs.size());
-  lay.meta_nc = static_cast<uint32_t>(Cn.vecs.size());
-  lay.meta_ni = static_cast<uint32_t>(I.vecs.size());
-  std::vector<uint16_t> meta;
-  meta.reserve(meta3 * I.vecs.size());
-  for (const BitVec *pv : P.vecs)
-    for (const BitVec *fv : F.vecs)
-      for (const BitVec *cv : Cn.vecs)
-        for (const BitVec *iv : I.vecs) {
-          if (!pv || !fv || !cv || !iv) { meta.push_back(PCN_CLS_MISS); continue; }
-          BitVec v(t.nrw);
-          for (uint32_t w = 0; w < t.nrw; ++w) v[w] = (*pv)[w] & (*fv)[w] & (*cv)[w] & (*iv)[w];
-          meta.push_back(pool.intern(v));
-        }
-  lay.proto_idx = blob.add(pidx);
-  lay.flags_idx = blob.add(fidx);
-  lay.ct_idx = blob.add(cidx);
-  lay.meta = blob.add(meta);
-  img.meta_entries = static_cast<uint32_t>(meta.size());
+  // meta index = sum of field index x stride (row-major over the joined fields)
+  {
+    const auto dims = meta_dims(merged);
+    const int field_of_dim[6] = {0, 1, 2, 3, 4, 5};   // proto, flags, ct, then joined sport/dport/iface
+    std::vector<int> fields{0, 1, 2};
+    for (int i = 0; i < 3; ++i)
+      if (merged[i]) fields.push_back(3 + i);
+    (void)field_of_dim;
+    uint32_t stride = 1;
+    for (size_t d = dims.size(); d-- > 0;) {
+      lay.meta_stride[fields[d]] = stride;
+      stride *= static_cast<uint32_t>(dims[d]->size());
+    }
+    std::vector<uint16_t> meta;
+    meta.reserve(stride);
+    for_each_entry(dims, [&](const BitVec *v) { meta.push_back(v ? pool.intern(*v) : PCN_CLS_MISS); });
+    lay.proto_idx = blob.add(pidx);
+    lay.flags_idx = blob.add(fidx);
+    lay.ct_idx = blob.add(cidx);
+    lay.meta = blob.add(meta);
+    img.meta_entries = static_cast<uint32_t>(meta.size());
+  }
   // Per class and 64-word block: SUMM (bit w: word w != 0), FULL (bit w: word w
   // holds every rule of its word) and the PART array of the remaining
   // "partial" words, stored in word order from PBASE (rank = popcount below w).
@@ -430,6 +510,37 @@ HostImage build_image(const ChainTables &t) {
   blob.bytes.resize(lay.bytes);
   img.tables = std::move(blob.bytes);
   return img;
+}
+
+}  // namespace
+
+// Joining key fields to the meta slot saves a slot (fewer summary and
+// partial-word reads per packet) but can grow the image; join greedily, one
+// field at a time, while the image keeps its partial words direct (i.e.
+// stays within kDirectMaxBytes, comfortably inside LDS).
+HostImage build_image(const ChainTables &t) {
+  HostImage best = build_image_with(t, 0);
+  if (t.nrules == 0 || !best.lay.part_direct) return best;
+  uint32_t join = 0;
+  for (;;) {
+    HostImage pick;
+    uint32_t pick_join = 0;
+    bool found = false;
+    for (uint32_t i = 0; i < 3; ++i) {
+      if ((join >> i) & 1) continue;
+      const uint32_t j = join | (1u << i);
+      HostImage trial = build_image_with(t, j);
+      if (trial.lay.nslots >= best.lay.nslots || !trial.lay.part_direct) continue;
+      if (!found || trial.lay.bytes < pick.lay.bytes) {
+        pick = std::move(trial);
+        pick_join = j;
+        found = true;
+      }
+    }
+    if (!found) return best;
+    best = std::move(pick);
+    join = pick_join;
+  }
 }
 
 }  // namespace pcn

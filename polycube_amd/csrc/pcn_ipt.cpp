@@ -516,7 +516,7 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     a.nbins = base;
     a.nlocal = static_cast<uint32_t>(ctx->localip.size());
     const uint32_t tail = (a.nbins * 8 + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * (PCN_WAVE_SCRATCH_BYTES + PCN_WAVE_HDR_BYTES);
+                          (PCN_BLOCK / 64) * PCN_WAVE_LDS_BYTES;
     if (kLdsDescBytes + img_bytes + tail <= kLdsBudget) {
       a.lds_images_bytes = img_bytes;
       a.bins_offset = kLdsDescBytes + img_bytes;
@@ -526,8 +526,7 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     }
     a.lds_localip = a.bins_offset + (a.nbins * 8 + 15) / 16 * 16;
     a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
-    a.lds_hdr = a.lds_scratch + (PCN_BLOCK / 64) * PCN_WAVE_SCRATCH_BYTES;
-    a.lds_bytes = a.lds_hdr + (PCN_BLOCK / 64) * PCN_WAVE_HDR_BYTES;
+    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * PCN_WAVE_LDS_BYTES;
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
     a.offsets = b->offsets;
@@ -558,13 +557,8 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     a.count_mask = b->direction == PCN_IPT_INGRESS
                        ? (1u << PCN_IPT_FORWARD) | (has_local ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
-    // slot count: 5 unless a chain that runs rules keeps iface in its own slot
-    int ns = 5;
-    for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
-      const bool runs = (c == PCN_IPT_FORWARD && reach_fw) || (c == PCN_IPT_INPUT && reach_in) ||
-                        (c == PCN_IPT_OUTPUT && reach_out);
-      if (runs && a.ch[c].nrules && !a.ch[c].lay.iface_merged) ns = 6;
-    }
+    // slot count of the chain program (the generic kernel always runs 6)
+    const int ns = ch < 3 ? static_cast<int>(a.ch[ch].lay.nslots) : 6;
     // chain program for this launch shape (jit.hpp), when enabled and ready
     void *fn = nullptr;
     if (ch < 3 && (reach_fw || reach_in || reach_out) && ctx->cfg.jit >= 0) {
@@ -626,12 +620,12 @@ int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
     d.lds_bins = d.ncounted <= kMaxLdsRuleBins ? 3 : -1;
     const uint32_t nbins = 3 + (d.lds_bins >= 0 ? d.ncounted : 0);
     const uint32_t tail = (nbins * 8 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * (PCN_WAVE_SCRATCH_BYTES + PCN_WAVE_HDR_BYTES);
+                          (PCN_BLOCK / 64) * PCN_WAVE_LDS_BYTES;
     JitShape shape;
     shape.fixed = true;
     shape.lds = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget;
     shape.ch = chain;
-    shape.ns = d.lay.iface_merged ? 5 : 6;
+    shape.ns = static_cast<int>(d.lay.nslots);
     const std::string spec = jit_spec(d, shape);
     ctx->jit.request(spec, true);
     if (!ctx->jit.ready(spec)) return fail(-EIO, "chain program compile failed: " + ctx->jit.last_log());

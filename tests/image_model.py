@@ -11,9 +11,10 @@ import numpy as np
 
 from polycube_amd import ffi
 
-LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_shift0", "ip_shift1", "ip_steps0", "ip_steps1", "ip_bnd0", "ip_bnd1", "ip_cls0", "ip_cls1",
-          "hash0", "hash1", "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "proto_idx",
-          "flags_idx", "ct_idx", "flags_skip", "meta", "meta_nf", "meta_nc", "meta_ni", "iface_merged",
+LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_shift0", "ip_shift1", "ip_steps0", "ip_steps1", "ip_win0", "ip_win1", "ip_bnd0", "ip_bnd1", "ip_cls0", "ip_cls1",
+          "hash0", "hash1", "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "skip0", "skip1",
+          "slot0", "slot1", "slot2", "nslots", "proto_idx", "flags_idx", "ct_idx", "flags_skip", "meta",
+          "stride_proto", "stride_flags", "stride_ct", "stride_sport", "stride_dport", "stride_iface",
           "sf", "pbase", "part", "part_wide", "part_direct", "pool", "zero", "perm"]
 MISS = 0xFFFF
 EMPTY = 0xFFFFFFFF
@@ -43,6 +44,11 @@ class ImageModel:
     def ip_class(self, side, h):
         L = self.lay
         e = self.u32(L[f"ip_bkt{side}"] + 4 * (h >> L[f"ip_shift{side}"]))
+        win = L[f"ip_win{side}"]
+        if win:
+            first = e & 0xFFFF
+            n = sum(self.u32(L[f"ip_bnd{side}"] + 4 * (first + k)) <= h for k in range(win))
+            return self.u16(L[f"ip_cls{side}"] + 2 * (first + min(n, e >> 16)))
         lo = e & 0xFFFF
         end = lo + (e >> 16)
         for k in reversed(range(L[f"ip_steps{side}"])):
@@ -66,35 +72,33 @@ class ImageModel:
 
     def run(self, saddr_h, daddr_h, proto, sport, dport, flags, port=1, ct=0):
         """-> (rule id or -1 for default, action bit or None).  Slots as in
-        classify.hip chain_classes: meta, src, dst, sport, dport (, iface)."""
+        classify.hip chain_classes: meta, src, dst, then own-slot key fields."""
         L, p = self.lay, self.present
-        ns = 5 if L["iface_merged"] else 6
+        ns = L["nslots"]
         cls = [self.all] * ns
-        pi = fi = ci = ii = 0
+        mi = 0
         if p & 1:
-            ci = self.u8(L["ct_idx"] + ct)
+            mi += self.u8(L["ct_idx"] + ct) * L["stride_ct"]
         if p & 8:
-            pi = self.u8(L["proto_idx"] + proto)
+            mi += self.u8(L["proto_idx"] + proto) * L["stride_proto"]
         if p & 128:
-            fi = self.u16(L["flags_idx"] + 2 * flags) if proto == 6 else L["flags_skip"]
-        if p & 64:
-            x = self.key_class(2, port)
-            if ns == 6:
-                cls[5] = x
+            mi += (self.u16(L["flags_idx"] + 2 * flags) if proto == 6 else L["flags_skip"]) * L["stride_flags"]
+        l4 = proto in (6, 17)
+        for i, (bit, key, name) in enumerate(((16, sport, "sport"), (32, dport, "dport"), (64, port, "iface"))):
+            if not p & bit:
+                continue
+            x = self.key_class(i, key)
+            if i < 2 and not l4:
+                x = L[f"skip{i}"]
+            if L[f"slot{i}"] == 0:
+                mi += x * L[f"stride_{name}"]
             else:
-                ii = x
-        cls[0] = self.u16(L["meta"] + 2 * (((pi * L["meta_nf"] + fi) * L["meta_nc"] + ci) * L["meta_ni"] + ii))
+                cls[L[f"slot{i}"]] = x
+        cls[0] = self.u16(L["meta"] + 2 * mi)
         if p & 2:
             cls[1] = self.ip_class(0, saddr_h)
         if p & 4:
             cls[2] = self.ip_class(1, daddr_h)
-        l4 = proto in (6, 17)
-        if p & 16:
-            c = self.key_class(0, sport)
-            cls[3] = c if l4 else self.all
-        if p & 32:
-            c = self.key_class(1, dport)
-            cls[4] = c if l4 else self.all
         if MISS in cls:
             return -1, None
         best = None

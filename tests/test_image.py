@@ -88,7 +88,10 @@ def test_ip_buckets_agree_with_a_full_interval_search():
     nb = int(((ent & 0xFFFF) + cnt).max())
     bnd = np.frombuffer(m.img, np.uint32, nb, bnd_off)
     assert (np.diff(bnd.astype(np.int64)) > 0).all()
-    assert cnt.max() < (1 << m.lay["ip_steps1"]) and m.lay["ip_steps1"] <= 3
+    if m.lay["ip_win1"]:
+        assert cnt.max() == m.lay["ip_win1"] <= 4 and m.lay["ip_steps1"] == 0
+    else:
+        assert cnt.max() < (1 << m.lay["ip_steps1"]) and m.lay["ip_steps1"] <= 3
     rng = np.random.default_rng(5)
     probes = np.concatenate([rng.integers(0, 1 << 32, 3000, dtype=np.uint64),
                              bnd.astype(np.uint64), bnd.astype(np.uint64) - 1]).astype(np.uint32)
@@ -114,10 +117,11 @@ def test_port_hash_two_probe_guarantee():
             assert slot in (home, (home + 1) & mask)
 
 
-@pytest.mark.parametrize("n_rules,n_ports,seed,many_flags,merged", [(60, 6, 1, False, 1), (400, 40, 2, True, 0)])
+@pytest.mark.parametrize("n_rules,n_ports,seed,many_flags,merged", [(60, 6, 1, False, 1), (400, 40, 2, True, 0),
+                                                                     (400, 300, 3, True, 0)])
 def test_image_meta_slot_with_ifaces_flags_conntrack(n_rules, n_ports, seed, many_flags, merged):
-    """proto x tcpflags x conntrack x iface in the META slot (merged while the
-    table is small; iface in its own slot otherwise): model == oracle."""
+    """proto x tcpflags x conntrack (x sport, dport, iface while the table is
+    small; own slots otherwise) in the META slot: model == oracle."""
     import random
     rnd = random.Random(seed)
     ports = {f"p{k}": k + 1 for k in range(n_ports)}
@@ -144,7 +148,10 @@ def test_image_meta_slot_with_ifaces_flags_conntrack(n_rules, n_ports, seed, man
         ch.append(**r)
     ch.apply_rules()
     m = ImageModel(ch)
-    assert m.lay["iface_merged"] == merged
+    if merged:
+        assert m.lay["slot2"] == 0 and m.lay["stride_iface"] > 0
+    else:
+        assert m.lay["nslots"] > 3
     rng = np.random.default_rng(seed)
     n = 1200
     src = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)

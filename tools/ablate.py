@@ -71,13 +71,16 @@ def main():
         env = dict(os.environ)
         if var == "jit":     # the product library's chain program
             lib, jit = "", 1
+        elif var.startswith("jit:"):  # jit:-DX=1+-DY=0: chain program built with extra defines
+            lib, jit = "", 1
+            env["PCN_IPT_JIT_DEFS"] = var[4:].replace("+", " ")
         elif var.startswith("jit"):   # jitN: chain program built with -DPCN_ABLATE=N
             lib, jit = "", 1
             env["PCN_IPT_JIT_DEFS"] = f"-DPCN_ABLATE={var[3:]}"
         elif var == "product":
             lib = ""
-        elif var.startswith("exp_"):
-            lib = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_{var}.so")
+        elif var.startswith("exp_"):   # another build of the product library (A/B), chain programs on
+            lib, jit = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_{var.split(':')[0]}.so"), 1
         else:
             lib = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_ablate{var}.so")
         for hit in a.hits.split(","):
