@@ -25,18 +25,23 @@ sys.path.insert(0, ROOT)
 METRIC = "Mpkt/s device-resident classify @64B, 1k-rule chain, 1 GPU; %HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_PKT = 64             # algorithmic bytes: the 64-byte frame slot
+WORKLOADS = {
+    2: "config2: 128-rule FORWARD chain, 64B IPv4/UDP frames resident in HBM",
+    3: "config3: 1k-rule FORWARD chain, 64B IPv4 50/50 TCP/UDP frames resident in HBM",
+    5: "config5: 10k-rule FORWARD chain, IMIX 64/576/1500B frames (30% 802.1Q, 30% IPv6) resident in HBM",
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_frames(n, rs, seed, chunk=1 << 22):
+def gen_frames(n, rs, seed, chunk=1 << 22, protos=(6, 17)):
     from polycube_amd import synth
     out = np.empty((n, 64), np.uint8)
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
-        cols = synth.make_headers(rs, m, seed + s // chunk)
+        cols = synth.make_headers(rs, m, seed + s // chunk, protos=protos)
         out[s:s + m] = synth.build_frames(*cols, frame_len=64)
     return out.reshape(-1)
 
@@ -56,11 +61,15 @@ def cpu_baseline(rules, frames, n, threads, min_seconds=8.0):
     return done / el / 1e6, done, el
 
 
-def parity_sample(o_rules, frames, v_dev, r_dev, k=1 << 16):
+def parity_sample(o_rules, frames, v_dev, r_dev, offsets=None, lens=None, hook=0, big=None, k=1 << 16):
     from oracle.ffi import Oracle
-    o = Oracle()
+    big = big or {}
+    o = Oracle(big.get("max_counted_rules", 0), big.get("max_action_rules", 0))
     o.set_chain(1, o_rules, "DROP")
-    v, r = o.classify(frames[:k * 64], n=k, nthreads=4)
+    if offsets is None:
+        v, r = o.classify(frames[:k * 64], n=k, nthreads=4, hook=hook)
+    else:
+        v, r = o.classify(frames, n=k, offsets=offsets[:k], lens=lens[:k], nthreads=4, hook=hook)
     return bool(np.array_equal(v, v_dev[:k]) and np.array_equal(r, r_dev[:k]))
 
 
@@ -97,6 +106,10 @@ def main():
     ap.add_argument("--log2n", type=int, default=24, help="frames per GPU = 2^log2n")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe end-to-end leg")
+    ap.add_argument("--config", type=int, default=3, choices=(2, 3, 5),
+                    help="BASELINE.json config: 3 = the headline (default); 2 and 5 are secondary measurements")
+    ap.add_argument("--hook", default="xdp", choices=("xdp", "tc"),
+                    help="attach-point semantics (tc: outer VLAN tags stripped before classification)")
     ap.add_argument("--jit", type=int, default=1,
                     help="chain programs: 1 compiled before the first launch (default), 0 background, -1 off")
     args = ap.parse_args()
@@ -114,10 +127,15 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    cfg = args.config
+    if cfg == 5 and args.log2n == 24:
+        args.log2n = 22                      # config 5 is 2^22 IMIX frames
     n = 1 << args.log2n
-    rs = synth.config_rules(3)
+    hook = 1 if args.hook == "tc" else 0
+    rs = synth.config_rules(cfg)
     rules = rs.rules()
-    ipt = Iptables(device=local, jit=args.jit)
+    big = dict(max_rules=16384, max_counted_rules=10000, max_action_rules=10000) if cfg == 5 else {}
+    ipt = Iptables(device=local, jit=args.jit, **big)
     ipt.interactive = False
     fw = ipt.chain("FORWARD")
     for r in rules:
@@ -130,15 +148,26 @@ def main():
         ipt.comm_init(world, rank, uid[0])
 
     t = time.perf_counter()
-    frames_host = gen_frames(n, rs, synth.CONFIG_SEEDS[3] + 7919 * rank)
+    offsets_host = lens_host = None
+    if cfg == 5:
+        frames_host, offsets_host, lens_host = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5] + 7919 * rank)
+    else:
+        frames_host = gen_frames(n, rs, synth.CONFIG_SEEDS[cfg] + 7919 * rank,
+                                 protos=(synth.UDP,) if cfg == 2 else (synth.TCP, synth.UDP))
     log(f"[rank {rank}] generated {n} frames in {time.perf_counter() - t:.1f}s")
     frames = torch.from_numpy(frames_host).to(dev)
+    offsets = None if offsets_host is None else torch.from_numpy(offsets_host.view(np.int32)).to(dev)
+    lens = None if lens_host is None else torch.from_numpy(lens_host.view(np.int16)).to(dev)
     verdicts = torch.empty(n, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     s_ptr = stream.cuda_stream
 
+    def classify(rid=False):
+        ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=rid, offsets=offsets, lens=lens, stream=s_ptr,
+                     hook=hook)
+
     def step():
-        ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=False, stream=s_ptr)
+        classify()
         if world > 1:
             ipt.sync_counters(s_ptr)
 
@@ -152,7 +181,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=False, stream=s_ptr)
+        classify()
         ev[k][1].record(stream)
         if world > 1:
             ipt.sync_counters(s_ptr)
@@ -167,40 +196,42 @@ def main():
         elapsed = float(tt.item())
 
     value = n * world * args.steps / elapsed / 1e6
-    achieved = BYTES_PER_PKT * n / (kern_ms * 1e-3) / 1e9
+    bytes_per_pkt = BYTES_PER_PKT + (6 if cfg == 5 else 0)   # + offset and length per frame (§8d)
+    achieved = bytes_per_pkt * n / (kern_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         with open(tf) as fh:
             pm = json.load(fh)
-        if pm.get("frames") == n:
+        if pm.get("frames") == n and cfg == 3:
             traffic = pm.get("hbm_bytes_per_launch")
 
     jit_info = ipt.jit_info()
-    kernel = ("pcn_classify_jit (chain program, config-3 layout baked in)" if jit_info["launches_jit"] > args.warmup
-              else "classify_kernel<true, true, 1, 5> (generic)")
+    kernel = (f"pcn_classify_jit (chain program, config-{cfg} layout baked in)"
+              if jit_info["launches_jit"] > args.warmup else "classify_kernel (generic)")
     if rank == 0:
         # one untimed pass with rule ids for the parity sample
         rid = torch.empty(n, dtype=torch.int32, device=dev)
         fw.read_counters(len(rules), flush=True)
-        ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=rid, stream=s_ptr)
+        classify(rid)
         torch.cuda.synchronize()
-        ok = parity_sample(rules, frames_host, verdicts[: 1 << 16].cpu().numpy(), rid[: 1 << 16].cpu().numpy())
+        ok = parity_sample(rules, frames_host, verdicts[: 1 << 16].cpu().numpy(), rid[: 1 << 16].cpu().numpy(),
+                           offsets_host, lens_host, hook, big)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded synth.config_rules(3) + make_headers; no captured traffic)",
-            "config": {"workload": "config3: 1k-rule FORWARD chain, 64B IPv4 50/50 TCP/UDP frames resident in HBM",
+            "config": {"workload": WORKLOADS[cfg] + (", TC hook" if hook else ""),
                        "rules": len(rules), "frames_per_gpu": n, "frame_bytes": 64,
                        "parallelism": f"dp{world} (packet-index shards, RCCL counter all-gather)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kernel, "kernel_ms": round(kern_ms, 4),
-                         "bytes_per_unit": BYTES_PER_PKT, "units_per_launch": n},
+                         "bytes_per_unit": bytes_per_pkt, "units_per_launch": n},
             "parity_sample_vs_oracle": ok,
         }
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and cfg != 5:
             threads = min(16, os.cpu_count() or 1)
             sample = 1 << 22
             v1, done1, el1 = cpu_baseline(rules, frames_host, sample, 1, min_seconds=3.0)
@@ -209,7 +240,7 @@ def main():
                 "value": round(vT, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
                 "sample": f"{doneT} frames ({doneT // n} passes over the same 2^{args.log2n} batch) in {elT:.1f}s",
                 "single_core": {"value": round(v1, 2), "sample": f"{done1} frames of the batch in {el1:.1f}s"}}
-        if world == 1 and not args.no_e2e:
+        if world == 1 and not args.no_e2e and cfg != 5:
             line["e2e"] = {"value": round(e2e_rate(ipt, frames_host, n, torch), 2), "unit": "Mpkt/s",
                            "what": "pinned host frames -> H2D -> classify -> D2H verdicts, 3 streams, 2^21-frame chunks"}
         print(json.dumps(line), flush=True)

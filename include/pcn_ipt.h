@@ -30,6 +30,15 @@ extern "C" {
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
 enum { PCN_IPT_INGRESS = 0, PCN_IPT_EGRESS = 1 };
+/* Attach point of the reference cube (CubeType XDP_* / TC, polycube-base.yang:93).
+ * XDP sees frames as on the wire, so an 802.1Q/802.1ad-tagged frame is not
+ * IPv4 and passes unclassified (Iptables_Parser_dp.c:102-106).  At the TC hook
+ * the kernel receive path has already removed the outer VLAN tag
+ * (skb_vlan_untag, outside the reference), so the inner IPv4 packet is
+ * classified and md->packet_len = skb->len excludes the 4 tag bytes
+ * (polycubed/src/cube_tc.cpp:374-432); a tagged frame shorter than 18 bytes
+ * is dropped by that untag step. */
+enum { PCN_IPT_HOOK_XDP = 0, PCN_IPT_HOOK_TC = 1 };
 /* Actions (ActionsInt, services/pcn-iptables/src/defines.h:79). */
 enum { PCN_IPT_DROP = 0, PCN_IPT_ACCEPT = 1 };
 /* Per-field module ids, same numbering as ModulesConstants (defines.h:48-56). */
@@ -91,6 +100,8 @@ typedef struct {
   const uint16_t *in_port;   /* NULL => const_in_port for every frame */
   uint16_t const_in_port;
   uint16_t direction;        /* PCN_IPT_INGRESS or PCN_IPT_EGRESS */
+  uint16_t hook;             /* PCN_IPT_HOOK_XDP (0) or PCN_IPT_HOOK_TC */
+  uint16_t reserved;         /* 0 */
   const uint8_t *ct_status;  /* NULL => status from an empty conntrack table */
   uint64_t n;                /* number of frames */
   uint8_t *verdicts;         /* out: 0 DROP (RX_DROP), 1 ACCEPT (RX_OK / pass / redirect) */

@@ -43,7 +43,7 @@ def lib():
         h.orc_add_port.argtypes = [vp, C.c_char_p, C.c_uint16]
         h.orc_set_chain.argtypes = [vp, C.c_int, C.POINTER(_Rule), C.c_uint32, C.c_int]
         h.orc_set_localip.argtypes = [vp, u32p, C.c_uint32]
-        h.orc_classify.argtypes = [vp, C.c_int, vp, vp, vp, C.c_uint32, C.c_uint32, vp, C.c_uint16,
+        h.orc_classify.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, C.c_uint32, C.c_uint32, vp, C.c_uint16,
                                    vp, C.c_uint64, vp, vp, C.c_int]
         h.orc_read_counters.argtypes = [vp, C.c_int, u64p, u64p, C.c_uint32, u64p, u64p, C.c_int]
         h.orc_export_map.argtypes = [vp, C.c_int, C.c_int, u32p, u8p, u64p, C.c_uint32, C.c_uint32]
@@ -99,7 +99,7 @@ class Oracle:
         assert lib().orc_set_localip(self._h, a, len(ips)) == 0
 
     def classify(self, frames, n=None, offsets=None, lens=None, stride=64, fixed_len=64,
-                 in_port=None, const_in_port=1, direction=0, ct_status=None, nthreads=1):
+                 in_port=None, const_in_port=1, direction=0, ct_status=None, nthreads=1, hook=0):
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         if n is None:
             n = len(offsets) if offsets is not None else frames.size // stride
@@ -109,7 +109,7 @@ class Oracle:
         ct_status = None if ct_status is None else np.ascontiguousarray(ct_status, dtype=np.uint8)
         verdicts = np.zeros(n, dtype=np.uint8)
         rule_ids = np.zeros(n, dtype=np.int32)
-        lib().orc_classify(self._h, direction, _ptr(frames), _ptr(offsets), _ptr(lens), stride,
+        lib().orc_classify(self._h, direction, hook, _ptr(frames), _ptr(offsets), _ptr(lens), stride,
                            fixed_len, _ptr(in_port), const_in_port, _ptr(ct_status), n,
                            _ptr(verdicts), _ptr(rule_ids), nthreads)
         return verdicts, rule_ids

@@ -594,9 +594,21 @@ static inline int default_verdict(const ochain_t *ch, pcpu_t *pc, int chain, uin
   return ch->default_action == 0 ? RX_DROP : RX_OK;
 }
 
-static int classify_one(const orc_ctx *c, int dir, const uint8_t *f, uint32_t L, uint16_t port,
+static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, uint32_t L, uint16_t port,
                         int ct_in, pcpu_t *pc, int32_t *rid) {
   *rid = -2;
+  /* TC hook: the receive path strips the outer 802.1Q / 802.1ad tag before
+   * the program runs (skb_vlan_untag; a frame too short to hold the tag is
+   * dropped there), and packet_len = skb->len no longer counts it. */
+  uint8_t untagged[128];
+  if (hook == ORC_HOOK_TC && L >= 14 && (be16(f + 12) == 0x8100 || be16(f + 12) == 0x88A8)) {
+    if (L < 18) return RX_DROP;
+    uint32_t keep = L - 4 < sizeof untagged ? L - 4 : (uint32_t)sizeof untagged;
+    memcpy(untagged, f, 12);
+    memcpy(untagged + 12, f + 16, keep - 12);
+    f = untagged;
+    L -= 4;
+  }
   /* Parser_dp.c:94-153 */
   if (L < 14) return RX_DROP;
   if (be16(f + 12) != 0x0800) return RX_OK;
@@ -716,7 +728,7 @@ static int classify_one(const orc_ctx *c, int dir, const uint8_t *f, uint32_t L,
 }
 
 typedef struct {
-  const orc_ctx *c; int dir; const uint8_t *frames; const uint32_t *offsets; const uint16_t *lens;
+  const orc_ctx *c; int dir; int hook; const uint8_t *frames; const uint32_t *offsets; const uint16_t *lens;
   uint32_t stride, fixed_len; const uint16_t *in_port; uint16_t const_port; const uint8_t *ct;
   uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc;
 } job_t;
@@ -729,14 +741,14 @@ static void *run_job(void *arg) {
     uint16_t port = j->in_port ? j->in_port[i] : j->const_port;
     int ct = j->ct ? j->ct[i] : -1;
     int32_t rid;
-    int v = classify_one(j->c, j->dir, f, L, port, ct, &j->pc, &rid);
+    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid);
     j->verdicts[i] = v == RX_DROP ? 0 : 1;
     if (j->rule_ids) j->rule_ids[i] = rid;
   }
   return NULL;
 }
 
-int orc_classify(orc_ctx *c, int dir, const uint8_t *frames, const uint32_t *offsets,
+int orc_classify(orc_ctx *c, int dir, int hook, const uint8_t *frames, const uint32_t *offsets,
                  const uint16_t *lens, uint32_t stride, uint32_t fixed_len,
                  const uint16_t *in_port, uint16_t const_port, const uint8_t *ct_status,
                  uint64_t n, uint8_t *verdicts, int32_t *rule_ids, int nthreads) {
@@ -746,7 +758,7 @@ int orc_classify(orc_ctx *c, int dir, const uint8_t *frames, const uint32_t *off
   pthread_t *th = calloc((size_t)nthreads, sizeof(pthread_t));
   for (int t = 0; t < nthreads; t++) {
     job_t *j = &jobs[t];
-    *j = (job_t){c, dir, frames, offsets, lens, stride, fixed_len, in_port, const_port, ct_status,
+    *j = (job_t){c, dir, hook, frames, offsets, lens, stride, fixed_len, in_port, const_port, ct_status,
                  n * t / nthreads, n * (t + 1) / nthreads, verdicts, rule_ids,
                  {{0}, {0}, {0}, {0}}};
     for (int k = 0; k < NCHAINS; k++) {

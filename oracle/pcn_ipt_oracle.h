@@ -40,6 +40,12 @@ typedef struct orc_ctx orc_ctx;
 
 enum { ORC_INPUT = 0, ORC_FORWARD = 1, ORC_OUTPUT = 2 };
 enum { ORC_INGRESS = 0, ORC_EGRESS = 1 };
+/* Attach point: XDP (frames as on the wire: an 802.1Q/802.1ad frame is not
+ * IPv4, Iptables_Parser_dp.c:102-106) or TC (the kernel receive path has
+ * removed the outer VLAN tag before the TC hook: skb_vlan_untag, Linux
+ * net/core/dev.c, outside /root/reference; md->packet_len = skb->len,
+ * polycubed/src/cube_tc.cpp:374-432). */
+enum { ORC_HOOK_XDP = 0, ORC_HOOK_TC = 1 };
 
 orc_ctx *orc_create(uint32_t max_counted_rules, uint32_t max_action_rules);
 void orc_destroy(orc_ctx *c);
@@ -52,7 +58,7 @@ int orc_set_localip(orc_ctx *c, const uint32_t *ips_nbo, uint32_t n);
 /* Classify a batch (host pointers).  offsets==NULL => packet i at i*stride;
  * lens==NULL => every packet fixed_len bytes; in_port==NULL => const_port;
  * ct_status==NULL => connection status from an empty conntrack table. */
-int orc_classify(orc_ctx *c, int direction, const uint8_t *frames,
+int orc_classify(orc_ctx *c, int direction, int hook, const uint8_t *frames,
                  const uint32_t *offsets, const uint16_t *lens, uint32_t stride,
                  uint32_t fixed_len, const uint16_t *in_port,
                  uint16_t const_port, const uint8_t *ct_status, uint64_t n,

@@ -8,7 +8,7 @@ so the parity tests read like the reference's own scenario tests.
 """
 from .ffi import lib, LibraryMissing  # noqa: F401
 from .iptables import Iptables, Chain, IptablesError, INPUT, FORWARD, OUTPUT  # noqa: F401
-from .iptables import INGRESS, EGRESS, DROP, ACCEPT  # noqa: F401
+from .iptables import INGRESS, EGRESS, DROP, ACCEPT, XDP, TC  # noqa: F401
 
 __all__ = ["lib", "LibraryMissing", "Iptables", "Chain", "IptablesError", "INPUT", "FORWARD",
-           "OUTPUT", "INGRESS", "EGRESS", "DROP", "ACCEPT"]
+           "OUTPUT", "INGRESS", "EGRESS", "DROP", "ACCEPT", "XDP", "TC"]

@@ -79,8 +79,10 @@ struct Tab {
   }
 };
 
-// 48-byte header window as 12 little-endian dwords.
-struct Hdr { uint32_t w[12]; };
+// Header window as little-endian dwords: bytes 0..47 (the fixed-stride path)
+// or 0..51 (the generic path, which also serves the TC hook, where an outer
+// VLAN tag shifts the IPv4 header by 4 bytes).
+struct Hdr { uint32_t w[13]; };
 
 // Fixed-stride frame: bytes 12..47 (ethertype .. TCP flags); the MAC
 // addresses (w0..w2) are never read.
@@ -89,26 +91,26 @@ __device__ __forceinline__ void load_fixed(const uint8_t *frame, Hdr &h) {
   const uint32_t w3 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(frame) + 3);
   u32x4 b = __builtin_nontemporal_load(p + 1);
   u32x4 c = __builtin_nontemporal_load(p + 2);
-  h.w[0] = h.w[1] = h.w[2] = 0;
+  h.w[0] = h.w[1] = h.w[2] = h.w[12] = 0;
   h.w[3] = w3;
   h.w[4] = b.x; h.w[5] = b.y; h.w[6] = b.z; h.w[7] = b.w;
   h.w[8] = c.x; h.w[9] = c.y; h.w[10] = c.z; h.w[11] = c.w;
 }
 
-// Unaligned frame start: 13 aligned dwords, each only if it lies inside the
+// Unaligned frame start: 14 aligned dwords, each only if it lies inside the
 // buffer, then byte-shifted into the window.
 __device__ __forceinline__ void load_generic(const uint8_t *frames, uint64_t frames_bytes,
                                              uint64_t off, Hdr &h) {
   uint64_t base = off & ~uint64_t(3);
   uint32_t sh = static_cast<uint32_t>(off & 3);
-  uint32_t d[13];
+  uint32_t d[14];
 #pragma unroll
-  for (int k = 0; k < 13; ++k) {
+  for (int k = 0; k < 14; ++k) {
     uint64_t at = base + 4u * k;
     d[k] = (at + 4 <= frames_bytes) ? *reinterpret_cast<const uint32_t *>(frames + at) : 0u;
   }
 #pragma unroll
-  for (int k = 0; k < 12; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+  for (int k = 0; k < 13; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
 }
 
 template <bool FIXED>
@@ -532,11 +534,11 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     } else {
 #pragma unroll
-      for (int k = 0; k < 12; ++k) asm volatile("" : "+v"(cur.h.w[k]));
+      for (int k = 0; k < 13; ++k) asm volatile("" : "+v"(cur.h.w[k]));
       h = cur.h;
     }
     asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
-    const uint32_t L = FIXED ? a.fixed_len : cur.L;
+    uint32_t L = FIXED ? a.fixed_len : cur.L;
     const uint32_t cur_port = cur.port, cur_ct = cur.ct;
     prefetch(cur, i + PCN_PREFETCH * step);
     uint32_t verdict = PCN_IPT_DROP;
@@ -547,9 +549,21 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     uint32_t port = 0;
     if (valid) {
       port = a.has_in_port ? cur_port : const_port;
+      // ---- TC hook: the outer VLAN tag is gone before the program runs ----
+      bool untag_drop = false;
+      if (!FIXED && a.hook == PCN_IPT_HOOK_TC && L >= 14 &&
+          ((h.w[3] & 0xffff) == 0x0081 || (h.w[3] & 0xffff) == 0xA888)) {   // 0x8100 / 0x88A8
+        if (L < 18) {
+          untag_drop = true;
+        } else {
+#pragma unroll
+          for (int k = 3; k < 12; ++k) h.w[k] = h.w[k + 1];
+          L -= 4;
+        }
+      }
       // ---- Parser_dp.c:94-153 ----
       bool done = true;
-      if (L < 14) verdict = PCN_IPT_DROP;
+      if (L < 14 || untag_drop) verdict = PCN_IPT_DROP;
       else if ((h.w[3] & 0xffff) != 0x0008) verdict = PCN_IPT_ACCEPT;   // ethertype != 0x0800
       else if (L < 34) verdict = PCN_IPT_DROP;
       else {

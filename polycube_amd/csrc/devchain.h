@@ -118,6 +118,7 @@ struct LaunchArgs {
   uint32_t lds_bytes;            // dynamic LDS per workgroup
   uint16_t const_in_port;
   uint16_t direction;
+  uint32_t hook;                 // PCN_IPT_HOOK_TC: strip an outer VLAN tag first (never with a fixed stride)
   uint32_t allow_logic;          // _INGRESS_ALLOWLOGIC (modules/ChainSelector.cpp:190-202)
   uint32_t empty_mask;           // bit c: chain c has no rules (ChainSelector default path)
   uint32_t drop_mask;            // bit c: chain c's default action is DROP

@@ -473,6 +473,7 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     if (b->n == 0) return 0;
     if (!b->frames || !b->verdicts) return fail(-EINVAL, "frames and verdicts are required");
     if (b->direction != PCN_IPT_INGRESS && b->direction != PCN_IPT_EGRESS) return fail(-EINVAL, "bad direction");
+    if (b->hook != PCN_IPT_HOOK_XDP && b->hook != PCN_IPT_HOOK_TC) return fail(-EINVAL, "bad hook");
     device_guard(ctx);
     LaunchArgs a{};
     for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
@@ -545,8 +546,10 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     a.fixed_len = b->fixed_len;
     a.const_in_port = b->const_in_port;
     a.direction = b->direction;
+    a.hook = b->hook;
     // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
-    bool fixed = !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
+    // (TC frames may carry a VLAN tag: the 52-byte window of the generic path)
+    bool fixed = b->hook == PCN_IPT_HOOK_XDP && !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
                  (reinterpret_cast<uintptr_t>(b->frames) % 16) == 0 &&
                  (b->n - 1) * uint64_t(b->stride) + 48 <= b->frames_bytes;
     if (!b->offsets) {

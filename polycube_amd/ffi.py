@@ -32,6 +32,7 @@ class Batch(C.Structure):
         ("frames", C.c_void_p), ("frames_bytes", C.c_uint64), ("offsets", C.c_void_p),
         ("lens", C.c_void_p), ("stride", C.c_uint32), ("fixed_len", C.c_uint32),
         ("in_port", C.c_void_p), ("const_in_port", C.c_uint16), ("direction", C.c_uint16),
+        ("hook", C.c_uint16), ("reserved", C.c_uint16),
         ("ct_status", C.c_void_p), ("n", C.c_uint64), ("verdicts", C.c_void_p),
         ("rule_ids", C.c_void_p),
     ]

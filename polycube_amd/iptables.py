@@ -17,6 +17,7 @@ from . import ffi
 
 INPUT, FORWARD, OUTPUT = 0, 1, 2
 INGRESS, EGRESS = 0, 1
+XDP, TC = 0, 1            # attach point (pcn_ipt_batch.hook)
 DROP, ACCEPT = 0, 1
 _CHAIN_NAMES = {"INPUT": INPUT, "FORWARD": FORWARD, "OUTPUT": OUTPUT}
 _ACTIONS = {"DROP": DROP, "ACCEPT": ACCEPT}
@@ -181,14 +182,14 @@ class Iptables:
     # ---- datapath (device pointers; torch tensors accepted for convenience) ----
     def classify_ptrs(self, frames, frames_bytes, n, verdicts, rule_ids=None, offsets=None,
                       lens=None, stride=64, fixed_len=64, in_port=None, const_in_port=1,
-                      direction=INGRESS, ct_status=None, stream=None):
+                      direction=INGRESS, ct_status=None, stream=None, hook=XDP):
         b = ffi.Batch(frames, frames_bytes, offsets, lens, stride, fixed_len, in_port, const_in_port,
-                      direction, ct_status, n, verdicts, rule_ids)
+                      direction, hook, 0, ct_status, n, verdicts, rule_ids)
         _check(ffi.lib().pcn_ipt_classify(self._h, C.byref(b), stream))
 
     def classify(self, frames, n=None, verdicts=None, rule_ids=None, offsets=None, lens=None,
                  stride=64, fixed_len=64, in_port=None, const_in_port=1, direction=INGRESS,
-                 ct_status=None, stream=None):
+                 ct_status=None, stream=None, hook=XDP):
         """Classify device-resident frames (torch uint8 tensor on cuda).  Returns
         (verdicts, rule_ids) tensors; the call is asynchronous on `stream`."""
         import torch
@@ -205,7 +206,7 @@ class Iptables:
         s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
         self.classify_ptrs(frames.data_ptr(), frames.numel(), n, verdicts.data_ptr(),
                            p(rule_ids) if rule_ids is not False else None, p(offsets), p(lens),
-                           stride, fixed_len, p(in_port), const_in_port, direction, p(ct_status), s)
+                           stride, fixed_len, p(in_port), const_in_port, direction, p(ct_status), s, hook)
         return verdicts, rule_ids
 
     def jit_info(self):

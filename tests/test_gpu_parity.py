@@ -50,10 +50,10 @@ def make_pair(rules_by_chain, defaults=None, localip=(), ports=PORTS, **cfg):
 
 
 def run_both(o, ipt, dev, frames, n, *, stride=64, fixed_len=64, offsets=None, lens=None, in_port=None,
-             const_in_port=1, direction=0, ct=None):
+             const_in_port=1, direction=0, ct=None, hook=0):
     v_o, r_o = o.classify(frames, n=n, offsets=offsets, lens=lens, stride=stride, fixed_len=fixed_len,
                           in_port=in_port, const_in_port=const_in_port, direction=direction, ct_status=ct,
-                          nthreads=NTHREADS)
+                          nthreads=NTHREADS, hook=hook)
 
     def t(a, dt=None):
         if a is None:
@@ -64,7 +64,7 @@ def run_both(o, ipt, dev, frames, n, *, stride=64, fixed_len=64, offsets=None, l
         return torch.from_numpy(a).to(dev)
     v_g, r_g = ipt.classify(t(frames), n=n, offsets=t(offsets, np.int32), lens=t(lens, np.int16),
                             stride=stride, fixed_len=fixed_len, in_port=t(in_port, np.int16),
-                            const_in_port=const_in_port, direction=direction, ct_status=t(ct))
+                            const_in_port=const_in_port, direction=direction, ct_status=t(ct), hook=hook)
     torch.cuda.synchronize()
     return v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy()
 
@@ -166,16 +166,46 @@ def test_fuzz_parity(dev, seed, jit):
 
 
 @JIT
-def test_imix_config5_parity(dev, jit):
-    """10k rules (extended limits), IMIX 64/576/1500 with VLAN/IPv6 mixed in (variable offsets)."""
+@pytest.mark.parametrize("hook", [0, 1], ids=["xdp", "tc"])
+def test_imix_config5_parity(dev, jit, hook):
+    """10k rules (extended limits), IMIX 64/576/1500 with VLAN/IPv6 mixed in
+    (variable offsets).  XDP: tagged and IPv6 frames pass unclassified; TC:
+    the outer VLAN tag is stripped first and the inner IPv4 is classified."""
     rs = synth.config_rules(5)
     o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, max_rules=16384, max_counted_rules=10000,
                        max_action_rules=10000, jit=jit)
     n = 1 << 17
     buf, offsets, lens = synth.imix_frames(rs, n, 5)
-    assert_same(*run_both(o, ipt, dev, buf, n, offsets=offsets, lens=lens))
+    v_o, r_o, v_g, r_g = run_both(o, ipt, dev, buf, n, offsets=offsets, lens=lens, hook=hook)
+    assert_same(v_o, r_o, v_g, r_g)
     assert_counters(o, ipt, n=10000)
     assert_jit_used(ipt, jit)
+    tagged = np.frombuffer(buf, np.uint8)[offsets.astype(np.int64) + 12] == 0x81
+    assert (r_o[tagged] >= 0).any() == (hook == 1)      # TC classifies tagged frames, XDP passes them
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_tc_hook_fuzz_parity(dev, seed):
+    """TC hook on fuzzed frames: VLAN tags (0x8100 / 0x88A8, short tagged
+    frames), odd offsets and lengths, all three chains."""
+    rng = np.random.default_rng(100 + seed)
+    rules = {c: quirky_rules(int(rng.integers(20, 150)), 300 + seed * 10 + c) for c in (0, 1, 2)}
+    localip = [ip_nbo(f"10.0.{k}.{k}") for k in range(0, 40)]
+    o, ipt = make_pair(rules, {0: "DROP", 1: "ACCEPT", 2: "DROP"}, localip, jit=1)
+    n = 1 << 15
+    frames, lens = synth.fuzz_frames(n, 200 + seed, synth.make_rules(64, seed, protos=(6, 17, 1)), stride=96)
+    f = frames.copy().reshape(n, 96)
+    tag = rng.random(n) < 0.4
+    f[tag, 16:96] = f[tag, 12:92].copy()
+    f[tag, 12:14] = np.where(rng.random((int(tag.sum()), 1)) < 0.7, [0x81, 0x00], [0x88, 0xA8])
+    f[tag, 14:16] = (0x00, 0x07)
+    lens = lens.copy()
+    lens[tag] = np.minimum(lens[tag].astype(np.int64) + 4, 96).astype(lens.dtype)
+    short = rng.random(n) < 0.02
+    lens[short] = rng.integers(12, 20, int(short.sum()))
+    for direction in (0, 1):
+        assert_same(*run_both(o, ipt, dev, f.reshape(-1), n, stride=96, lens=lens, direction=direction, hook=1))
+    assert_counters(o, ipt)
 
 
 def test_full_size_headline_config3(dev):
