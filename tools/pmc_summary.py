@@ -61,7 +61,7 @@ def main():
                                                                + s.get("hbm_write_bytes_per_launch", 0)),
              "read_bytes": round(s["hbm_read_bytes_per_launch"]),
              "write_bytes": round(s.get("hbm_write_bytes_per_launch", 0)),
-             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), classify_kernel, "
+             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over the classify kernel the product runs, "
                        "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count correction)"}
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
             json.dump(t, fh, indent=1)
