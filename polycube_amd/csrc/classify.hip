@@ -255,7 +255,9 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
 struct WaveScratch {
   u32x4 item[64];        // (owner lane << 8 | candidate bit, the owner's classes as u16 pairs)
   uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
-  u32x4 cls[64];         // PCN_ITEM_CLS == 0: each owner's classes
+#if !PCN_ITEM_CLS
+  u32x4 cls[64];         // each owner's classes
+#endif
 };
 static_assert(sizeof(WaveScratch) <= PCN_WAVE_LDS_BYTES, "scratch fits the per-wave region");
 
@@ -311,7 +313,9 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     if (!staged) {
       staged = true;
       ws->best[lane] = kNoRule;
-      if (!PCN_ITEM_CLS) ws->cls[lane] = mine;
+#if !PCN_ITEM_CLS
+      ws->cls[lane] = mine;
+#endif
     }
     for (uint32_t done = 0; done < total; done += 64) {
       // deal: each owner writes its candidates that fall in [done, done + 64)
@@ -331,7 +335,9 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
           it = ws->item[lane];
         } else {
           const uint32_t x = reinterpret_cast<const uint32_t *>(ws->item)[lane];
+#if !PCN_ITEM_CLS
           it = ws->cls[x >> 8];
+#endif
           it.x = x;
         }
         const uint32_t owner = it.x >> 8, bit = it.x & 63;
@@ -428,7 +434,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
   // frames per workgroup so neither can wrap; the flush widens to u64)
   uint32_t *bins = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);
-  WaveScratch *ws = reinterpret_cast<WaveScratch *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * PCN_WAVE_LDS_BYTES);
+  WaveScratch *ws = reinterpret_cast<WaveScratch *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   // stage every chain's table image in LDS and zero the counter histogram
   if (LDS) {
 #pragma unroll
@@ -440,7 +446,10 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       for (uint32_t k = threadIdx.x; k < ch.lay.bytes / 16; k += blockDim.x) dst[k] = src[k];
     }
   }
-  for (uint32_t b = threadIdx.x; b < 2 * a.nbins; b += blockDim.x) bins[b] = 0;
+  // pkts[nbins], then (variable lengths only) bytes[nbins]; with a fixed
+  // length every bin's bytes are pkts * len at the flush
+  for (uint32_t b = threadIdx.x; b < (FIXED ? 1u : 2u) * a.nbins; b += blockDim.x) bins[b] = 0;
+  uint32_t *const byte_bins = bins + a.nbins;
   for (uint32_t k = threadIdx.x; k < a.nlocal; k += blockDim.x)
     reinterpret_cast<uint32_t *>(pcn_smem + a.lds_localip)[k] = a.localip[k];
   __syncthreads();
@@ -475,7 +484,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     cf[q] = t / 3;
     co[q] = 16 * (t - 3 * cf[q]);
   }
-  u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch) + (threadIdx.x >> 6) * (PCN_WAVE_LDS_BYTES / 16);
+  u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   Stage st[PCN_PREFETCH];
   auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
     if (FIXED && PCN_HDR_LDS) {
@@ -651,18 +660,16 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       const bool mine = valid && cchain == c && rid == PCN_IPT_RID_DEFAULT;
       const uint64_t m = __ballot(mine);
       if (m) {
-        uint32_t bytes;
-        if (FIXED) {
-          bytes = static_cast<uint32_t>(__builtin_popcountll(m)) * a.fixed_len;
-        } else {
+        uint32_t bytes = 0;
+        if (!FIXED) {
           uint32_t x = mine ? L : 0u;
 #pragma unroll
           for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
           bytes = x;
         }
         if ((threadIdx.x & 63) == 0) {
-          atomicAdd(&bins[2 * c], static_cast<uint32_t>(__builtin_popcountll(m)));
-          atomicAdd(&bins[2 * c + 1], bytes);
+          atomicAdd(&bins[c], static_cast<uint32_t>(__builtin_popcountll(m)));
+          if (!FIXED) atomicAdd(&byte_bins[c], bytes);
         }
       }
       // per-rule bins: only chains that run rules in this variant
@@ -671,8 +678,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       if (valid && cchain == c && rid >= 0 && static_cast<uint32_t>(rid) < ch.ncounted) {
         if (ch.lds_bins >= 0) {
           uint32_t b = static_cast<uint32_t>(ch.lds_bins) + static_cast<uint32_t>(rid);
-          atomicAdd(&bins[2 * b], 1u);
-          if (!FIXED) atomicAdd(&bins[2 * b + 1], L);   // fixed length: bytes = pkts * len at flush
+          atomicAdd(&bins[b], 1u);
+          if (!FIXED) atomicAdd(&byte_bins[b], L);
         } else {
           atomicAdd(&ch.ctr[2 + 2 * rid], 1ull);
           atomicAdd(&ch.ctr[3 + 2 * rid], static_cast<unsigned long long>(L));
@@ -688,8 +695,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   __syncthreads();
   // ---- flush the workgroup histogram ----
   for (uint32_t b = threadIdx.x; b < a.nbins; b += blockDim.x) {
-    const unsigned long long pk = bins[2 * b];
-    const unsigned long long by = (FIXED && b >= 3) ? pk * a.fixed_len : bins[2 * b + 1];
+    const unsigned long long pk = bins[b];
+    const unsigned long long by = FIXED ? pk * a.fixed_len : byte_bins[b];
     if (!pk) continue;
     unsigned long long *dst = nullptr;
     if (b < 3) {
@@ -718,7 +725,10 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
 
 #ifdef PCN_JIT
 // The one kernel of a JIT chain program (looked up by name after hiprtc).
-extern "C" __global__ __launch_bounds__(kBlock) void pcn_classify_jit(const LaunchArgs a) {
+#ifndef PCN_WAVES_PER_SIMD
+#define PCN_WAVES_PER_SIMD 1   // >= 8: two 1024-thread workgroups per CU (<= 64 VGPRs)
+#endif
+extern "C" __global__ __launch_bounds__(kBlock, PCN_WAVES_PER_SIMD) void pcn_classify_jit(const LaunchArgs a) {
   classify_body<PCN_JIT_FIXED, PCN_JIT_LDS, PCN_JIT_CH, PCN_JIT_NS, true>(a);
 }
 #else

@@ -115,6 +115,7 @@ struct LaunchArgs {
   uint32_t lds_images_bytes;     // bytes of chain images staged in LDS (0: read from HBM)
   uint32_t lds_localip;          // byte offset of the staged localip table in LDS
   uint32_t lds_scratch;          // byte offset of the per-wave regions (header transpose / candidate scratch)
+  uint32_t wave_bytes;           // bytes per wave region
   uint32_t lds_bytes;            // dynamic LDS per workgroup
   uint16_t const_in_port;
   uint16_t direction;

@@ -2,6 +2,7 @@
 #include "image.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -19,7 +20,15 @@ constexpr uint32_t kHashMul = 0x9E3779B1u;
 constexpr size_t kMetaMaxEntries = 8192;   // key fields join the meta slot while its table stays this small
 constexpr size_t kMetaMaxClasses = 1024;   // ... and holds at most this many distinct vectors
 constexpr size_t kDirectMaxBytes = 96 * 1024;
-constexpr uint32_t kIpWindowMax = 4;           // IP buckets read whole up to this many boundaries   // images up to this size store partial words directly
+constexpr uint32_t kIpWindowMax = 4;           // IP buckets read whole up to this many boundaries
+
+// Measurement knob (tools/ablate.py experiments): PCN_IPT_DEBUG_COMPACT=1
+// builds the smallest image (indexed partial words, searched IP buckets of at
+// most 2^10) to try two workgroups per CU.
+bool compact_images() {
+  static const bool v = std::getenv("PCN_IPT_DEBUG_COMPACT") != nullptr;
+  return v;
+}   // images up to this size store partial words directly
 
 inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
 inline uint32_t prefix_mask(uint8_t len) { return len == 0 ? 0u : ~uint32_t(0) << (32 - len); }
@@ -252,18 +261,19 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     // (one dependent read instead of a search).  A prefix's two boundaries
     // usually share a bucket, so this is the common case.
     uint32_t bits = 0, win = 0;
-    for (uint32_t b = 4; b <= PCN_IP_BUCKET_BITS_MAX && !bits; ++b)
+    const uint32_t max_bits = compact_images() ? 10 : PCN_IP_BUCKET_BITS_MAX;
+    for (uint32_t b = 4; b <= max_bits && !bits && !compact_images(); ++b)
       if (max_count(first_of(b)) <= kIpWindowMax) bits = b;
     if (bits) {
       win = std::max(1u, max_count(first_of(bits)));
     } else {
       for (uint32_t limit : {3u, 7u}) {
-        for (uint32_t b = 4; b <= PCN_IP_BUCKET_BITS_MAX && !bits; ++b)
+        for (uint32_t b = 4; b <= max_bits && !bits; ++b)
           if (max_count(first_of(b)) <= limit) bits = b;
         if (bits) break;
       }
     }
-    if (!bits) bits = PCN_IP_BUCKET_BITS_MAX;
+    if (!bits) bits = max_bits;
     const std::vector<uint32_t> first = first_of(bits);
     uint32_t steps = 0;
     while ((1u << steps) - 1 < max_count(first)) ++steps;
@@ -489,7 +499,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
   // Partial words stored directly (one dependent LDS read less per field in
   // the candidate stage) while the whole image stays within kDirectMaxBytes.
   const size_t direct_bytes = blob.bytes.size() + part.size() * 8 + perm.perm.size() * 2 + 4 * kAlign;
-  lay.part_direct = direct_bytes <= kDirectMaxBytes;
+  lay.part_direct = direct_bytes <= kDirectMaxBytes && !compact_images();
   lay.part_wide = !lay.part_direct && words.size() > 0xFFFF;
   if (lay.part_direct) {
     std::vector<uint64_t> direct(part.size());

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -55,6 +56,17 @@ void hip_check(hipError_t e, const char *what) {
 #endif
 constexpr uint32_t kMaxLdsRuleBins = PCN_DEBUG_MAX_RULE_BINS;   // per-workgroup LDS histogram budget (16 KB of u32 pairs)
 constexpr uint32_t kLdsBudget = PCN_DEBUG_LDS_BUDGET;  // gfx950 LDS per CU (one workgroup may take it all)
+
+// Measurement knob (tools/ablate.py experiments): bytes per wave region
+// (default PCN_WAVE_LDS_BYTES; a kernel built without the header transpose
+// needs only its candidate scratch).
+uint32_t wave_region_bytes() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_WAVE_BYTES");
+    return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : uint32_t(PCN_WAVE_LDS_BYTES);
+  }();
+  return v;
+}
 
 struct ImageSlot {
   void *tables = nullptr;
@@ -514,10 +526,17 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       if (nc && base - 3 + nc <= kMaxLdsRuleBins) { a.ch[c].lds_bins = static_cast<int32_t>(base); base += nc; }
       else a.ch[c].lds_bins = -1;
     }
+    // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
+    // (TC frames may carry a VLAN tag: the 52-byte window of the generic path)
+    bool fixed = b->hook == PCN_IPT_HOOK_XDP && !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
+                 (reinterpret_cast<uintptr_t>(b->frames) % 16) == 0 &&
+                 (b->n - 1) * uint64_t(b->stride) + 48 <= b->frames_bytes;
     a.nbins = base;
     a.nlocal = static_cast<uint32_t>(ctx->localip.size());
-    const uint32_t tail = (a.nbins * 8 + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * PCN_WAVE_LDS_BYTES;
+    // counter bins: u32 pkts, plus u32 bytes unless every frame has the same length
+    const uint32_t bin_bytes = (fixed ? 4 : 8) * a.nbins;
+    const uint32_t tail = (bin_bytes + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
+                          (PCN_BLOCK / 64) * wave_region_bytes();
     if (kLdsDescBytes + img_bytes + tail <= kLdsBudget) {
       a.lds_images_bytes = img_bytes;
       a.bins_offset = kLdsDescBytes + img_bytes;
@@ -525,9 +544,9 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       a.lds_images_bytes = 0;
       a.bins_offset = kLdsDescBytes;
     }
-    a.lds_localip = a.bins_offset + (a.nbins * 8 + 15) / 16 * 16;
+    a.lds_localip = a.bins_offset + (bin_bytes + 15) / 16 * 16;
     a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
-    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * PCN_WAVE_LDS_BYTES;
+    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * wave_region_bytes();
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
     a.offsets = b->offsets;
@@ -547,11 +566,6 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     a.const_in_port = b->const_in_port;
     a.direction = b->direction;
     a.hook = b->hook;
-    // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
-    // (TC frames may carry a VLAN tag: the 52-byte window of the generic path)
-    bool fixed = b->hook == PCN_IPT_HOOK_XDP && !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
-                 (reinterpret_cast<uintptr_t>(b->frames) % 16) == 0 &&
-                 (b->n - 1) * uint64_t(b->stride) + 48 <= b->frames_bytes;
     if (!b->offsets) {
       uint64_t last = (b->n - 1) * uint64_t(b->stride);
       if (last >= b->frames_bytes) return fail(-EINVAL, "frames_bytes smaller than n*stride");
@@ -622,8 +636,8 @@ int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
     d.lds_image = kLdsDescBytes;
     d.lds_bins = d.ncounted <= kMaxLdsRuleBins ? 3 : -1;
     const uint32_t nbins = 3 + (d.lds_bins >= 0 ? d.ncounted : 0);
-    const uint32_t tail = (nbins * 8 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * PCN_WAVE_LDS_BYTES;
+    const uint32_t tail = (nbins * 4 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
+                          (PCN_BLOCK / 64) * wave_region_bytes();
     JitShape shape;
     shape.fixed = true;
     shape.lds = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget;

@@ -47,6 +47,7 @@ def child(lib, hit, log2n, iters, cfg, jit):
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
     print(json.dumps({"lib": os.path.basename(lib or "product"), "jit": ipt.jit_info()["launches_jit"] > 0,
                       "defs": os.environ.get("PCN_IPT_JIT_DEFS", ""),
+                      "knobs": {k[14:]: v for k, v in os.environ.items() if k.startswith("PCN_IPT_DEBUG_")},
                       "hit": hit, "ms": ms,
                       "gpkt_s": n / ms / 1e6, "frac": 64 * n / (ms * 1e-3) / 8e12}))
 
@@ -69,6 +70,11 @@ def main():
     for var in a.variants.split(","):
         jit = -1
         env = dict(os.environ)
+        if "@" in var:   # ...@KEY=V;KEY2=V2: PCN_IPT_DEBUG_KEY=V environment knobs
+            var, knobs = var.split("@", 1)
+            for kv in knobs.split(";"):
+                k, v = kv.split("=", 1)
+                env["PCN_IPT_DEBUG_" + k] = v
         if var == "jit":     # the product library's chain program
             lib, jit = "", 1
         elif var.startswith("jit:"):  # jit:-DX=1+-DY=0: chain program built with extra defines
