@@ -56,27 +56,29 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t bswap16u(uint32_t x) { return ((x & 0xff) << 8) | ((x >> 8) & 0xff); }
 
-// Table image accessor: LDS-staged (LDS=true) or read from HBM/L2.
+// Table image accessor.  With LDS, the image prefix [0, limit) is staged in
+// LDS (the whole image, or its per-packet tables when the whole does not fit)
+// and a table at or past `limit` is read from HBM/L2.  Tables never straddle
+// the limit, so the choice depends on the table's base only: a wave-uniform
+// branch in the generic kernel, a constant in a chain program.
 template <bool LDS>
 struct Tab {
   const uint8_t *g;
-  uint32_t base;
-  __device__ __forceinline__ uint32_t u32(uint32_t off) const {
-    return LDS ? *reinterpret_cast<const uint32_t *>(pcn_smem + base + off)
-               : *reinterpret_cast<const uint32_t *>(g + off);
+  uint32_t base;    // LDS byte offset of the image
+  uint32_t limit;   // staged image bytes
+  // `off` may be "negative" (a u32 wrap: the candidate stage addresses PART
+  // through POOL's base), so the image offset is formed in 32 bits first.
+  template <typename T>
+  __device__ __forceinline__ T ld(uint32_t tbl, uint32_t off) const {
+    const uint32_t at = tbl + off;
+    return (LDS && tbl < limit) ? *reinterpret_cast<const T *>(pcn_smem + base + at)
+                                : *reinterpret_cast<const T *>(g + at);
   }
-  __device__ __forceinline__ uint32_t u16(uint32_t off) const {
-    return LDS ? *reinterpret_cast<const uint16_t *>(pcn_smem + base + off)
-               : *reinterpret_cast<const uint16_t *>(g + off);
-  }
-  __device__ __forceinline__ uint32_t u8(uint32_t off) const {
-    return LDS ? *reinterpret_cast<const uint8_t *>(pcn_smem + base + off)
-               : *reinterpret_cast<const uint8_t *>(g + off);
-  }
-  __device__ __forceinline__ uint64_t u64(uint32_t off) const {
-    return LDS ? *reinterpret_cast<const uint64_t *>(pcn_smem + base + off)
-               : *reinterpret_cast<const uint64_t *>(g + off);
-  }
+  __device__ __forceinline__ uint32_t u32(uint32_t tbl, uint32_t off) const { return ld<uint32_t>(tbl, off); }
+  __device__ __forceinline__ uint32_t u16(uint32_t tbl, uint32_t off) const { return ld<uint16_t>(tbl, off); }
+  __device__ __forceinline__ uint32_t u8(uint32_t tbl, uint32_t off) const { return ld<uint8_t>(tbl, off); }
+  __device__ __forceinline__ uint64_t u64(uint32_t tbl, uint32_t off) const { return ld<uint64_t>(tbl, off); }
+  __device__ __forceinline__ u32x4 u128(uint32_t tbl, uint32_t off) const { return ld<u32x4>(tbl, off); }
 };
 
 // Header window as little-endian dwords: bytes 0..47 (the fixed-stride path)
@@ -149,23 +151,23 @@ __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
 template <bool LDS>
 __device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t shift, uint32_t steps,
                                              uint32_t win, uint32_t bnd, uint32_t cls, uint32_t h) {
-  const uint32_t e = t.u32(bkt + 4 * (h >> shift));
+  const uint32_t e = t.u32(bkt, 4 * (h >> shift));
   if (win) {
     const uint32_t first = e & 0xFFFFu;
     uint32_t n = 0;
-    for (uint32_t k = 0; k < win; ++k) n += t.u32(bnd + 4 * (first + k)) <= h ? 1u : 0u;
+    for (uint32_t k = 0; k < win; ++k) n += t.u32(bnd, 4 * (first + k)) <= h ? 1u : 0u;
     const uint32_t count = e >> 16;
-    return t.u16(cls + 2 * (first + (n < count ? n : count)));
+    return t.u16(cls, 2 * (first + (n < count ? n : count)));
   }
   uint32_t lo = e & 0xFFFFu;
   const uint32_t end = lo + (e >> 16);
   for (uint32_t k = steps; k-- > 0;) {
     const uint32_t probe = lo + (1u << k);          // candidate: bnd[lo .. probe) all <= h
     const uint32_t idx = (probe <= end ? probe : lo + 1) - 1;
-    const bool ok = probe <= end && t.u32(bnd + 4 * idx) <= h;
+    const bool ok = probe <= end && t.u32(bnd, 4 * idx) <= h;
     lo = ok ? probe : lo;
   }
-  return t.u16(cls + 2 * lo);
+  return t.u16(cls, 2 * lo);
 }
 
 // Port / iface hash: the key is in its home slot or the next one (the image
@@ -174,7 +176,7 @@ template <bool LDS>
 __device__ __forceinline__ uint32_t key_class(const Tab<LDS> &t, uint32_t tab, uint32_t mask, uint32_t wild,
                                               uint32_t key) {
   const uint32_t h = (key * kHashMul) >> __builtin_clz(mask);
-  const uint32_t e0 = t.u32(tab + 4 * h), e1 = t.u32(tab + 4 * h + 4);
+  const uint32_t e0 = t.u32(tab, 4 * h), e1 = t.u32(tab, 4 * h + 4);
   const bool m0 = e0 != PCN_HASH_EMPTY && (e0 >> 16) == key;
   const bool m1 = e1 != PCN_HASH_EMPTY && (e1 >> 16) == key;
   return m0 ? (e0 & 0xffff) : (m1 ? (e1 & 0xffff) : wild);
@@ -197,7 +199,7 @@ struct Parsed {
 template <bool LDS, int NS>
 __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &p, uint32_t port, uint32_t cls[NS],
                                               uint32_t &verdict, int32_t &rid) {
-  const Tab<LDS> t{ch.image, ch.lds_image};
+  const Tab<LDS> t{ch.image, ch.lds_image, ch.lds_limit};
   const TableLayout &lay = ch.lay;
   const uint32_t present = ch.present;
   const uint32_t all = ch.all_cls;
@@ -206,11 +208,11 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
   uint32_t mi = 0;   // meta index
   if (present & (1u << PCN_IPT_F_CONNTRACK)) {
     if (p.ct > 3) { rid = PCN_IPT_RID_NOCHAIN; verdict = PCN_IPT_DROP; return false; }   // array miss => RX_DROP
-    mi += t.u8(lay.ct_idx + p.ct) * lay.meta_stride[2];
+    mi += t.u8(lay.ct_idx, p.ct) * lay.meta_stride[2];
   }
-  if (present & (1u << PCN_IPT_F_L4PROTO)) mi += t.u8(lay.proto_idx + p.proto) * lay.meta_stride[0];
+  if (present & (1u << PCN_IPT_F_L4PROTO)) mi += t.u8(lay.proto_idx, p.proto) * lay.meta_stride[0];
   if (present & (1u << PCN_IPT_F_TCPFLAGS))                        // TcpFlagsLookup_dp.c:93-97
-    mi += (p.proto == 6 ? t.u16(lay.flags_idx + 2 * p.flags) : lay.flags_skip) * lay.meta_stride[1];
+    mi += (p.proto == 6 ? t.u16(lay.flags_idx, 2 * p.flags) : lay.flags_skip) * lay.meta_stride[1];
   const bool l4 = p.proto == 6 || p.proto == 17;                    // L4PortLookup_dp.c:99-103
   const int key_field[3] = {PCN_IPT_F_SPORT, PCN_IPT_F_DPORT, PCN_IPT_F_IFACE};
   const uint32_t key[3] = {p.sport, p.dport, port};
@@ -227,7 +229,7 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
       for (int f = 3; f < NS; ++f) cls[f] = slot == static_cast<uint32_t>(f) ? x : cls[f];
     }
   }
-  cls[0] = t.u16(lay.meta + 2 * mi);
+  cls[0] = t.u16(lay.meta, 2 * mi);
   if (present & (1u << PCN_IPT_F_IPSRC))
     cls[1] = ip_class(t, lay.ip_bkt[0], lay.ip_shift[0], lay.ip_steps[0], lay.ip_win[0], lay.ip_bnd[0], lay.ip_cls[0], __builtin_bswap32(p.saddr));
   if (present & (1u << PCN_IPT_F_IPDST))
@@ -273,7 +275,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
                                                      WaveScratch *ws) {
   const uint32_t lane = __lane_id();
   if (__ballot(active) == 0) return kNoRule;
-  const Tab<LDS> t{ch.image, ch.lds_image};
+  const Tab<LDS> t{ch.image, ch.lds_image, ch.lds_limit};
   const TableLayout &lay = ch.lay;
   const uint32_t nrw = ch.nrw, nsw = ch.nsw;
   bool staged = false;  // class rows / best slots written (only once some lane has a candidate)
@@ -285,7 +287,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       m = live >= 64 ? ~0ull : ((1ull << live) - 1);
       uint64_t sm[NS];
 #pragma unroll
-      for (int f = 0; f < NS; ++f) sm[f] = t.u64(lay.sf + 16 * (cls[f] * nsw + k));
+      for (int f = 0; f < NS; ++f) sm[f] = t.u64(lay.sf, 16 * (cls[f] * nsw + k));
 #pragma unroll
       for (int f = 0; f < NS; ++f) m &= sm[f];
     }
@@ -355,25 +357,24 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
 #pragma unroll
         for (int f = 0; f < NS; ++f) {
           const uint32_t rec = oc[f] * nsw + k;
-          const u32x4 r = LDS ? *reinterpret_cast<const u32x4 *>(pcn_smem + ch.lds_image + lay.sf + 16 * rec)
-                              : *reinterpret_cast<const u32x4 *>(ch.image + lay.sf + 16 * rec);
+          const u32x4 r = t.u128(lay.sf, 16 * rec);
           const uint64_t pm = (static_cast<uint64_t>(r.y) << 32 | r.x) & ~(static_cast<uint64_t>(r.w) << 32 | r.z);
-          const uint32_t j = t.u32(lay.pbase + 4 * rec) + static_cast<uint32_t>(__builtin_popcountll(pm & below));
+          const uint32_t j = t.u32(lay.pbase, 4 * rec) + static_cast<uint32_t>(__builtin_popcountll(pm & below));
           const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
           if (lay.part_direct) {
             at[f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));
           } else {
-            const bool wide = !LDS && lay.part_wide;
+            const bool wide = lay.part_wide;
             const uint32_t ia = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
-            at[f] = lay.pool + 8 * (wide ? t.u32(ia) : t.u16(ia));
+            at[f] = lay.pool + 8 * (wide ? t.u32(lay.part, ia - lay.part) : t.u16(lay.part, ia - lay.part));
           }
         }
         uint64_t acc = ~0ull;
 #pragma unroll
-        for (int f = 0; f < NS; ++f) acc &= t.u64(at[f]);
+        for (int f = 0; f < NS; ++f) acc &= t.u64(lay.pool, at[f] - lay.pool);   // (PART and POOL are on the same side of the limit)
         if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
           const uint32_t w = k * 64 + bit;
-          const uint32_t e = t.u16(lay.perm + 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
+          const uint32_t e = t.u16(lay.perm, 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
           atomicMin(&ws->best[owner], e);
         }
       }
@@ -440,10 +441,10 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const DevChain &ch = c == CH ? run_ch : a.ch[c];
-      if (!ch.nrules) continue;
+      if (!ch.lds_limit) continue;
       const u32x4 *src = reinterpret_cast<const u32x4 *>(ch.image);
       u32x4 *dst = reinterpret_cast<u32x4 *>(pcn_smem + ch.lds_image);
-      for (uint32_t k = threadIdx.x; k < ch.lay.bytes / 16; k += blockDim.x) dst[k] = src[k];
+      for (uint32_t k = threadIdx.x; k < ch.lds_limit / 16; k += blockDim.x) dst[k] = src[k];
     }
   }
   // pkts[nbins], then (variable lengths only) bytes[nbins]; with a fixed

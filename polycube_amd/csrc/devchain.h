@@ -88,6 +88,8 @@ struct DevChain {
   uint32_t ncounted, max_action;
   int32_t default_action;
   uint32_t lds_image;            // byte offset of this chain's image in LDS
+  uint32_t lds_limit;            // image bytes staged in LDS: all, the per-packet prefix
+                                 // [0, lay.pbase) when the whole does not fit, or 0
   int32_t lds_bins;              // first LDS counter bin of this chain's rules; -1 => global atomics
 };
 

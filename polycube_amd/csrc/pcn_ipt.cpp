@@ -506,9 +506,10 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     if (reach_fw && reach_in) ch = 3;
     else if (reach_in) ch = PCN_IPT_INPUT;
     else if (reach_out) ch = PCN_IPT_OUTPUT;
-    // LDS: the table images of every chain with rules (when they fit; the chain
-    // that runs rules first, at offset 0), then the counter histogram: 3
-    // default bins + rule bins (that chain first, then FORWARD, INPUT, OUTPUT).
+    // LDS: the table images of the chains that run rules in this launch (the
+    // one chain first, at offset 0), then the counter histogram: 3 default
+    // bins + rule bins (that chain first, then FORWARD, INPUT, OUTPUT), then
+    // localip and the per-wave regions.
     int order[3] = {PCN_IPT_FORWARD, PCN_IPT_INPUT, PCN_IPT_OUTPUT};
     if (ch < 3) {
       int k = 1;
@@ -516,10 +517,10 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       for (int c : {PCN_IPT_FORWARD, PCN_IPT_INPUT, PCN_IPT_OUTPUT})
         if (c != ch) order[k++] = c;
     }
-    uint32_t img_bytes = 0;
-    for (int c : order) {
-      if (a.ch[c].nrules) { a.ch[c].lds_image = kLdsDescBytes + img_bytes; img_bytes += a.ch[c].lay.bytes; }
-    }
+    const bool any_rules = reach_fw || reach_in || reach_out;
+    auto runs = [&](int c) {
+      return any_rules && (ch < 3 ? c == ch : (c == PCN_IPT_FORWARD || c == PCN_IPT_INPUT));
+    };
     uint32_t base = 3;
     for (int c : order) {
       uint32_t nc = a.ch[c].ncounted;
@@ -537,16 +538,27 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     const uint32_t bin_bytes = (fixed ? 4 : 8) * a.nbins;
     const uint32_t tail = (bin_bytes + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
                           (PCN_BLOCK / 64) * wave_region_bytes();
-    if (kLdsDescBytes + img_bytes + tail <= kLdsBudget) {
-      a.lds_images_bytes = img_bytes;
-      a.bins_offset = kLdsDescBytes + img_bytes;
-    } else {
-      a.lds_images_bytes = 0;
-      a.bins_offset = kLdsDescBytes;
+    // whole images if they fit, else their per-packet prefix [0, pbase) (the
+    // candidate-stage tables are then read from L2/HBM), else nothing
+    uint32_t img_bytes = 0;
+    for (int mode = 0; mode < 3; ++mode) {
+      img_bytes = 0;
+      for (int c : order) {
+        a.ch[c].lds_image = 0;
+        a.ch[c].lds_limit = 0;
+        if (!runs(c) || mode == 2) continue;
+        a.ch[c].lds_image = kLdsDescBytes + img_bytes;
+        a.ch[c].lds_limit = mode == 0 ? a.ch[c].lay.bytes : a.ch[c].lay.pbase;
+        img_bytes += a.ch[c].lds_limit;
+      }
+      if (mode == 2 || kLdsDescBytes + img_bytes + tail <= kLdsBudget) break;
     }
+    a.lds_images_bytes = img_bytes;
+    a.bins_offset = kLdsDescBytes + img_bytes;
     a.lds_localip = a.bins_offset + (bin_bytes + 15) / 16 * 16;
     a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
-    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * wave_region_bytes();
+    a.wave_bytes = wave_region_bytes();
+    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
     a.offsets = b->offsets;
@@ -638,9 +650,12 @@ int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
     const uint32_t nbins = 3 + (d.lds_bins >= 0 ? d.ncounted : 0);
     const uint32_t tail = (nbins * 4 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
                           (PCN_BLOCK / 64) * wave_region_bytes();
+    d.lds_limit = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget   ? d.lay.bytes
+                  : kLdsDescBytes + d.lay.pbase + tail <= kLdsBudget ? d.lay.pbase
+                                                                     : 0;
     JitShape shape;
     shape.fixed = true;
-    shape.lds = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget;
+    shape.lds = d.lds_limit > 0;
     shape.ch = chain;
     shape.ns = static_cast<int>(d.lay.nslots);
     const std::string spec = jit_spec(d, shape);
