@@ -206,6 +206,55 @@ int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out);
  * pcn_ipt_last_error(). */
 int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain);
 
+/* ---- host ingest ring -------------------------------------------------- */
+/* Frames that start in host memory (a NIC / AF_XDP / AF_PACKET RX ring, a
+ * veth) are received into pinned slots, copied to HBM, classified and their
+ * verdicts copied back, pipelined over HIP streams so PCIe traffic overlaps
+ * the kernels of other slots.  Replaces the per-frame packet entry
+ * (polycubed/src/extiface_xdp.cpp:178-200, cube_xdp.cpp:403-449,
+ * cube_tc.cpp:374-432) for batches.  Producer: acquire -> fill -> submit;
+ * consumer: complete (oldest first) -> read verdicts -> release.  The ring
+ * is used by one producer and one consumer thread; classify counters are
+ * bumped as by pcn_ipt_classify.  Destroy rings before their context. */
+typedef struct pcn_ipt_ring pcn_ipt_ring;
+#define PCN_IPT_RING_RULE_IDS 1u     /* also return matched rule ids */
+typedef struct {
+  uint32_t slots;         /* pinned slots, >= 2 */
+  uint32_t slot_frames;   /* frames per slot, at most */
+  uint64_t slot_bytes;    /* frame bytes per slot */
+  uint32_t streams;       /* HIP streams the slots rotate over (0 => one per slot) */
+  uint32_t flags;         /* PCN_IPT_RING_* */
+} pcn_ipt_ring_config;
+typedef struct {
+  uint32_t slot;
+  uint8_t *frames;        /* pinned host: slot_bytes */
+  uint32_t *offsets;      /* pinned host: slot_frames entries */
+  uint16_t *lens;
+  uint16_t *in_port;
+} pcn_ipt_ring_slot;
+typedef struct {
+  uint64_t n;             /* frames in the slot */
+  uint64_t frames_bytes;  /* bytes to copy (0 => n * stride) */
+  uint32_t stride;
+  uint32_t fixed_len;
+  uint8_t use_offsets, use_lens, use_in_port, reserved;
+  uint16_t const_in_port;
+  uint16_t direction;     /* PCN_IPT_INGRESS / PCN_IPT_EGRESS */
+  uint16_t hook;          /* PCN_IPT_HOOK_XDP / PCN_IPT_HOOK_TC */
+  uint16_t reserved2;
+} pcn_ipt_ring_batch;
+int pcn_ipt_ring_create(pcn_ipt *ctx, const pcn_ipt_ring_config *cfg, pcn_ipt_ring **out);
+void pcn_ipt_ring_destroy(pcn_ipt_ring *ring);
+/* A free slot to fill; -EAGAIN when every slot is in flight or unreleased. */
+int pcn_ipt_ring_acquire(pcn_ipt_ring *ring, pcn_ipt_ring_slot *out);
+/* Copy the filled slot in, classify it, copy its verdicts out (asynchronous). */
+int pcn_ipt_ring_submit(pcn_ipt_ring *ring, uint32_t slot, const pcn_ipt_ring_batch *batch);
+/* The oldest submitted slot's results (pinned host, valid until release).
+ * wait = 0: -EAGAIN while it is in flight; -ENOENT: nothing submitted. */
+int pcn_ipt_ring_complete(pcn_ipt_ring *ring, int wait, uint32_t *slot, uint64_t *n, const uint8_t **verdicts,
+                          const int32_t **rule_ids);
+int pcn_ipt_ring_release(pcn_ipt_ring *ring, uint32_t slot);
+
 /* ---- counters ---------------------------------------------------------- */
 /* Per-rule pkts/bytes (ActionLookup pkts_/bytes_<CHAIN>) and default counters
  * (pkts_/bytes_default_<CHAIN>).  flush != 0 zeroes the per-rule counters after

@@ -29,9 +29,7 @@ int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint
                      hipStream_t stream);
 }  // namespace pcn
 
-namespace {
-
-using namespace pcn;
+namespace pcn {
 
 thread_local std::string g_last_error;
 
@@ -39,6 +37,12 @@ int fail(int code, const std::string &msg) {
   g_last_error = msg;
   return code;
 }
+
+}  // namespace pcn
+
+namespace {
+
+using namespace pcn;
 
 struct HipError : std::runtime_error {
   using std::runtime_error::runtime_error;
@@ -122,6 +126,11 @@ struct pcn_ipt {
   JitCache jit;                                // chain programs (per launch shape)
   uint64_t launches_generic = 0, launches_jit = 0;
 };
+
+namespace pcn {
+// HIP device of a context, or -1 for a control-plane-only context (ring.cpp).
+int device_of(const pcn_ipt *ctx) { return ctx && ctx->has_device ? ctx->cfg.device : -1; }
+}  // namespace pcn
 
 namespace {
 

@@ -1,0 +1,251 @@
+// ring.cpp — host ingest ring: frames that start in host memory (a NIC or
+// AF_XDP/AF_PACKET RX ring, a veth) go through pinned slots to HBM, are
+// classified there, and their verdicts come back to pinned host memory.
+//
+// This is the MI355X counterpart of the reference's packet entry, where the
+// kernel hands each received frame to the cube's first program
+// (extiface_xdp.cpp:178-200 -> cube_xdp.cpp:403-449 handle_rx_xdp_wrapper,
+// cube_tc.cpp:374-432 for TC): instead of one frame per call, a slot of frames
+// per submit, pipelined over HIP streams so the PCIe copies in and out overlap
+// the classify kernels of other slots.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "pcn_ipt.h"
+
+namespace {
+
+enum SlotState { kFree, kFilling, kInFlight, kReturned };
+
+struct Slot {
+  SlotState state = kFree;
+  // pinned host memory
+  uint8_t *h_frames = nullptr;
+  uint32_t *h_offsets = nullptr;
+  uint16_t *h_lens = nullptr;
+  uint16_t *h_in_port = nullptr;
+  uint8_t *h_verdicts = nullptr;
+  int32_t *h_rule_ids = nullptr;
+  // device memory
+  uint8_t *d_frames = nullptr;
+  uint32_t *d_offsets = nullptr;
+  uint16_t *d_lens = nullptr;
+  uint16_t *d_in_port = nullptr;
+  uint8_t *d_verdicts = nullptr;
+  int32_t *d_rule_ids = nullptr;
+  hipEvent_t done = nullptr;
+  uint64_t n = 0;
+};
+
+}  // namespace
+
+namespace pcn {
+int fail(int code, const std::string &msg);   // pcn_ipt.cpp: sets pcn_ipt_last_error()
+int device_of(const pcn_ipt *ctx);
+}  // namespace pcn
+
+namespace {
+int ring_fail(int code, const std::string &msg) { return pcn::fail(code, msg); }
+}  // namespace
+
+struct pcn_ipt_ring {
+  pcn_ipt *ctx = nullptr;
+  int device = 0;
+  pcn_ipt_ring_config cfg{};
+  std::vector<Slot> slots;
+  std::vector<hipStream_t> streams;
+  std::deque<uint32_t> inflight;   // submission order
+  std::mutex mu;
+};
+
+namespace {
+
+void free_slot(Slot &s) {
+  if (s.h_frames) (void)hipHostFree(s.h_frames);
+  if (s.h_offsets) (void)hipHostFree(s.h_offsets);
+  if (s.h_lens) (void)hipHostFree(s.h_lens);
+  if (s.h_in_port) (void)hipHostFree(s.h_in_port);
+  if (s.h_verdicts) (void)hipHostFree(s.h_verdicts);
+  if (s.h_rule_ids) (void)hipHostFree(s.h_rule_ids);
+  if (s.d_frames) (void)hipFree(s.d_frames);
+  if (s.d_offsets) (void)hipFree(s.d_offsets);
+  if (s.d_lens) (void)hipFree(s.d_lens);
+  if (s.d_in_port) (void)hipFree(s.d_in_port);
+  if (s.d_verdicts) (void)hipFree(s.d_verdicts);
+  if (s.d_rule_ids) (void)hipFree(s.d_rule_ids);
+  if (s.done) (void)hipEventDestroy(s.done);
+  s = Slot{};
+}
+
+bool alloc_slot(Slot &s, const pcn_ipt_ring_config &c) {
+  const size_t f = c.slot_frames;
+  bool ok = hipHostMalloc(reinterpret_cast<void **>(&s.h_frames), c.slot_bytes, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(reinterpret_cast<void **>(&s.h_offsets), 4 * f, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(reinterpret_cast<void **>(&s.h_lens), 2 * f, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(reinterpret_cast<void **>(&s.h_in_port), 2 * f, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(reinterpret_cast<void **>(&s.h_verdicts), f, hipHostMallocDefault) == hipSuccess &&
+            hipMalloc(reinterpret_cast<void **>(&s.d_frames), c.slot_bytes) == hipSuccess &&
+            hipMalloc(reinterpret_cast<void **>(&s.d_offsets), 4 * f) == hipSuccess &&
+            hipMalloc(reinterpret_cast<void **>(&s.d_lens), 2 * f) == hipSuccess &&
+            hipMalloc(reinterpret_cast<void **>(&s.d_in_port), 2 * f) == hipSuccess &&
+            hipMalloc(reinterpret_cast<void **>(&s.d_verdicts), f) == hipSuccess &&
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+  if (ok && (c.flags & PCN_IPT_RING_RULE_IDS))
+    ok = hipHostMalloc(reinterpret_cast<void **>(&s.h_rule_ids), 4 * f, hipHostMallocDefault) == hipSuccess &&
+         hipMalloc(reinterpret_cast<void **>(&s.d_rule_ids), 4 * f) == hipSuccess;
+  return ok;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pcn_ipt_ring_create(pcn_ipt *ctx, const pcn_ipt_ring_config *cfg, pcn_ipt_ring **out) {
+  if (!ctx || !cfg || !out) return ring_fail(-EINVAL, "null argument");
+  *out = nullptr;
+  const int device = pcn::device_of(ctx);
+  if (device < 0) return ring_fail(-ENODEV, "context has no HIP device (created with device=-1)");
+  if (cfg->slots < 2 || cfg->slot_frames == 0 || cfg->slot_bytes == 0)
+    return ring_fail(-EINVAL, "need >= 2 slots of >= 1 frame and >= 1 byte");
+  if (cfg->flags & ~uint32_t(PCN_IPT_RING_RULE_IDS)) return ring_fail(-EINVAL, "unknown ring flags");
+  if (hipSetDevice(device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
+  auto *r = new pcn_ipt_ring();
+  r->ctx = ctx;
+  r->device = device;
+  r->cfg = *cfg;
+  if (!r->cfg.streams || r->cfg.streams > r->cfg.slots) r->cfg.streams = r->cfg.slots;
+  r->slots.resize(r->cfg.slots);
+  bool ok = true;
+  for (auto &s : r->slots) ok = ok && alloc_slot(s, r->cfg);
+  for (uint32_t k = 0; ok && k < r->cfg.streams; ++k) {
+    hipStream_t st = nullptr;
+    ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+    if (ok) r->streams.push_back(st);
+  }
+  if (!ok) {
+    (void)hipGetLastError();
+    pcn_ipt_ring_destroy(r);
+    return ring_fail(-ENOMEM, "ring allocation failed (pinned host or device memory)");
+  }
+  *out = r;
+  return 0;
+}
+
+void pcn_ipt_ring_destroy(pcn_ipt_ring *r) {
+  if (!r) return;
+  (void)hipSetDevice(r->device);
+  for (hipStream_t st : r->streams) (void)hipStreamSynchronize(st);
+  for (auto &s : r->slots) free_slot(s);
+  for (hipStream_t st : r->streams) (void)hipStreamDestroy(st);
+  delete r;
+}
+
+int pcn_ipt_ring_acquire(pcn_ipt_ring *r, pcn_ipt_ring_slot *out) {
+  if (!r || !out) return ring_fail(-EINVAL, "null argument");
+  std::lock_guard<std::mutex> l(r->mu);
+  for (uint32_t k = 0; k < r->slots.size(); ++k) {
+    Slot &s = r->slots[k];
+    if (s.state != kFree) continue;
+    s.state = kFilling;
+    out->slot = k;
+    out->frames = s.h_frames;
+    out->offsets = s.h_offsets;
+    out->lens = s.h_lens;
+    out->in_port = s.h_in_port;
+    return 0;
+  }
+  return ring_fail(-EAGAIN, "every slot is in flight or not yet released");
+}
+
+int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch *b) {
+  if (!r || !b) return ring_fail(-EINVAL, "null argument");
+  std::lock_guard<std::mutex> l(r->mu);
+  if (slot >= r->slots.size() || r->slots[slot].state != kFilling) return ring_fail(-EINVAL, "slot not acquired");
+  Slot &s = r->slots[slot];
+  if (b->n > r->cfg.slot_frames) return ring_fail(-EINVAL, "more frames than the slot holds");
+  const uint64_t bytes = b->frames_bytes ? b->frames_bytes : b->n * uint64_t(b->stride);
+  if (bytes > r->cfg.slot_bytes) return ring_fail(-EINVAL, "frame bytes exceed the slot");
+  if (hipSetDevice(r->device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
+  hipStream_t st = r->streams[slot % r->streams.size()];
+  const size_t n = b->n;
+  // PCIe in: frames and the per-frame arrays the batch uses
+  bool ok = hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (ok && b->use_offsets) ok = hipMemcpyAsync(s.d_offsets, s.h_offsets, 4 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (ok && b->use_lens) ok = hipMemcpyAsync(s.d_lens, s.h_lens, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (ok && b->use_in_port) ok = hipMemcpyAsync(s.d_in_port, s.h_in_port, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+  if (!ok) return ring_fail(-EIO, "hipMemcpyAsync (H2D) failed");
+  pcn_ipt_batch batch{};
+  batch.frames = s.d_frames;
+  batch.frames_bytes = bytes;
+  batch.offsets = b->use_offsets ? s.d_offsets : nullptr;
+  batch.lens = b->use_lens ? s.d_lens : nullptr;
+  batch.stride = b->stride;
+  batch.fixed_len = b->fixed_len;
+  batch.in_port = b->use_in_port ? s.d_in_port : nullptr;
+  batch.const_in_port = b->const_in_port;
+  batch.direction = b->direction;
+  batch.hook = b->hook;
+  batch.n = n;
+  batch.verdicts = s.d_verdicts;
+  batch.rule_ids = s.d_rule_ids;
+  if (n) {
+    const int rc = pcn_ipt_classify(r->ctx, &batch, st);
+    if (rc) return ring_fail(rc, std::string("classify: ") + pcn_ipt_last_error());
+  }
+  // PCIe out: verdicts (and rule ids)
+  ok = hipMemcpyAsync(s.h_verdicts, s.d_verdicts, n, hipMemcpyDeviceToHost, st) == hipSuccess;
+  if (ok && s.d_rule_ids) ok = hipMemcpyAsync(s.h_rule_ids, s.d_rule_ids, 4 * n, hipMemcpyDeviceToHost, st) == hipSuccess;
+  if (ok) ok = hipEventRecord(s.done, st) == hipSuccess;
+  if (!ok) return ring_fail(-EIO, "hipMemcpyAsync (D2H) / hipEventRecord failed");
+  s.n = n;
+  s.state = kInFlight;
+  r->inflight.push_back(slot);
+  return 0;
+}
+
+int pcn_ipt_ring_complete(pcn_ipt_ring *r, int wait, uint32_t *slot, uint64_t *n, const uint8_t **verdicts,
+                          const int32_t **rule_ids) {
+  if (!r) return ring_fail(-EINVAL, "null ring");
+  uint32_t k;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> l(r->mu);
+    if (r->inflight.empty()) return ring_fail(-ENOENT, "nothing in flight");
+    k = r->inflight.front();
+    ev = r->slots[k].done;
+  }
+  if (hipSetDevice(r->device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
+  if (wait) {
+    if (hipEventSynchronize(ev) != hipSuccess) return ring_fail(-EIO, "hipEventSynchronize failed");
+  } else {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipErrorNotReady) return ring_fail(-EAGAIN, "oldest slot still in flight");
+    if (q != hipSuccess) return ring_fail(-EIO, "hipEventQuery failed");
+  }
+  std::lock_guard<std::mutex> l(r->mu);
+  r->inflight.pop_front();
+  Slot &s = r->slots[k];
+  s.state = kReturned;
+  if (slot) *slot = k;
+  if (n) *n = s.n;
+  if (verdicts) *verdicts = s.h_verdicts;
+  if (rule_ids) *rule_ids = s.h_rule_ids;
+  return 0;
+}
+
+int pcn_ipt_ring_release(pcn_ipt_ring *r, uint32_t slot) {
+  if (!r) return ring_fail(-EINVAL, "null ring");
+  std::lock_guard<std::mutex> l(r->mu);
+  if (slot >= r->slots.size() || (r->slots[slot].state != kReturned && r->slots[slot].state != kFilling))
+    return ring_fail(-EINVAL, "slot is not held by the caller");
+  r->slots[slot].state = kFree;
+  return 0;
+}
+
+}  // extern "C"

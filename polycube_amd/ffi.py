@@ -53,6 +53,23 @@ class JitInfo(C.Structure):
                 ("programs_ready", C.c_uint32), ("programs_failed", C.c_uint32)]
 
 
+class RingConfig(C.Structure):
+    _fields_ = [("slots", C.c_uint32), ("slot_frames", C.c_uint32), ("slot_bytes", C.c_uint64),
+                ("streams", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class RingSlot(C.Structure):
+    _fields_ = [("slot", C.c_uint32), ("frames", C.POINTER(C.c_uint8)), ("offsets", C.POINTER(C.c_uint32)),
+                ("lens", C.POINTER(C.c_uint16)), ("in_port", C.POINTER(C.c_uint16))]
+
+
+class RingBatch(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("frames_bytes", C.c_uint64), ("stride", C.c_uint32), ("fixed_len", C.c_uint32),
+                ("use_offsets", C.c_uint8), ("use_lens", C.c_uint8), ("use_in_port", C.c_uint8),
+                ("reserved", C.c_uint8), ("const_in_port", C.c_uint16), ("direction", C.c_uint16),
+                ("hook", C.c_uint16), ("reserved2", C.c_uint16)]
+
+
 class ChainInfo(C.Structure):
     _fields_ = [("nrules", C.c_uint32), ("nrw", C.c_uint32), ("nsw", C.c_uint32), ("nvec", C.c_uint32),
                 ("ngroups", C.c_uint32), ("present", C.c_uint32), ("table_bytes", C.c_uint32),
@@ -95,6 +112,13 @@ SIGNATURES = {
                                       C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64)]),
     "pcn_ipt_chain_reset_counters": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_ring_create": (C.c_int, [C.c_void_p, C.POINTER(RingConfig), C.POINTER(C.c_void_p)]),
+    "pcn_ipt_ring_destroy": (None, [C.c_void_p]),
+    "pcn_ipt_ring_acquire": (C.c_int, [C.c_void_p, C.POINTER(RingSlot)]),
+    "pcn_ipt_ring_submit": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(RingBatch)]),
+    "pcn_ipt_ring_complete": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.POINTER(C.c_int32))]),
+    "pcn_ipt_ring_release": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pcn_ipt_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "pcn_ipt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     "pcn_ipt_sync_counters": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -218,6 +218,10 @@ class Iptables:
     def synchronize(self):
         _check(ffi.lib().pcn_ipt_synchronize(self._h))
 
+    def ring(self, slots=4, slot_frames=1 << 20, slot_bytes=None, streams=0, rule_ids=False):
+        """Host ingest ring (pcn_ipt_ring_*): pinned slots -> HBM -> classify -> verdicts."""
+        return IngestRing(self, slots, slot_frames, slot_bytes or 64 * slot_frames, streams, rule_ids)
+
     # ---- multi-GPU counters over RCCL ----
     @staticmethod
     def comm_unique_id():
@@ -231,3 +235,66 @@ class Iptables:
 
     def sync_counters(self, stream=None):
         _check(ffi.lib().pcn_ipt_sync_counters(self._h, stream))
+
+
+class IngestRing:
+    """Pinned host slots feeding the GPU classifier (include/pcn_ipt.h, ring).
+
+    acquire() returns (slot, frames, offsets, lens, in_port) as numpy views of
+    the slot's pinned memory; submit(slot, n, ...) copies it in and classifies
+    it; complete() returns the oldest slot's (slot, verdicts[, rule_ids]) views,
+    valid until release(slot)."""
+
+    def __init__(self, ipt, slots, slot_frames, slot_bytes, streams, rule_ids):
+        import numpy as np
+        self._np = np
+        self._ipt = ipt
+        self.slot_frames = slot_frames
+        self.slot_bytes = slot_bytes
+        cfg = ffi.RingConfig(slots, slot_frames, slot_bytes, streams, 1 if rule_ids else 0)
+        h = C.c_void_p()
+        _check(ffi.lib().pcn_ipt_ring_create(ipt._h, C.byref(cfg), C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            ffi.lib().pcn_ipt_ring_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def acquire(self):
+        np = self._np
+        s = ffi.RingSlot()
+        _check(ffi.lib().pcn_ipt_ring_acquire(self._h, C.byref(s)))
+        f = self.slot_frames
+        return (s.slot, np.ctypeslib.as_array(s.frames, (self.slot_bytes,)),
+                np.ctypeslib.as_array(s.offsets, (f,)), np.ctypeslib.as_array(s.lens, (f,)),
+                np.ctypeslib.as_array(s.in_port, (f,)))
+
+    def submit(self, slot, n, *, frames_bytes=0, stride=64, fixed_len=64, offsets=False, lens=False,
+               in_port=False, const_in_port=1, direction=INGRESS, hook=XDP):
+        b = ffi.RingBatch(n, frames_bytes, stride, fixed_len, int(offsets), int(lens), int(in_port), 0,
+                          const_in_port, direction, hook, 0)
+        _check(ffi.lib().pcn_ipt_ring_submit(self._h, slot, C.byref(b)))
+
+    def complete(self, wait=True):
+        """(slot, verdicts, rule_ids or None), or None when nothing is ready (wait=False)."""
+        np = self._np
+        slot, n = C.c_uint32(), C.c_uint64()
+        v, r = C.POINTER(C.c_uint8)(), C.POINTER(C.c_int32)()
+        rc = ffi.lib().pcn_ipt_ring_complete(self._h, int(wait), C.byref(slot), C.byref(n), C.byref(v), C.byref(r))
+        if rc == -11 and not wait:     # -EAGAIN
+            return None
+        _check(rc)
+        k = int(n.value)
+        verdicts = np.ctypeslib.as_array(v, (k,)) if k else np.zeros(0, np.uint8)
+        rids = np.ctypeslib.as_array(r, (k,)) if (k and bool(r)) else None
+        return slot.value, verdicts, rids
+
+    def release(self, slot):
+        _check(ffi.lib().pcn_ipt_ring_release(self._h, slot))

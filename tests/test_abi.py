@@ -63,6 +63,15 @@ def test_chain_program_compiles_without_a_device():
     ipt.close()
 
 
+def test_ingest_ring_needs_a_device():
+    from polycube_amd import Iptables, IptablesError
+    ipt = Iptables(device=-1)
+    with pytest.raises(IptablesError) as e:
+        ipt.ring(slots=2, slot_frames=16)
+    assert e.value.code == -19
+    ipt.close()
+
+
 def test_null_context_is_an_error():
     assert ffi.lib().pcn_ipt_chain_flush(None, 0) < 0
     assert b"null" in ffi.lib().pcn_ipt_last_error()

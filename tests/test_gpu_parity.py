@@ -334,3 +334,43 @@ def test_localip_input_output_from_lds(dev):
         v_o, r_o, v_g, r_g = run_both(o, ipt, dev, frames.reshape(-1), n, direction=direction)
         assert_same(v_o, r_o, v_g, r_g)
     assert_counters(o, ipt)
+
+
+def test_ingest_ring_parity(dev):
+    """Host ingest ring: frames filled into pinned slots, copied in, classified
+    and the verdicts / rule ids copied back -- fixed-stride slots and IMIX
+    slots (offsets, lens, in_port, TC hook) interleaved; equal to the oracle,
+    counters included."""
+    rs = synth.config_rules(2)
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
+    ring = ipt.ring(slots=3, slot_frames=1 << 14, slot_bytes=(1 << 14) * 1600, rule_ids=True)
+    expect = {}
+    for k in range(8):
+        slot, frames, offsets, lens, in_port = ring.acquire()
+        n = (1 << 14) - 37 * k
+        if k % 2 == 0:
+            f = synth.config_frames(2, n, rs, seed=k).reshape(-1)
+            frames[:f.size] = f
+            ring.submit(slot, n)
+            expect[slot] = o.classify(f, n=n, nthreads=NTHREADS)
+        else:
+            buf, off, ln = synth.imix_frames(rs, n, 40 + k)
+            frames[:buf.size] = buf
+            offsets[:n] = off
+            lens[:n] = ln
+            ports = np.random.default_rng(k).choice(np.array([0, 1, 2], np.uint16), size=n)
+            in_port[:n] = ports
+            ring.submit(slot, n, frames_bytes=buf.size, offsets=True, lens=True, in_port=True, hook=1)
+            expect[slot] = o.classify(buf, n=n, offsets=off, lens=ln, in_port=ports, hook=1, nthreads=NTHREADS)
+        if k >= 2:
+            done, v, r = ring.complete()
+            v_o, r_o = expect.pop(done)
+            assert_same(v_o, r_o, v.copy(), r.copy())
+            ring.release(done)
+    while expect:
+        done, v, r = ring.complete()
+        v_o, r_o = expect.pop(done)
+        assert_same(v_o, r_o, v.copy(), r.copy())
+        ring.release(done)
+    ring.close()
+    assert_counters(o, ipt)
