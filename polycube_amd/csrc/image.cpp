@@ -28,6 +28,19 @@ constexpr uint32_t kIpWindowMax = 4;           // IP buckets read whole up to th
 bool compact_images() {
   static const bool v = std::getenv("PCN_IPT_DEBUG_COMPACT") != nullptr;
   return v;
+}
+// ... PCN_IPT_DEBUG_IPSEARCH=1: searched IP buckets only; PCN_IPT_DEBUG_JOIN=m:
+// join exactly the key fields in mask m (1 sport, 2 dport, 4 iface) to META.
+bool ip_search_only() {
+  static const bool v = std::getenv("PCN_IPT_DEBUG_IPSEARCH") != nullptr;
+  return v;
+}
+int forced_join() {
+  static const int v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_JOIN");
+    return e ? std::atoi(e) : -1;
+  }();
+  return v;
 }   // images up to this size store partial words directly
 
 inline uint32_t host_order(uint32_t nbo) { return __builtin_bswap32(nbo); }
@@ -262,7 +275,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     // usually share a bucket, so this is the common case.
     uint32_t bits = 0, win = 0;
     const uint32_t max_bits = compact_images() ? 10 : PCN_IP_BUCKET_BITS_MAX;
-    for (uint32_t b = 4; b <= max_bits && !bits && !compact_images(); ++b)
+    for (uint32_t b = 4; b <= max_bits && !bits && !compact_images() && !ip_search_only(); ++b)
       if (max_count(first_of(b)) <= kIpWindowMax) bits = b;
     if (bits) {
       win = std::max(1u, max_count(first_of(bits)));
@@ -529,6 +542,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
 // field at a time, while the image keeps its partial words direct (i.e.
 // stays within kDirectMaxBytes, comfortably inside LDS).
 HostImage build_image(const ChainTables &t) {
+  if (forced_join() >= 0) return build_image_with(t, static_cast<uint32_t>(forced_join()));
   HostImage best = build_image_with(t, 0);
   if (t.nrules == 0 || !best.lay.part_direct) return best;
   uint32_t join = 0;

@@ -23,7 +23,8 @@ def child(lib, hit, log2n, iters, cfg, jit):
         ffi.LIB_PATH = lib
     from polycube_amd import Iptables, synth
     rs = synth.config_rules(cfg)
-    ipt = Iptables(device=0, jit=jit)
+    big = dict(max_rules=16384, max_counted_rules=10000, max_action_rules=10000) if cfg == 5 else {}
+    ipt = Iptables(device=0, jit=jit, **big)
     ipt.interactive = False
     fw = ipt.chain("FORWARD")
     for r in rs.rules():
@@ -31,17 +32,24 @@ def child(lib, hit, log2n, iters, cfg, jit):
     fw.default = "DROP"
     fw.apply_rules()
     n = 1 << log2n
-    cols = synth.make_headers(rs, n, synth.CONFIG_SEEDS[3], hit_frac=hit,
-                              protos=(6, 17) if cfg == 3 else (17,))
-    frames = torch.from_numpy(synth.build_frames(*cols).reshape(-1)).cuda()
+    kw = {}
+    if cfg == 5:      # IMIX offsets/lens, TC hook when CFG5_HOOK=tc
+        buf, off, ln = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5])
+        frames = torch.from_numpy(buf).cuda()
+        kw = dict(offsets=torch.from_numpy(off.view(np.int32)).cuda(), lens=torch.from_numpy(ln.view(np.int16)).cuda(),
+                  hook=1 if os.environ.get("CFG5_HOOK") == "tc" else 0)
+    else:
+        cols = synth.make_headers(rs, n, synth.CONFIG_SEEDS[3], hit_frac=hit,
+                                  protos=(6, 17) if cfg == 3 else (17,))
+        frames = torch.from_numpy(synth.build_frames(*cols).reshape(-1)).cuda()
     v = torch.empty(n, dtype=torch.uint8, device="cuda")
     for _ in range(3):
-        ipt.classify(frames, n=n, verdicts=v, rule_ids=False)
+        ipt.classify(frames, n=n, verdicts=v, rule_ids=False, **kw)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
     for a, b in evs:
         a.record()
-        ipt.classify(frames, n=n, verdicts=v, rule_ids=False)
+        ipt.classify(frames, n=n, verdicts=v, rule_ids=False, **kw)
         b.record()
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
