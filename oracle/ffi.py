@@ -50,8 +50,23 @@ def lib():
         h.orc_chain_nrw.restype = C.c_uint32
         h.orc_chain_nrw.argtypes = [vp, C.c_int]
         h.orc_index64.argtypes = [u16p]
+        h.orc_ct_enable.argtypes = [vp, C.c_int]
+        h.orc_ct_set_time.argtypes = [vp, C.c_uint64]
+        h.orc_ct_dump.argtypes = [vp, vp, C.c_uint32]
+        h.orc_apply_accept_established.argtypes = [vp, C.c_int]
+        h.orc_set_accept_established.argtypes = [vp, C.c_int, C.c_int]
+        h.orc_get_accept_established.argtypes = [vp, C.c_int]
+        h.orc_read_accept_established.argtypes = [vp, C.c_int, u64p, u64p, C.c_int]
         _lib = h
     return _lib
+
+
+# orc_ct_entry / pcn_ipt_ct_entry (same layout)
+CT_ENTRY = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
+                     ("l4proto", "u1"), ("state", "u1"), ("ip_rev", "u1"), ("port_rev", "u1"),
+                     ("sequence", "<u4"), ("ttl", "<u8")], align=True)
+CT_STATES = ["NEW", "ESTABLISHED", "RELATED", "INVALID", "SYN_SENT", "SYN_RECV", "FIN_WAIT_1",
+             "FIN_WAIT_2", "LAST_ACK", "TIME_WAIT"]
 
 
 def _enc(v):
@@ -120,6 +135,33 @@ class Oracle:
         dp, db = C.c_uint64(), C.c_uint64()
         lib().orc_read_counters(self._h, chain, pk, by, n, C.byref(dp), C.byref(db), int(flush))
         return list(pk[:n]), list(by[:n]), dp.value, db.value
+
+    # ---- stateful conntrack ----
+    def ct_enable(self, on=True):
+        assert lib().orc_ct_enable(self._h, int(on)) == 0
+
+    def ct_set_time(self, ns):
+        assert lib().orc_ct_set_time(self._h, int(ns)) == 0
+
+    def ct_dump(self, cap=1 << 20):
+        out = np.zeros(cap, CT_ENTRY)
+        n = lib().orc_ct_dump(self._h, out.ctypes.data, cap)
+        assert n >= 0, n
+        return out[:n]
+
+    def apply_accept_established(self, chain):
+        assert lib().orc_apply_accept_established(self._h, chain) == 0
+
+    def set_accept_established(self, chain, on):
+        assert lib().orc_set_accept_established(self._h, chain, int(on)) == 0
+
+    def accept_established(self, chain):
+        return bool(lib().orc_get_accept_established(self._h, chain))
+
+    def read_accept_established(self, chain, flush=False):
+        pk, by = C.c_uint64(), C.c_uint64()
+        lib().orc_read_accept_established(self._h, chain, C.byref(pk), C.byref(by), int(flush))
+        return pk.value, by.value
 
     def export_map(self, chain, field, cap=70000):
         nrw = lib().orc_chain_nrw(self._h, chain)

@@ -94,6 +94,10 @@ struct orc_ctx {
   uint32_t max_counted, max_action;
   uint16_t index64[64];
   pthread_mutex_t mu;
+  /* stateful conntrack (see "conntrack" below) */
+  struct ctstate *ct;
+  int ae[NCHAINS];                       /* accept_established_enabled_<chain>_ (Iptables.h) */
+  uint64_t ae_pkts[NCHAINS], ae_bytes[NCHAINS]; /* pkts_/bytes_acceptestablished_<Chain> */
 };
 
 /* ---------------- rule parsing ---------------- */
@@ -494,8 +498,10 @@ orc_ctx *orc_create(uint32_t max_counted, uint32_t max_action) {
   return c;
 }
 
+static void ct_free(struct ctstate *t);
 void orc_destroy(orc_ctx *c) {
   if (!c) return;
+  ct_free(c->ct);
   for (int i = 0; i < NCHAINS; i++) chain_free(&c->ch[i]);
   free(c);
 }
@@ -567,6 +573,7 @@ int orc_read_counters(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes, ui
 typedef struct {        /* per-CPU counters (percpu arrays) */
   uint64_t *pkts[NCHAINS], *bytes[NCHAINS];
   uint64_t dpk[NCHAINS], dby[NCHAINS];
+  uint64_t ae_pkts[NCHAINS], ae_bytes[NCHAINS];   /* pkts_/bytes_acceptestablished_<Chain> */
 } pcpu_t;
 
 static inline uint16_t be16(const uint8_t *p) { return (uint16_t)(p[0] << 8 | p[1]); }
@@ -586,6 +593,286 @@ static int ct_label_empty(int proto, uint8_t flags, int icmp_type) {
   return CT_INVALID;                         /* :562-566 */
 }
 
+/* ---------------- conntrack (stateful mode) ----------------
+ * The `connections` table (Iptables_ConntrackLabel_dp.c:111-113: BPF lru_hash
+ * of 65536 `ct_k` -> `ct_v`), ConntrackLabel (:190-531) and
+ * ConntrackTableUpdate (Iptables_ConntrackTableUpdate_dp.c:141-655), run for
+ * one packet at a time in batch order, as one CPU would run them.
+ *  - Entries never expire: the datapath writes `ttl` but nothing compares it
+ *    (the control plane only lists it, Iptables.cpp:527-566).  `now` is the
+ *    `timestamp` percpu value the control plane refreshes every second
+ *    (modules/ConntrackTableUpdate.cpp:108-137); tests set it explicitly.
+ *  - The table here is unbounded: parity with the kernel LRU holds while the
+ *    live flows fit its 65536 entries (LRU eviction is not restated).
+ *  - `packet` is one per-CPU struct shared by ingress and egress
+ *    (Iptables_Parser_dp.c:44-56): the Parser writes srcPort/dstPort only for
+ *    TCP/UDP (:122-143), so an ICMP packet's conntrack key carries the ports
+ *    of the last TCP/UDP packet parsed before it (quirk Q4). */
+enum { ST_NEW = 0, ST_ESTABLISHED, ST_RELATED, ST_INVALID, ST_SYN_SENT, ST_SYN_RECV,
+       ST_FIN_WAIT_1, ST_FIN_WAIT_2, ST_LAST_ACK, ST_TIME_WAIT };
+#define TCPHDR_FIN 0x01
+#define TCPHDR_SYN 0x02
+#define TCPHDR_RST 0x04
+#define TCPHDR_ACK 0x10
+#define HEX_BE_ONE 0x1000000u
+/* ConntrackTableUpdate_dp.c:38-48 (ns) */
+#define UDP_ESTABLISHED_TIMEOUT 180000000000ull
+#define UDP_NEW_TIMEOUT 30000000000ull
+#define ICMP_TIMEOUT 30000000000ull
+#define TCP_ESTABLISHED 432000000000000ull
+#define TCP_SYN_SENT 120000000000ull
+#define TCP_SYN_RECV 60000000000ull
+#define TCP_LAST_ACK 30000000000ull
+#define TCP_FIN_WAIT 120000000000ull
+
+typedef struct { uint32_t src, dst; uint8_t proto; uint16_t sport, dport; } ctk_t;  /* struct ct_k */
+typedef struct { uint64_t ttl; uint8_t state, ipRev, portRev; uint32_t seq; } ctv_t; /* struct ct_v */
+typedef struct { ctk_t k; ctv_t v; int used; } cte_t;    /* used: 0 empty, 1 live, 2 deleted */
+
+struct ctstate {
+  cte_t *tab; size_t cap, live, used;
+  uint64_t now;
+  /* the shared per-CPU `packet` struct: fields the Parser leaves stale */
+  uint16_t sport, dport; uint32_t seq, ack; uint8_t flags;
+};
+
+static void ct_free(struct ctstate *t) {
+  if (!t) return;
+  free(t->tab); free(t);
+}
+
+static uint64_t ctk_hash(const ctk_t *k) {
+  uint64_t h = ((uint64_t)k->src << 32 | k->dst) * 0x9E3779B97F4A7C15ull;
+  h ^= ((uint64_t)k->proto << 32 | (uint64_t)k->sport << 16 | k->dport) * 0xC2B2AE3D27D4EB4Full;
+  return h ^ (h >> 29);
+}
+static int ctk_eq(const ctk_t *a, const ctk_t *b) {
+  return a->src == b->src && a->dst == b->dst && a->proto == b->proto && a->sport == b->sport &&
+         a->dport == b->dport;
+}
+static cte_t *ct_find(struct ctstate *t, const ctk_t *k) {     /* connections.lookup */
+  if (!t->cap) return NULL;
+  for (size_t i = ctk_hash(k) & (t->cap - 1), s = 0; s < t->cap; s++, i = (i + 1) & (t->cap - 1)) {
+    cte_t *e = &t->tab[i];
+    if (e->used == 0) return NULL;
+    if (e->used == 1 && ctk_eq(&e->k, k)) return e;
+  }
+  return NULL;
+}
+static void ct_grow(struct ctstate *t) {
+  size_t oc = t->cap;
+  cte_t *old = t->tab;
+  t->cap = oc ? oc * 2 : 1024;
+  t->tab = calloc(t->cap, sizeof(cte_t));
+  t->used = t->live = 0;
+  for (size_t i = 0; i < oc; i++) {
+    if (old[i].used != 1) continue;
+    size_t j = ctk_hash(&old[i].k) & (t->cap - 1);
+    while (t->tab[j].used) j = (j + 1) & (t->cap - 1);
+    t->tab[j] = old[i];
+    t->used++; t->live++;
+  }
+  free(old);
+}
+/* connections.update (BPF_ANY) / .insert (BPF_NOEXIST: an existing key is left as is) */
+static void ct_put(struct ctstate *t, const ctk_t *k, const ctv_t *v, int noexist) {
+  cte_t *e = ct_find(t, k);
+  if (e) { if (!noexist) e->v = *v; return; }
+  if ((t->used + 1) * 2 > t->cap) ct_grow(t);
+  size_t i = ctk_hash(k) & (t->cap - 1);
+  while (t->tab[i].used == 1) i = (i + 1) & (t->cap - 1);
+  if (t->tab[i].used == 0) t->used++;
+  t->tab[i].k = *k; t->tab[i].v = *v; t->tab[i].used = 1;
+  t->live++;
+}
+static void ct_delete(struct ctstate *t, const ctk_t *k) {        /* connections.delete */
+  cte_t *e = ct_find(t, k);
+  if (e) { e->used = 2; t->live--; }
+}
+
+typedef struct {          /* struct packetHeaders as the conntrack modules read it */
+  uint32_t src, dst; uint8_t proto; uint16_t sport, dport; uint8_t flags; uint32_t seq, ack;
+} ctpkt_t;
+
+/* ConntrackLabel_dp.c:200-228 and ConntrackTableUpdate_dp.c:166-194: the key
+ * orders IPs and ports as little-endian loads of their network-order bytes. */
+static ctk_t ct_key(const ctpkt_t *p, uint8_t *ipRev, uint8_t *portRev) {
+  ctk_t k;
+  if (p->src <= p->dst) { k.src = p->src; k.dst = p->dst; *ipRev = 0; }
+  else { k.src = p->dst; k.dst = p->src; *ipRev = 1; }
+  k.proto = p->proto;
+  if (p->sport < p->dport) { k.sport = p->sport; k.dport = p->dport; *portRev = 0; }
+  else if (p->sport > p->dport) { k.sport = p->dport; k.dport = p->sport; *portRev = 1; }
+  else { k.sport = p->sport; k.dport = p->dport; *portRev = *ipRev; }
+  return k;
+}
+static inline int syn_only(uint8_t f) { return (f & TCPHDR_SYN) && (f | TCPHDR_SYN) == TCPHDR_SYN; }
+static inline int ack_only(uint8_t f) { return (f & TCPHDR_ACK) && (f | TCPHDR_ACK) == TCPHDR_ACK; }
+static inline int synack_only(uint8_t f) {
+  return (f & TCPHDR_ACK) && (f & TCPHDR_SYN) && (f | (TCPHDR_SYN | TCPHDR_ACK)) == (TCPHDR_SYN | TCPHDR_ACK);
+}
+static inline uint16_t ld16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+
+/* ConntrackLabel_dp.c:190-531: the packet's connStatus, or -1 for RX_DROP
+ * (the ICMP length checks, :441-443, :486-505). */
+static int ct_label(struct ctstate *t, const ctpkt_t *p, const uint8_t *f, uint32_t L) {
+  uint8_t ipRev, portRev;
+  ctk_t key = ct_key(p, &ipRev, &portRev);
+  cte_t *e;
+  if (p->proto == 6) {
+    e = ct_find(t, &key);
+    if (e && e->v.ipRev == ipRev && e->v.portRev == portRev) {            /* TCP_FORWARD :245 */
+      if (p->flags & TCPHDR_RST) return ST_ESTABLISHED;
+      uint8_t s = e->v.state;
+      if (s == ST_SYN_SENT) return syn_only(p->flags) ? ST_NEW : ST_INVALID;
+      if (s == ST_SYN_RECV) return ack_only(p->flags) && p->ack == e->v.seq ? ST_ESTABLISHED : ST_INVALID;
+      if (s == ST_ESTABLISHED || s == ST_FIN_WAIT_1 || s == ST_FIN_WAIT_2 || s == ST_LAST_ACK)
+        return ST_ESTABLISHED;
+      if (s == ST_TIME_WAIT && syn_only(p->flags)) return ST_NEW;
+      return ST_INVALID;
+    }
+    if (e && e->v.ipRev != ipRev && e->v.portRev != portRev) {            /* TCP_REVERSE :310 */
+      if (p->flags & TCPHDR_RST) return ST_ESTABLISHED;
+      uint8_t s = e->v.state;
+      if (s == ST_SYN_SENT || s == ST_SYN_RECV)
+        return synack_only(p->flags) && p->ack == e->v.seq ? ST_ESTABLISHED : ST_INVALID;
+      if (s == ST_ESTABLISHED || s == ST_FIN_WAIT_1 || s == ST_FIN_WAIT_2 || s == ST_LAST_ACK)
+        return ST_ESTABLISHED;
+      if (s == ST_TIME_WAIT && syn_only(p->flags)) return ST_NEW;
+      return ST_INVALID;
+    }
+    return syn_only(p->flags) ? ST_NEW : ST_INVALID;                      /* TCP_MISS :372-383 */
+  }
+  if (p->proto == 17) {
+    e = ct_find(t, &key);
+    if (e && e->v.ipRev == ipRev && e->v.portRev == portRev)              /* UDP_FORWARD */
+      return e->v.state == ST_NEW ? ST_NEW : ST_ESTABLISHED;
+    if (e && e->v.ipRev != ipRev && e->v.portRev != portRev) return ST_ESTABLISHED; /* UDP_REVERSE */
+    return ST_NEW;                                                       /* UDP_MISS */
+  }
+  if (p->proto == 1) {
+    if (L < 42) return -1;
+    uint8_t type = f[34];
+    if (type == 8) return ST_NEW;
+    if (type == 0) {
+      e = ct_find(t, &key);
+      if (!e) return ST_INVALID;
+      if (e->v.ipRev != ipRev && e->v.portRev != portRev) return ST_ESTABLISHED;
+      /* else ICMP_MISS (:468) */
+    }
+    if (type >= 13 && type <= 18) return ST_INVALID;
+    if (L < 62) return -1;
+    /* the encapsulated IP header and 8 bytes of its payload (:491-529) */
+    uint32_t is = ld32(f + 54), id = ld32(f + 58);
+    ctk_t ik;
+    if (is <= id) { ik.src = is; ik.dst = id; } else { ik.src = id; ik.dst = is; }
+    ik.proto = f[51];
+    if (L < 70) return -1;
+    uint16_t a = ld16(f + 62), b = ld16(f + 64);
+    if (a <= b) { ik.sport = a; ik.dport = b; } else { ik.sport = b; ik.dport = a; }
+    return ct_find(t, &ik) ? ST_RELATED : ST_INVALID;
+  }
+  return ST_INVALID;                                                     /* :562-566 */
+}
+
+/* ConntrackTableUpdate_dp.c:141-655, run for every accepted labelled packet. */
+static void ct_update(struct ctstate *t, const ctpkt_t *p, const uint8_t *f, int label) {
+  if (label == ST_INVALID) return;
+  uint8_t ipRev, portRev;
+  ctk_t key = ct_key(p, &ipRev, &portRev);
+  const uint64_t now = t->now;
+  ctv_t nv = {0, 0, 0, 0, 0};
+  if (p->proto == 6) {
+    if (p->flags & TCPHDR_RST) return;
+    cte_t *e = ct_find(t, &key);
+    int dir = !e ? 0 : (e->v.ipRev == ipRev && e->v.portRev == portRev) ? 1
+                     : (e->v.ipRev != ipRev && e->v.portRev != portRev) ? 2 : 0;
+    if (dir) {
+      ctv_t *v = &e->v;
+      if (v->state == ST_SYN_SENT) {
+        if (dir == 1) { if (syn_only(p->flags)) v->ttl = now + TCP_SYN_SENT; return; }
+        if (synack_only(p->flags) && p->ack == v->seq) {
+          v->state = ST_SYN_RECV; v->ttl = now + TCP_SYN_RECV; v->seq = p->seq + HEX_BE_ONE;
+        }
+        return;
+      }
+      if (v->state == ST_SYN_RECV) {
+        if (dir == 1) {
+          if (ack_only(p->flags) && p->ack == v->seq) { v->state = ST_ESTABLISHED; v->ttl = now + TCP_ESTABLISHED; }
+        } else if (synack_only(p->flags) && p->ack == v->seq) {
+          v->ttl = now + TCP_SYN_RECV;
+        }
+        return;
+      }
+      if (v->state == ST_ESTABLISHED) {
+        if (p->flags & TCPHDR_FIN) { v->state = ST_FIN_WAIT_1; v->ttl = now + TCP_FIN_WAIT; v->seq = p->ack; }
+        else v->ttl = now + TCP_ESTABLISHED;
+        return;
+      }
+      if (v->state == ST_FIN_WAIT_1) {
+        if ((p->flags & TCPHDR_ACK) && p->seq == v->seq) { v->state = ST_FIN_WAIT_2; v->ttl = now + TCP_FIN_WAIT; }
+        else return;
+        /* no goto: falls into the FIN_WAIT_2 test (:259-281) */
+      }
+      if (v->state == ST_FIN_WAIT_2) {
+        if (p->flags & TCPHDR_FIN) { v->state = ST_LAST_ACK; v->ttl = now + TCP_LAST_ACK; v->seq = p->ack; }
+        else v->ttl = now + TCP_FIN_WAIT;
+        return;
+      }
+      if (v->state == ST_LAST_ACK) {
+        if ((p->flags & TCPHDR_ACK) && p->seq == v->seq) v->state = ST_TIME_WAIT;
+        v->ttl = now + TCP_LAST_ACK;
+        return;
+      }
+      if (v->state == ST_TIME_WAIT) {
+        if (label != ST_NEW) return;
+        /* goto TCP_MISS */
+      } else {
+        return;
+      }
+    }
+    if (syn_only(p->flags)) {                                            /* TCP_MISS :540-555 */
+      nv.state = ST_SYN_SENT; nv.ttl = now + TCP_SYN_SENT; nv.seq = p->seq + HEX_BE_ONE;
+      nv.ipRev = ipRev; nv.portRev = portRev;
+      ct_put(t, &key, &nv, 0);
+    }
+    return;
+  }
+  if (p->proto == 17) {
+    cte_t *e = ct_find(t, &key);
+    if (e && e->v.ipRev == ipRev && e->v.portRev == portRev) {
+      e->v.ttl = now + (e->v.state == ST_NEW ? UDP_NEW_TIMEOUT : UDP_ESTABLISHED_TIMEOUT);
+      return;
+    }
+    if (e && e->v.ipRev != ipRev && e->v.portRev != portRev) {
+      if (e->v.state == ST_NEW) { e->v.ttl = now + UDP_NEW_TIMEOUT; e->v.state = ST_ESTABLISHED; }
+      else e->v.ttl = now + UDP_ESTABLISHED_TIMEOUT;
+      return;
+    }
+    nv.ttl = now + UDP_NEW_TIMEOUT; nv.state = ST_NEW; nv.ipRev = ipRev; nv.portRev = portRev;
+    ct_put(t, &key, &nv, 1);                                             /* UDP_MISS insert */
+    return;
+  }
+  if (p->proto == 1) {
+    uint8_t type = f[34];
+    if (type == 8) {
+      nv.ttl = now + ICMP_TIMEOUT; nv.state = ST_NEW; nv.ipRev = ipRev; nv.portRev = portRev;
+      ct_put(t, &key, &nv, 1);
+    } else if (type == 0) {
+      ct_delete(t, &key);
+    }
+  }
+}
+
+/* ChainRule::acceptEstablishedOptimizationFound (ChainRule.cpp:218-238): rule 0
+ * is exactly {conntrack ESTABLISHED, action ACCEPT}. */
+static int ae_found(const ochain_t *ch) {
+  if (ch->nrules == 0) return 0;
+  const prule_t *r = &ch->rules[0];
+  return r->ct_set && r->ct == CT_ESTABLISHED && r->action == 1 && !r->src_set && !r->dst_set &&
+         !r->proto_set && !r->sport_set && !r->dport_set && !r->flags_set_ && !r->in_set && !r->out_set;
+}
+
 /* default action tail: Program.cpp:88-111 (+ default counters from each module) */
 static inline int default_verdict(const ochain_t *ch, pcpu_t *pc, int chain, uint32_t L,
                                   int32_t *rid) {
@@ -594,8 +881,10 @@ static inline int default_verdict(const ochain_t *ch, pcpu_t *pc, int chain, uin
   return ch->default_action == 0 ? RX_DROP : RX_OK;
 }
 
+/* st != NULL: stateful conntrack (labels from and updates to st, one packet
+ * at a time); else labels come from ct_in or an empty table. */
 static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, uint32_t L, uint16_t port,
-                        int ct_in, pcpu_t *pc, int32_t *rid) {
+                        int ct_in, pcpu_t *pc, int32_t *rid, struct ctstate *st) {
   *rid = -2;
   /* TC hook: the receive path strips the outer 802.1Q / 802.1ad tag before
    * the program runs (skb_vlan_untag; a frame too short to hold the tag is
@@ -621,10 +910,14 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     if (L < 54) return RX_DROP;
     memcpy(&sport, f + 34, 2); memcpy(&dport, f + 36, 2);
     flags = f[47];
+    if (st) { st->sport = sport; st->dport = dport; st->seq = ld32(f + 38); st->ack = ld32(f + 42); st->flags = flags; }
   } else if (proto == 17) {
     if (L < 42) return RX_DROP;
     memcpy(&sport, f + 34, 2); memcpy(&dport, f + 36, 2);
+    if (st) { st->sport = sport; st->dport = dport; }
   }
+  ctpkt_t cp;
+  if (st) cp = (ctpkt_t){saddr, daddr, (uint8_t)proto, st->sport, st->dport, st->flags, st->seq, st->ack};
   /* ports as the NBO u16 the eBPF hash keys hold; the maps store ntohs(port) */
   sport = (uint16_t)(sport >> 8 | sport << 8);
   dport = (uint16_t)(dport >> 8 | dport << 8);
@@ -649,18 +942,38 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     if (c->ch[chain].default_action == 0) return RX_DROP; /* DROP_NO_LABELING */
     pass_labeling = 1;
   }
-  /* ConntrackLabel_dp.c:436-531: ICMP length checks (stateless: empty table) */
-  int icmp_type = -1;
-  if (proto == 1) {
-    if (L < 42) return RX_DROP;
-    icmp_type = f[34];
-    if (icmp_type != 8 && icmp_type != 0 && !(icmp_type >= 13 && icmp_type <= 18)) {
-      if (L < 62) return RX_DROP;
-      if (L < 70) return RX_DROP;
+  int ct;
+  if (st) {
+    ct = ct_label(st, &cp, f, L);                    /* ConntrackLabel_dp.c:190-531 */
+    if (ct < 0) return RX_DROP;
+    /* PASS_LABELING → ChainForwarder → ConntrackTableUpdate → RX_OK */
+    if (pass_labeling) { ct_update(st, &cp, f, ct); return RX_OK; }
+    /* _CONNTRACK_MODE_<CHAIN> == ON: accept established (ConntrackLabel_dp.c:580-616) */
+    if (c->ae[chain] && ct == ST_ESTABLISHED) {
+      pc->ae_pkts[chain] += 1; pc->ae_bytes[chain] += L;
+      *rid = -3;
+      ct_update(st, &cp, f, ct);
+      return RX_OK;
+    }
+  } else {
+    /* ConntrackLabel_dp.c:436-531: ICMP length checks (stateless: empty table) */
+    int icmp_type = -1;
+    if (proto == 1) {
+      if (L < 42) return RX_DROP;
+      icmp_type = f[34];
+      if (icmp_type != 8 && icmp_type != 0 && !(icmp_type >= 13 && icmp_type <= 18)) {
+        if (L < 62) return RX_DROP;
+        if (L < 70) return RX_DROP;
+      }
+    }
+    ct = ct_in >= 0 ? ct_in : ct_label_empty(proto, flags, icmp_type);
+    if (pass_labeling) return RX_OK; /* ChainForwarder → ConntrackTableUpdate → RX_OK */
+    if (c->ae[chain] && ct == CT_ESTABLISHED) {
+      pc->ae_pkts[chain] += 1; pc->ae_bytes[chain] += L;
+      *rid = -3;
+      return RX_OK;
     }
   }
-  int ct = ct_in >= 0 ? ct_in : ct_label_empty(proto, flags, icmp_type);
-  if (pass_labeling) return RX_OK; /* ChainForwarder → ConntrackTableUpdate → RX_OK */
 
   const ochain_t *ch = &c->ch[chain];
   int nrw = ch->nrw;
@@ -724,13 +1037,15 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     }
   }
   if (vv != v) free(vv);
+  /* ActionLookup / default ACCEPT → ConntrackTableUpdate (ActionLookup_dp.c:100-104, Program.cpp:88-111) */
+  if (st && verdict == RX_OK) ct_update(st, &cp, f, ct);
   return verdict;
 }
 
 typedef struct {
   const orc_ctx *c; int dir; int hook; const uint8_t *frames; const uint32_t *offsets; const uint16_t *lens;
   uint32_t stride, fixed_len; const uint16_t *in_port; uint16_t const_port; const uint8_t *ct;
-  uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc;
+  uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc; struct ctstate *st;
 } job_t;
 
 static void *run_job(void *arg) {
@@ -741,7 +1056,7 @@ static void *run_job(void *arg) {
     uint16_t port = j->in_port ? j->in_port[i] : j->const_port;
     int ct = j->ct ? j->ct[i] : -1;
     int32_t rid;
-    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid);
+    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st);
     j->verdicts[i] = v == RX_DROP ? 0 : 1;
     if (j->rule_ids) j->rule_ids[i] = rid;
   }
@@ -752,6 +1067,8 @@ int orc_classify(orc_ctx *c, int dir, int hook, const uint8_t *frames, const uin
                  const uint16_t *lens, uint32_t stride, uint32_t fixed_len,
                  const uint16_t *in_port, uint16_t const_port, const uint8_t *ct_status,
                  uint64_t n, uint8_t *verdicts, int32_t *rule_ids, int nthreads) {
+  if (c->ct && ct_status) return -EINVAL;   /* labels come from the table */
+  if (c->ct) nthreads = 1;                   /* one packet at a time, in batch order */
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   job_t *jobs = calloc((size_t)nthreads, sizeof(job_t));
@@ -760,7 +1077,7 @@ int orc_classify(orc_ctx *c, int dir, int hook, const uint8_t *frames, const uin
     job_t *j = &jobs[t];
     *j = (job_t){c, dir, hook, frames, offsets, lens, stride, fixed_len, in_port, const_port, ct_status,
                  n * t / nthreads, n * (t + 1) / nthreads, verdicts, rule_ids,
-                 {{0}, {0}, {0}, {0}}};
+                 {{0}, {0}, {0}, {0}, {0}, {0}}, c->ct};
     for (int k = 0; k < NCHAINS; k++) {
       j->pc.pkts[k] = calloc(c->max_counted, 8);
       j->pc.bytes[k] = calloc(c->max_counted, 8);
@@ -778,9 +1095,92 @@ int orc_classify(orc_ctx *c, int dir, int hook, const uint8_t *frames, const uin
       }
       c->ch[k].def_pkts += jobs[t].pc.dpk[k];
       c->ch[k].def_bytes += jobs[t].pc.dby[k];
+      c->ae_pkts[k] += jobs[t].pc.ae_pkts[k];
+      c->ae_bytes[k] += jobs[t].pc.ae_bytes[k];
       free(jobs[t].pc.pkts[k]); free(jobs[t].pc.bytes[k]);
     }
   }
   free(jobs); free(th);
+  return 0;
+}
+
+/* ---------------- conntrack control ---------------- */
+
+int orc_ct_enable(orc_ctx *c, int on) {
+  if (on && !c->ct) {
+    c->ct = calloc(1, sizeof(struct ctstate));
+    if (!c->ct) return -ENOMEM;
+  } else if (!on && c->ct) {
+    ct_free(c->ct);
+    c->ct = NULL;
+  }
+  return 0;
+}
+
+int orc_ct_set_time(orc_ctx *c, uint64_t ns) {
+  if (!c->ct) return -EINVAL;
+  c->ct->now = ns;
+  return 0;
+}
+
+static int cmp_entry(const void *a, const void *b) {
+  const orc_ct_entry *x = a, *y = b;
+  if (x->src_ip != y->src_ip) return x->src_ip < y->src_ip ? -1 : 1;
+  if (x->dst_ip != y->dst_ip) return x->dst_ip < y->dst_ip ? -1 : 1;
+  if (x->l4proto != y->l4proto) return x->l4proto < y->l4proto ? -1 : 1;
+  if (x->sport != y->sport) return x->sport < y->sport ? -1 : 1;
+  if (x->dport != y->dport) return x->dport < y->dport ? -1 : 1;
+  return 0;
+}
+
+/* The live `connections` entries (Iptables::getSessionTableList reads them,
+ * Iptables.cpp:527-566), as stored (key order fields), sorted by key. */
+int orc_ct_dump(orc_ctx *c, orc_ct_entry *out, uint32_t cap) {
+  if (!c->ct) return -EINVAL;
+  struct ctstate *t = c->ct;
+  if (t->live > cap) return -ENOSPC;
+  uint32_t n = 0;
+  for (size_t i = 0; i < t->cap; i++) {
+    const cte_t *e = &t->tab[i];
+    if (e->used != 1) continue;
+    out[n++] = (orc_ct_entry){e->k.src, e->k.dst, e->k.sport, e->k.dport, e->k.proto, e->v.state,
+                              e->v.ipRev, e->v.portRev, e->v.seq, e->v.ttl};
+  }
+  qsort(out, n, sizeof *out, cmp_entry);
+  return (int)n;
+}
+
+/* ChainRule::applyAcceptEstablishedOptimization (ChainRule.cpp:211-216) →
+ * Iptables::enable/disableAcceptEstablished (Iptables.cpp:351-449).  The
+ * disable switch has no `break`: disabling INPUT also disables FORWARD and
+ * OUTPUT, disabling FORWARD also disables OUTPUT. */
+int orc_apply_accept_established(orc_ctx *c, int chain) {
+  if (chain < 0 || chain >= NCHAINS) return -EINVAL;
+  if (ae_found(&c->ch[chain])) {
+    c->ae[chain] = 1;
+  } else {
+    for (int k = chain; k < NCHAINS; k++) c->ae[k] = 0;
+  }
+  return 0;
+}
+
+int orc_set_accept_established(orc_ctx *c, int chain, int on) {
+  if (chain < 0 || chain >= NCHAINS) return -EINVAL;
+  c->ae[chain] = on != 0;
+  return 0;
+}
+
+int orc_get_accept_established(orc_ctx *c, int chain) {
+  if (chain < 0 || chain >= NCHAINS) return -EINVAL;
+  return c->ae[chain];
+}
+
+/* pkts_/bytes_acceptestablished_<Chain> (ConntrackLabel.cpp:38-112): read, and
+ * flush when asked (ChainStats::fetchCounters for id 0, ChainStats.cpp:64-103). */
+int orc_read_accept_established(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes, int flush) {
+  if (chain < 0 || chain >= NCHAINS) return -EINVAL;
+  if (pkts) *pkts = c->ae_pkts[chain];
+  if (bytes) *bytes = c->ae_bytes[chain];
+  if (flush) c->ae_pkts[chain] = c->ae_bytes[chain] = 0;
   return 0;
 }

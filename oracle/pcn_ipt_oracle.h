@@ -76,6 +76,26 @@ int orc_read_counters(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes,
 int orc_export_map(orc_ctx *c, int chain, int field, uint32_t *keys,
                    uint8_t *plen, uint64_t *vecs, uint32_t cap, uint32_t nrw);
 uint32_t orc_chain_nrw(orc_ctx *c, int chain);
+/* ---- stateful conntrack (ConntrackLabel / ConntrackTableUpdate) ----
+ * on: packets are labelled from, and accepted packets update, a connection
+ * table, one packet at a time in batch order (orc_classify ignores nthreads;
+ * ct_status must be NULL).  off: stateless labels (ct_status or empty table). */
+typedef struct {
+  uint32_t src_ip, dst_ip;   /* ct_k: ordered, network-order u32 as stored */
+  uint16_t sport, dport;     /* ct_k ports, network-order u16 as stored */
+  uint8_t l4proto, state, ip_rev, port_rev;
+  uint32_t sequence;
+  uint64_t ttl;
+} orc_ct_entry;
+int orc_ct_enable(orc_ctx *c, int on);
+int orc_ct_set_time(orc_ctx *c, uint64_t ns);
+int orc_ct_dump(orc_ctx *c, orc_ct_entry *out, uint32_t cap);
+/* accept-established optimization (rule 0 == {conntrack ESTABLISHED, ACCEPT}) */
+int orc_apply_accept_established(orc_ctx *c, int chain);
+int orc_set_accept_established(orc_ctx *c, int chain, int on);
+int orc_get_accept_established(orc_ctx *c, int chain);
+int orc_read_accept_established(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes, int flush);
+
 /* De Bruijn index table restated from Iptables_BitScan_dp.c:88-110. */
 void orc_index64(uint16_t out[64]);
 

@@ -257,3 +257,103 @@ def fuzz_frames(n, seed, rs=None, stride=96):
     lens = np.where(common, rng.choice(np.array([13, 14, 33, 34, 41, 42, 53, 54, 61, 62, 69, 70, 64, 96]), size=n),
                     lens).astype(np.uint16)
     return f, lens
+
+
+# ---------------------------------------------------------------------------
+# Stateful traffic (conntrack): flows with handshakes, replies and ICMP errors
+# ---------------------------------------------------------------------------
+
+def set_tcp_seq(frames, mask, seq, ack):
+    """TCP sequence/ack numbers (host order in, network order in the frame)."""
+    f = frames.reshape(len(mask), -1)
+    f[mask, 38:42] = _be32(np.asarray(seq, np.uint64)[mask])
+    f[mask, 42:46] = _be32(np.asarray(ack, np.uint64)[mask])
+
+
+def set_icmp_inner(frames, mask, isrc, idst, iproto, isport, idport):
+    """The offending IP header + 8 payload bytes an ICMP error carries at byte 42
+    (what ConntrackLabel_dp.c:491-529 reads)."""
+    f = frames.reshape(len(mask), -1)
+    m = np.asarray(mask)
+    f[m, 42] = 0x45
+    f[m, 50] = 64
+    f[m, 51] = np.asarray(iproto)[m]
+    f[m, 54:58] = _be32(np.asarray(isrc, np.uint64)[m])
+    f[m, 58:62] = _be32(np.asarray(idst, np.uint64)[m])
+    f[m, 62:64] = _be16(np.asarray(isport, np.int64)[m])
+    f[m, 64:66] = _be16(np.asarray(idport, np.int64)[m])
+
+
+def flow_traffic(n, nflows, seed, *, stride=128, rs=None, hit_frac=0.5, p_noise=0.05, p_icmp=0.1,
+                 p_err=0.02, lens_mode="fixed"):
+    """n frames from `nflows` interleaved connections, in packet-arrival order.
+
+    TCP flows run SYN, SYN-ACK, ACK, data, FIN-ACK, FIN-ACK, ACK with consistent
+    sequence numbers; UDP flows alternate directions; ICMP flows are echo
+    request/reply pairs.  A `p_noise` fraction of packets get random flags or a
+    swapped direction (INVALID paths), and `p_err` are ICMP errors quoting
+    another flow's header (RELATED lookups).  A `hit_frac` share of the flows
+    take their endpoints from a rule of `rs` so the chain's rules are exercised.
+    Returns (frames [n*stride], lens u16 or None)."""
+    rng = np.random.default_rng(seed)
+    nflows = max(1, min(nflows, n))
+    src, dst, proto, sport, dport, _ = make_headers(rs, nflows, seed, hit_frac=hit_frac)
+    kind = rng.random(nflows)
+    proto = np.where(kind < p_icmp, ICMP, proto).astype(np.int32)
+    # packets per flow: a multinomial split of n
+    per = rng.multinomial(n, np.full(nflows, 1.0 / nflows))
+    fid = np.repeat(np.arange(nflows), per)
+    pos = np.arange(n) - np.repeat(np.cumsum(per) - per, per)      # index inside the flow
+    last = np.repeat(per, per) - 1
+    # arrival order: each flow starts at a random time and spreads its packets out
+    t0 = rng.random(nflows)[fid]
+    span = (rng.random(nflows) * 0.5 + 0.05)[fid]
+    t = t0 + span * (pos + rng.random(n) * 0.5) / np.maximum(last + 1, 1)
+    order = np.argsort(t, kind="stable")
+    fid, pos, last = fid[order], pos[order], last[order]
+    p = proto[fid]
+    # direction: TCP script, UDP/ICMP alternate
+    tcp_dir = np.select([pos == 0, pos == 1, pos == 2, pos == last - 1], [0, 1, 0, 1], pos % 2)
+    tcp_dir = np.where((pos == last) & (last >= 5), 0, tcp_dir)
+    rev = np.where(p == TCP, tcp_dir, pos % 2).astype(bool)
+    swap = rng.random(n) < p_noise
+    rev ^= swap
+    a_ip, b_ip = src[fid], dst[fid]
+    a_pt, b_pt = sport[fid], dport[fid]
+    s_ip = np.where(rev, b_ip, a_ip).astype(np.uint32)
+    d_ip = np.where(rev, a_ip, b_ip).astype(np.uint32)
+    s_pt = np.where(rev, b_pt, a_pt)
+    d_pt = np.where(rev, a_pt, b_pt)
+    # TCP flags and sequence numbers (client X, server Y)
+    X = rng.integers(0, 2**32, size=nflows, dtype=np.uint64)[fid]
+    Y = rng.integers(0, 2**32, size=nflows, dtype=np.uint64)[fid]
+    M = np.uint64(0xFFFFFFFF)
+    fin_c = (pos == last - 2) & (last >= 5)
+    fin_s = (pos == last - 1) & (last >= 5)
+    ack_l = (pos == last) & (last >= 5)
+    flags = np.select([pos == 0, pos == 1, fin_c | fin_s], [0x02, 0x12, 0x11], 0x10)
+    flags = np.where((~(pos <= 2)) & (~fin_c) & (~fin_s) & (~ack_l) & (rng.random(n) < 0.3), 0x18, flags)
+    seq = np.select([pos == 0, pos == 1, fin_s, ack_l], [X, Y, (Y + 1) & M, (X + 2) & M],
+                    np.where(rev, (Y + 1) & M, (X + 1) & M))
+    ack = np.select([pos == 0, pos == 1, fin_s, ack_l], [np.zeros_like(X), (X + 1) & M, (X + 2) & M, (Y + 2) & M],
+                    np.where(rev, (X + 1) & M, (Y + 1) & M))
+    noisy = rng.random(n) < p_noise
+    flags = np.where(noisy, rng.integers(0, 256, size=n), flags).astype(np.int32)
+    # ICMP: echo request / reply; some packets become errors quoting another flow
+    itype = np.where(rev, 0, 8)
+    err = rng.random(n) < p_err
+    p = np.where(err, ICMP, p).astype(np.int32)
+    itype = np.where(err, rng.choice(np.array([3, 11, 5, 13]), size=n), itype)
+    f = build_frames(s_ip, d_ip, p, s_pt, d_pt, flags, frame_len=stride, icmp_type=itype)
+    tcp = p == TCP
+    set_tcp_seq(f, tcp, seq, ack)
+    if stride >= 66:
+        q = rng.integers(0, nflows, size=n)      # the quoted flow (its forward direction)
+        qrev = rng.random(n) < 0.5
+        set_icmp_inner(f, err, np.where(qrev, dst[q], src[q]), np.where(qrev, src[q], dst[q]), proto[q],
+                       np.where(qrev, dport[q], sport[q]), np.where(qrev, sport[q], dport[q]))
+    lens = None
+    if lens_mode == "mixed":
+        lens = np.where(rng.random(n) < 0.2, rng.choice(np.array([41, 42, 54, 61, 62, 69, 70, 98]), size=n),
+                        stride).astype(np.uint16)
+    return f.reshape(-1), lens

@@ -44,6 +44,38 @@ def probe_frames(packets, stride=128):
     return f.reshape(-1), lens, ports, ct
 
 
+def ct_probe_frames(packets, stride=128):
+    """Like probe_frames, plus TCP seq/ack and the quoted header of ICMP errors."""
+    f, lens, ports, _ = probe_frames(packets, stride)
+    n = len(packets)
+    tcp = np.array([p["proto"] == 6 and "seq" in p for p in packets])
+    seq = np.array([p.get("seq", 0) & 0xFFFFFFFF for p in packets], np.uint64)
+    ack = np.array([p.get("ack", 0) & 0xFFFFFFFF for p in packets], np.uint64)
+    synth.set_tcp_seq(f, tcp, seq, ack)
+    inner = np.array(["inner" in p for p in packets])
+    if inner.any():
+        g = [p.get("inner", {"src": "0.0.0.0", "dst": "0.0.0.0", "proto": 0, "sport": 0, "dport": 0})
+             for p in packets]
+        synth.set_icmp_inner(f, inner, np.array([ip_host(x["src"]) for x in g], np.uint32),
+                             np.array([ip_host(x["dst"]) for x in g], np.uint32),
+                             np.array([x["proto"] for x in g], np.int32), np.array([x["sport"] for x in g]),
+                             np.array([x["dport"] for x in g]))
+    return f.reshape(-1), lens, ports
+
+
+def session_states(entries, ip):
+    """States of the session-table rows naming `ip` (Iptables::getSessionTableList:
+    src/dst restored from ipRev), as `polycubectl ... session-table show | grep ip`."""
+    from oracle.ffi import CT_STATES
+    want = ip_nbo(ip)
+    return [CT_STATES[e["state"]] for e in entries if int(e["src_ip"]) == want or int(e["dst_ip"]) == want]
+
+
+def load_ct_scenarios():
+    with open(os.path.join(GOLDEN, "ct_scenarios.json")) as fh:
+        return json.load(fh)
+
+
 def norm_rule(r):
     r = dict(r)
     r["action"] = str(r.get("action", "DROP")).upper()
@@ -68,6 +100,11 @@ class OracleCube:
 
     def _apply(self, c):
         self.o.set_chain(CHAINS[c], self.rules[c], self.default[c])
+
+    def _ae(self, c):
+        # ChainRule::applyAcceptEstablishedOptimization after append/insert
+        # (interactive only), deletes and applyRules (Chain.cpp:187,307,368,408)
+        self.o.apply_accept_established(CHAINS[c])
 
     def op(self, op):
         kind = op[0]
@@ -95,11 +132,30 @@ class OracleCube:
             return
         elif kind == "apply":
             self._apply(c)
+            self._ae(c)
             return
         else:
             raise ValueError(kind)
         if self.interactive:
             self._apply(c)
+        if kind == "deletes" or (self.interactive and kind in ("append", "insert")):
+            self._ae(c)
+
+    def ct_probe(self, packets):
+        """Stateful: the packets in order (direction runs split into batches)."""
+        out = []
+        i = 0
+        while i < len(packets):
+            j = i
+            while j < len(packets) and packets[j]["dir"] == packets[i]["dir"]:
+                j += 1
+            sel = packets[i:j]
+            f, lens, ports = ct_probe_frames(sel)
+            v, r = self.o.classify(f, n=len(sel), lens=lens, stride=128, in_port=ports,
+                                   direction=DIRS[sel[0]["dir"]])
+            out.extend(int(x) for x in v)
+            i = j
+        return out
 
     def probe(self, packets):
         out = []
