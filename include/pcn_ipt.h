@@ -269,6 +269,52 @@ int pcn_ipt_chain_stats(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes
 /* Chain::resetCounters (Chain.cpp:354-380) */
 int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain);
 
+/* ---- stateful connection tracking -------------------------------------- */
+/* The `connections` table (Iptables_ConntrackLabel_dp.c:111-113, an LRU hash
+ * of 65536 entries) kept in HBM, with the reference's labels
+ * (ConntrackLabel_dp.c:190-531) and updates (ConntrackTableUpdate_dp.c:141-655).
+ * While enabled, pcn_ipt_classify labels every IPv4 packet from the table and
+ * every accepted packet updates it, with the result of running the batch one
+ * packet at a time in index order (and batches in submission order).
+ * Differences from the kernel LRU: entries are never evicted; an insert into a
+ * full table is dropped and counted (pcn_ipt_ct_info.inserts_lost).  Entries
+ * never expire in the reference either (ttl is written, never compared).
+ * batch.ct_status must be NULL while enabled. */
+typedef struct {
+  uint32_t src_ip, dst_ip;   /* ct_k as stored: ordered NBO u32 */
+  uint16_t sport, dport;     /* ct_k ports as stored: ordered NBO u16 */
+  uint8_t l4proto, state, ip_rev, port_rev;   /* state: 0 NEW .. 9 TIME_WAIT (ConntrackLabel_dp.c:70-81) */
+  uint32_t sequence;
+  uint64_t ttl;
+} pcn_ipt_ct_entry;
+typedef struct {
+  uint32_t enabled, capacity_log2;
+  uint64_t now;              /* timestamp used for new ttl values */
+  uint64_t inserts_lost;     /* inserts refused because the table was full */
+} pcn_ipt_ct_info;
+/* capacity = 2^capacity_log2 slots (0 => 2^18); the table persists across enable/disable. */
+int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2);
+int pcn_ipt_ct_disable(pcn_ipt *ctx);
+int pcn_ipt_ct_clear(pcn_ipt *ctx);
+/* The `timestamp` percpu value ConntrackTableUpdate::updateTimestamp writes
+ * every second (modules/ConntrackTableUpdate.cpp:108-137). */
+int pcn_ipt_ct_set_time(pcn_ipt *ctx, uint64_t ns);
+/* Live entries sorted by key (Iptables::getSessionTableList, Iptables.cpp:527-566);
+ * copies min(count, cap), returns count. */
+int pcn_ipt_ct_dump(pcn_ipt *ctx, pcn_ipt_ct_entry *out, uint32_t cap);
+int pcn_ipt_ct_get_info(pcn_ipt *ctx, pcn_ipt_ct_info *out);
+
+/* Accept-established optimization: set by the rule-level verbs exactly where
+ * the reference calls ChainRule::applyAcceptEstablishedOptimization (rule 0 ==
+ * {conntrack ESTABLISHED, ACCEPT}); explicit for the table-level boundary.
+ * ESTABLISHED packets are then accepted before the chain (rule id -3) and
+ * counted in pkts/bytes_acceptestablished_<Chain> (ConntrackLabel_dp.c:580-616),
+ * which pcn_ipt_chain_stats adds to rule 0 (ChainStats.cpp:64-103). */
+#define PCN_IPT_RID_ACCEPT_ESTABLISHED (-3)
+int pcn_ipt_set_accept_established(pcn_ipt *ctx, int chain, int on);
+int pcn_ipt_get_accept_established(pcn_ipt *ctx, int chain);
+int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, int flush);
+
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ------------------- */
 /* 128-byte ncclUniqueId produced on rank 0 and shared out of band. */
 int pcn_ipt_comm_unique_id(uint8_t out[128]);

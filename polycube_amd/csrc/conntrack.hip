@@ -1,0 +1,697 @@
+// conntrack.hip — stateful connection tracking on the GPU (see conntrack.hpp).
+//
+// Semantics restated from the reference (paths under
+// src/services/pcn-iptables/src/datapaths/):
+//   key + labels      Iptables_ConntrackLabel_dp.c:190-531
+//   accept-established Iptables_ConntrackLabel_dp.c:580-650
+//   table update      Iptables_ConntrackTableUpdate_dp.c:141-655
+//   stale ports (Q4)  Iptables_Parser_dp.c:122-143 (ports written for TCP/UDP only)
+// Everything here is integer work on HBM-resident state: the parse/prep
+// kernels stream the 72-byte header window once, the walk is latency-bound
+// (one dependent table access per packet of a run), the sort is hipCUB's
+// onesweep radix sort on a key-bucket id.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "conntrack.hpp"
+#include "pcn_ipt.h"
+
+namespace pcn {
+
+namespace {
+
+enum : uint8_t { K_NONE = 0, K_INV, K_TCP, K_UDP, K_ECHO, K_REPLY, K_ERR, K_HARD };
+enum { ST_NEW = 0, ST_EST, ST_REL, ST_INV, ST_SYN_SENT, ST_SYN_RECV, ST_FIN_WAIT_1, ST_FIN_WAIT_2, ST_LAST_ACK,
+       ST_TIME_WAIT };
+constexpr uint8_t FIN = 0x01, SYN = 0x02, RST = 0x04, ACK = 0x10;
+constexpr uint32_t HEX_BE_ONE = 0x1000000u;
+// ConntrackTableUpdate_dp.c:38-48 (ns)
+constexpr unsigned long long UDP_ESTABLISHED_TIMEOUT = 180000000000ull, UDP_NEW_TIMEOUT = 30000000000ull,
+                             ICMP_TIMEOUT = 30000000000ull, TCP_ESTABLISHED_T = 432000000000000ull,
+                             TCP_SYN_SENT_T = 120000000000ull, TCP_SYN_RECV_T = 60000000000ull,
+                             TCP_LAST_ACK_T = 30000000000ull, TCP_FIN_WAIT_T = 120000000000ull;
+
+// Per-packet record written by ct_prep (32 B).
+struct CtRec {
+  uint32_t src, dst;       // table key: the packet's own (ordered), or the quoted header's for K_ERR
+  uint16_t sport, dport;
+  uint32_t seq, ack;       // TCP; for K_HARD: the quoted header's ordered src / dst
+  uint16_t len;            // packet_len after a TC untag (counters)
+  uint8_t proto, kind;
+  uint8_t rev;             // bit0 ipRev, bit1 portRev
+  uint8_t flags;           // TCP flags; for K_HARD: the quoted header's protocol
+  uint8_t cinfo;           // bits 0-1: chain (3: none), bit 2: PASS_LABELING
+  uint8_t icmp;
+  uint32_t iports;         // K_HARD: the quoted header's ordered ports (sport | dport << 16)
+};
+static_assert(sizeof(CtRec) == 32, "CtRec is 32 bytes");
+
+struct Parsed {
+  uint32_t L;
+  int status;              // 0 RX_DROP in the parser, 1 not IPv4 (pass), 2 IPv4 parsed
+  bool ports_ok;           // the Parser wrote srcPort/dstPort
+  uint32_t src, dst, seq, ack, isrc, idst;
+  uint16_t sport, dport, isport, idport;
+  uint8_t proto, flags, icmp, iproto;
+};
+
+// The first 72 bytes of frame i (dword-aligned loads that stay inside the buffer).
+__device__ __forceinline__ void load_window(const CtBatch &b, uint64_t i, uint32_t w[18], uint32_t &L) {
+  const uint64_t off = b.offsets ? b.offsets[i] : i * uint64_t(b.stride);
+  L = b.lens ? b.lens[i] : b.fixed_len;
+  const uint64_t base = off & ~uint64_t(3);
+  const uint32_t sh = static_cast<uint32_t>(off & 3);
+  uint32_t d[19];
+#pragma unroll
+  for (int k = 0; k < 19; ++k) {
+    const uint64_t at = base + 4u * k;
+    d[k] = at + 4 <= b.frames_bytes ? *reinterpret_cast<const uint32_t *>(b.frames + at) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 18; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
+// Iptables_Parser_dp.c:94-153 (+ the TC-hook untag, see pcn_ipt.h), reading the
+// fields the conntrack modules use.  Multi-byte fields are little-endian loads
+// of network-order bytes, as the eBPF reads them.
+__device__ __forceinline__ Parsed parse(const uint32_t w[18], uint32_t L, uint32_t hook) {
+  Parsed p{};
+  int s = 0;
+  if (L >= 14 && hook == PCN_IPT_HOOK_TC) {
+    const uint32_t et = ((w[3] & 0xff) << 8) | ((w[3] >> 8) & 0xff);
+    if (et == 0x8100 || et == 0x88A8) {
+      if (L < 18) { p.status = 0; return p; }
+      s = 1;
+      L -= 4;
+    }
+  }
+  p.L = L;
+  auto W = [&](int k) { return s ? w[k + 1] : w[k]; };   // bytes >= 12 move by one dword
+  if (L < 14) { p.status = 0; return p; }
+  const uint32_t et = ((W(3) & 0xff) << 8) | ((W(3) >> 8) & 0xff);
+  if (et != 0x0800) { p.status = 1; return p; }
+  if (L < 34) { p.status = 0; return p; }
+  p.proto = static_cast<uint8_t>(W(5) >> 24);
+  p.src = (W(6) >> 16) | (W(7) << 16);
+  p.dst = (W(7) >> 16) | (W(8) << 16);
+  if (p.proto == 6) {
+    if (L < 54) { p.status = 0; return p; }
+    p.seq = (W(9) >> 16) | (W(10) << 16);
+    p.ack = (W(10) >> 16) | (W(11) << 16);
+    p.flags = static_cast<uint8_t>(W(11) >> 24);
+    p.ports_ok = true;
+  } else if (p.proto == 17) {
+    if (L < 42) { p.status = 0; return p; }
+    p.ports_ok = true;
+  }
+  p.sport = static_cast<uint16_t>(W(8) >> 16);
+  p.dport = static_cast<uint16_t>(W(9) & 0xffff);
+  p.icmp = static_cast<uint8_t>((W(8) >> 16) & 0xff);
+  p.iproto = static_cast<uint8_t>(W(12) >> 24);
+  p.isrc = (W(13) >> 16) | (W(14) << 16);
+  p.idst = (W(14) >> 16) | (W(15) << 16);
+  p.isport = static_cast<uint16_t>(W(15) >> 16);
+  p.idport = static_cast<uint16_t>(W(16) & 0xffff);
+  p.status = 2;
+  return p;
+}
+
+__device__ __forceinline__ bool localip_has(const CtBatch &b, uint32_t ip) {
+  uint32_t lo = 0, hi = b.nlocal;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint32_t v = b.localip[mid];
+    if (v == ip) return true;
+    if (v < ip) lo = mid + 1; else hi = mid;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint64_t key_hash(uint32_t src, uint32_t dst, uint8_t proto, uint16_t sp, uint16_t dp) {
+  uint64_t h = ((uint64_t(src) << 32) | dst) * 0x9E3779B97F4A7C15ull;
+  h ^= ((uint64_t(proto) << 32) | (uint64_t(sp) << 16) | dp) * 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 32);
+}
+
+__global__ void ct_parse_kernel(CtBatch b, uint32_t *pp, uint32_t *pports) {
+  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < b.n; i += step) {
+    uint32_t w[18], L;
+    load_window(b, i, w, L);
+    const Parsed p = parse(w, L, b.hook);
+    const bool ok = p.status == 2 && p.ports_ok;
+    pp[i] = ok ? static_cast<uint32_t>(i + 1) : 0u;
+    pports[i] = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
+  }
+}
+
+// Chain selection (ChainSelector_dp.c:131-298), the conntrack key and kind;
+// packets that need no table access get their final outcome here.
+__global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *pports, const uint32_t *carry,
+                               CtRec *rec, uint32_t *keys, uint32_t *idx, uint32_t kbits, uint32_t *hard_cnt,
+                               uint32_t *hard_list) {
+  const uint32_t sentinel = (1u << kbits) - 1;
+  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < b.n; i += step) {
+    uint32_t w[18], L;
+    load_window(b, i, w, L);
+    const Parsed p = parse(w, L, b.hook);
+    CtRec r{};
+    r.len = static_cast<uint16_t>(p.L);
+    r.kind = K_NONE;
+    uint32_t chain = 3;
+    bool pass = false;
+    if (p.status == 2) {
+      bool labeled = true;
+      if (b.direction == PCN_IPT_INGRESS) {
+        if (b.allow_logic) pass = true;
+        else chain = (b.nlocal && localip_has(b, p.dst)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
+      } else if (b.nlocal && localip_has(b, p.src)) {
+        chain = PCN_IPT_OUTPUT;
+      } else {
+        labeled = false;                                   // egress PASS, no labeling
+      }
+      if (labeled && chain < 3 && ((b.empty_mask >> chain) & 1)) {
+        if ((b.drop_mask >> chain) & 1) labeled = false;  // DROP_NO_LABELING (default counters)
+        else pass = true;                                  // PASS_LABELING
+      }
+      if (labeled) {
+        // the shared `packet` struct: ports stale for anything but TCP/UDP (Q4)
+        uint32_t ports;
+        if (p.ports_ok) ports = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
+        else if (i > 0 && last[i - 1]) ports = pports[last[i - 1] - 1];
+        else ports = *carry;
+        const uint16_t sp = static_cast<uint16_t>(ports & 0xffff), dp = static_cast<uint16_t>(ports >> 16);
+        // ConntrackLabel_dp.c:200-228
+        uint8_t ipRev, portRev;
+        if (p.src <= p.dst) { r.src = p.src; r.dst = p.dst; ipRev = 0; }
+        else { r.src = p.dst; r.dst = p.src; ipRev = 1; }
+        if (sp < dp) { r.sport = sp; r.dport = dp; portRev = 0; }
+        else if (sp > dp) { r.sport = dp; r.dport = sp; portRev = 1; }
+        else { r.sport = sp; r.dport = dp; portRev = ipRev; }
+        r.proto = p.proto;
+        r.rev = static_cast<uint8_t>(ipRev | (portRev << 1));
+        r.seq = p.seq;
+        r.ack = p.ack;
+        r.flags = p.flags;
+        r.icmp = p.icmp;
+        if (p.proto == 6) r.kind = K_TCP;
+        else if (p.proto == 17) r.kind = K_UDP;
+        else if (p.proto == 1) {
+          if (p.L < 42) r.kind = K_NONE;                   // RX_DROP (:441-443)
+          else if (p.icmp == 8) r.kind = K_ECHO;
+          else if (p.icmp == 0) r.kind = p.L >= 70 ? K_HARD : K_REPLY;
+          else if (p.icmp >= 13 && p.icmp <= 18) r.kind = K_INV;
+          else if (p.L < 70) r.kind = K_NONE;              // RX_DROP (:486-505)
+          else r.kind = K_ERR;
+          if (r.kind == K_ERR || r.kind == K_HARD) {      // the quoted header's key (:491-529)
+            const uint32_t qs = p.isrc <= p.idst ? p.isrc : p.idst, qd = p.isrc <= p.idst ? p.idst : p.isrc;
+            const uint16_t qa = p.isport <= p.idport ? p.isport : p.idport;
+            const uint16_t qb = p.isport <= p.idport ? p.idport : p.isport;
+            if (r.kind == K_ERR) {
+              r.src = qs; r.dst = qd; r.sport = qa; r.dport = qb; r.proto = p.iproto;
+            } else {
+              r.seq = qs; r.ack = qd; r.flags = p.iproto; r.iports = uint32_t(qa) | (uint32_t(qb) << 16);
+            }
+          }
+        } else {
+          r.kind = K_INV;                                  // :562-566
+        }
+      }
+    }
+    r.cinfo = static_cast<uint8_t>((chain & 3) | (pass ? 4 : 0));
+    rec[i] = r;
+    idx[i] = static_cast<uint32_t>(i);
+    const bool member = r.kind >= K_TCP && r.kind <= K_ERR;
+    keys[i] = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
+                     : sentinel;
+    if (r.kind == K_HARD) hard_list[atomicAdd(hard_cnt, 1u)] = static_cast<uint32_t>(i);
+    if (!member && r.kind != K_HARD) {
+      // no table access: the outcome of label INVALID (K_INV) or of any label
+      const uint32_t l = (r.kind == K_INV && !pass && b.nlab == 4) ? 3u : 0u;
+      b.verdicts[i] = b.a_verdict[l * b.n + i];
+      b.rule_ids[i] = b.a_rid[l * b.n + i];
+    }
+  }
+}
+
+__global__ void ct_carry_kernel(uint64_t n, const uint32_t *last, const uint32_t *pports, uint32_t *carry) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && last[n - 1]) *carry = pports[last[n - 1] - 1];
+}
+
+// ---- the table ----------------------------------------------------------
+struct Key {
+  uint32_t src, dst;
+  uint16_t sport, dport;
+  uint8_t proto;
+};
+
+__device__ __forceinline__ bool same(const Key &a, const Key &b) {
+  return a.src == b.src && a.dst == b.dst && a.sport == b.sport && a.dport == b.dport && a.proto == b.proto;
+}
+
+// The slot holding `k` (live or deleted), or null; with claim, an empty slot
+// is taken for it.  One lane owns each key in a launch, so a slot another
+// lane is claiming (tag 2) never holds ours.
+__device__ CtSlot *table_slot(const CtTable &t, const Key &k, bool claim) {
+  const uint64_t mask = (uint64_t(1) << t.cap_log2) - 1;
+  uint64_t s = key_hash(k.src, k.dst, k.proto, k.sport, k.dport) >> 7;
+  for (uint64_t probe = 0; probe <= mask; ++probe, ++s) {
+    CtSlot *e = &t.slots[s & mask];
+    uint32_t tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tag == 0) {
+      if (!claim) return nullptr;
+      if (atomicCAS(&e->tag, 0u, 2u) == 0u) {
+        e->src = k.src; e->dst = k.dst; e->sport = k.sport; e->dport = k.dport; e->proto = k.proto;
+        e->valid = 0;
+        __hip_atomic_store(&e->tag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return e;
+      }
+      tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tag != 1) continue;
+    if (e->src == k.src && e->dst == k.dst && e->sport == k.sport && e->dport == k.dport && e->proto == k.proto)
+      return e;
+  }
+  if (claim) atomicAdd(&t.stats[0], 1ull);          // table full: the insert is lost
+  return nullptr;
+}
+
+struct Cache {              // the last key a walking lane touched
+  Key k;
+  CtSlot *e;
+  bool valid;
+};
+
+__device__ __forceinline__ CtSlot *lookup(const CtTable &t, Cache &c, const Key &k) {
+  if (!c.valid || !same(c.k, k)) {
+    c.k = k;
+    c.e = table_slot(t, k, false);
+    c.valid = true;
+  }
+  return c.e && c.e->valid ? c.e : nullptr;
+}
+
+// connections.update (noexist = false) / .insert (BPF_NOEXIST)
+__device__ __forceinline__ void put(const CtTable &t, Cache &c, const Key &k, unsigned long long ttl, uint8_t state,
+                                   uint32_t seq, uint8_t rev, bool noexist) {
+  CtSlot *e = lookup(t, c, k);
+  if (e && noexist) return;
+  if (!e) {
+    e = c.e ? c.e : table_slot(t, k, true);
+    c.e = e;
+    if (!e) return;
+  }
+  e->ttl = ttl; e->state = state; e->seq = seq; e->rev = rev; e->valid = 1;
+}
+
+__device__ __forceinline__ bool syn_only(uint8_t f) { return (f & SYN) && (f | SYN) == SYN; }
+__device__ __forceinline__ bool ack_only(uint8_t f) { return (f & ACK) && (f | ACK) == ACK; }
+__device__ __forceinline__ bool synack_only(uint8_t f) {
+  return (f & ACK) && (f & SYN) && (f | (SYN | ACK)) == (SYN | ACK);
+}
+
+// ConntrackLabel_dp.c:230-433 for TCP/UDP/echo/echo-reply(short)/errors
+// against the entry e (live, or null); -1 = RX_DROP.
+__device__ int label_of(const CtRec &r, const CtSlot *e) {
+  const bool fwd = e && e->rev == r.rev;
+  const bool rev = e && ((e->rev ^ r.rev) == 3);
+  switch (r.kind) {
+  case K_TCP:
+    if (fwd || rev) {
+      if (r.flags & RST) return ST_EST;
+      const uint8_t s = e->state;
+      if (s == ST_SYN_SENT)
+        return fwd ? (syn_only(r.flags) ? ST_NEW : ST_INV) : (synack_only(r.flags) && r.ack == e->seq ? ST_EST : ST_INV);
+      if (s == ST_SYN_RECV)
+        return fwd ? (ack_only(r.flags) && r.ack == e->seq ? ST_EST : ST_INV)
+                   : (synack_only(r.flags) && r.ack == e->seq ? ST_EST : ST_INV);
+      if (s == ST_EST || s == ST_FIN_WAIT_1 || s == ST_FIN_WAIT_2 || s == ST_LAST_ACK) return ST_EST;
+      if (s == ST_TIME_WAIT && syn_only(r.flags)) return ST_NEW;
+      return ST_INV;
+    }
+    return syn_only(r.flags) ? ST_NEW : ST_INV;
+  case K_UDP:
+    if (fwd) return e->state == ST_NEW ? ST_NEW : ST_EST;
+    if (rev) return ST_EST;
+    return ST_NEW;
+  case K_ECHO:
+    return ST_NEW;
+  case K_REPLY:                                   // < 70 bytes: the miss path drops
+    if (!e) return ST_INV;
+    return rev ? ST_EST : -1;
+  case K_ERR:
+    return e ? ST_REL : ST_INV;
+  default:
+    return ST_INV;
+  }
+}
+
+// ConntrackTableUpdate_dp.c:141-655 for an accepted packet with label l.
+__device__ void update(const CtTable &t, Cache &c, const CtRec &r, const Key &k, CtSlot *e, int l) {
+  if (l == ST_INV) return;
+  const unsigned long long now = t.now;
+  if (r.kind == K_TCP) {
+    if (r.flags & RST) return;
+    const int dir = !e ? 0 : e->rev == r.rev ? 1 : ((e->rev ^ r.rev) == 3) ? 2 : 0;
+    if (dir) {
+      const uint8_t s = e->state;
+      if (s == ST_SYN_SENT) {
+        if (dir == 1) { if (syn_only(r.flags)) e->ttl = now + TCP_SYN_SENT_T; return; }
+        if (synack_only(r.flags) && r.ack == e->seq) {
+          e->state = ST_SYN_RECV; e->ttl = now + TCP_SYN_RECV_T; e->seq = r.seq + HEX_BE_ONE;
+        }
+        return;
+      }
+      if (s == ST_SYN_RECV) {
+        if (dir == 1) {
+          if (ack_only(r.flags) && r.ack == e->seq) { e->state = ST_EST; e->ttl = now + TCP_ESTABLISHED_T; }
+        } else if (synack_only(r.flags) && r.ack == e->seq) {
+          e->ttl = now + TCP_SYN_RECV_T;
+        }
+        return;
+      }
+      if (s == ST_EST) {
+        if (r.flags & FIN) { e->state = ST_FIN_WAIT_1; e->ttl = now + TCP_FIN_WAIT_T; e->seq = r.ack; }
+        else e->ttl = now + TCP_ESTABLISHED_T;
+        return;
+      }
+      if (s == ST_FIN_WAIT_1 || s == ST_FIN_WAIT_2) {
+        if (s == ST_FIN_WAIT_1) {
+          if (!((r.flags & ACK) && r.seq == e->seq)) return;
+          e->state = ST_FIN_WAIT_2;                // no goto: falls into FIN_WAIT_2
+        }
+        if (r.flags & FIN) { e->state = ST_LAST_ACK; e->ttl = now + TCP_LAST_ACK_T; e->seq = r.ack; }
+        else e->ttl = now + TCP_FIN_WAIT_T;
+        return;
+      }
+      if (s == ST_LAST_ACK) {
+        if ((r.flags & ACK) && r.seq == e->seq) e->state = ST_TIME_WAIT;
+        e->ttl = now + TCP_LAST_ACK_T;
+        return;
+      }
+      if (s != ST_TIME_WAIT || l != ST_NEW) return;   // TIME_WAIT + NEW: goto TCP_MISS
+    }
+    if (syn_only(r.flags)) put(t, c, k, now + TCP_SYN_SENT_T, ST_SYN_SENT, r.seq + HEX_BE_ONE, r.rev, false);
+    return;
+  }
+  if (r.kind == K_UDP) {
+    if (e && e->rev == r.rev) { e->ttl = now + (e->state == ST_NEW ? UDP_NEW_TIMEOUT : UDP_ESTABLISHED_TIMEOUT); return; }
+    if (e && (e->rev ^ r.rev) == 3) {
+      if (e->state == ST_NEW) { e->ttl = now + UDP_NEW_TIMEOUT; e->state = ST_EST; }
+      else e->ttl = now + UDP_ESTABLISHED_TIMEOUT;
+      return;
+    }
+    put(t, c, k, now + UDP_NEW_TIMEOUT, ST_NEW, 0, r.rev, true);
+    return;
+  }
+  if (r.kind == K_ECHO) { put(t, c, k, now + ICMP_TIMEOUT, ST_NEW, 0, r.rev, true); return; }
+  if (r.kind == K_REPLY || r.kind == K_HARD) {
+    if (e) e->valid = 0;                           // connections.delete
+  }
+}
+
+// Final outcome of a labelled packet (label -1: dropped by ConntrackLabel).
+__device__ __forceinline__ bool finish(const CtBatch &b, uint64_t i, const CtRec &r, int l) {
+  const bool pass = r.cinfo & 4;
+  const uint32_t chain = r.cinfo & 3;
+  uint8_t v;
+  int32_t rid;
+  if (l < 0) { v = PCN_IPT_DROP; rid = pass ? b.a_rid[i] : PCN_IPT_RID_NOCHAIN; }
+  else if (pass) { v = b.a_verdict[i]; rid = b.a_rid[i]; }
+  else if (((b.ae_mask >> chain) & 1) && l == ST_EST) { v = PCN_IPT_ACCEPT; rid = -3; }
+  else {
+    const uint64_t o = (b.nlab == 4 ? uint64_t(l) : 0) * b.n + i;
+    v = b.a_verdict[o];
+    rid = b.a_rid[o];
+  }
+  b.verdicts[i] = v;
+  b.rule_ids[i] = rid;
+  return v == PCN_IPT_ACCEPT && l >= 0;
+}
+
+__device__ __forceinline__ void process(const CtBatch &b, const CtTable &t, Cache &c, uint64_t i, const CtRec &r) {
+  const Key k{r.src, r.dst, r.sport, r.dport, r.proto};
+  CtSlot *e = lookup(t, c, k);
+  const int l = label_of(r, e);
+  if (finish(b, i, r, l) && r.kind != K_ERR) update(t, c, r, k, e, l);
+}
+
+// One lane per run of equal key buckets (in batch order), over the packets
+// with index < hi it has not done yet.
+__global__ void ct_walk_kernel(CtBatch b, CtTable t, const CtRec *rec, const uint32_t *skeys, const uint32_t *sidx,
+                               uint32_t *cursor, uint64_t hi, int first, uint32_t sentinel) {
+  const uint64_t p = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (p >= b.n) return;
+  const uint32_t k = skeys[p];
+  if (k == sentinel || (p > 0 && skeys[p - 1] == k)) return;
+  uint64_t q = first ? p : cursor[p];
+  Cache c{};
+  for (; q < b.n && skeys[q] == k; ++q) {
+    const uint32_t i = sidx[q];
+    if (i >= hi) break;
+    process(b, t, c, i, rec[i]);
+  }
+  cursor[p] = static_cast<uint32_t>(q);
+}
+
+// An echo reply long enough to quote a header (ConntrackLabel_dp.c:450-531):
+// its own key decides ESTABLISHED; otherwise ICMP_MISS reads the quoted key.
+__global__ void ct_hard_kernel(CtBatch b, CtTable t, const CtRec *rec, uint32_t i) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const CtRec r = rec[i];
+  Cache c{};
+  const Key k{r.src, r.dst, r.sport, r.dport, r.proto};
+  CtSlot *e = lookup(t, c, k);
+  int l;
+  if (!e) l = ST_INV;
+  else if ((e->rev ^ r.rev) == 3) l = ST_EST;
+  else {
+    Cache c2{};
+    const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
+    l = lookup(t, c2, q) ? ST_REL : ST_INV;
+  }
+  if (finish(b, i, r, l)) update(t, c, r, k, e, l);
+}
+
+// Counters from the final rule ids: per-rule and default (ActionLookup_dp.c:96-111,
+// Parser_dp.c:47-58) and accept-established (ConntrackLabel_dp.c:137-188).
+constexpr uint32_t kCountBlock = 1024;
+constexpr uint32_t kLdsRules = 1024;          // LDS bins per chain; rules above use global atomics
+constexpr uint64_t kCountChunk = 65536;       // packets per workgroup: u32 byte bins cannot wrap
+
+__global__ void ct_count_kernel(CtBatch b, const CtRec *rec) {
+  constexpr uint32_t per = 2 + kLdsRules;
+  __shared__ uint32_t pk[3 * per], by[3 * per];
+  for (uint32_t k = threadIdx.x; k < 3 * per; k += blockDim.x) { pk[k] = 0; by[k] = 0; }
+  __syncthreads();
+  const uint64_t lo = uint64_t(blockIdx.x) * kCountChunk;
+  const uint64_t hi = lo + kCountChunk < b.n ? lo + kCountChunk : b.n;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int32_t rid = b.rule_ids[i];
+    const CtRec &r = rec[i];
+    const uint32_t c = r.cinfo & 3;
+    if (c == 3) continue;
+    uint32_t bin;
+    if (rid >= 0) {
+      if (uint32_t(rid) >= b.ncounted[c]) continue;
+      if (uint32_t(rid) >= kLdsRules) {
+        atomicAdd(&b.ctr[c][2 + 2 * uint64_t(rid)], 1ull);
+        atomicAdd(&b.ctr[c][3 + 2 * uint64_t(rid)], static_cast<unsigned long long>(r.len));
+        continue;
+      }
+      bin = 2 + uint32_t(rid);
+    } else if (rid == PCN_IPT_RID_DEFAULT) {
+      bin = 0;
+    } else if (rid == -3) {
+      bin = 1;
+    } else {
+      continue;
+    }
+    atomicAdd(&pk[c * per + bin], 1u);
+    atomicAdd(&by[c * per + bin], uint32_t(r.len));
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < 3 * per; k += blockDim.x) {
+    if (!pk[k]) continue;
+    const uint32_t c = k / per, bin = k % per;
+    unsigned long long *dp, *db;
+    if (bin == 0) { dp = &b.ctr[c][0]; db = &b.ctr[c][1]; }
+    else if (bin == 1) { dp = &b.ae_ctr[2 * c]; db = &b.ae_ctr[2 * c + 1]; }
+    else { dp = &b.ctr[c][2 + 2 * (bin - 2)]; db = &b.ctr[c][3 + 2 * (bin - 2)]; }
+    atomicAdd(dp, static_cast<unsigned long long>(pk[k]));
+    atomicAdd(db, static_cast<unsigned long long>(by[k]));
+  }
+}
+
+// Stateless accept-established: rule 0 of an AE chain is exactly
+// {conntrack ESTABLISHED, ACCEPT}, so its hits are the packets the reference
+// accepts before the chain (ConntrackLabel_dp.c:580-616).
+__global__ void ae_move_kernel(CtBatch b) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int c = 0; c < 3; ++c) {
+    if (!((b.ae_mask >> c) & 1) || !b.ncounted[c]) continue;
+    b.ae_ctr[2 * c] += b.ctr[c][2];
+    b.ae_ctr[2 * c + 1] += b.ctr[c][3];
+    b.ctr[c][2] = 0;
+    b.ctr[c][3] = 0;
+  }
+}
+
+__global__ void ae_rid_kernel(CtBatch b) {
+  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < b.n; i += step) {
+    if (b.rule_ids[i] != 0) continue;
+    uint32_t w[18], L;
+    load_window(b, i, w, L);
+    const Parsed p = parse(w, L, b.hook);
+    const uint32_t chain = b.direction == PCN_IPT_EGRESS ? PCN_IPT_OUTPUT
+                           : (b.nlocal && localip_has(b, p.dst)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
+    if ((b.ae_mask >> chain) & 1) b.rule_ids[i] = -3;
+  }
+}
+
+unsigned grid_for(uint64_t n, unsigned block, int num_cus) {
+  const uint64_t want = (n + block - 1) / block;
+  const uint64_t cap = uint64_t(num_cus) * 16;
+  return static_cast<unsigned>(want < cap ? (want ? want : 1) : cap);
+}
+
+}  // namespace
+
+struct CtScratch {
+  uint64_t cap = 0;
+  uint32_t *pp = nullptr, *last = nullptr, *pports = nullptr, *keys = nullptr, *keys2 = nullptr;
+  uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *hard_cnt = nullptr;
+  CtRec *rec = nullptr;
+  void *temp = nullptr;
+  size_t temp_bytes = 0;
+};
+
+CtScratch *ct_scratch_new() { return new CtScratch(); }
+
+void ct_scratch_free(CtScratch *s) {
+  if (!s) return;
+  for (void *p : {static_cast<void *>(s->pp), static_cast<void *>(s->last), static_cast<void *>(s->pports),
+                  static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
+                  static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
+                  static_cast<void *>(s->hard_cnt), static_cast<void *>(s->rec), s->temp})
+    if (p) (void)hipFree(p);
+  delete s;
+}
+
+int ct_table_init(CtTable &t, uint32_t cap_log2) {
+  ct_table_free(t);
+  const uint64_t n = uint64_t(1) << cap_log2;
+  hipError_t e = hipMalloc(&t.slots, n * sizeof(CtSlot));
+  if (e == hipSuccess) e = hipMemset(t.slots, 0, n * sizeof(CtSlot));
+  if (e == hipSuccess) e = hipMalloc(&t.carry, 64);
+  if (e == hipSuccess) e = hipMemset(t.carry, 0, 64);
+  if (e == hipSuccess) t.stats = reinterpret_cast<unsigned long long *>(t.carry + 2);
+  t.cap_log2 = cap_log2;
+  return e;
+}
+
+void ct_table_free(CtTable &t) {
+  if (t.slots) (void)hipFree(t.slots);
+  if (t.carry) (void)hipFree(t.carry);
+  t.slots = nullptr;
+  t.carry = nullptr;
+  t.stats = nullptr;
+}
+
+#define CT_CHECK(x)                         \
+  do {                                      \
+    const int e_ = int(x);                  \
+    if (e_ != hipSuccess) return int(e_);   \
+  } while (0)
+
+static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
+  if (s.cap < n) {
+    for (uint32_t **p : {&s.pp, &s.last, &s.pports, &s.keys, &s.keys2, &s.idx, &s.idx2, &s.cursor, &s.hard_list}) {
+      if (*p) CT_CHECK(hipFree(*p));
+      CT_CHECK(hipMalloc(p, n * 4));
+    }
+    if (s.rec) CT_CHECK(hipFree(s.rec));
+    CT_CHECK(hipMalloc(&s.rec, n * sizeof(CtRec)));
+    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));
+    s.cap = n;
+  }
+  size_t need_scan = 0, need_sort = 0;
+  CT_CHECK(hipcub::DeviceScan::InclusiveScan(nullptr, need_scan, s.pp, s.last, hipcub::Max(), int(n), st));
+  CT_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, need_sort, s.keys, s.keys2, s.idx, s.idx2, int(n), 0,
+                                              int(kbits), st));
+  const size_t need = std::max(need_scan, need_sort);
+  if (s.temp_bytes < need) {
+    if (s.temp) CT_CHECK(hipFree(s.temp));
+    CT_CHECK(hipMalloc(&s.temp, need));
+    s.temp_bytes = need;
+  }
+  return hipSuccess;
+}
+
+int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream) {
+  if (b.n == 0) return hipSuccess;
+  if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);   // hipCUB item counts are int
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  uint32_t kbits = 8;
+  while (kbits < 30 && (uint64_t(1) << kbits) < 2 * b.n) ++kbits;
+  const uint32_t sentinel = (1u << kbits) - 1;
+  CT_CHECK(grow(s, b.n, kbits, st));
+  const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
+  hipLaunchKernelGGL(ct_parse_kernel, dim3(grid), dim3(blk), 0, st, b, s.pp, s.pports);
+  CT_CHECK(hipGetLastError());
+  size_t tb = s.temp_bytes;
+  CT_CHECK(hipcub::DeviceScan::InclusiveScan(s.temp, tb, s.pp, s.last, hipcub::Max(), int(b.n), st));
+  CT_CHECK(hipMemsetAsync(s.hard_cnt, 0, 4, st));
+  hipLaunchKernelGGL(ct_prep_kernel, dim3(grid), dim3(blk), 0, st, b, s.last, s.pports, t.carry, s.rec, s.keys,
+                     s.idx, kbits, s.hard_cnt, s.hard_list);
+  CT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(ct_carry_kernel, dim3(1), dim3(64), 0, st, b.n, s.last, s.pports, t.carry);
+  CT_CHECK(hipGetLastError());
+  tb = s.temp_bytes;
+  CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
+                                              st));
+  uint32_t nhard = 0;
+  CT_CHECK(hipMemcpyAsync(&nhard, s.hard_cnt, 4, hipMemcpyDeviceToHost, st));
+  CT_CHECK(hipStreamSynchronize(st));
+  std::vector<uint32_t> hard(nhard);
+  if (nhard) {
+    CT_CHECK(hipMemcpy(hard.data(), s.hard_list, nhard * 4ull, hipMemcpyDeviceToHost));
+    std::sort(hard.begin(), hard.end());
+  }
+  const unsigned wgrid = static_cast<unsigned>((b.n + blk - 1) / blk);
+  int first = 1;
+  for (size_t h = 0; h <= hard.size(); ++h) {
+    const uint64_t hi = h < hard.size() ? hard[h] : b.n;
+    hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(blk), 0, st, b, t, s.rec, s.keys2, s.idx2, s.cursor, hi,
+                       first, sentinel);
+    CT_CHECK(hipGetLastError());
+    first = 0;
+    if (h < hard.size()) {
+      hipLaunchKernelGGL(ct_hard_kernel, dim3(1), dim3(64), 0, st, b, t, s.rec, hard[h]);
+      CT_CHECK(hipGetLastError());
+    }
+  }
+  const unsigned cgrid = static_cast<unsigned>((b.n + kCountChunk - 1) / kCountChunk);
+  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.rec);
+  CT_CHECK(hipGetLastError());
+  return hipSuccess;
+}
+
+int ct_ae_fixup(const CtBatch &b, void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (b.rule_ids && b.n) {
+    hipLaunchKernelGGL(ae_rid_kernel, dim3(grid_for(b.n, 256, 256)), dim3(256), 0, st, b);
+    CT_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(ae_move_kernel, dim3(1), dim3(64), 0, st, b);
+  return int(hipGetLastError());
+}
+
+}  // namespace pcn

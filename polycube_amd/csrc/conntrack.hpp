@@ -1,0 +1,88 @@
+// conntrack.hpp — stateful connection tracking on the GPU (host-visible types).
+//
+// The reference labels every IPv4 packet with its connection state from the
+// `connections` table (Iptables_ConntrackLabel_dp.c:190-531) and updates the
+// table for every accepted packet (Iptables_ConntrackTableUpdate_dp.c:141-655),
+// one packet at a time per CPU.  Here a batch runs as:
+//   A. the classify kernel once per possible label (1 run when no reachable
+//      chain has conntrack rules, else 4), counters off, giving each packet's
+//      outcome as a function of its label;
+//   B. ct_parse -> max-scan -> ct_prep: stale ports (quirk Q4), the chain,
+//      the packet's conntrack key and kind; packets that need no table access
+//      are finished here;
+//   C. a stable radix sort of the table-touching packets by key bucket, so
+//      every key's packets form one run in batch order;
+//   D. ct_walk: one lane per run walks its packets in order against the
+//      HBM-resident table (label -> outcome -> update), so the result equals
+//      processing the batch one packet at a time;
+//   E. ct_count: per-rule / default / accept-established counters from the
+//      final rule ids.
+// Echo replies long enough to carry a quoted header (>= 70 B) may read a
+// second key's state: they split the batch into segments and are run one at a
+// time between the walks of the segments (ct_hard).
+#pragma once
+#include <cstdint>
+
+namespace pcn {
+
+// One table slot (32 B).  `tag`: 0 empty, 1 published, 2 being claimed.
+// Slots are never freed (a deleted connection keeps its key with valid = 0),
+// so linear probing stops at the first empty slot.
+struct CtSlot {
+  uint32_t tag;
+  uint32_t src, dst;          // ct_k, ordered (network-order u32 as loaded)
+  uint16_t sport, dport;      // ct_k ports, ordered
+  unsigned long long ttl;     // ct_v
+  uint32_t seq;
+  uint8_t proto, valid, state, rev;   // rev: bit0 ipRev, bit1 portRev
+};
+static_assert(sizeof(CtSlot) == 32, "CtSlot is 32 bytes");
+
+struct CtBatch {
+  const uint8_t *frames;
+  uint64_t frames_bytes;
+  const uint32_t *offsets;
+  const uint16_t *lens;
+  uint32_t stride, fixed_len;
+  uint32_t direction, hook;
+  uint64_t n;
+  const uint32_t *localip;    // sorted NBO u32
+  uint32_t nlocal;
+  uint32_t allow_logic, empty_mask, drop_mask;
+  uint32_t ae_mask;           // bit c: accept-established optimization on for chain c
+  uint32_t nlab;              // outcomes per packet from stage A: 1 or 4
+  const uint8_t *a_verdict;   // [nlab][n]
+  const int32_t *a_rid;       // [nlab][n]
+  uint8_t *verdicts;          // final
+  int32_t *rule_ids;          // final (never null: scratch when the caller has none)
+  unsigned long long *ctr[3];
+  uint32_t ncounted[3];
+  unsigned long long *ae_ctr; // [3][2] pkts, bytes
+};
+
+struct CtTable {
+  CtSlot *slots = nullptr;
+  uint32_t cap_log2 = 0;
+  uint32_t *carry = nullptr;             // stale ports of the shared `packet` struct
+  unsigned long long *stats = nullptr;   // [0] inserts refused because the table was full
+  unsigned long long now = 0;            // the `timestamp` the control plane sets
+};
+
+struct CtScratch;   // device buffers, grown as batches need (conntrack.hip)
+CtScratch *ct_scratch_new();
+void ct_scratch_free(CtScratch *s);
+
+// Stages B-E for one batch whose stage-A outcomes are in b.a_*.  Synchronises
+// the stream once when the batch holds long echo replies.  Returns a hipError_t.
+int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream);
+
+// Stateless batches (labels given per packet) on chains with accept-established
+// on: move rule-0 hits to the accept-established path (rule id -3 and its
+// counters), as ConntrackLabel_dp.c:580-616 takes ESTABLISHED packets there
+// before the chain runs.  rule_ids may be null.
+int ct_ae_fixup(const CtBatch &b, void *stream);
+
+int ct_table_init(CtTable &t, uint32_t cap_log2);
+void ct_table_free(CtTable &t);
+
+}  // namespace pcn

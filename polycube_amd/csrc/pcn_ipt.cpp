@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "conntrack.hpp"
 #include "devchain.h"
 #include "image.hpp"
 #include "jit.hpp"
@@ -125,6 +126,17 @@ struct pcn_ipt {
   int nranks = 1, rank = 0;
   JitCache jit;                                // chain programs (per launch shape)
   uint64_t launches_generic = 0, launches_jit = 0;
+  // accept-established optimization per chain (Iptables.h accept_established_enabled_*)
+  bool ae[PCN_IPT_NCHAINS] = {false, false, false};
+  unsigned long long *d_ae = nullptr;          // [3][2] pkts/bytes_acceptestablished_<Chain>
+  // stateful conntrack (conntrack.hpp)
+  bool ct_on = false;
+  CtTable ct;
+  CtScratch *cts = nullptr;
+  uint8_t *d_labels = nullptr;                 // {0, 1, 2, 3}: constant labels of the stage-A runs
+  unsigned long long *ctr_scratch = nullptr;   // [3][ctr_words]: stage-A counters (discarded)
+  void *ct_buf = nullptr;                      // stage-A outcomes + a rule-id array
+  size_t ct_buf_cap = 0;
 };
 
 namespace pcn {
@@ -202,6 +214,31 @@ void fetch_stats(pcn_ipt *ctx, int chain) {
     cs.stats[id].second += buf[3 + 2 * id];
   }
   hip_check(hipMemset(cs.ctr + 2, 0, 2 * size_t(n) * 8), "hipMemset(counters)");
+  // rule 0 of an accept-established chain also takes (and flushes) the
+  // accept-established counters (ChainStats.cpp:64-103)
+  if (ctx->ae[chain] && !cs.stats.empty()) {
+    unsigned long long ae[2];
+    hip_check(hipMemcpy(ae, ctx->d_ae + 2 * chain, 16, hipMemcpyDeviceToHost), "hipMemcpy(ae counters)");
+    cs.stats[0].first += ae[0];
+    cs.stats[0].second += ae[1];
+    hip_check(hipMemset(ctx->d_ae + 2 * chain, 0, 16), "hipMemset(ae counters)");
+  }
+}
+
+// ChainRule::applyAcceptEstablishedOptimization (ChainRule.cpp:211-238) ->
+// Iptables::enable/disableAcceptEstablished (Iptables.cpp:351-449): rule 0 is
+// exactly {conntrack ESTABLISHED, action ACCEPT}.  The disable switch has no
+// `break`, so disabling INPUT also disables FORWARD and OUTPUT.
+void apply_ae(pcn_ipt *ctx, int chain) {
+  const auto &rules = ctx->chains[chain].rules;
+  bool found = false;
+  if (!rules.empty()) {
+    const Rule &r = rules[0];
+    found = r.conntrack && *r.conntrack == 1 && r.action == PCN_IPT_ACCEPT && !r.src && !r.dst && !r.l4proto &&
+            !r.sport && !r.dport && !r.tcpflags && !r.in_iface && !r.out_iface;
+  }
+  if (found) ctx->ae[chain] = true;
+  else for (int c = chain; c < PCN_IPT_NCHAINS; ++c) ctx->ae[c] = false;
 }
 
 void update_chain(pcn_ipt *ctx, int chain) {       // Chain::updateChain
@@ -256,6 +293,12 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
       hip_check(hipMalloc(&ctx->d_localip, PCN_MAX_LOCALIP * 4), "hipMalloc(localip)");
       hip_check(hipMalloc(&ctx->d_zero, 64), "hipMalloc(zero cell)");
       hip_check(hipMemset(ctx->d_zero, 0, 64), "hipMemset(zero cell)");
+      hip_check(hipMalloc(&ctx->d_ae, 64), "hipMalloc(ae counters)");
+      hip_check(hipMemset(ctx->d_ae, 0, 64), "hipMemset(ae counters)");
+      hip_check(hipMalloc(&ctx->d_labels, 64), "hipMalloc(labels)");
+      const uint8_t labels[4] = {0, 1, 2, 3};
+      hip_check(hipMemcpy(ctx->d_labels, labels, 4, hipMemcpyHostToDevice), "hipMemcpy(labels)");
+      hip_check(hipMalloc(&ctx->ctr_scratch, 3 * ctx->ctr_words * 8), "hipMalloc(scratch counters)");
       for (auto &cs : ctx->chains) {
         hip_check(hipMalloc(&cs.ctr, ctx->ctr_words * 8), "hipMalloc(counters)");
         hip_check(hipMemset(cs.ctr, 0, ctx->ctr_words * 8), "hipMemset(counters)");
@@ -288,6 +331,12 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     }
     if (ctx->d_localip) (void)hipFree(ctx->d_localip);
     if (ctx->d_zero) (void)hipFree(ctx->d_zero);
+    if (ctx->d_ae) (void)hipFree(ctx->d_ae);
+    if (ctx->d_labels) (void)hipFree(ctx->d_labels);
+    if (ctx->ctr_scratch) (void)hipFree(ctx->ctr_scratch);
+    if (ctx->ct_buf) (void)hipFree(ctx->ct_buf);
+    ct_table_free(ctx->ct);
+    ct_scratch_free(ctx->cts);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
   }
   delete ctx;
@@ -327,7 +376,10 @@ int pcn_ipt_chain_append(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule) {
     fetch_stats(ctx, chain);                          // Chain::addRule -> getStatsList
     cs.rules.push_back(std::move(r));
     cs.stats.resize(cs.rules.size());
-    if (ctx->interactive) update_chain(ctx, chain);
+    if (ctx->interactive) {
+      update_chain(ctx, chain);
+      apply_ae(ctx, chain);                           // Chain.cpp:186-188
+    }
     return 0;
   });
 }
@@ -342,7 +394,10 @@ int pcn_ipt_chain_insert(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rul
     fetch_stats(ctx, chain);
     cs.rules.insert(cs.rules.begin() + id, std::move(r));
     cs.stats.insert(cs.stats.begin() + id, {0, 0});
-    if (ctx->interactive) update_chain(ctx, chain);
+    if (ctx->interactive) {
+      update_chain(ctx, chain);
+      apply_ae(ctx, chain);                           // Chain.cpp:306-308
+    }
     return 0;
   });
 }
@@ -376,9 +431,10 @@ int pcn_ipt_chain_delete_match(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule
         cs.rules.erase(cs.rules.begin() + i);
         cs.stats.erase(cs.stats.begin() + i);
         if (ctx->interactive) update_chain(ctx, chain);
-        return 0;
+        return 0;                                     // delRule(i); return; (Chain.cpp:358-361)
       }
     }
+    apply_ae(ctx, chain);                             // only reached without a match (Chain.cpp:368)
     return 0;   // no match: the reference returns without error
   });
 }
@@ -421,6 +477,7 @@ int pcn_ipt_chain_apply_rules(pcn_ipt *ctx, int chain) {
     if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
     fetch_stats(ctx, chain);
     update_chain(ctx, chain);
+    apply_ae(ctx, chain);                             // Chain.cpp:408
     return 0;
   });
 }
@@ -487,8 +544,20 @@ uint32_t pcn_ipt_chain_nrw(pcn_ipt *ctx, int chain) {
   return ctx->chains[chain].tables.nrw;
 }
 
-int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
-  return guarded(ctx, [&] {
+}  // extern "C"
+
+namespace {
+
+// Overrides of one stage-A launch of a stateful batch (conntrack.hpp): a
+// constant label for every packet, outcomes into scratch, counters discarded.
+struct StageA {
+  const uint8_t *ct;
+  uint8_t *verdicts;
+  int32_t *rule_ids;
+};
+
+int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa) {
+  {
     if (!b) return fail(-EINVAL, "null batch");
     if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
     if (b->n == 0) return 0;
@@ -573,13 +642,15 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     a.offsets = b->offsets;
     a.lens = b->lens;
     a.has_in_port = b->in_port != nullptr;
-    a.has_ct = b->ct_status != nullptr;
+    a.has_ct = sa || b->ct_status != nullptr;
     a.in_port = a.has_in_port ? b->in_port : reinterpret_cast<const uint16_t *>(ctx->d_zero);
-    a.ct_status = a.has_ct ? b->ct_status : ctx->d_zero;
+    a.ct_status = sa ? sa->ct : a.has_ct ? b->ct_status : ctx->d_zero;
     a.in_port_mask = a.has_in_port ? ~uint64_t(0) : 0;
-    a.ct_mask = a.has_ct ? ~uint64_t(0) : 0;
-    a.verdicts = b->verdicts;
-    a.rule_ids = b->rule_ids;
+    a.ct_mask = a.has_ct && !sa ? ~uint64_t(0) : 0;
+    a.verdicts = sa ? sa->verdicts : b->verdicts;
+    a.rule_ids = sa ? sa->rule_ids : b->rule_ids;
+    if (sa)
+      for (int c = 0; c < PCN_IPT_NCHAINS; ++c) a.ch[c].ctr = ctx->ctr_scratch + c * ctx->ctr_words;
     a.localip = ctx->d_localip;
     a.n = b->n;
     a.stride = b->stride;
@@ -622,6 +693,96 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
     int rc = launch_classify(a, fixed, ch, ns, ctx->num_cus, fn, static_cast<hipStream_t>(stream));
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
+    return 0;
+  }
+}
+
+// The conntrack kernels' view of a batch (conntrack.hpp).
+CtBatch ct_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, uint32_t ae_mask) {
+  CtBatch cb{};
+  cb.frames = b->frames;
+  cb.frames_bytes = b->frames_bytes;
+  cb.offsets = b->offsets;
+  cb.lens = b->lens;
+  cb.stride = b->stride;
+  cb.fixed_len = b->fixed_len;
+  cb.direction = b->direction;
+  cb.hook = b->hook;
+  cb.n = b->n;
+  cb.localip = ctx->d_localip;
+  cb.nlocal = static_cast<uint32_t>(ctx->localip.size());
+  const ChainState &in = ctx->chains[PCN_IPT_INPUT], &fw = ctx->chains[PCN_IPT_FORWARD];
+  cb.allow_logic = in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
+                   in.rules.size() == 0 && fw.rules.size() == 0 && in.desc.nrules == 0 && fw.desc.nrules == 0;
+  for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
+    const ChainState &cs = ctx->chains[c];
+    if (!cs.desc.nrules) cb.empty_mask |= 1u << c;
+    if (cs.desc.default_action == PCN_IPT_DROP) cb.drop_mask |= 1u << c;
+    cb.ctr[c] = cs.ctr;
+    cb.ncounted[c] = cs.desc.ncounted;
+  }
+  cb.ae_mask = ae_mask;
+  cb.ae_ctr = ctx->d_ae;
+  cb.verdicts = b->verdicts;
+  cb.rule_ids = b->rule_ids;
+  return cb;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
+  return guarded(ctx, [&]() -> int {
+    if (!b) return fail(-EINVAL, "null batch");
+    if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
+    if (b->n == 0) return 0;
+    // chains this batch can reach, and which of them run accept-established
+    const uint32_t reach = b->direction == PCN_IPT_EGRESS ? 1u << PCN_IPT_OUTPUT
+                                                          : (1u << PCN_IPT_INPUT) | (1u << PCN_IPT_FORWARD);
+    uint32_t ae_mask = 0, ct_rules = 0;
+    for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
+      if (!((reach >> c) & 1)) continue;
+      if (ctx->ae[c] && ctx->chains[c].desc.nrules) ae_mask |= 1u << c;
+      if (ctx->chains[c].desc.nrules && (ctx->chains[c].desc.present & (1u << PCN_IPT_F_CONNTRACK))) ct_rules = 1;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (!ctx->ct_on) {
+      int rc = launch_batch(ctx, b, stream, nullptr);
+      if (rc || !ae_mask) return rc;
+      device_guard(ctx);
+      const int e = ct_ae_fixup(ct_batch(ctx, b, ae_mask), st);
+      if (e != hipSuccess) return fail(-EIO, std::string("accept-established fixup: ") + hipGetErrorString(hipError_t(e)));
+      return 0;
+    }
+    // stateful: stage A (one classify run per label that can change the outcome), then conntrack.hpp B-E
+    if (b->ct_status) return fail(-EINVAL, "stateful conntrack labels packets from its table: ct_status must be NULL");
+    if (!b->frames || !b->verdicts) return fail(-EINVAL, "frames and verdicts are required");
+    device_guard(ctx);
+    const uint32_t nlab = ct_rules ? 4 : 1;
+    const size_t n = b->n;
+    const size_t need = nlab * n * 5 + (b->rule_ids ? 0 : n * 4) + 64;
+    if (ctx->ct_buf_cap < need) {
+      if (ctx->ct_buf) hip_check(hipFree(ctx->ct_buf), "hipFree");
+      ctx->ct_buf = nullptr;
+      hip_check(hipMalloc(&ctx->ct_buf, need), "hipMalloc(conntrack outcomes)");
+      ctx->ct_buf_cap = need;
+    }
+    int32_t *a_rid = static_cast<int32_t *>(ctx->ct_buf);
+    int32_t *rids = b->rule_ids ? b->rule_ids : a_rid + nlab * n;
+    uint8_t *a_v = reinterpret_cast<uint8_t *>(a_rid + nlab * n + (b->rule_ids ? 0 : n));
+    for (uint32_t l = 0; l < nlab; ++l) {
+      StageA sa{ctx->d_labels + l, a_v + l * n, a_rid + l * n};
+      int rc = launch_batch(ctx, b, stream, &sa);
+      if (rc) return rc;
+    }
+    CtBatch cb = ct_batch(ctx, b, ae_mask);
+    cb.nlab = nlab;
+    cb.a_verdict = a_v;
+    cb.a_rid = a_rid;
+    cb.rule_ids = rids;
+    const int e = ct_run(cb, ctx->ct, *ctx->cts, ctx->num_cus, st);
+    if (e != hipSuccess) return fail(-EIO, std::string("conntrack: ") + hipGetErrorString(hipError_t(e)));
     return 0;
   });
 }
@@ -819,6 +980,128 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
       int rc = launch_sum_ranks(cs.gather, cs.ctr_global, count[c], ctx->nranks, s);
       if (rc != hipSuccess) return fail(-EIO, "sum_ranks launch failed");
     }
+    return 0;
+  });
+}
+
+// ---- stateful conntrack ---------------------------------------------------
+
+int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2) {
+  return guarded(ctx, [&] {
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (capacity_log2 == 0) capacity_log2 = 18;
+    if (capacity_log2 < 10 || capacity_log2 > 30) return fail(-EINVAL, "capacity_log2 must be 10..30");
+    device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    if (!ctx->ct.slots || ctx->ct.cap_log2 != capacity_log2) {
+      const unsigned long long now = ctx->ct.now;
+      hip_check(hipError_t(ct_table_init(ctx->ct, capacity_log2)), "conntrack table");
+      ctx->ct.now = now;
+    }
+    if (!ctx->cts) ctx->cts = ct_scratch_new();
+    ctx->ct_on = true;
+    return 0;
+  });
+}
+
+int pcn_ipt_ct_disable(pcn_ipt *ctx) {
+  return guarded(ctx, [&] {
+    ctx->ct_on = false;
+    return 0;
+  });
+}
+
+int pcn_ipt_ct_clear(pcn_ipt *ctx) {
+  return guarded(ctx, [&] {
+    if (!ctx->ct.slots) return 0;
+    device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    hip_check(hipMemset(ctx->ct.slots, 0, (size_t(1) << ctx->ct.cap_log2) * sizeof(CtSlot)), "hipMemset(conntrack)");
+    hip_check(hipMemset(ctx->ct.carry, 0, 64), "hipMemset(conntrack)");
+    return 0;
+  });
+}
+
+int pcn_ipt_ct_set_time(pcn_ipt *ctx, uint64_t ns) {
+  return guarded(ctx, [&] {
+    ctx->ct.now = ns;
+    return 0;
+  });
+}
+
+int pcn_ipt_ct_dump(pcn_ipt *ctx, pcn_ipt_ct_entry *out, uint32_t cap) {
+  return guarded(ctx, [&] {
+    if (!ctx->ct.slots) return fail(-EINVAL, "conntrack is not enabled");
+    device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    std::vector<CtSlot> slots(size_t(1) << ctx->ct.cap_log2);
+    hip_check(hipMemcpy(slots.data(), ctx->ct.slots, slots.size() * sizeof(CtSlot), hipMemcpyDeviceToHost),
+              "hipMemcpy(conntrack)");
+    std::vector<pcn_ipt_ct_entry> v;
+    for (const CtSlot &e : slots) {
+      if (e.tag != 1 || !e.valid) continue;
+      pcn_ipt_ct_entry x{};
+      x.src_ip = e.src; x.dst_ip = e.dst; x.sport = e.sport; x.dport = e.dport; x.l4proto = e.proto;
+      x.state = e.state; x.ip_rev = e.rev & 1; x.port_rev = (e.rev >> 1) & 1; x.sequence = e.seq; x.ttl = e.ttl;
+      v.push_back(x);
+    }
+    std::sort(v.begin(), v.end(), [](const pcn_ipt_ct_entry &a, const pcn_ipt_ct_entry &b) {
+      if (a.src_ip != b.src_ip) return a.src_ip < b.src_ip;
+      if (a.dst_ip != b.dst_ip) return a.dst_ip < b.dst_ip;
+      if (a.l4proto != b.l4proto) return a.l4proto < b.l4proto;
+      if (a.sport != b.sport) return a.sport < b.sport;
+      return a.dport < b.dport;
+    });
+    if (out) std::memcpy(out, v.data(), std::min<size_t>(v.size(), cap) * sizeof(pcn_ipt_ct_entry));
+    return static_cast<int>(v.size());
+  });
+}
+
+int pcn_ipt_ct_get_info(pcn_ipt *ctx, pcn_ipt_ct_info *out) {
+  return guarded(ctx, [&] {
+    if (!out) return fail(-EINVAL, "null output");
+    *out = pcn_ipt_ct_info{};
+    out->enabled = ctx->ct_on;
+    out->capacity_log2 = ctx->ct.cap_log2;
+    out->now = ctx->ct.now;
+    if (ctx->ct.carry) {
+      device_guard(ctx);
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      unsigned long long lost = 0;
+      hip_check(hipMemcpy(&lost, ctx->ct.stats, 8, hipMemcpyDeviceToHost), "hipMemcpy(conntrack stats)");
+      out->inserts_lost = lost;
+    }
+    return 0;
+  });
+}
+
+int pcn_ipt_set_accept_established(pcn_ipt *ctx, int chain, int on) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    ctx->ae[chain] = on != 0;
+    return 0;
+  });
+}
+
+int pcn_ipt_get_accept_established(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    return ctx->ae[chain] ? 1 : 0;
+  });
+}
+
+int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, int flush) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    unsigned long long v[2] = {0, 0};
+    if (ctx->has_device) {
+      device_guard(ctx);
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      hip_check(hipMemcpy(v, ctx->d_ae + 2 * chain, 16, hipMemcpyDeviceToHost), "hipMemcpy(ae counters)");
+      if (flush) hip_check(hipMemset(ctx->d_ae + 2 * chain, 0, 16), "hipMemset(ae counters)");
+    }
+    if (pkts) *pkts = v[0];
+    if (bytes) *bytes = v[1];
     return 0;
   });
 }

@@ -76,6 +76,11 @@ class ChainInfo(C.Structure):
                 ("part_bytes", C.c_uint64)]
 
 
+class CtInfo(C.Structure):
+    _fields_ = [("enabled", C.c_uint32), ("capacity_log2", C.c_uint32), ("now", C.c_uint64),
+                ("inserts_lost", C.c_uint64)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
@@ -122,6 +127,16 @@ SIGNATURES = {
     "pcn_ipt_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "pcn_ipt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     "pcn_ipt_sync_counters": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pcn_ipt_ct_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "pcn_ipt_ct_disable": (C.c_int, [C.c_void_p]),
+    "pcn_ipt_ct_clear": (C.c_int, [C.c_void_p]),
+    "pcn_ipt_ct_set_time": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "pcn_ipt_ct_dump": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "pcn_ipt_ct_get_info": (C.c_int, [C.c_void_p, C.POINTER(CtInfo)]),
+    "pcn_ipt_set_accept_established": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "pcn_ipt_get_accept_established": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_read_accept_established": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
+                                                  C.POINTER(C.c_uint64), C.c_int]),
 }
 
 _lib = None

@@ -23,6 +23,19 @@ _CHAIN_NAMES = {"INPUT": INPUT, "FORWARD": FORWARD, "OUTPUT": OUTPUT}
 _ACTIONS = {"DROP": DROP, "ACCEPT": ACCEPT}
 
 
+def _ct_entry_dtype():
+    import numpy as np
+    # pcn_ipt_ct_entry (include/pcn_ipt.h)
+    return np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
+                     ("l4proto", "u1"), ("state", "u1"), ("ip_rev", "u1"), ("port_rev", "u1"),
+                     ("sequence", "<u4"), ("ttl", "<u8")], align=True)
+
+
+CT_ENTRY = _ct_entry_dtype()
+CT_STATES = ["NEW", "ESTABLISHED", "RELATED", "INVALID", "SYN_SENT", "SYN_RECV", "FIN_WAIT_1",
+             "FIN_WAIT_2", "LAST_ACK", "TIME_WAIT"]
+
+
 class IptablesError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"{msg} (errno {-code})")
@@ -102,6 +115,22 @@ class Chain:
 
     def reset_counters(self):
         _check(ffi.lib().pcn_ipt_chain_reset_counters(self._h(), self.id))
+
+    @property
+    def accept_established(self):
+        """Accept-established optimization on for this chain (Iptables.h accept_established_enabled_*)."""
+        return bool(_check(ffi.lib().pcn_ipt_get_accept_established(self._h(), self.id)))
+
+    @accept_established.setter
+    def accept_established(self, on):
+        _check(ffi.lib().pcn_ipt_set_accept_established(self._h(), self.id, int(bool(on))))
+
+    def read_accept_established(self, flush=False):
+        """(pkts, bytes) of pkts/bytes_acceptestablished_<Chain>."""
+        pk, by = C.c_uint64(), C.c_uint64()
+        _check(ffi.lib().pcn_ipt_read_accept_established(self._h(), self.id, C.byref(pk), C.byref(by),
+                                                          int(flush)))
+        return pk.value, by.value
 
     def read_counters(self, n, flush=False, scope=0):
         """Raw datapath counters: (pkts[n], bytes[n], def_pkts, def_bytes)."""
@@ -221,6 +250,32 @@ class Iptables:
     def ring(self, slots=4, slot_frames=1 << 20, slot_bytes=None, streams=0, rule_ids=False):
         """Host ingest ring (pcn_ipt_ring_*): pinned slots -> HBM -> classify -> verdicts."""
         return IngestRing(self, slots, slot_frames, slot_bytes or 64 * slot_frames, streams, rule_ids)
+
+    # ---- stateful connection tracking ----
+    def ct_enable(self, capacity_log2=0):
+        _check(ffi.lib().pcn_ipt_ct_enable(self._h, capacity_log2))
+
+    def ct_disable(self):
+        _check(ffi.lib().pcn_ipt_ct_disable(self._h))
+
+    def ct_clear(self):
+        _check(ffi.lib().pcn_ipt_ct_clear(self._h))
+
+    def ct_set_time(self, ns):
+        _check(ffi.lib().pcn_ipt_ct_set_time(self._h, int(ns)))
+
+    def ct_dump(self):
+        """Live connections (session table), as a numpy array of CT_ENTRY, sorted by key."""
+        import numpy as np
+        n = _check(ffi.lib().pcn_ipt_ct_dump(self._h, None, 0))
+        out = np.zeros(max(n, 1), CT_ENTRY)
+        n = _check(ffi.lib().pcn_ipt_ct_dump(self._h, out.ctypes.data, len(out)))
+        return out[:n]
+
+    def ct_info(self):
+        out = ffi.CtInfo()
+        _check(ffi.lib().pcn_ipt_ct_get_info(self._h, C.byref(out)))
+        return {k: getattr(out, k) for k, _ in ffi.CtInfo._fields_}
 
     # ---- multi-GPU counters over RCCL ----
     @staticmethod

@@ -124,6 +124,8 @@ class OracleCube:
                 if norm_rule(r) == want:
                     self.rules[c].pop(i)
                     break
+            else:
+                self._ae(c)            # Chain::deletes applies it only when nothing matched (Chain.cpp:368)
         elif kind == "flush":
             self.rules[c] = []
         elif kind == "default":
@@ -138,7 +140,7 @@ class OracleCube:
             raise ValueError(kind)
         if self.interactive:
             self._apply(c)
-        if kind == "deletes" or (self.interactive and kind in ("append", "insert")):
+        if self.interactive and kind in ("append", "insert"):
             self._ae(c)
 
     def ct_probe(self, packets):
@@ -203,6 +205,27 @@ class GpuCube:
             ch.apply_rules()
         else:
             raise ValueError(kind)
+
+    def ct_probe(self, packets):
+        """Stateful: the packets in order (direction runs split into batches)."""
+        torch = self.torch
+        dev = torch.device("cuda", self.ipt.device)
+        out = []
+        i = 0
+        while i < len(packets):
+            j = i
+            while j < len(packets) and packets[j]["dir"] == packets[i]["dir"]:
+                j += 1
+            sel = packets[i:j]
+            f, lens, ports = ct_probe_frames(sel)
+            v, _ = self.ipt.classify(torch.from_numpy(f).to(dev), n=len(sel),
+                                     lens=torch.from_numpy(lens.astype(np.int16)).to(dev), stride=128,
+                                     in_port=torch.from_numpy(ports.astype(np.int16)).to(dev),
+                                     direction=DIRS[sel[0]["dir"]])
+            torch.cuda.synchronize()
+            out.extend(int(x) for x in v.cpu().numpy())
+            i = j
+        return out
 
     def probe(self, packets):
         torch = self.torch

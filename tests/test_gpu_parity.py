@@ -41,6 +41,7 @@ def make_pair(rules_by_chain, defaults=None, localip=(), ports=PORTS, **cfg):
         rules = rules_by_chain.get(chain, [])
         d = defaults.get(chain, "ACCEPT")
         o.set_chain(chain, rules, d)
+        o.apply_accept_established(chain)          # Chain::applyRules (Chain.cpp:408)
         ch = ipt.chain(chain)
         for r in rules:
             ch.append(**r)
