@@ -109,6 +109,32 @@ def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3):
     return best
 
 
+def ct_rate(ipt, rs, n, dev, steps=5, warmup=2, flows=1 << 16, seed=0xC7):
+    """Stateful conntrack (pcn_ipt_ct_*) on the same chain: n 64-byte frames of
+    `flows` interleaved connections (TCP handshakes/closes, UDP, ICMP), the
+    table carried across steps.  Returns (Mpkt/s, ms per step, live entries)."""
+    import torch
+
+    from polycube_amd import synth
+    f, _ = synth.flow_traffic(n, flows, seed, stride=64, rs=rs)
+    frames = torch.from_numpy(f).to(dev)
+    verdicts = torch.empty(n, dtype=torch.uint8, device=dev)
+    ipt.ct_enable(20)
+    ipt.ct_set_time(1_700_000_000 * 10**9)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(warmup):
+        ipt.classify(frames, n=n, verdicts=verdicts, stream=stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ipt.classify(frames, n=n, verdicts=verdicts, stream=stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    live = len(ipt.ct_dump())
+    ipt.ct_disable()
+    return n * steps / el / 1e6, el / steps * 1e3, live
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,6 +147,7 @@ def main():
                     help="BASELINE.json config: 3 = the headline (default); 2 and 5 are secondary measurements")
     ap.add_argument("--hook", default="xdp", choices=("xdp", "tc"),
                     help="attach-point semantics (tc: outer VLAN tags stripped before classification)")
+    ap.add_argument("--no-ct", action="store_true", help="skip the stateful-conntrack leg")
     ap.add_argument("--jit", type=int, default=1,
                     help="chain programs: 1 compiled before the first launch (default), 0 background, -1 off")
     args = ap.parse_args()
@@ -255,6 +282,13 @@ def main():
             line["e2e"] = {"value": round(e2e_rate(ipt, frames_host, n), 2), "unit": "Mpkt/s",
                            "what": "host ingest ring (pcn_ipt_ring): pinned slots -> H2D -> classify -> D2H verdicts, "
                                    "4 slots x 2^21 frames in flight over 4 streams"}
+        if world == 1 and not args.no_ct and cfg == 3:
+            rate, ms, live = ct_rate(ipt, rs, n, dev)
+            line["stateful_conntrack"] = {
+                "value": round(rate, 2), "unit": "Mpkt/s", "ms_per_step": round(ms, 3),
+                "what": f"same chain with the connection table on (pcn_ipt_ct_enable): 2^{args.log2n} 64B frames of "
+                        f"2^16 interleaved flows, labels from and updates to the HBM table in batch order "
+                        f"({live} live entries after the run)"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

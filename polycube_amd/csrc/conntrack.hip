@@ -282,32 +282,52 @@ __device__ CtSlot *table_slot(const CtTable &t, const Key &k, bool claim) {
   return nullptr;
 }
 
-struct Cache {              // the last key a walking lane touched
-  Key k;
-  CtSlot *e;
-  bool valid;
+// A connection's value (ct_v) while a walking lane owns it, in registers.
+// Everything below passes values, never addresses of locals, so the lane's
+// state stays in VGPRs (an address-taken local would live in scratch).
+struct Ent {
+  unsigned long long ttl;
+  uint32_t seq;
+  uint8_t state, rev, live;
 };
 
-__device__ __forceinline__ CtSlot *lookup(const CtTable &t, Cache &c, const Key &k) {
-  if (!c.valid || !same(c.k, k)) {
-    c.k = k;
-    c.e = table_slot(t, k, false);
-    c.valid = true;
+struct Cache {              // the key a walking lane last touched, its slot and value
+  Key k;
+  CtSlot *e;                // slot holding k (live or deleted), or null
+  Ent v;
+  bool valid, dirty;
+};
+
+__device__ __forceinline__ void flush(Cache &c) {
+  if (c.dirty && c.e) {
+    c.e->ttl = c.v.ttl; c.e->seq = c.v.seq; c.e->state = c.v.state; c.e->rev = c.v.rev; c.e->valid = c.v.live;
   }
-  return c.e && c.e->valid ? c.e : nullptr;
+  c.dirty = false;
 }
 
-// connections.update (noexist = false) / .insert (BPF_NOEXIST)
-__device__ __forceinline__ void put(const CtTable &t, Cache &c, const Key &k, unsigned long long ttl, uint8_t state,
-                                   uint32_t seq, uint8_t rev, bool noexist) {
-  CtSlot *e = lookup(t, c, k);
-  if (e && noexist) return;
-  if (!e) {
-    e = c.e ? c.e : table_slot(t, k, true);
-    c.e = e;
-    if (!e) return;
+// connections.lookup: makes k the cached key; returns whether it is live (value in c.v).
+__device__ __forceinline__ bool lookup(const CtTable &t, Cache &c, const Key &k) {
+  if (!c.valid || !same(c.k, k)) {
+    flush(c);
+    c.k = k;
+    c.e = table_slot(t, k, false);
+    c.v = Ent{};
+    if (c.e) { c.v.ttl = c.e->ttl; c.v.seq = c.e->seq; c.v.state = c.e->state; c.v.rev = c.e->rev; c.v.live = c.e->valid; }
+    c.valid = true;
   }
-  e->ttl = ttl; e->state = state; e->seq = seq; e->rev = rev; e->valid = 1;
+  return c.v.live;
+}
+
+// connections.update (noexist = false) / .insert (BPF_NOEXIST) of the cached key
+__device__ __forceinline__ void put(const CtTable &t, Cache &c, unsigned long long ttl, uint8_t state, uint32_t seq,
+                                   uint8_t rev, bool noexist) {
+  if (c.v.live && noexist) return;
+  if (!c.e) {
+    c.e = table_slot(t, c.k, true);
+    if (!c.e) return;
+  }
+  c.v = Ent{ttl, seq, state, rev, 1};
+  c.dirty = true;
 }
 
 __device__ __forceinline__ bool syn_only(uint8_t f) { return (f & SYN) && (f | SYN) == SYN; }
@@ -317,147 +337,211 @@ __device__ __forceinline__ bool synack_only(uint8_t f) {
 }
 
 // ConntrackLabel_dp.c:230-433 for TCP/UDP/echo/echo-reply(short)/errors
-// against the entry e (live, or null); -1 = RX_DROP.
-__device__ int label_of(const CtRec &r, const CtSlot *e) {
-  const bool fwd = e && e->rev == r.rev;
-  const bool rev = e && ((e->rev ^ r.rev) == 3);
+// against the entry e (live or not); -1 = RX_DROP.
+__device__ int label_of(const CtRec &r, bool live, const Ent &e) {
+  const bool fwd = live && e.rev == r.rev;
+  const bool rev = live && ((e.rev ^ r.rev) == 3);
   switch (r.kind) {
   case K_TCP:
     if (fwd || rev) {
       if (r.flags & RST) return ST_EST;
-      const uint8_t s = e->state;
+      const uint8_t s = e.state;
       if (s == ST_SYN_SENT)
-        return fwd ? (syn_only(r.flags) ? ST_NEW : ST_INV) : (synack_only(r.flags) && r.ack == e->seq ? ST_EST : ST_INV);
+        return fwd ? (syn_only(r.flags) ? ST_NEW : ST_INV) : (synack_only(r.flags) && r.ack == e.seq ? ST_EST : ST_INV);
       if (s == ST_SYN_RECV)
-        return fwd ? (ack_only(r.flags) && r.ack == e->seq ? ST_EST : ST_INV)
-                   : (synack_only(r.flags) && r.ack == e->seq ? ST_EST : ST_INV);
+        return fwd ? (ack_only(r.flags) && r.ack == e.seq ? ST_EST : ST_INV)
+                   : (synack_only(r.flags) && r.ack == e.seq ? ST_EST : ST_INV);
       if (s == ST_EST || s == ST_FIN_WAIT_1 || s == ST_FIN_WAIT_2 || s == ST_LAST_ACK) return ST_EST;
       if (s == ST_TIME_WAIT && syn_only(r.flags)) return ST_NEW;
       return ST_INV;
     }
     return syn_only(r.flags) ? ST_NEW : ST_INV;
   case K_UDP:
-    if (fwd) return e->state == ST_NEW ? ST_NEW : ST_EST;
+    if (fwd) return e.state == ST_NEW ? ST_NEW : ST_EST;
     if (rev) return ST_EST;
     return ST_NEW;
   case K_ECHO:
     return ST_NEW;
   case K_REPLY:                                   // < 70 bytes: the miss path drops
-    if (!e) return ST_INV;
+    if (!live) return ST_INV;
     return rev ? ST_EST : -1;
   case K_ERR:
-    return e ? ST_REL : ST_INV;
+    return live ? ST_REL : ST_INV;
   default:
     return ST_INV;
   }
 }
 
-// ConntrackTableUpdate_dp.c:141-655 for an accepted packet with label l.
-__device__ void update(const CtTable &t, Cache &c, const CtRec &r, const Key &k, CtSlot *e, int l) {
+// ConntrackTableUpdate_dp.c:141-655 for an accepted packet with label l; the
+// cached key is the packet's own.
+__device__ void update(const CtTable &t, Cache &c, const CtRec &r, int l) {
   if (l == ST_INV) return;
   const unsigned long long now = t.now;
+  const bool live = c.v.live;
+  Ent &e = c.v;
+  if (live) c.dirty = true;
   if (r.kind == K_TCP) {
     if (r.flags & RST) return;
-    const int dir = !e ? 0 : e->rev == r.rev ? 1 : ((e->rev ^ r.rev) == 3) ? 2 : 0;
+    const int dir = !live ? 0 : e.rev == r.rev ? 1 : ((e.rev ^ r.rev) == 3) ? 2 : 0;
     if (dir) {
-      const uint8_t s = e->state;
+      const uint8_t s = e.state;
       if (s == ST_SYN_SENT) {
-        if (dir == 1) { if (syn_only(r.flags)) e->ttl = now + TCP_SYN_SENT_T; return; }
-        if (synack_only(r.flags) && r.ack == e->seq) {
-          e->state = ST_SYN_RECV; e->ttl = now + TCP_SYN_RECV_T; e->seq = r.seq + HEX_BE_ONE;
+        if (dir == 1) { if (syn_only(r.flags)) e.ttl = now + TCP_SYN_SENT_T; return; }
+        if (synack_only(r.flags) && r.ack == e.seq) {
+          e.state = ST_SYN_RECV; e.ttl = now + TCP_SYN_RECV_T; e.seq = r.seq + HEX_BE_ONE;
         }
         return;
       }
       if (s == ST_SYN_RECV) {
         if (dir == 1) {
-          if (ack_only(r.flags) && r.ack == e->seq) { e->state = ST_EST; e->ttl = now + TCP_ESTABLISHED_T; }
-        } else if (synack_only(r.flags) && r.ack == e->seq) {
-          e->ttl = now + TCP_SYN_RECV_T;
+          if (ack_only(r.flags) && r.ack == e.seq) { e.state = ST_EST; e.ttl = now + TCP_ESTABLISHED_T; }
+        } else if (synack_only(r.flags) && r.ack == e.seq) {
+          e.ttl = now + TCP_SYN_RECV_T;
         }
         return;
       }
       if (s == ST_EST) {
-        if (r.flags & FIN) { e->state = ST_FIN_WAIT_1; e->ttl = now + TCP_FIN_WAIT_T; e->seq = r.ack; }
-        else e->ttl = now + TCP_ESTABLISHED_T;
+        if (r.flags & FIN) { e.state = ST_FIN_WAIT_1; e.ttl = now + TCP_FIN_WAIT_T; e.seq = r.ack; }
+        else e.ttl = now + TCP_ESTABLISHED_T;
         return;
       }
       if (s == ST_FIN_WAIT_1 || s == ST_FIN_WAIT_2) {
         if (s == ST_FIN_WAIT_1) {
-          if (!((r.flags & ACK) && r.seq == e->seq)) return;
-          e->state = ST_FIN_WAIT_2;                // no goto: falls into FIN_WAIT_2
+          if (!((r.flags & ACK) && r.seq == e.seq)) return;
+          e.state = ST_FIN_WAIT_2;                 // no goto: falls into FIN_WAIT_2
         }
-        if (r.flags & FIN) { e->state = ST_LAST_ACK; e->ttl = now + TCP_LAST_ACK_T; e->seq = r.ack; }
-        else e->ttl = now + TCP_FIN_WAIT_T;
+        if (r.flags & FIN) { e.state = ST_LAST_ACK; e.ttl = now + TCP_LAST_ACK_T; e.seq = r.ack; }
+        else e.ttl = now + TCP_FIN_WAIT_T;
         return;
       }
       if (s == ST_LAST_ACK) {
-        if ((r.flags & ACK) && r.seq == e->seq) e->state = ST_TIME_WAIT;
-        e->ttl = now + TCP_LAST_ACK_T;
+        if ((r.flags & ACK) && r.seq == e.seq) e.state = ST_TIME_WAIT;
+        e.ttl = now + TCP_LAST_ACK_T;
         return;
       }
       if (s != ST_TIME_WAIT || l != ST_NEW) return;   // TIME_WAIT + NEW: goto TCP_MISS
     }
-    if (syn_only(r.flags)) put(t, c, k, now + TCP_SYN_SENT_T, ST_SYN_SENT, r.seq + HEX_BE_ONE, r.rev, false);
+    if (syn_only(r.flags)) put(t, c, now + TCP_SYN_SENT_T, ST_SYN_SENT, r.seq + HEX_BE_ONE, r.rev, false);
     return;
   }
   if (r.kind == K_UDP) {
-    if (e && e->rev == r.rev) { e->ttl = now + (e->state == ST_NEW ? UDP_NEW_TIMEOUT : UDP_ESTABLISHED_TIMEOUT); return; }
-    if (e && (e->rev ^ r.rev) == 3) {
-      if (e->state == ST_NEW) { e->ttl = now + UDP_NEW_TIMEOUT; e->state = ST_EST; }
-      else e->ttl = now + UDP_ESTABLISHED_TIMEOUT;
+    if (live && e.rev == r.rev) { e.ttl = now + (e.state == ST_NEW ? UDP_NEW_TIMEOUT : UDP_ESTABLISHED_TIMEOUT); return; }
+    if (live && (e.rev ^ r.rev) == 3) {
+      if (e.state == ST_NEW) { e.ttl = now + UDP_NEW_TIMEOUT; e.state = ST_EST; }
+      else e.ttl = now + UDP_ESTABLISHED_TIMEOUT;
       return;
     }
-    put(t, c, k, now + UDP_NEW_TIMEOUT, ST_NEW, 0, r.rev, true);
+    put(t, c, now + UDP_NEW_TIMEOUT, ST_NEW, 0, r.rev, true);
     return;
   }
-  if (r.kind == K_ECHO) { put(t, c, k, now + ICMP_TIMEOUT, ST_NEW, 0, r.rev, true); return; }
+  if (r.kind == K_ECHO) { put(t, c, now + ICMP_TIMEOUT, ST_NEW, 0, r.rev, true); return; }
   if (r.kind == K_REPLY || r.kind == K_HARD) {
-    if (e) e->valid = 0;                           // connections.delete
+    if (live) e.live = 0;                          // connections.delete
   }
 }
 
-// Final outcome of a labelled packet (label -1: dropped by ConntrackLabel).
-__device__ __forceinline__ bool finish(const CtBatch &b, uint64_t i, const CtRec &r, int l) {
+// Outcome (rule id << 1 | verdict) of a labelled packet with label l (-1:
+// dropped by ConntrackLabel), from its stage-A outcomes o0..o3 (per label).
+__device__ __forceinline__ int32_t outcome(const CtBatch &b, int32_t o0, int32_t o1, int32_t o2, int32_t o3,
+                                           const CtRec &r, int l) {
   const bool pass = r.cinfo & 4;
   const uint32_t chain = r.cinfo & 3;
-  uint8_t v;
-  int32_t rid;
-  if (l < 0) { v = PCN_IPT_DROP; rid = pass ? b.a_rid[i] : PCN_IPT_RID_NOCHAIN; }
-  else if (pass) { v = b.a_verdict[i]; rid = b.a_rid[i]; }
-  else if (((b.ae_mask >> chain) & 1) && l == ST_EST) { v = PCN_IPT_ACCEPT; rid = -3; }
-  else {
-    const uint64_t o = (b.nlab == 4 ? uint64_t(l) : 0) * b.n + i;
-    v = b.a_verdict[o];
-    rid = b.a_rid[o];
-  }
-  b.verdicts[i] = v;
-  b.rule_ids[i] = rid;
-  return v == PCN_IPT_ACCEPT && l >= 0;
+  if (l < 0) return pass ? (o0 & ~1) : int32_t(PCN_IPT_RID_NOCHAIN) * 2;   // RX_DROP
+  if (pass) return o0;
+  if (((b.ae_mask >> chain) & 1) && l == ST_EST) return -3 * 2 + PCN_IPT_ACCEPT;
+  if (b.nlab != 4) return o0;
+  return l == 0 ? o0 : l == 1 ? o1 : l == 2 ? o2 : o3;
 }
 
-__device__ __forceinline__ void process(const CtBatch &b, const CtTable &t, Cache &c, uint64_t i, const CtRec &r) {
-  const Key k{r.src, r.dst, r.sport, r.dport, r.proto};
-  CtSlot *e = lookup(t, c, k);
-  const int l = label_of(r, e);
-  if (finish(b, i, r, l) && r.kind != K_ERR) update(t, c, r, k, e, l);
+// A packet's walk input in sorted order (64 B: one line): its record, key
+// bucket, batch index and stage-A outcomes (rule id << 1 | verdict per label).
+struct WalkRec {
+  CtRec r;
+  uint32_t key, idx;
+  int32_t o0, o1, o2, o3;
+  uint32_t pad[2];
+};
+static_assert(sizeof(WalkRec) == 64, "WalkRec is 64 bytes");
+
+__device__ __forceinline__ int32_t process(const CtBatch &b, const CtTable &t, Cache &c, const WalkRec &w) {
+  const CtRec &r = w.r;
+  const bool live = lookup(t, c, Key{r.src, r.dst, r.sport, r.dport, r.proto});
+  const int l = label_of(r, live, c.v);
+  const int32_t o = outcome(b, w.o0, w.o1, w.o2, w.o3, r, l);
+  if ((o & 1) == PCN_IPT_ACCEPT && l >= 0 && r.kind != K_ERR) update(t, c, r, l);
+  return o;
 }
 
-// One lane per run of equal key buckets (in batch order), over the packets
-// with index < hi it has not done yet.
-__global__ void ct_walk_kernel(CtBatch b, CtTable t, const CtRec *rec, const uint32_t *skeys, const uint32_t *sidx,
-                               uint32_t *cursor, uint64_t hi, int first, uint32_t sentinel) {
-  const uint64_t p = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= b.n) return;
-  const uint32_t k = skeys[p];
-  if (k == sentinel || (p > 0 && skeys[p - 1] == k)) return;
-  uint64_t q = first ? p : cursor[p];
-  Cache c{};
-  for (; q < b.n && skeys[q] == k; ++q) {
+__device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, uint64_t i) {
+  return l < b.nlab ? (b.a_rid[l * b.n + i] * 2) | b.a_verdict[l * b.n + i] : 0;
+}
+
+// After the sort: walk records in sorted order (each walking lane then reads
+// consecutive lines) and the list of run heads.
+__global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *skeys, const uint32_t *sidx,
+                                 WalkRec *wrec, uint32_t *heads, uint32_t *nheads, uint32_t sentinel) {
+  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < b.n; q += step) {
+    const uint32_t k = skeys[q];
+    if (k == sentinel) continue;
     const uint32_t i = sidx[q];
-    if (i >= hi) break;
-    process(b, t, c, i, rec[i]);
+    WalkRec w;
+    w.r = rec[i];
+    w.key = k;
+    w.idx = i;
+    w.o0 = pack_outcome(b, 0, i);
+    w.o1 = pack_outcome(b, 1, i);
+    w.o2 = pack_outcome(b, 2, i);
+    w.o3 = pack_outcome(b, 3, i);
+    w.pad[0] = w.pad[1] = 0;
+    wrec[q] = w;
+    if (q == 0 || skeys[q - 1] != k) heads[atomicAdd(nheads, 1u)] = static_cast<uint32_t>(q);
   }
-  cursor[p] = static_cast<uint32_t>(q);
+}
+
+// One lane per run of equal key buckets, in batch order, over the packets with
+// index < hi it has not done yet.  The lane keeps its connection in registers
+// and its next two records in flight.  The walk's time is the longest run
+// (the heaviest flow of the batch) times the per-packet cost of one lane
+// (~0.9 us measured: instruction-bound, the wave executes the union of its
+// lanes' paths); 4 records in flight measured the same.
+__global__ void ct_walk_kernel(CtBatch b, CtTable t, const WalkRec *wrec, int32_t *sres, const uint32_t *heads,
+                               const uint32_t *nheads, uint32_t *cursor, uint64_t hi, int first) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= *nheads) return;
+  const uint32_t p = heads[j];
+  const uint32_t k = wrec[p].key;
+  uint64_t q = first ? p : cursor[j];
+  const uint64_t last = b.n - 1;
+  Cache c{};
+  // two records in flight in named registers, A/B alternating (a register
+  // move of an in-flight load would wait for it)
+  WalkRec A = wrec[q < last ? q : last];
+  WalkRec B = wrec[q + 1 < last ? q + 1 : last];
+  for (;;) {
+    if (q >= b.n || A.key != k || A.idx >= hi) break;
+    sres[q] = process(b, t, c, A);
+    A = wrec[q + 2 < last ? q + 2 : last];
+    ++q;
+    if (q >= b.n || B.key != k || B.idx >= hi) break;
+    sres[q] = process(b, t, c, B);
+    B = wrec[q + 2 < last ? q + 2 : last];
+    ++q;
+  }
+  flush(c);
+  cursor[j] = static_cast<uint32_t>(q);
+}
+
+__global__ void ct_scatter_kernel(CtBatch b, const uint32_t *skeys, const uint32_t *sidx, const int32_t *sres,
+                                  uint32_t sentinel) {
+  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < b.n; q += step) {
+    if (skeys[q] == sentinel) continue;
+    const uint32_t i = sidx[q];
+    const int32_t o = sres[q];
+    b.verdicts[i] = static_cast<uint8_t>(o & 1);
+    b.rule_ids[i] = o >> 1;
+  }
 }
 
 // An echo reply long enough to quote a header (ConntrackLabel_dp.c:450-531):
@@ -465,18 +549,18 @@ __global__ void ct_walk_kernel(CtBatch b, CtTable t, const CtRec *rec, const uin
 __global__ void ct_hard_kernel(CtBatch b, CtTable t, const CtRec *rec, uint32_t i) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const CtRec r = rec[i];
+  Cache c2{};
+  const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
+  const bool quoted = lookup(t, c2, q);            // read-only
   Cache c{};
-  const Key k{r.src, r.dst, r.sport, r.dport, r.proto};
-  CtSlot *e = lookup(t, c, k);
-  int l;
-  if (!e) l = ST_INV;
-  else if ((e->rev ^ r.rev) == 3) l = ST_EST;
-  else {
-    Cache c2{};
-    const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
-    l = lookup(t, c2, q) ? ST_REL : ST_INV;
-  }
-  if (finish(b, i, r, l)) update(t, c, r, k, e, l);
+  const bool live = lookup(t, c, Key{r.src, r.dst, r.sport, r.dport, r.proto});
+  const int l = !live ? ST_INV : ((c.v.rev ^ r.rev) == 3) ? ST_EST : quoted ? ST_REL : ST_INV;
+  const int32_t o = outcome(b, pack_outcome(b, 0, i), pack_outcome(b, 1, i), pack_outcome(b, 2, i),
+                            pack_outcome(b, 3, i), r, l);
+  if ((o & 1) == PCN_IPT_ACCEPT && l >= 0) update(t, c, r, l);
+  flush(c);
+  b.verdicts[i] = static_cast<uint8_t>(o & 1);
+  b.rule_ids[i] = o >> 1;
 }
 
 // Counters from the final rule ids: per-rule and default (ActionLookup_dp.c:96-111,
@@ -568,7 +652,10 @@ struct CtScratch {
   uint64_t cap = 0;
   uint32_t *pp = nullptr, *last = nullptr, *pports = nullptr, *keys = nullptr, *keys2 = nullptr;
   uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *hard_cnt = nullptr;
+  uint32_t *heads = nullptr;
+  int32_t *sres = nullptr;
   CtRec *rec = nullptr;
+  WalkRec *wrec = nullptr;
   void *temp = nullptr;
   size_t temp_bytes = 0;
 };
@@ -580,7 +667,8 @@ void ct_scratch_free(CtScratch *s) {
   for (void *p : {static_cast<void *>(s->pp), static_cast<void *>(s->last), static_cast<void *>(s->pports),
                   static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
-                  static_cast<void *>(s->hard_cnt), static_cast<void *>(s->rec), s->temp})
+                  static_cast<void *>(s->hard_cnt), static_cast<void *>(s->rec), static_cast<void *>(s->wrec),
+                  static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -613,13 +701,16 @@ void ct_table_free(CtTable &t) {
 
 static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
   if (s.cap < n) {
-    for (uint32_t **p : {&s.pp, &s.last, &s.pports, &s.keys, &s.keys2, &s.idx, &s.idx2, &s.cursor, &s.hard_list}) {
+    for (uint32_t **p : {&s.pp, &s.last, &s.pports, &s.keys, &s.keys2, &s.idx, &s.idx2, &s.cursor, &s.hard_list,
+                         &s.heads, reinterpret_cast<uint32_t **>(&s.sres)}) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, n * 4));
     }
     if (s.rec) CT_CHECK(hipFree(s.rec));
     CT_CHECK(hipMalloc(&s.rec, n * sizeof(CtRec)));
-    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));
+    if (s.wrec) CT_CHECK(hipFree(s.wrec));
+    CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
+    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1] run heads
     s.cap = n;
   }
   size_t need_scan = 0, need_sort = 0;
@@ -657,27 +748,36 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   tb = s.temp_bytes;
   CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
                                               st));
-  uint32_t nhard = 0;
-  CT_CHECK(hipMemcpyAsync(&nhard, s.hard_cnt, 4, hipMemcpyDeviceToHost, st));
+  CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 4, st));
+  hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.rec, s.keys2, s.idx2, s.wrec,
+                     s.heads, s.hard_cnt + 1, sentinel);
+  CT_CHECK(hipGetLastError());
+  uint32_t cnt[2] = {0, 0};
+  CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, 8, hipMemcpyDeviceToHost, st));
   CT_CHECK(hipStreamSynchronize(st));
+  const uint32_t nhard = cnt[0], nheads = cnt[1];
   std::vector<uint32_t> hard(nhard);
   if (nhard) {
     CT_CHECK(hipMemcpy(hard.data(), s.hard_list, nhard * 4ull, hipMemcpyDeviceToHost));
     std::sort(hard.begin(), hard.end());
   }
-  const unsigned wgrid = static_cast<unsigned>((b.n + blk - 1) / blk);
+  const unsigned wblk = 64, wgrid = (nheads + wblk - 1) / wblk;
   int first = 1;
   for (size_t h = 0; h <= hard.size(); ++h) {
     const uint64_t hi = h < hard.size() ? hard[h] : b.n;
-    hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(blk), 0, st, b, t, s.rec, s.keys2, s.idx2, s.cursor, hi,
-                       first, sentinel);
-    CT_CHECK(hipGetLastError());
+    if (nheads) {
+      hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(wblk), 0, st, b, t, s.wrec, s.sres, s.heads,
+                         s.hard_cnt + 1, s.cursor, hi, first);
+      CT_CHECK(hipGetLastError());
+    }
     first = 0;
     if (h < hard.size()) {
       hipLaunchKernelGGL(ct_hard_kernel, dim3(1), dim3(64), 0, st, b, t, s.rec, hard[h]);
       CT_CHECK(hipGetLastError());
     }
   }
+  hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
+  CT_CHECK(hipGetLastError());
   const unsigned cgrid = static_cast<unsigned>((b.n + kCountChunk - 1) / kCountChunk);
   hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.rec);
   CT_CHECK(hipGetLastError());
