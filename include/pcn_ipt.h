@@ -102,7 +102,8 @@ typedef struct {
   uint16_t direction;        /* PCN_IPT_INGRESS or PCN_IPT_EGRESS */
   uint16_t hook;             /* PCN_IPT_HOOK_XDP (0) or PCN_IPT_HOOK_TC */
   uint16_t reserved;         /* 0 */
-  const uint8_t *ct_status;  /* NULL => status from an empty conntrack table */
+  const uint8_t *ct_status;  /* per-frame label 0..3; NULL => empty-table labels (or the
+                                table, with pcn_ipt_ct_enable: then it must be NULL) */
   uint64_t n;                /* number of frames */
   uint8_t *verdicts;         /* out: 0 DROP (RX_DROP), 1 ACCEPT (RX_OK / pass / redirect) */
   int32_t *rule_ids;         /* out, nullable: matched rule, or PCN_IPT_RID_* */
