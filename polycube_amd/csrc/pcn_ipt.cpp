@@ -102,6 +102,7 @@ struct ChainState {
   unsigned long long *ctr = nullptr;           // [2 + 2*max_counted]
   unsigned long long *ctr_global = nullptr;    // summed over ranks
   unsigned long long *gather = nullptr;        // [nranks][2 + 2*max_counted]
+  unsigned long long *stage = nullptr;         // snapshot of ctr the all-gather sends
   // chain program of the last launch shape (jit.hpp): descriptor + shape it was made for
   DevChain jit_desc{};
   JitShape jit_shape{};
@@ -123,6 +124,11 @@ struct pcn_ipt {
   int num_cus = 256;
   size_t ctr_words = 0;
   ncclComm_t comm = nullptr;
+  // the counter all-gather runs on its own stream, off the classify stream's
+  // critical path: the classify stream only snapshots the counters
+  hipStream_t comm_stream = nullptr;
+  hipEvent_t ev_staged = nullptr, ev_gathered = nullptr;
+  bool gather_pending = false;
   int nranks = 1, rank = 0;
   JitCache jit;                                // chain programs (per launch shape)
   uint64_t launches_generic = 0, launches_jit = 0;
@@ -328,6 +334,7 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
       if (cs.ctr) (void)hipFree(cs.ctr);
       if (cs.ctr_global) (void)hipFree(cs.ctr_global);
       if (cs.gather) (void)hipFree(cs.gather);
+      if (cs.stage) (void)hipFree(cs.stage);
     }
     if (ctx->d_localip) (void)hipFree(ctx->d_localip);
     if (ctx->d_zero) (void)hipFree(ctx->d_zero);
@@ -338,6 +345,9 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     ct_table_free(ctx->ct);
     ct_scratch_free(ctx->cts);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
+    if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
+    if (ctx->ev_staged) (void)hipEventDestroy(ctx->ev_staged);
+    if (ctx->ev_gathered) (void)hipEventDestroy(ctx->ev_gathered);
   }
   delete ctx;
 }
@@ -938,6 +948,7 @@ int pcn_ipt_comm_init(pcn_ipt *ctx, int nranks, int rank, const uint8_t uid[128]
     if (!ctx->has_device) return fail(-ENODEV, "no device");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(-EINVAL, "bad rank/nranks");
     device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");   // no gather in flight
     if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
     ncclUniqueId id;
     std::memcpy(&id, uid, 128);
@@ -948,7 +959,12 @@ int pcn_ipt_comm_init(pcn_ipt *ctx, int nranks, int rank, const uint8_t uid[128]
     for (auto &cs : ctx->chains) {
       if (cs.gather) hip_check(hipFree(cs.gather), "hipFree");
       hip_check(hipMalloc(&cs.gather, ctx->ctr_words * 8 * size_t(nranks)), "hipMalloc(gather)");
+      if (!cs.stage) hip_check(hipMalloc(&cs.stage, ctx->ctr_words * 8), "hipMalloc(stage)");
     }
+    if (!ctx->comm_stream) hip_check(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!ctx->ev_staged) hip_check(hipEventCreateWithFlags(&ctx->ev_staged, hipEventDisableTiming), "hipEventCreate");
+    if (!ctx->ev_gathered) hip_check(hipEventCreateWithFlags(&ctx->ev_gathered, hipEventDisableTiming), "hipEventCreate");
+    ctx->gather_pending = false;
     return 0;
   });
 }
@@ -958,28 +974,39 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
     if (!ctx->has_device) return fail(-ENODEV, "no device");
     device_guard(ctx);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!ctx->comm || ctx->nranks == 1) {
+    if (!ctx->comm) {
       for (auto &cs : ctx->chains)
         hip_check(hipMemcpyAsync(cs.ctr_global, cs.ctr, ctx->ctr_words * 8, hipMemcpyDeviceToDevice, s),
                   "hipMemcpyAsync(counters)");
       return 0;
     }
-    // one all-gather per chain of its live prefix (defaults + counted rules)
+    // The classify stream snapshots each chain's live prefix (defaults +
+    // counted rules) once the previous all-gather has sent its snapshot; the
+    // all-gather and the rank sum then run on the communicator's stream while
+    // the classify stream goes on with the next batch.
+    if (ctx->gather_pending) hip_check(hipStreamWaitEvent(s, ctx->ev_gathered, 0), "hipStreamWaitEvent");
     size_t count[PCN_IPT_NCHAINS];
-    ncclResult_t r = ncclGroupStart();
-    for (int c = 0; c < PCN_IPT_NCHAINS && r == ncclSuccess; ++c) {
+    for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
       ChainState &cs = ctx->chains[c];
       count[c] = 2 + 2 * size_t(cs.desc.ncounted);
-      r = ncclAllGather(cs.ctr, cs.gather, count[c], ncclUint64, ctx->comm, s);
+      hip_check(hipMemcpyAsync(cs.stage, cs.ctr, count[c] * 8, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(stage)");
     }
+    hip_check(hipEventRecord(ctx->ev_staged, s), "hipEventRecord");
+    hipStream_t cs_ = ctx->comm_stream;
+    hip_check(hipStreamWaitEvent(cs_, ctx->ev_staged, 0), "hipStreamWaitEvent");
+    ncclResult_t r = ncclGroupStart();
+    for (int c = 0; c < PCN_IPT_NCHAINS && r == ncclSuccess; ++c)
+      r = ncclAllGather(ctx->chains[c].stage, ctx->chains[c].gather, count[c], ncclUint64, ctx->comm, cs_);
     ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
       return fail(-EIO, std::string("ncclAllGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
     for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
       ChainState &cs = ctx->chains[c];
-      int rc = launch_sum_ranks(cs.gather, cs.ctr_global, count[c], ctx->nranks, s);
+      int rc = launch_sum_ranks(cs.gather, cs.ctr_global, count[c], ctx->nranks, cs_);
       if (rc != hipSuccess) return fail(-EIO, "sum_ranks launch failed");
     }
+    hip_check(hipEventRecord(ctx->ev_gathered, cs_), "hipEventRecord");
+    ctx->gather_pending = true;
     return 0;
   });
 }

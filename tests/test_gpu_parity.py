@@ -290,12 +290,17 @@ def test_rccl_single_rank_counter_sync(dev):
     uid = Iptables.comm_unique_id()
     ipt.comm_init(1, 0, uid)
     n = 1 << 16
-    tf = torch.from_numpy(synth.config_frames(2, n, rs).reshape(-1)).to(dev)
-    ipt.classify(tf, n=n)
-    ipt.sync_counters(torch.cuda.current_stream().cuda_stream)
+    frames = synth.config_frames(2, n, rs).reshape(-1)
+    tf = torch.from_numpy(frames).to(dev)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(5):          # the all-gather of step k overlaps classify k+1 (comm stream)
+        ipt.classify(tf, n=n, stream=s)
+        ipt.sync_counters(s)
+        o.classify(frames, n=n, nthreads=4)
     torch.cuda.synchronize()
     fw = ipt.chain("FORWARD")
     assert fw.read_counters(128, scope=1) == fw.read_counters(128, scope=0)
+    assert fw.read_counters(128, scope=1) == o.read_counters(1, 128)
 
 
 def test_u32_bins_split_launch_counts_exactly(dev):
