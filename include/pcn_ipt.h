@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 2
+#define PCN_IPT_ABI_VERSION 3
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -315,6 +315,45 @@ int pcn_ipt_ct_get_info(pcn_ipt *ctx, pcn_ipt_ct_info *out);
 int pcn_ipt_set_accept_established(pcn_ipt *ctx, int chain, int on);
 int pcn_ipt_get_accept_established(pcn_ipt *ctx, int chain);
 int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, int flush);
+
+/* ---- pcn-firewall personality ------------------------------------------ */
+/* pcn-firewall (src/services/pcn-firewall) runs the same field modules,
+ * BitScan, ActionLookup and rule compiler as pcn-iptables
+ * (Firewall_{IpLookup,L4ProtocolLookup,L4PortLookup,TcpFlagsLookup,
+ * ConntrackMatch,BitScan,ActionLookup}_dp.c, Utils.cpp) behind a transparent
+ * cube, so a context can serve it instead.  Differences, all applied by the
+ * same kernel:
+ *  - two chains, INGRESS and EGRESS (firewall.yang:175-176), selected by the
+ *    batch direction alone (Firewall_ChainForwarder_dp.c:20-42); they live in
+ *    the FORWARD and OUTPUT slots of the chain verbs, INPUT is refused;
+ *  - no localip, no allow logic: an empty chain takes its default action and
+ *    bumps its default counters (DefaultAction, Firewall_DefaultAction_dp.c);
+ *  - no in/out-iface fields; a rule must carry an action (Chain.cpp:89-92,
+ *    612-620); a conntrack field needs conntrack on (ChainRule.cpp:29-33);
+ *    `deletes` without a match fails (Chain.cpp:760-771); `update` replaces
+ *    the rule at id or appends at id == size (Chain::addRule, :612-644);
+ *  - the ConntrackLabel stage (ICMP length checks, labels) runs only while
+ *    conntrack is on (modules/Parser.cpp:41-45).  AUTOMATIC mode
+ *    (accept-established ON, the default) accepts ESTABLISHED packets before
+ *    the chain, uncounted, rule id PCN_IPT_RID_ACCEPT_ESTABLISHED
+ *    (Firewall_ConntrackLabel_dp.c:474-478).  Without the connection table
+ *    (pcn_ipt_ct_enable is refused for a firewall context) labels come from
+ *    batch.ct_status or an empty table; with conntrack off the label is NEW.
+ * Set the service on a fresh context, before any rule. */
+enum { PCN_IPT_SERVICE_IPTABLES = 0, PCN_IPT_SERVICE_FIREWALL = 1 };
+enum { PCN_FW_INGRESS = PCN_IPT_FORWARD, PCN_FW_EGRESS = PCN_IPT_OUTPUT };
+/* ConntrackModes (pcn-firewall defines.h:56-58); a new firewall is AUTOMATIC (Firewall.h:323) */
+enum { PCN_FW_CT_DISABLED = 0, PCN_FW_CT_MANUAL = 1, PCN_FW_CT_AUTOMATIC = 2 };
+int pcn_ipt_set_service(pcn_ipt *ctx, int service);
+int pcn_ipt_get_service(pcn_ipt *ctx);
+/* Firewall::setConntrack (Firewall.cpp:151-195): off -> DISABLED; on from DISABLED -> MANUAL */
+int pcn_fw_set_conntrack(pcn_ipt *ctx, int on);
+/* Firewall::setAcceptEstablished (Firewall.cpp:119-142): -EINVAL while DISABLED */
+int pcn_fw_set_accept_established(pcn_ipt *ctx, int on);
+int pcn_fw_get_conntrack_mode(pcn_ipt *ctx);
+/* Chain::addRule / replaceRule (`rule add <id>`, batch UPDATE): replace the
+ * rule at id (its counters carry on), or append when id == number of rules. */
+int pcn_fw_chain_update(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rule *rule);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ------------------- */
 /* 128-byte ncclUniqueId produced on rank 0 and shared out of band. */

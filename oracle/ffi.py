@@ -43,8 +43,11 @@ def lib():
         h.orc_add_port.argtypes = [vp, C.c_char_p, C.c_uint16]
         h.orc_set_chain.argtypes = [vp, C.c_int, C.POINTER(_Rule), C.c_uint32, C.c_int]
         h.orc_set_localip.argtypes = [vp, u32p, C.c_uint32]
+        h.orc_set_service.argtypes = [vp, C.c_int, C.c_int]
         h.orc_classify.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, C.c_uint32, C.c_uint32, vp, C.c_uint16,
                                    vp, C.c_uint64, vp, vp, C.c_int]
+        h.orc_classify_labels.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, C.c_uint32, C.c_uint32, vp,
+                                          C.c_uint16, vp, C.c_uint64, vp, vp, vp, C.c_int]
         h.orc_read_counters.argtypes = [vp, C.c_int, u64p, u64p, C.c_uint32, u64p, u64p, C.c_int]
         h.orc_export_map.argtypes = [vp, C.c_int, C.c_int, u32p, u8p, u64p, C.c_uint32, C.c_uint32]
         h.orc_chain_nrw.restype = C.c_uint32
@@ -109,12 +112,18 @@ class Oracle:
         if rc:
             raise ValueError(f"oracle rejected chain (rc={rc})")
 
+    def set_service(self, service, fw_ct_mode=0):
+        """0 = pcn-iptables, 1 = pcn-firewall with conntrack mode 0 DISABLED /
+        1 MANUAL / 2 AUTOMATIC (pcn-firewall defines.h:56-58)."""
+        assert lib().orc_set_service(self._h, service, fw_ct_mode) == 0
+
     def set_localip(self, ips):
         a = (C.c_uint32 * max(len(ips), 1))(*ips)
         assert lib().orc_set_localip(self._h, a, len(ips)) == 0
 
     def classify(self, frames, n=None, offsets=None, lens=None, stride=64, fixed_len=64,
-                 in_port=None, const_in_port=1, direction=0, ct_status=None, nthreads=1, hook=0):
+                 in_port=None, const_in_port=1, direction=0, ct_status=None, nthreads=1, hook=0,
+                 with_labels=False):
         frames = np.ascontiguousarray(frames, dtype=np.uint8)
         if n is None:
             n = len(offsets) if offsets is not None else frames.size // stride
@@ -124,9 +133,12 @@ class Oracle:
         ct_status = None if ct_status is None else np.ascontiguousarray(ct_status, dtype=np.uint8)
         verdicts = np.zeros(n, dtype=np.uint8)
         rule_ids = np.zeros(n, dtype=np.int32)
-        lib().orc_classify(self._h, direction, hook, _ptr(frames), _ptr(offsets), _ptr(lens), stride,
-                           fixed_len, _ptr(in_port), const_in_port, _ptr(ct_status), n,
-                           _ptr(verdicts), _ptr(rule_ids), nthreads)
+        labels = np.zeros(n, dtype=np.uint8) if with_labels else None
+        lib().orc_classify_labels(self._h, direction, hook, _ptr(frames), _ptr(offsets), _ptr(lens), stride,
+                                  fixed_len, _ptr(in_port), const_in_port, _ptr(ct_status), n,
+                                  _ptr(verdicts), _ptr(rule_ids), _ptr(labels), nthreads)
+        if with_labels:
+            return verdicts, rule_ids, labels
         return verdicts, rule_ids
 
     def read_counters(self, chain, n, flush=False):

@@ -88,6 +88,8 @@ typedef struct {
 typedef struct { char name[64]; uint16_t index; } port_t;
 
 struct orc_ctx {
+  int service;                           /* ORC_SVC_IPTABLES / ORC_SVC_FIREWALL */
+  int fw_ct_mode;                        /* pcn-firewall conntrackMode (defines.h:56-58) */
   ochain_t ch[NCHAINS];
   port_t ports[1024]; int nports;
   uint32_t localip[256]; int nlocal;
@@ -529,6 +531,14 @@ int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n, int 
   return compile_chain(c, chain);
 }
 
+int orc_set_service(orc_ctx *c, int service, int fw_ct_mode) {
+  if (service != ORC_SVC_IPTABLES && service != ORC_SVC_FIREWALL) return -EINVAL;
+  if (fw_ct_mode < FW_CT_DISABLED || fw_ct_mode > FW_CT_AUTOMATIC) return -EINVAL;
+  c->service = service;
+  c->fw_ct_mode = fw_ct_mode;
+  return 0;
+}
+
 int orc_set_localip(orc_ctx *c, const uint32_t *ips, uint32_t n) {
   if (n > 256) return -ENOSPC; /* ChainSelector_dp.c:54 hash(256) */
   memcpy(c->localip, ips, n * 4); c->nlocal = (int)n;
@@ -884,8 +894,9 @@ static inline int default_verdict(const ochain_t *ch, pcpu_t *pc, int chain, uin
 /* st != NULL: stateful conntrack (labels from and updates to st, one packet
  * at a time); else labels come from ct_in or an empty table. */
 static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, uint32_t L, uint16_t port,
-                        int ct_in, pcpu_t *pc, int32_t *rid, struct ctstate *st) {
+                        int ct_in, pcpu_t *pc, int32_t *rid, struct ctstate *st, int *label) {
   *rid = -2;
+  *label = 255;
   /* TC hook: the receive path strips the outer 802.1Q / 802.1ad tag before
    * the program runs (skb_vlan_untag; a frame too short to hold the tag is
    * dropped there), and packet_len = skb->len no longer counts it. */
@@ -922,8 +933,50 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
   sport = (uint16_t)(sport >> 8 | sport << 8);
   dport = (uint16_t)(dport >> 8 | dport << 8);
 
+  int chain, ct;
+  if (c->service == ORC_SVC_FIREWALL) {
+    /* pcn-firewall: Firewall_Parser_dp.c:94-165 -> [ConntrackLabel, when the
+     * conntrack mode is not DISABLED (modules/Parser.cpp:41-45)] ->
+     * ChainForwarder (Firewall_ChainForwarder_dp.c:20-42).  The chain is the
+     * program's direction: INGRESS or EGRESS, kept in the FORWARD / OUTPUT
+     * slots.  No localip, no allow logic. */
+    chain = dir == ORC_INGRESS ? ORC_FORWARD : ORC_OUTPUT;
+    if (c->fw_ct_mode == FW_CT_DISABLED) st = NULL;   /* ConntrackTableUpdate: "conntrack disabled - pass" */
+    ct = ct_in >= 0 ? ct_in : CT_NEW; /* DISABLED: connStatus is never written (per-CPU zero) */
+    if (c->fw_ct_mode != FW_CT_DISABLED) {
+      if (st) {
+        ct = ct_label(st, &cp, f, L);                  /* Firewall_ConntrackLabel_dp.c:116-460 */
+        if (ct < 0) return RX_DROP;
+      } else {
+        int icmp_type = -1;                            /* the same ICMP length checks */
+        if (proto == 1) {
+          if (L < 42) return RX_DROP;
+          icmp_type = f[34];
+          if (icmp_type != 8 && icmp_type != 0 && !(icmp_type >= 13 && icmp_type <= 18) && L < 70) return RX_DROP;
+        }
+        ct = ct_in >= 0 ? ct_in : ct_label_empty(proto, flags, icmp_type);
+      }
+      *label = ct;
+      /* _CONNTRACK_MODE == 2 (AUTOMATIC): ESTABLISHED -> ConntrackTableUpdate
+       * -> RX_OK, before any chain and without counters
+       * (Firewall_ConntrackLabel_dp.c:474-478) */
+      if (c->fw_ct_mode == FW_CT_AUTOMATIC && ct == CT_ESTABLISHED) {
+        *rid = -3;
+        if (st) ct_update(st, &cp, f, ct);
+        return RX_OK;
+      }
+    }
+    *label = ct;
+    if (c->ch[chain].nrules == 0) {
+      /* _NR_ELEMENTS_<CHAIN> == 0: DefaultAction (Firewall_DefaultAction_dp.c:37-43) */
+      int v = default_verdict(&c->ch[chain], pc, chain, L, rid);
+      if (st && v == RX_OK) ct_update(st, &cp, f, ct);
+      return v;
+    }
+    goto rules;
+  }
   /* ChainSelector_dp.c:131-298 */
-  int chain, pass_labeling = 0;
+  int pass_labeling = 0;
   if (dir == ORC_INGRESS) {
     const ochain_t *in = &c->ch[ORC_INPUT], *fw = &c->ch[ORC_FORWARD];
     if (in->default_action == 1 && fw->default_action == 1 && in->nrules == 0 &&
@@ -942,10 +995,10 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     if (c->ch[chain].default_action == 0) return RX_DROP; /* DROP_NO_LABELING */
     pass_labeling = 1;
   }
-  int ct;
   if (st) {
     ct = ct_label(st, &cp, f, L);                    /* ConntrackLabel_dp.c:190-531 */
     if (ct < 0) return RX_DROP;
+    *label = ct;
     /* PASS_LABELING → ChainForwarder → ConntrackTableUpdate → RX_OK */
     if (pass_labeling) { ct_update(st, &cp, f, ct); return RX_OK; }
     /* _CONNTRACK_MODE_<CHAIN> == ON: accept established (ConntrackLabel_dp.c:580-616) */
@@ -967,6 +1020,7 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
       }
     }
     ct = ct_in >= 0 ? ct_in : ct_label_empty(proto, flags, icmp_type);
+    *label = ct;
     if (pass_labeling) return RX_OK; /* ChainForwarder → ConntrackTableUpdate → RX_OK */
     if (c->ae[chain] && ct == CT_ESTABLISHED) {
       pc->ae_pkts[chain] += 1; pc->ae_bytes[chain] += L;
@@ -975,6 +1029,7 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     }
   }
 
+rules:;
   const ochain_t *ch = &c->ch[chain];
   int nrw = ch->nrw;
   uint64_t v[1024];
@@ -1045,7 +1100,7 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
 typedef struct {
   const orc_ctx *c; int dir; int hook; const uint8_t *frames; const uint32_t *offsets; const uint16_t *lens;
   uint32_t stride, fixed_len; const uint16_t *in_port; uint16_t const_port; const uint8_t *ct;
-  uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc; struct ctstate *st;
+  uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc; struct ctstate *st; uint8_t *labels;
 } job_t;
 
 static void *run_job(void *arg) {
@@ -1056,7 +1111,9 @@ static void *run_job(void *arg) {
     uint16_t port = j->in_port ? j->in_port[i] : j->const_port;
     int ct = j->ct ? j->ct[i] : -1;
     int32_t rid;
-    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st);
+    int lab;
+    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st, &lab);
+    if (j->labels) j->labels[i] = (uint8_t)lab;
     j->verdicts[i] = v == RX_DROP ? 0 : 1;
     if (j->rule_ids) j->rule_ids[i] = rid;
   }
@@ -1067,6 +1124,14 @@ int orc_classify(orc_ctx *c, int dir, int hook, const uint8_t *frames, const uin
                  const uint16_t *lens, uint32_t stride, uint32_t fixed_len,
                  const uint16_t *in_port, uint16_t const_port, const uint8_t *ct_status,
                  uint64_t n, uint8_t *verdicts, int32_t *rule_ids, int nthreads) {
+  return orc_classify_labels(c, dir, hook, frames, offsets, lens, stride, fixed_len, in_port, const_port,
+                             ct_status, n, verdicts, rule_ids, NULL, nthreads);
+}
+
+int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, const uint32_t *offsets,
+                        const uint16_t *lens, uint32_t stride, uint32_t fixed_len,
+                        const uint16_t *in_port, uint16_t const_port, const uint8_t *ct_status,
+                        uint64_t n, uint8_t *verdicts, int32_t *rule_ids, uint8_t *labels, int nthreads) {
   if (c->ct && ct_status) return -EINVAL;   /* labels come from the table */
   if (c->ct) nthreads = 1;                   /* one packet at a time, in batch order */
   if (nthreads < 1) nthreads = 1;
@@ -1077,7 +1142,7 @@ int orc_classify(orc_ctx *c, int dir, int hook, const uint8_t *frames, const uin
     job_t *j = &jobs[t];
     *j = (job_t){c, dir, hook, frames, offsets, lens, stride, fixed_len, in_port, const_port, ct_status,
                  n * t / nthreads, n * (t + 1) / nthreads, verdicts, rule_ids,
-                 {{0}, {0}, {0}, {0}, {0}, {0}}, c->ct};
+                 {{0}, {0}, {0}, {0}, {0}, {0}}, c->ct, labels};
     for (int k = 0; k < NCHAINS; k++) {
       j->pc.pkts[k] = calloc(c->max_counted, 8);
       j->pc.bytes[k] = calloc(c->max_counted, 8);

@@ -54,6 +54,16 @@ int orc_add_port(orc_ctx *c, const char *name, uint16_t index);
  * (Chain::updateChain).  Returns 0 or a negative errno. */
 int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n,
                   int default_action);
+/* Service personality.  ORC_SVC_FIREWALL restates pcn-firewall
+ * (src/services/pcn-firewall/src/datapaths/Firewall_*_dp.c): the same field
+ * modules, BitScan and ActionLookup, but the chain is the program's direction
+ * (INGRESS chain in the ORC_FORWARD slot, EGRESS in ORC_OUTPUT), there is no
+ * localip / allow logic, and the ConntrackLabel stage (ICMP length checks,
+ * labels) runs only when fw_ct_mode != FW_CT_DISABLED; FW_CT_AUTOMATIC
+ * accepts ESTABLISHED packets before the chain, uncounted (rule id -3). */
+enum { ORC_SVC_IPTABLES = 0, ORC_SVC_FIREWALL = 1 };
+enum { FW_CT_DISABLED = 0, FW_CT_MANUAL = 1, FW_CT_AUTOMATIC = 2 };   /* defines.h:56-58 */
+int orc_set_service(orc_ctx *c, int service, int fw_ct_mode);
 int orc_set_localip(orc_ctx *c, const uint32_t *ips_nbo, uint32_t n);
 /* Classify a batch (host pointers).  offsets==NULL => packet i at i*stride;
  * lens==NULL => every packet fixed_len bytes; in_port==NULL => const_port;
@@ -63,6 +73,14 @@ int orc_classify(orc_ctx *c, int direction, int hook, const uint8_t *frames,
                  uint32_t fixed_len, const uint16_t *in_port,
                  uint16_t const_port, const uint8_t *ct_status, uint64_t n,
                  uint8_t *verdicts, int32_t *rule_ids, int nthreads);
+/* orc_classify that also reports each packet's connection label (0..3, the
+ * connStatus the field modules see), or 255 when the packet was decided
+ * before labelling (parser, PASS, ICMP length checks). */
+int orc_classify_labels(orc_ctx *c, int direction, int hook, const uint8_t *frames,
+                        const uint32_t *offsets, const uint16_t *lens, uint32_t stride,
+                        uint32_t fixed_len, const uint16_t *in_port, uint16_t const_port,
+                        const uint8_t *ct_status, uint64_t n, uint8_t *verdicts,
+                        int32_t *rule_ids, uint8_t *labels, int nthreads);
 /* Per-rule counters (read-and-flush when flush != 0) and default counters. */
 int orc_read_counters(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes,
                       uint32_t n, uint64_t *def_pkts, uint64_t *def_bytes,

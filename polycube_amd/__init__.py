@@ -1,4 +1,4 @@
-"""polycube_amd — MI355X-native pcn-iptables classification datapath.
+"""polycube_amd — MI355X-native pcn-iptables (and pcn-firewall) classification datapath.
 
 The product is the C-ABI library ``libpcn_ipt.so`` (HIP kernels for gfx950 +
 the C++ control-plane mirror, see include/pcn_ipt.h).  This package is the thin
@@ -9,6 +9,7 @@ so the parity tests read like the reference's own scenario tests.
 from .ffi import lib, LibraryMissing  # noqa: F401
 from .iptables import Iptables, Chain, IptablesError, INPUT, FORWARD, OUTPUT  # noqa: F401
 from .iptables import INGRESS, EGRESS, DROP, ACCEPT, XDP, TC  # noqa: F401
+from .firewall import Firewall, FwChain  # noqa: F401
 
 __all__ = ["lib", "LibraryMissing", "Iptables", "Chain", "IptablesError", "INPUT", "FORWARD",
-           "OUTPUT", "INGRESS", "EGRESS", "DROP", "ACCEPT", "XDP", "TC"]
+           "OUTPUT", "INGRESS", "EGRESS", "DROP", "ACCEPT", "XDP", "TC", "Firewall", "FwChain"]

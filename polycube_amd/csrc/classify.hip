@@ -42,6 +42,9 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #ifndef PCN_PREFETCH
 #define PCN_PREFETCH 1   // frames per lane in flight ahead of the one being classified
 #endif
+#ifndef PCN_STAGE_FAST
+#define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
+#endif
 // Tuning switches (tools/ablate.py builds experiment variants with -D...).
 
 namespace pcn {
@@ -187,6 +190,24 @@ struct Parsed {
   uint32_t proto, sport, dport, flags;
   uint32_t ct;                 // conntrack status 0..3 (or >3: invalid input)
 };
+
+// ConntrackLabel_dp.c:436-531 (Firewall_ConntrackLabel_dp.c: the same code):
+// the ICMP length checks that drop before any rule.  Sets the ICMP type
+// (0xffffffff for other protocols).
+__device__ __forceinline__ bool icmp_drop(const Parsed &p, const Hdr &h, uint32_t L, uint32_t &icmp_type) {
+  icmp_type = 0xffffffffu;
+  if (p.proto != 1) return false;
+  icmp_type = (h.w[8] >> 16) & 0xff;
+  if (L < 42) return true;
+  return icmp_type != 8 && icmp_type != 0 && !(icmp_type >= 13 && icmp_type <= 18) && L < 70;
+}
+
+// The label an empty connection table gives (ConntrackLabel_dp.c:372-383).
+__device__ __forceinline__ uint32_t empty_table_label(const Parsed &p, uint32_t icmp_type) {
+  if (p.proto == 6) return (p.flags & 0x02) && ((p.flags | 0x02) == 0x02) ? 0u : 3u;
+  if (p.proto == 17) return 0u;
+  return icmp_type == 8 ? 0u : 3u;
+}
 
 // ---- rule-chain stage, part 1 (per lane) ----
 // Maps the packet to its NS slot classes: 0 = META (proto x tcpflags x
@@ -436,25 +457,37 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // frames per workgroup so neither can wrap; the flush widens to u64)
   uint32_t *bins = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);
   WaveScratch *ws = reinterpret_cast<WaveScratch *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
-  // stage every chain's table image in LDS and zero the counter histogram
-  if (LDS) {
+  // stage every chain's table image in LDS and zero the counter histogram.
+  // (The first frames' headers are already in flight: the prefetch below is
+  // issued before this when PCN_STAGE_FAST.)  Every load of a pass is issued
+  // before its stores, so a 128 KB image costs one L2 round trip, not eight.
+  auto stage_images = [&]() {
+    if (!LDS) return;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const DevChain &ch = c == CH ? run_ch : a.ch[c];
       if (!ch.lds_limit) continue;
       const u32x4 *src = reinterpret_cast<const u32x4 *>(ch.image);
       u32x4 *dst = reinterpret_cast<u32x4 *>(pcn_smem + ch.lds_image);
-      for (uint32_t k = threadIdx.x; k < ch.lds_limit / 16; k += blockDim.x) dst[k] = src[k];
+      const uint32_t n16 = ch.lds_limit / 16;
+      if (PCN_STAGE_FAST) {
+        constexpr uint32_t U = 10;   // 160 KB / (1024 threads x 16 B)
+        for (uint32_t k0 = threadIdx.x; k0 < n16; k0 += U * kBlock) {
+          u32x4 r[U];
+#pragma unroll
+          for (uint32_t u = 0; u < U; ++u)
+            if (k0 + u * kBlock < n16) r[u] = src[k0 + u * kBlock];
+#pragma unroll
+          for (uint32_t u = 0; u < U; ++u)
+            if (k0 + u * kBlock < n16) dst[k0 + u * kBlock] = r[u];
+        }
+      } else {
+        for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+      }
     }
-  }
-  // pkts[nbins], then (variable lengths only) bytes[nbins]; with a fixed
-  // length every bin's bytes are pkts * len at the flush
-  for (uint32_t b = threadIdx.x; b < (FIXED ? 1u : 2u) * a.nbins; b += blockDim.x) bins[b] = 0;
+  };
+  if (!PCN_STAGE_FAST) stage_images();
   uint32_t *const byte_bins = bins + a.nbins;
-  for (uint32_t k = threadIdx.x; k < a.nlocal; k += blockDim.x)
-    reinterpret_cast<uint32_t *>(pcn_smem + a.lds_localip)[k] = a.localip[k];
-  __syncthreads();
-
   const uint32_t const_port = a.const_in_port;
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -511,6 +544,13 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   };
 #pragma unroll
   for (int d = 0; d < PCN_PREFETCH; ++d) prefetch(st[d], first + d * step);
+  if (PCN_STAGE_FAST) stage_images();
+  // pkts[nbins], then (variable lengths only) bytes[nbins]; with a fixed
+  // length every bin's bytes are pkts * len at the flush
+  for (uint32_t b = threadIdx.x; b < (FIXED ? 1u : 2u) * a.nbins; b += blockDim.x) bins[b] = 0;
+  for (uint32_t k = threadIdx.x; k < a.nlocal; k += blockDim.x)
+    reinterpret_cast<uint32_t *>(pcn_smem + a.lds_localip)[k] = a.localip[k];
+  __syncthreads();
   // Stage d always holds the frames i with (i - first) / step == d (mod
   // PCN_PREFETCH): the loop is unrolled PCN_PREFETCH times so no stage is
   // ever copied (a register move of an in-flight load waits for it).
@@ -590,7 +630,33 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         p.sport = bswap16u(h.w[8] >> 16);
         p.dport = bswap16u(h.w[9] & 0xffff);
       }
-      if (!done) {
+      if (!done && a.fw) {
+        // ---- pcn-firewall: Parser -> [ConntrackLabel] -> ChainForwarder ----
+        // (Firewall_Parser_dp.c:94-165, Firewall_ChainForwarder_dp.c:20-42):
+        // the chain is the program's direction, INGRESS / EGRESS in the
+        // FORWARD / OUTPUT slots.  The ConntrackLabel stage (the same ICMP
+        // length checks and labels as pcn-iptables) runs only when conntrack
+        // is on (modules/Parser.cpp:41-45); with it off the label is never
+        // written (per-CPU zero: NEW).
+        chain = a.direction == PCN_IPT_INGRESS ? PCN_IPT_FORWARD : PCN_IPT_OUTPUT;
+        p.ct = a.has_ct ? cur_ct : 0u;
+        if (a.fw != PCN_FW_LAUNCH_CT_OFF) {
+          uint32_t icmp_type;
+          if (icmp_drop(p, h, L, icmp_type)) { verdict = PCN_IPT_DROP; done = true; }
+          else if (!a.has_ct) p.ct = empty_table_label(p, icmp_type);
+          // AUTOMATIC: ESTABLISHED -> ConntrackTableUpdate -> RX_OK before the
+          // chain, uncounted (Firewall_ConntrackLabel_dp.c:474-478)
+          if (!done && a.fw == PCN_FW_LAUNCH_CT_AUTO && p.ct == 1) {
+            verdict = PCN_IPT_ACCEPT; rid = PCN_IPT_RID_ACCEPT_ESTABLISHED; done = true;
+          }
+        }
+        if (!done && ((a.empty_mask >> chain) & 1)) {    // DefaultAction (Firewall_DefaultAction_dp.c:37-43)
+          cchain = chain; rid = PCN_IPT_RID_DEFAULT;
+          verdict = ((a.drop_mask >> chain) & 1) ? PCN_IPT_DROP : PCN_IPT_ACCEPT;
+          done = true;
+        }
+        if (done) chain = -1;
+      } else if (!done) {
         // ---- ChainSelector_dp.c:131-298 ----
         bool pass = false;
         if (a.direction == PCN_IPT_INGRESS) {
@@ -608,23 +674,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         }
         // ---- ConntrackLabel_dp.c:436-531 ICMP length checks ----
         uint32_t icmp_type = 0xffffffffu;
-        if (!done && p.proto == 1) {
-          icmp_type = (h.w[8] >> 16) & 0xff;
-          if (L < 42) { verdict = PCN_IPT_DROP; done = true; }
-          else if (icmp_type != 8 && icmp_type != 0 && !(icmp_type >= 13 && icmp_type <= 18) && L < 70) {
-            verdict = PCN_IPT_DROP; done = true;
-          }
-        }
+        if (!done && icmp_drop(p, h, L, icmp_type)) { verdict = PCN_IPT_DROP; done = true; }
         if (!done) {
-          if (a.has_ct) {
-            p.ct = cur_ct;
-          } else if (p.proto == 6) {      // empty-table labels, ConntrackLabel_dp.c:372-383
-            p.ct = (p.flags & 0x02) && ((p.flags | 0x02) == 0x02) ? 0u : 3u;
-          } else if (p.proto == 17) {
-            p.ct = 0;
-          } else {
-            p.ct = icmp_type == 8 ? 0u : 3u;
-          }
+          p.ct = a.has_ct ? cur_ct : empty_table_label(p, icmp_type);
           if (pass) { verdict = PCN_IPT_ACCEPT; done = true; }
         }
         if (done) chain = -1;

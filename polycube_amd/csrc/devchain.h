@@ -126,6 +126,12 @@ struct LaunchArgs {
   uint32_t empty_mask;           // bit c: chain c has no rules (ChainSelector default path)
   uint32_t drop_mask;            // bit c: chain c's default action is DROP
   uint32_t count_mask;           // bit c: packets of this launch can select chain c
+  uint32_t fw;                   // 0: pcn-iptables dispatch; else pcn-firewall, PCN_FW_LAUNCH_*
 };
+
+// LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)
+#define PCN_FW_LAUNCH_CT_OFF 1     // DISABLED: no ConntrackLabel stage
+#define PCN_FW_LAUNCH_CT_MANUAL 2  // labels + ICMP checks, then the chain
+#define PCN_FW_LAUNCH_CT_AUTO 3    // MANUAL + ESTABLISHED accepted before the chain
 
 }  // namespace pcn

@@ -120,6 +120,8 @@ struct pcn_ipt {
   uint32_t *d_localip = nullptr;
   uint8_t *d_zero = nullptr;                   // 64 zero bytes: stand-in in_port / ct_status
   bool interactive = true;                     // Iptables.h:181
+  int service = PCN_IPT_SERVICE_IPTABLES;      // pcn_ipt_set_service
+  int fw_ct_mode = PCN_FW_CT_AUTOMATIC;        // pcn-firewall conntrackMode (Firewall.h:323)
   bool has_device = false;
   int num_cus = 256;
   size_t ctr_words = 0;
@@ -236,6 +238,7 @@ void fetch_stats(pcn_ipt *ctx, int chain) {
 // exactly {conntrack ESTABLISHED, action ACCEPT}.  The disable switch has no
 // `break`, so disabling INPUT also disables FORWARD and OUTPUT.
 void apply_ae(pcn_ipt *ctx, int chain) {
+  if (ctx->service == PCN_IPT_SERVICE_FIREWALL) return;   // pcn-firewall has no per-chain optimization
   const auto &rules = ctx->chains[chain].rules;
   bool found = false;
   if (!rules.empty()) {
@@ -253,6 +256,25 @@ void update_chain(pcn_ipt *ctx, int chain) {       // Chain::updateChain
 }
 
 bool valid_chain(int c) { return c >= 0 && c < PCN_IPT_NCHAINS; }
+
+// A chain verb's chain: pcn-firewall has only INGRESS / EGRESS (the FORWARD /
+// OUTPUT slots).
+bool valid_chain(const pcn_ipt *ctx, int c) {
+  return valid_chain(c) && (ctx->service != PCN_IPT_SERVICE_FIREWALL || c != PCN_IPT_INPUT);
+}
+
+// ChainRule::update for the context's service.  pcn-firewall: no interface
+// fields; the action must be set (Chain.cpp:89-92, 612-620); a conntrack
+// match needs conntrack on (ChainRule.cpp:29-33).
+Rule rule_from_c(const pcn_ipt *ctx, const pcn_ipt_rule &r) {
+  if (ctx->service == PCN_IPT_SERVICE_FIREWALL) {
+    if (r.in_iface || r.out_iface) throw std::runtime_error("pcn-firewall rules have no in-iface/out-iface");
+    if (r.action < 0) throw std::runtime_error("action not specified for the rule");
+    if (r.conntrack && ctx->fw_ct_mode == PCN_FW_CT_DISABLED)
+      throw std::runtime_error("Please enable the connection tracking module.");
+  }
+  return Rule::from_c(r, ctx->ports);
+}
 
 template <typename F>
 int guarded(pcn_ipt *ctx, F &&f) {
@@ -379,9 +401,9 @@ int pcn_ipt_set_localip(pcn_ipt *ctx, const uint32_t *ips, size_t n) {
 
 int pcn_ipt_chain_append(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule) {
   return guarded(ctx, [&] {
-    if (!valid_chain(chain) || !rule) return fail(-EINVAL, "bad chain or rule");
+    if (!valid_chain(ctx, chain) || !rule) return fail(-EINVAL, "bad chain or rule");
     ChainState &cs = ctx->chains[chain];
-    Rule r = Rule::from_c(*rule, ctx->ports);
+    Rule r = rule_from_c(ctx, *rule);
     if (cs.rules.size() >= ctx->cfg.max_rules) return fail(-ENOSPC, "too many rules");
     fetch_stats(ctx, chain);                          // Chain::addRule -> getStatsList
     cs.rules.push_back(std::move(r));
@@ -396,10 +418,10 @@ int pcn_ipt_chain_append(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule) {
 
 int pcn_ipt_chain_insert(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rule *rule) {
   return guarded(ctx, [&] {
-    if (!valid_chain(chain) || !rule) return fail(-EINVAL, "bad chain or rule");
+    if (!valid_chain(ctx, chain) || !rule) return fail(-EINVAL, "bad chain or rule");
     ChainState &cs = ctx->chains[chain];
     if (id > cs.rules.size()) return fail(-EINVAL, "id not allowed");   // Chain.cpp:238-240
-    Rule r = Rule::from_c(*rule, ctx->ports);
+    Rule r = rule_from_c(ctx, *rule);
     if (cs.rules.size() >= ctx->cfg.max_rules) return fail(-ENOSPC, "too many rules");
     fetch_stats(ctx, chain);
     cs.rules.insert(cs.rules.begin() + id, std::move(r));
@@ -414,7 +436,7 @@ int pcn_ipt_chain_insert(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rul
 
 int pcn_ipt_chain_delete_id(pcn_ipt *ctx, int chain, uint32_t id) {
   return guarded(ctx, [&] {
-    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    if (!valid_chain(ctx, chain)) return fail(-EINVAL, "bad chain");
     ChainState &cs = ctx->chains[chain];
     if (id >= cs.rules.size()) return fail(-ENOENT, "There is no rule " + std::to_string(id));
     fetch_stats(ctx, chain);
@@ -427,7 +449,7 @@ int pcn_ipt_chain_delete_id(pcn_ipt *ctx, int chain, uint32_t id) {
 
 int pcn_ipt_chain_delete_match(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule) {
   return guarded(ctx, [&] {
-    if (!valid_chain(chain) || !rule) return fail(-EINVAL, "bad chain or rule");
+    if (!valid_chain(ctx, chain) || !rule) return fail(-EINVAL, "bad chain or rule");
     ChainState &cs = ctx->chains[chain];
     Rule r;
     try {
@@ -444,6 +466,8 @@ int pcn_ipt_chain_delete_match(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule
         return 0;                                     // delRule(i); return; (Chain.cpp:358-361)
       }
     }
+    if (ctx->service == PCN_IPT_SERVICE_FIREWALL)
+      return fail(-ENOENT, "no matching rule to delete");   // pcn-firewall Chain.cpp:760-771
     apply_ae(ctx, chain);                             // only reached without a match (Chain.cpp:368)
     return 0;   // no match: the reference returns without error
   });
@@ -451,7 +475,7 @@ int pcn_ipt_chain_delete_match(pcn_ipt *ctx, int chain, const pcn_ipt_rule *rule
 
 int pcn_ipt_chain_flush(pcn_ipt *ctx, int chain) {
   return guarded(ctx, [&] {
-    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    if (!valid_chain(ctx, chain)) return fail(-EINVAL, "bad chain");
     ChainState &cs = ctx->chains[chain];
     cs.rules.clear();
     cs.stats.clear();
@@ -462,7 +486,7 @@ int pcn_ipt_chain_flush(pcn_ipt *ctx, int chain) {
 
 int pcn_ipt_chain_set_default(pcn_ipt *ctx, int chain, int action) {
   return guarded(ctx, [&] {
-    if (!valid_chain(chain) || (action != PCN_IPT_DROP && action != PCN_IPT_ACCEPT))
+    if (!valid_chain(ctx, chain) || (action != PCN_IPT_DROP && action != PCN_IPT_ACCEPT))
       return fail(-EINVAL, "bad chain or action");
     ChainState &cs = ctx->chains[chain];
     if (cs.default_action == action) return 0;
@@ -582,13 +606,19 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       if (a.ch[c].default_action == PCN_IPT_DROP) a.drop_mask |= 1u << c;
     }
     const ChainState &in = ctx->chains[PCN_IPT_INPUT], &fw = ctx->chains[PCN_IPT_FORWARD];
-    a.allow_logic = in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
+    const bool firewall = ctx->service == PCN_IPT_SERVICE_FIREWALL;
+    a.allow_logic = !firewall && in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
                     in.rules.size() == 0 && fw.rules.size() == 0 && in.desc.nrules == 0 &&
                     fw.desc.nrules == 0;
-    // which chains can reach the rule stage (ChainSelector_dp.c:157-168, 243-260)
-    const bool has_local = !ctx->localip.empty();
+    if (firewall)
+      a.fw = ctx->fw_ct_mode == PCN_FW_CT_DISABLED ? PCN_FW_LAUNCH_CT_OFF
+             : ctx->fw_ct_mode == PCN_FW_CT_MANUAL ? PCN_FW_LAUNCH_CT_MANUAL : PCN_FW_LAUNCH_CT_AUTO;
+    // which chains can reach the rule stage (ChainSelector_dp.c:157-168, 243-260;
+    // pcn-firewall: the direction's chain, Firewall_ChainForwarder_dp.c:20-42)
+    const bool has_local = firewall || !ctx->localip.empty();
     const bool reach_fw = b->direction == PCN_IPT_INGRESS && !a.allow_logic && a.ch[PCN_IPT_FORWARD].nrules;
-    const bool reach_in = b->direction == PCN_IPT_INGRESS && !a.allow_logic && has_local && a.ch[PCN_IPT_INPUT].nrules;
+    const bool reach_in = !firewall && b->direction == PCN_IPT_INGRESS && !a.allow_logic && has_local &&
+                          a.ch[PCN_IPT_INPUT].nrules;
     const bool reach_out = b->direction == PCN_IPT_EGRESS && has_local && a.ch[PCN_IPT_OUTPUT].nrules;
     int ch = PCN_IPT_FORWARD;
     if (reach_fw && reach_in) ch = 3;
@@ -674,7 +704,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     }
     // chains a packet of this launch can select (ChainSelector_dp.c:157-168, 243-260)
     a.count_mask = b->direction == PCN_IPT_INGRESS
-                       ? (1u << PCN_IPT_FORWARD) | (has_local ? 1u << PCN_IPT_INPUT : 0u)
+                       ? (1u << PCN_IPT_FORWARD) | (has_local && !firewall ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
     // slot count of the chain program (the generic kernel always runs 6)
     const int ns = ch < 3 ? static_cast<int>(a.ch[ch].lay.nslots) : 6;
@@ -753,7 +783,7 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     uint32_t ae_mask = 0, ct_rules = 0;
     for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
       if (!((reach >> c) & 1)) continue;
-      if (ctx->ae[c] && ctx->chains[c].desc.nrules) ae_mask |= 1u << c;
+      if (ctx->ae[c] && ctx->chains[c].desc.nrules && ctx->service == PCN_IPT_SERVICE_IPTABLES) ae_mask |= 1u << c;
       if (ctx->chains[c].desc.nrules && (ctx->chains[c].desc.present & (1u << PCN_IPT_F_CONNTRACK))) ct_rules = 1;
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1016,6 +1046,8 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
 int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2) {
   return guarded(ctx, [&] {
     if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (ctx->service == PCN_IPT_SERVICE_FIREWALL)
+      return fail(-EOPNOTSUPP, "the connection table serves pcn-iptables contexts only");
     if (capacity_log2 == 0) capacity_log2 = 18;
     if (capacity_log2 < 10 || capacity_log2 > 30) return fail(-EINVAL, "capacity_log2 must be 10..30");
     device_guard(ctx);
@@ -1105,6 +1137,8 @@ int pcn_ipt_ct_get_info(pcn_ipt *ctx, pcn_ipt_ct_info *out) {
 int pcn_ipt_set_accept_established(pcn_ipt *ctx, int chain, int on) {
   return guarded(ctx, [&] {
     if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    if (ctx->service == PCN_IPT_SERVICE_FIREWALL)
+      return fail(-EINVAL, "pcn-firewall: use pcn_fw_set_accept_established");
     ctx->ae[chain] = on != 0;
     return 0;
   });
@@ -1133,4 +1167,70 @@ int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uin
   });
 }
 
+// ---- pcn-firewall personality -------------------------------------------
+
+int pcn_ipt_set_service(pcn_ipt *ctx, int service) {
+  return guarded(ctx, [&] {
+    if (service != PCN_IPT_SERVICE_IPTABLES && service != PCN_IPT_SERVICE_FIREWALL)
+      return fail(-EINVAL, "unknown service");
+    for (const ChainState &cs : ctx->chains)
+      if (!cs.rules.empty() || cs.desc.nrules) return fail(-EBUSY, "set the service before adding rules");
+    if (ctx->ct_on) return fail(-EBUSY, "disable the connection table first");
+    ctx->service = service;
+    ctx->fw_ct_mode = PCN_FW_CT_AUTOMATIC;            // Firewall.h:323
+    for (bool &on : ctx->ae) on = false;
+    return 0;
+  });
+}
+
+int pcn_ipt_get_service(pcn_ipt *ctx) {
+  return guarded(ctx, [&] { return ctx->service; });
+}
+
+int pcn_fw_set_conntrack(pcn_ipt *ctx, int on) {
+  return guarded(ctx, [&] {
+    if (ctx->service != PCN_IPT_SERVICE_FIREWALL) return fail(-EINVAL, "not a pcn-firewall context");
+    if (!on) ctx->fw_ct_mode = PCN_FW_CT_DISABLED;                       // Firewall.cpp:152-174
+    else if (ctx->fw_ct_mode == PCN_FW_CT_DISABLED) ctx->fw_ct_mode = PCN_FW_CT_MANUAL;   // :176-193
+    return 0;
+  });
+}
+
+int pcn_fw_set_accept_established(pcn_ipt *ctx, int on) {
+  return guarded(ctx, [&] {
+    if (ctx->service != PCN_IPT_SERVICE_FIREWALL) return fail(-EINVAL, "not a pcn-firewall context");
+    if (ctx->fw_ct_mode == PCN_FW_CT_DISABLED) return fail(-EINVAL, "Please enable conntrack first.");
+    ctx->fw_ct_mode = on ? PCN_FW_CT_AUTOMATIC : PCN_FW_CT_MANUAL;   // Firewall.cpp:119-142
+    return 0;
+  });
+}
+
+int pcn_fw_get_conntrack_mode(pcn_ipt *ctx) {
+  return guarded(ctx, [&] {
+    if (ctx->service != PCN_IPT_SERVICE_FIREWALL) return fail(-EINVAL, "not a pcn-firewall context");
+    return ctx->fw_ct_mode;
+  });
+}
+
+int pcn_fw_chain_update(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rule *rule) {
+  return guarded(ctx, [&] {
+    if (ctx->service != PCN_IPT_SERVICE_FIREWALL) return fail(-EINVAL, "not a pcn-firewall context");
+    if (!valid_chain(ctx, chain) || !rule) return fail(-EINVAL, "bad chain or rule");
+    ChainState &cs = ctx->chains[chain];
+    if (id > cs.rules.size()) return fail(-EINVAL, "rule id not allowed");   // Chain.cpp:614-616
+    Rule r = rule_from_c(ctx, *rule);
+    if (id == cs.rules.size() && cs.rules.size() >= ctx->cfg.max_rules) return fail(-ENOSPC, "too many rules");
+    fetch_stats(ctx, chain);                          // "Forcing counters update" (Chain.cpp:624-625)
+    if (id == cs.rules.size()) {
+      cs.rules.push_back(std::move(r));
+      cs.stats.resize(cs.rules.size());
+    } else {
+      cs.rules[id] = std::move(r);                    // the rule's counters carry on (counters_[id] kept)
+    }
+    if (ctx->interactive) update_chain(ctx, chain);
+    return 0;
+  });
+}
+
 }  // extern "C"
+

@@ -137,6 +137,12 @@ SIGNATURES = {
     "pcn_ipt_get_accept_established": (C.c_int, [C.c_void_p, C.c_int]),
     "pcn_ipt_read_accept_established": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
                                                   C.POINTER(C.c_uint64), C.c_int]),
+    "pcn_ipt_set_service": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_get_service": (C.c_int, [C.c_void_p]),
+    "pcn_fw_set_conntrack": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_fw_set_accept_established": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_fw_get_conntrack_mode": (C.c_int, [C.c_void_p]),
+    "pcn_fw_chain_update": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32, C.POINTER(Rule)]),
 }
 
 _lib = None

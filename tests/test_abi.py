@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_functions():
     txt = open(os.path.join(ROOT, "include", "pcn_ipt.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(pcn_ipt_[a-z0-9_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(pcn_(?:ipt|fw)_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_declares_the_boundary():
@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     lib = ffi.lib()
     out = subprocess.run(["nm", "-D", "--defined-only", ffi.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r"\bT (pcn_ipt_\w+)", out))
+    exported = set(re.findall(r"\bT (pcn_(?:ipt|fw)_\w+)", out))
     for name in header_functions():
         assert name in exported, name
         assert getattr(lib, name) is not None
@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert ffi.lib().pcn_ipt_abi_version() == 2
+    assert ffi.lib().pcn_ipt_abi_version() == 3
 
 
 def test_classify_fails_loudly_without_device():
