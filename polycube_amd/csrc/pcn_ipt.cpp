@@ -957,7 +957,9 @@ int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain) {
     if (ctx->has_device) {
       device_guard(ctx);
       hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-      hip_check(hipMemset(cs.ctr + 2, 0, (ctx->ctr_words - 2) * 8), "hipMemset(counters)");
+      // pcn-firewall also flushes the DefaultAction counters (pcn-firewall Chain.cpp:154-155)
+      const size_t from = ctx->service == PCN_IPT_SERVICE_FIREWALL ? 0 : 2;
+      hip_check(hipMemset(cs.ctr + from, 0, (ctx->ctr_words - from) * 8), "hipMemset(counters)");
     }
     cs.stats.assign(cs.rules.size(), {0, 0});     // counters_.clear()
     return 0;

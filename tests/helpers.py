@@ -245,3 +245,246 @@ class GpuCube:
             torch.cuda.synchronize()
             out.extend(int(x) for x in v.cpu().numpy())
         return out
+
+
+# ---- pcn-firewall (tests/golden/fw_scenarios.json) ----
+FW_CHAINS = {"INGRESS": 1, "EGRESS": 2}      # PCN_FW_INGRESS / PCN_FW_EGRESS slots
+
+
+def load_fw_scenarios():
+    with open(os.path.join(GOLDEN, "fw_scenarios.json")) as fh:
+        return json.load(fh)
+
+
+class FwOpError(Exception):
+    pass
+
+
+class OracleFwCube:
+    """pcn-firewall chain semantics (Chain.cpp:89-819) driving the CPU oracle
+    in its firewall mode, with the connection table on (AUTOMATIC by default,
+    Firewall.h:323).  Counters follow ChainStats: per-rule read-and-flush
+    deltas accumulated whenever the reference calls getStatsList."""
+
+    def __init__(self, oracle):
+        self.o = oracle
+        self.mode = 2
+        self.o.set_service(1, self.mode)
+        self.o.ct_enable(True)
+        self.rules = {c: [] for c in FW_CHAINS}
+        self.default = {c: "ACCEPT" for c in FW_CHAINS}
+        self.stats = {c: [] for c in FW_CHAINS}
+        self.def_base = {c: (0, 0) for c in FW_CHAINS}
+        self.interactive = True
+        for c in FW_CHAINS:
+            self._apply(c)
+
+    def _apply(self, c):
+        self.o.set_chain(FW_CHAINS[c], self.rules[c], self.default[c])
+
+    def _fetch(self, c):                      # Chain::getStatsList
+        n = len(self.rules[c])
+        pk, by, _, _ = self.o.read_counters(FW_CHAINS[c], n, flush=True)
+        st = self.stats[c]
+        st.extend([[0, 0]] * (n - len(st)))
+        for i in range(n):
+            st[i] = [st[i][0] + pk[i], st[i][1] + by[i]]
+
+    def _check_rule(self, r):
+        if "action" not in r:
+            raise FwOpError("action not specified for the rule")
+        if "in_iface" in r or "out_iface" in r:
+            raise FwOpError("no interface fields")
+        if "conntrack" in r and self.mode == 0:
+            raise FwOpError("Please enable the connection tracking module.")
+
+    def op(self, op):
+        kind = op[0]
+        if kind == "expect_error":
+            try:
+                self.op(op[1])
+            except FwOpError:
+                return
+            raise AssertionError(f"op did not fail: {op[1]}")
+        if kind == "conntrack":
+            self.mode = (self.mode or 1) if op[1] == "ON" else 0
+            self.o.set_service(1, self.mode)
+            return
+        if kind == "accept_established":
+            if self.mode == 0:
+                raise FwOpError("Please enable conntrack first.")
+            self.mode = 2 if op[1] == "ON" else 1
+            self.o.set_service(1, self.mode)
+            return
+        c = op[1]
+        rules, st = self.rules[c], self.stats[c]
+        if kind == "default":
+            self.default[c] = op[2]
+            self._fetch(c)
+            self._apply(c)
+            return
+        if kind == "reset_counters":
+            self._fetch(c)
+            self.stats[c] = [[0, 0] for _ in rules]
+            _, _, dp, db = self.o.read_counters(FW_CHAINS[c], 0)
+            self.def_base[c] = (dp, db)
+            return
+        if kind == "batch":
+            was, self.interactive = self.interactive, False
+            failed = []
+            for k, b in enumerate(op[2], 1):
+                b = dict(b)
+                what, rid = b.pop("operation"), b.pop("id", None)
+                sub = {"delete": ["delete", c, rid] if rid is not None else ["deletes", c, b],
+                       "insert": ["insert", c, rid, b], "append": ["append", c, b],
+                       "update": ["add", c, rid, b]}[what]
+                try:
+                    self.op(sub)
+                except FwOpError:
+                    failed.append(k)
+            self.interactive = was
+            self._fetch(c)
+            self._apply(c)
+            if failed:
+                raise FwOpError(f"batch ops failed: {failed}")
+            return
+        if kind in ("append", "insert", "add"):
+            r = op[2] if kind == "append" else op[3]
+            self._check_rule(r)
+        self._fetch(c)
+        if kind == "append":
+            rules.append(op[2])
+            st.append([0, 0])
+        elif kind == "insert":
+            i = 0 if op[2] is None else op[2]
+            if i < 0 or i > len(rules):
+                raise FwOpError("id not allowed")
+            rules.insert(i, op[3])
+            st.insert(i, [0, 0])
+        elif kind == "add":
+            i = op[2]
+            if i < 0 or i > len(rules):
+                raise FwOpError("rule id not allowed")
+            if i == len(rules):
+                rules.append(op[3])
+                st.append([0, 0])
+            else:
+                rules[i] = op[3]
+        elif kind == "delete":
+            i = op[2]
+            if i < 0 or i >= len(rules):
+                raise FwOpError(f"There is no rule {i}")
+            rules.pop(i)
+            st.pop(i)
+        elif kind == "deletes":
+            want = norm_rule(op[2])
+            for i, r in enumerate(rules):
+                if norm_rule(r) == want:
+                    rules.pop(i)
+                    st.pop(i)
+                    break
+            else:
+                raise FwOpError("no matching rule to delete")
+        else:
+            raise ValueError(kind)
+        if self.interactive:
+            self._apply(c)
+
+    def chain_stats(self, c):
+        """[(pkts, bytes) per rule] + (DEFAULT pkts, bytes), like FwChain.stats()."""
+        self._fetch(c)
+        _, _, dp, db = self.o.read_counters(FW_CHAINS[c], 0)
+        b = self.def_base[c]
+        return [tuple(x) for x in self.stats[c]], (dp - b[0], db - b[1])
+
+    def probe(self, packets):
+        """In order, direction runs split into batches; returns (verdicts, labels)."""
+        out, labels = [], []
+        i = 0
+        while i < len(packets):
+            j = i
+            while j < len(packets) and packets[j]["dir"] == packets[i]["dir"]:
+                j += 1
+            sel = packets[i:j]
+            f, lens, ports = ct_probe_frames(sel)
+            v, _, lab = self.o.classify(f, n=len(sel), lens=lens, stride=128, in_port=ports,
+                                        direction=DIRS[sel[0]["dir"]], with_labels=True)
+            out.extend(int(x) for x in v)
+            labels.extend(int(x) for x in lab)
+            i = j
+        return out, labels
+
+
+class GpuFwCube:
+    """The same ops through the product C ABI (polycube_amd.Firewall).  The
+    GPU firewall has no connection table: each probe packet carries the label
+    the oracle's table gave it (batch.ct_status), which is how a deployment
+    feeds conntrack labels from outside."""
+
+    def __init__(self, fw):
+        import torch
+        self.torch = torch
+        self.fw = fw
+
+    def op(self, op):
+        from polycube_amd import IptablesError
+        kind = op[0]
+        if kind == "expect_error":
+            try:
+                self.op(op[1])
+            except IptablesError:     # (a negative id wraps to a uint32 beyond every chain: refused too)
+                return
+            raise AssertionError(f"op did not fail: {op[1]}")
+        if kind == "conntrack":
+            self.fw.conntrack = op[1]
+            return
+        if kind == "accept_established":
+            self.fw.accept_established = op[1]
+            return
+        ch = self.fw.chain(op[1])
+        if kind == "default":
+            ch.default = op[2]
+        elif kind == "reset_counters":
+            ch.reset_counters()
+        elif kind == "batch":
+            ch.batch(op[2])
+        elif kind == "append":
+            ch.append(**op[2])
+        elif kind == "insert":
+            ch.insert(0 if op[2] is None else op[2], **op[3])
+        elif kind == "add":
+            ch.add(op[2], **op[3])
+        elif kind == "delete":
+            ch.delete(op[2])
+        elif kind == "deletes":
+            ch.deletes(**op[2])
+        else:
+            raise ValueError(kind)
+
+    def chain_stats(self, c):
+        rows = self.fw.chain(c).stats()
+        return [(p, b) for _, p, b in rows[:-1]], (rows[-1][1], rows[-1][2])
+
+    def probe(self, packets, labels):
+        torch = self.torch
+        dev = torch.device("cuda", self.fw.device)
+        out, rids = [], []
+        i = 0
+        while i < len(packets):
+            j = i
+            while j < len(packets) and packets[j]["dir"] == packets[i]["dir"]:
+                j += 1
+            sel = packets[i:j]
+            f, lens, ports = ct_probe_frames(sel)
+            lab = np.array([0 if x == 255 else x for x in labels[i:j]], np.uint8)
+            v, r = self.fw.classify(torch.from_numpy(f).to(dev), n=len(sel),
+                                    lens=torch.from_numpy(lens.astype(np.int16)).to(dev), stride=128,
+                                    in_port=torch.from_numpy(ports.astype(np.int16)).to(dev),
+                                    direction=DIRS[sel[0]["dir"]],
+                                    ct_status=None if self.fw.conntrack_mode == 0 else torch.from_numpy(lab).to(dev))
+            torch.cuda.synchronize()
+            out.extend(int(x) for x in v.cpu().numpy())
+            rids.extend(int(x) for x in r.cpu().numpy())
+            i = j
+        return out, rids
+
