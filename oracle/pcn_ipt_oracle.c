@@ -523,9 +523,15 @@ int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n, int 
     if (parse_rule(c, &rules[i], &pr[i])) { free(pr); return -EINVAL; }
   ochain_t *ch = &c->ch[chain];
   uint64_t *pk = ch->pkts, *by = ch->bytes;
+  /* the default counters live outside the reloaded rule modules
+   * (pkts_/bytes_default_<CHAIN> are shared tables, Iptables_Parser_dp.c:47-58;
+   * pcn-firewall's DefaultAction is not part of the chain, Firewall.cpp:60-70):
+   * they survive Chain::updateChain.  The per-rule ActionLookup counters do not. */
+  const uint64_t dp = ch->def_pkts, db = ch->def_bytes;
   ch->pkts = ch->bytes = NULL;
   chain_free(ch);
   ch->pkts = pk; ch->bytes = by;
+  ch->def_pkts = dp; ch->def_bytes = db;
   memset(pk, 0, c->max_counted * 8); memset(by, 0, c->max_counted * 8);
   ch->rules = pr; ch->nrules = (int)n; ch->default_action = def;
   return compile_chain(c, chain);
