@@ -336,9 +336,12 @@ int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uin
  *    conntrack is on (modules/Parser.cpp:41-45).  AUTOMATIC mode
  *    (accept-established ON, the default) accepts ESTABLISHED packets before
  *    the chain, uncounted, rule id PCN_IPT_RID_ACCEPT_ESTABLISHED
- *    (Firewall_ConntrackLabel_dp.c:474-478).  Without the connection table
- *    (pcn_ipt_ct_enable is refused for a firewall context) labels come from
- *    batch.ct_status or an empty table; with conntrack off the label is NEW.
+ *    (Firewall_ConntrackLabel_dp.c:474-478).  With the connection table
+ *    (pcn_ipt_ct_enable) labels and updates are the pcn-iptables ones (the
+ *    label and update code is the same, Firewall_ConntrackLabel_dp.c:116-460,
+ *    Firewall_ConntrackTableUpdate_dp.c:141-650); without it they come from
+ *    batch.ct_status or an empty table.  With conntrack off the label is NEW
+ *    and the table is neither read nor updated.
  * Set the service on a fresh context, before any rule. */
 enum { PCN_IPT_SERVICE_IPTABLES = 0, PCN_IPT_SERVICE_FIREWALL = 1 };
 enum { PCN_FW_INGRESS = PCN_IPT_FORWARD, PCN_FW_EGRESS = PCN_IPT_OUTPUT };

@@ -168,7 +168,12 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *
     bool pass = false;
     if (p.status == 2) {
       bool labeled = true;
-      if (b.direction == PCN_IPT_INGRESS) {
+      if (b.fw) {
+        // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder
+        // (Firewall_ChainForwarder_dp.c:20-42).  An empty chain goes to
+        // DefaultAction after labelling, which stage A already resolved.
+        chain = b.direction == PCN_IPT_INGRESS ? PCN_IPT_FORWARD : PCN_IPT_OUTPUT;
+      } else if (b.direction == PCN_IPT_INGRESS) {
         if (b.allow_logic) pass = true;
         else chain = (b.nlocal && localip_has(b, p.dst)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
       } else if (b.nlocal && localip_has(b, p.src)) {
@@ -176,7 +181,7 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *
       } else {
         labeled = false;                                   // egress PASS, no labeling
       }
-      if (labeled && chain < 3 && ((b.empty_mask >> chain) & 1)) {
+      if (!b.fw && labeled && chain < 3 && ((b.empty_mask >> chain) & 1)) {
         if ((b.drop_mask >> chain) & 1) labeled = false;  // DROP_NO_LABELING (default counters)
         else pass = true;                                  // PASS_LABELING
       }

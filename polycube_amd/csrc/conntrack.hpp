@@ -49,6 +49,7 @@ struct CtBatch {
   const uint32_t *localip;    // sorted NBO u32
   uint32_t nlocal;
   uint32_t allow_logic, empty_mask, drop_mask;
+  uint32_t fw;                // pcn-firewall dispatch: the direction's chain, labels before the chain
   uint32_t ae_mask;           // bit c: accept-established optimization on for chain c
   uint32_t nlab;              // outcomes per packet from stage A: 1 or 4
   const uint8_t *a_verdict;   // [nlab][n]

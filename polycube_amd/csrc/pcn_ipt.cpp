@@ -752,7 +752,8 @@ CtBatch ct_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, uint32_t ae_mask) {
   cb.localip = ctx->d_localip;
   cb.nlocal = static_cast<uint32_t>(ctx->localip.size());
   const ChainState &in = ctx->chains[PCN_IPT_INPUT], &fw = ctx->chains[PCN_IPT_FORWARD];
-  cb.allow_logic = in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
+  cb.fw = ctx->service == PCN_IPT_SERVICE_FIREWALL;
+  cb.allow_logic = !cb.fw && in.default_action == PCN_IPT_ACCEPT && fw.default_action == PCN_IPT_ACCEPT &&
                    in.rules.size() == 0 && fw.rules.size() == 0 && in.desc.nrules == 0 && fw.desc.nrules == 0;
   for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
     const ChainState &cs = ctx->chains[c];
@@ -787,7 +788,10 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       if (ctx->chains[c].desc.nrules && (ctx->chains[c].desc.present & (1u << PCN_IPT_F_CONNTRACK))) ct_rules = 1;
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (!ctx->ct_on) {
+    const bool firewall = ctx->service == PCN_IPT_SERVICE_FIREWALL;
+    // pcn-firewall with conntrack DISABLED: no labels and no table updates
+    // (Firewall_ConntrackTableUpdate_dp.c:136-138), whatever the table holds
+    if (!ctx->ct_on || (firewall && ctx->fw_ct_mode == PCN_FW_CT_DISABLED)) {
       int rc = launch_batch(ctx, b, stream, nullptr);
       if (rc || !ae_mask) return rc;
       device_guard(ctx);
@@ -816,6 +820,11 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       int rc = launch_batch(ctx, b, stream, &sa);
       if (rc) return rc;
     }
+    // pcn-firewall AUTOMATIC: ESTABLISHED packets are accepted before the chain
+    // (Firewall_ConntrackLabel_dp.c:474-478); uncounted -- the firewall has no
+    // accept-established counters, so what ct_count puts there is never read
+    if (firewall && ctx->fw_ct_mode == PCN_FW_CT_AUTOMATIC)
+      ae_mask = b->direction == PCN_IPT_EGRESS ? 1u << PCN_IPT_OUTPUT : 1u << PCN_IPT_FORWARD;
     CtBatch cb = ct_batch(ctx, b, ae_mask);
     cb.nlab = nlab;
     cb.a_verdict = a_v;
@@ -1048,8 +1057,6 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
 int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2) {
   return guarded(ctx, [&] {
     if (!ctx->has_device) return fail(-ENODEV, "no device");
-    if (ctx->service == PCN_IPT_SERVICE_FIREWALL)
-      return fail(-EOPNOTSUPP, "the connection table serves pcn-iptables contexts only");
     if (capacity_log2 == 0) capacity_log2 = 18;
     if (capacity_log2 < 10 || capacity_log2 > 30) return fail(-EINVAL, "capacity_log2 must be 10..30");
     device_guard(ctx);

@@ -476,12 +476,13 @@ class GpuFwCube:
                 j += 1
             sel = packets[i:j]
             f, lens, ports = ct_probe_frames(sel)
-            lab = np.array([0 if x == 255 else x for x in labels[i:j]], np.uint8)
+            ct = None          # labels=None: the context's own connection table labels them
+            if labels is not None and self.fw.conntrack_mode != 0:
+                ct = torch.from_numpy(np.array([0 if x == 255 else x for x in labels[i:j]], np.uint8)).to(dev)
             v, r = self.fw.classify(torch.from_numpy(f).to(dev), n=len(sel),
                                     lens=torch.from_numpy(lens.astype(np.int16)).to(dev), stride=128,
                                     in_port=torch.from_numpy(ports.astype(np.int16)).to(dev),
-                                    direction=DIRS[sel[0]["dir"]],
-                                    ct_status=None if self.fw.conntrack_mode == 0 else torch.from_numpy(lab).to(dev))
+                                    direction=DIRS[sel[0]["dir"]], ct_status=ct)
             torch.cuda.synchronize()
             out.extend(int(x) for x in v.cpu().numpy())
             rids.extend(int(x) for x in r.cpu().numpy())

@@ -130,3 +130,84 @@ def test_firewall_headline_shape_fixed_stride(dev):
     po, bo, dpo, dbo = o.read_counters(1, 1000)
     pg, bg, dpg, dbg = fw.chain("INGRESS").read_counters(1000)
     assert (po, bo, dpo, dbo) == (pg, bg, dpg, dbg)
+
+
+# ---- stateful: the connection table on the GPU (conntrack.hip) ----
+NOW = 1_700_000_000_123_456_789
+
+
+def assert_tables(o, fw):
+    a, b = o.ct_dump(), fw.ct_dump()
+    assert len(a) == len(b), (len(a), len(b))
+    for f in a.dtype.names:
+        bad = np.nonzero(a[f] != b[f])[0]
+        assert bad.size == 0, f"session table field {f}: {bad.size} differ"
+
+
+@pytest.mark.parametrize("sc", SCEN["scenarios"], ids=[s["name"] for s in SCEN["scenarios"]])
+def test_reference_firewall_scenarios_stateful_gpu(dev, sc):
+    """The scripts again, now labelled from the GPU's own connection table
+    (pcn_ipt_ct_enable): verdicts, outcomes, counters and the session table
+    equal the oracle's."""
+    from polycube_amd import Firewall
+    ocube = OracleFwCube(Oracle())
+    fw = Firewall(device=0, jit=1)
+    fw.ct_enable(16)
+    ocube.o.ct_set_time(NOW)
+    fw.ct_set_time(NOW)
+    gcube = GpuFwCube(fw)
+    for k, st in enumerate(sc["steps"]):
+        where = f"{sc['name']} step {k} ({st.get('ref_line', '')})"
+        for op in st["ops"]:
+            ocube.op(op)
+            gcube.op(op)
+        if "probe" in st:
+            v_o, _ = ocube.probe(st["probe"])
+            v_g, _ = gcube.probe(st["probe"], None)
+            assert v_g == v_o, f"{where}: oracle {v_o} gpu {v_g}"
+            got = "pass" if all(v == 1 for v in v_g) else "fail"
+            assert got == st["expect"], where
+        for c in ("INGRESS", "EGRESS"):
+            assert gcube.chain_stats(c) == ocube.chain_stats(c), f"{where}: {c} stats"
+        assert_tables(ocube.o, fw)
+
+
+CT_RULES = [{"conntrack": "ESTABLISHED", "action": "ACCEPT"}, {"conntrack": "NEW", "l4proto": "TCP", "action": "ACCEPT"},
+            {"conntrack": "INVALID", "action": "DROP"}]
+
+
+@pytest.mark.parametrize("mode", [1, 2], ids=["manual", "automatic"])
+def test_firewall_stateful_flow_parity(dev, mode):
+    """Interleaved flows (handshakes, replies, ICMP errors quoting live flows,
+    noise) through INGRESS and EGRESS in several batches; conntrack rules in
+    INGRESS; the table carried across batches and directions."""
+    rs = synth.config_rules(2)
+    base = [dict(r, action=r.get("action", "DROP")) for r in rs.rules()]
+    o, fw = make_fw_pair({"INGRESS": CT_RULES + base, "EGRESS": base[:40]},
+                         {"INGRESS": "DROP", "EGRESS": "ACCEPT"}, mode, 1)
+    o.ct_enable()
+    o.ct_set_time(NOW)
+    fw.ct_enable(16)
+    fw.ct_set_time(NOW)
+    n = 24000
+    f, lens = synth.flow_traffic(n, 900, 11 + mode, rs=rs, lens_mode="mixed", p_noise=0.1, p_err=0.05)
+    nb = f.reshape(n, 128)
+    for k, (lo, hi) in enumerate(((0, 6000), (6000, 6001), (6001, 15000), (15000, 24000))):
+        direction = k % 2
+        fr = np.ascontiguousarray(nb[lo:hi]).reshape(-1)
+        v_o, r_o = o.classify(fr, n=hi - lo, lens=lens[lo:hi], stride=128, fixed_len=128, direction=direction)
+        v_g, r_g = fw.classify(torch.from_numpy(fr).to(dev), n=hi - lo,
+                               lens=torch.from_numpy(lens[lo:hi].view(np.int16)).to(dev), stride=128,
+                               fixed_len=128, direction=direction)
+        torch.cuda.synchronize()
+        v_g, r_g = v_g.cpu().numpy(), r_g.cpu().numpy()
+        bad = np.nonzero((v_o != v_g) | (r_o != r_g))[0]
+        assert bad.size == 0, f"batch {k}: {bad.size} mismatches at {bad[:5]}"
+        if mode == 2 and k > 0:
+            assert np.any(r_g == -3)
+    assert_tables(o, fw)
+    for name, slot, nr in (("INGRESS", 1, len(base) + 3), ("EGRESS", 2, 40)):
+        po, bo, dpo, dbo = o.read_counters(slot, nr)
+        pg, bg, dpg, dbg = fw.chain(name).read_counters(nr)
+        assert (po, bo, dpo, dbo) == (pg, bg, dpg, dbg), name
+    assert fw.ct_info()["inserts_lost"] == 0
