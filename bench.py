@@ -135,6 +135,34 @@ def ct_rate(ipt, rs, n, dev, steps=5, warmup=2, flows=1 << 16, seed=0xC7):
     return n * steps / el / 1e6, el / steps * 1e3, live
 
 
+def fw_rate(rules, frames, n, dev, s_ptr, jit, steps=20):
+    """The headline rules in a pcn-firewall INGRESS chain (conntrack OFF), same
+    resident frames: kernel time per launch (HIP events) and Mpkt/s."""
+    import torch
+    from polycube_amd import Firewall
+    fw = Firewall(device=dev.index, jit=jit)
+    fw.conntrack = "OFF"
+    fw.interactive = False
+    ing = fw.chain("INGRESS")
+    for r in rules:
+        ing.append(**dict(r, action=r.get("action", "DROP")))
+    ing.default = "DROP"
+    ing.apply_rules()
+    v = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        fw.classify(frames, n=n, verdicts=v, rule_ids=False, stream=s_ptr)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record(stream)
+        fw.classify(frames, n=n, verdicts=v, rule_ids=False, stream=s_ptr)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    fw.close()
+    return n / (ms * 1e-3) / 1e6, ms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,6 +176,7 @@ def main():
     ap.add_argument("--hook", default="xdp", choices=("xdp", "tc"),
                     help="attach-point semantics (tc: outer VLAN tags stripped before classification)")
     ap.add_argument("--no-ct", action="store_true", help="skip the stateful-conntrack leg")
+    ap.add_argument("--no-fw", action="store_true", help="skip the pcn-firewall leg")
     ap.add_argument("--jit", type=int, default=1,
                     help="chain programs: 1 compiled before the first launch (default), 0 background, -1 off")
     args = ap.parse_args()
@@ -282,6 +311,12 @@ def main():
             line["e2e"] = {"value": round(e2e_rate(ipt, frames_host, n), 2), "unit": "Mpkt/s",
                            "what": "host ingest ring (pcn_ipt_ring): pinned slots -> H2D -> classify -> D2H verdicts, "
                                    "4 slots x 2^21 frames in flight over 4 streams"}
+        if world == 1 and not args.no_fw and cfg == 3:
+            rate, ms = fw_rate(rules, frames, n, dev, s_ptr, args.jit)
+            line["firewall"] = {
+                "value": round(rate, 2), "unit": "Mpkt/s", "kernel_ms": round(ms, 4),
+                "what": "the same rules and frames through the pcn-firewall personality (pcn_ipt_set_service): "
+                        "INGRESS chain, conntrack OFF"}
         if world == 1 and not args.no_ct and cfg == 3:
             rate, ms, live = ct_rate(ipt, rs, n, dev)
             line["stateful_conntrack"] = {
