@@ -42,6 +42,12 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #ifndef PCN_PREFETCH
 #define PCN_PREFETCH 1   // frames per lane in flight ahead of the one being classified
 #endif
+#ifndef PCN_FASTPATH
+#define PCN_FASTPATH 1   // wave fast path: all 64 frames plain IPv4 TCP/UDP -> straight-line parse
+#endif
+#ifndef PCN_PF_FAST
+#define PCN_PF_FAST 1    // whole-wave frame groups: uniform base + per-lane constant offsets
+#endif
 #ifndef PCN_STAGE_FAST
 #define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
 #endif
@@ -435,8 +441,10 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
 // and field set into the code as immediates; only its pointers stay kernargs.
 #ifdef PCN_JIT
 constexpr DevChain kJitChain = PCN_JIT_CHAIN;
+constexpr int kJitInputs = PCN_JIT_INPUTS;   // bit 0: in_port array, bits 1-2: ct_status (array / stage-A label)
 #else
 constexpr DevChain kJitChain{};
+constexpr int kJitInputs = 7;
 #endif
 template <bool JIT, int CH>
 __device__ __forceinline__ DevChain chain_desc(const LaunchArgs &a) {
@@ -511,23 +519,39 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     uint32_t L, port, ct;
   };
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t cf[3], co[3];   // (the transpose buffer is the wave's LDS region, shared with WaveScratch)   // fixed path: frame within the wave's group, byte offset of the chunk
+  // fixed path: frame within the wave's group, byte offset of the chunk, and
+  // the chunk's byte offset from the group's first frame
+  uint32_t cf[3], co[3], loff[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const uint32_t t = 64 * q + lane;
     cf[q] = t / 3;
     co[q] = 16 * (t - 3 * cf[q]);
+    loff[q] = cf[q] * a.stride + co[q];
   }
+  // per-frame side inputs a chain program knows it does not have are never loaded
+  constexpr bool kLoadPort = !JIT || (kJitInputs & 1);
+  constexpr bool kLoadCt = !JIT || (kJitInputs & 6);
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   Stage st[PCN_PREFETCH];
   auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
     if (FIXED && PCN_HDR_LDS) {
-      const uint64_t group = j - lane;           // wave-uniform
+      uint64_t group = j - lane;                 // wave-uniform
+      group = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(group >> 32))) << 32) |
+              __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(group));
+      if (PCN_PF_FAST && group + 64 <= a.n) {
+        // the whole group is in the batch: scalar base + loop-invariant lane offsets
+        const uint8_t *gb = a.frames + group * a.stride;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        uint64_t f = group + cf[q];
-        f = f < a.n ? f : last;
-        x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]));
+        for (int q = 0; q < 3; ++q)
+          x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(gb + loff[q]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          uint64_t f = group + cf[q];
+          f = f < a.n ? f : last;
+          x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]));
+        }
       }
     } else if (FIXED) {
       const uint64_t f = j < a.n ? j : last;
@@ -539,8 +563,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       load_header<FIXED>(a, j < a.n ? j : last, x.h, x.L);
     }
     const uint64_t jc = j < a.n ? j : last;
-    x.port = a.in_port[jc & a.in_port_mask];
-    x.ct = a.ct_status[jc & a.ct_mask];
+    x.port = kLoadPort ? a.in_port[jc & a.in_port_mask] : 0u;
+    x.ct = kLoadCt ? a.ct_status[jc & a.ct_mask] : 0u;
   };
 #pragma unroll
   for (int d = 0; d < PCN_PREFETCH; ++d) prefetch(st[d], first + d * step);
@@ -597,7 +621,33 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     int32_t chain = -1;     // chain whose rules must run (-1: decided already)
     Parsed p{};
     uint32_t port = 0;
-    if (valid) {
+    // Wave fast path: when every lane holds a plain IPv4 TCP/UDP frame long
+    // enough for its L4 header (fixed stride: XDP, one length) and the launch
+    // has a chain every such frame selects, the Parser / ChainSelector /
+    // ConntrackLabel steps below reduce to straight-line field extraction.
+    bool fast = false;
+    if (PCN_FASTPATH && FIXED && a.fast_chain >= 0) {
+      const uint32_t pr = h.w[5] >> 24;
+      const bool plain = valid && (h.w[3] & 0xffff) == 0x0008 &&
+                         ((pr == 6 && L >= 54) || (pr == 17 && L >= 42));
+      fast = __ballot(!plain) == 0;
+    }
+    if (fast) {
+      port = a.has_in_port ? cur_port : const_port;
+      p.proto = h.w[5] >> 24;
+      p.saddr = (h.w[6] >> 16) | (h.w[7] << 16);
+      p.daddr = (h.w[7] >> 16) | (h.w[8] << 16);
+      p.flags = p.proto == 6 ? h.w[11] >> 24 : 0u;
+      p.sport = bswap16u(h.w[8] >> 16);
+      p.dport = bswap16u(h.w[9] & 0xffff);
+      chain = a.fast_chain;
+      // labels: given, or the empty-table ones (ConntrackLabel_dp.c:372-383)
+      p.ct = a.has_ct ? cur_ct : empty_table_label(p, 0xffffffffu);
+      if (a.fw == PCN_FW_LAUNCH_CT_OFF && !a.has_ct) p.ct = 0;
+      if (a.fw == PCN_FW_LAUNCH_CT_AUTO && p.ct == 1) {   // Firewall_ConntrackLabel_dp.c:474-478
+        verdict = PCN_IPT_ACCEPT; rid = PCN_IPT_RID_ACCEPT_ESTABLISHED; chain = -1;
+      }
+    } else if (valid) {
       port = a.has_in_port ? cur_port : const_port;
       // ---- TC hook: the outer VLAN tag is gone before the program runs ----
       bool untag_drop = false;

@@ -127,6 +127,8 @@ struct LaunchArgs {
   uint32_t drop_mask;            // bit c: chain c's default action is DROP
   uint32_t count_mask;           // bit c: packets of this launch can select chain c
   uint32_t fw;                   // 0: pcn-iptables dispatch; else pcn-firewall, PCN_FW_LAUNCH_*
+  int32_t fast_chain;            // >= 0: every IPv4 TCP/UDP frame selects this chain (no localip,
+                                 // allow logic or empty chain involved); -1: no wave fast path
 };
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)

@@ -30,6 +30,7 @@ struct JitShape {
   bool lds = true;     // chain images staged in LDS
   int ch = 1;          // the one chain that runs rules (0..2)
   int ns = 5;          // class slots
+  int inputs = 0;      // bit 0: per-frame in_port array, bit 1: per-frame ct_status array
 };
 
 // Source of the generated "pcn_jit_spec.h" for one chain descriptor (its

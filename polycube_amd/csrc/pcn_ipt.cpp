@@ -703,6 +703,16 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       if (last >= b->frames_bytes) return fail(-EINVAL, "frames_bytes smaller than n*stride");
     }
     // chains a packet of this launch can select (ChainSelector_dp.c:157-168, 243-260)
+    // wave fast path (classify.hip): the chain every IPv4 TCP/UDP frame of the
+    // launch selects, when that needs no per-packet choice
+    a.fast_chain = -1;
+    if (firewall) {
+      const int c = b->direction == PCN_IPT_INGRESS ? PCN_IPT_FORWARD : PCN_IPT_OUTPUT;
+      if (a.ch[c].nrules) a.fast_chain = c;
+    } else if (b->direction == PCN_IPT_INGRESS && !a.allow_logic && ctx->localip.empty() &&
+               a.ch[PCN_IPT_FORWARD].nrules) {
+      a.fast_chain = PCN_IPT_FORWARD;
+    }
     a.count_mask = b->direction == PCN_IPT_INGRESS
                        ? (1u << PCN_IPT_FORWARD) | (has_local && !firewall ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
@@ -717,12 +727,14 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.lds = a.lds_images_bytes > 0;
       shape.ch = ch;
       shape.ns = ns;
+      shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0);
       DevChain key = a.ch[ch];
       key.image = nullptr;
       key.ctr = nullptr;
       if (cs.jit_spec.empty() || std::memcmp(&key, &cs.jit_desc, sizeof(DevChain)) != 0 ||
           shape.fixed != cs.jit_shape.fixed ||
-          shape.lds != cs.jit_shape.lds || shape.ch != cs.jit_shape.ch || shape.ns != cs.jit_shape.ns) {
+          shape.lds != cs.jit_shape.lds || shape.ch != cs.jit_shape.ch || shape.ns != cs.jit_shape.ns ||
+          shape.inputs != cs.jit_shape.inputs) {
         cs.jit_desc = key;
         cs.jit_shape = shape;
         cs.jit_spec = jit_spec(key, shape);

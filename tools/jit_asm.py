@@ -57,7 +57,7 @@ def spec_for(cfg):
     ns = lay[LAYOUT.index("nslots")]
     vals = ", ".join(f"{x}u" for x in lay)
     return ("#pragma once\n#define PCN_JIT_FIXED true\n#define PCN_JIT_LDS true\n#define PCN_JIT_CH 1\n"
-            f"#define PCN_JIT_NS {ns}\n#define PCN_JIT_CHAIN {{{vals}, nullptr, nullptr, {info['nrules']}u, {nrw}u, "
+            f"#define PCN_JIT_NS {ns}\n#define PCN_JIT_INPUTS 0\n#define PCN_JIT_CHAIN {{{vals}, nullptr, nullptr, {info['nrules']}u, {nrw}u, "
             f"{nsw}u, {present}u, {info['nvec']}u, {all_cls}u, {ncounted}u, 10000u, 0, 0u, {lay[0]}u, {lds_bins}}}\n")
 
 
