@@ -48,6 +48,9 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #ifndef PCN_PF_FAST
 #define PCN_PF_FAST 1    // whole-wave frame groups: uniform base + per-lane constant offsets
 #endif
+#ifndef PCN_FLUSH_ROT
+#define PCN_FLUSH_ROT 1  // per-workgroup rotation of the counter flush order
+#endif
 #ifndef PCN_STAGE_FAST
 #define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
 #endif
@@ -797,7 +800,12 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   }
   __syncthreads();
   // ---- flush the workgroup histogram ----
-  for (uint32_t b = threadIdx.x; b < a.nbins; b += blockDim.x) {
+  // Workgroups finish together and all add into the same counters; each
+  // starts at its own rotation of the bins so the global atomics of
+  // concurrent flushes mostly land on different addresses.
+  const uint32_t rot = PCN_FLUSH_ROT ? (blockIdx.x * 97u) % a.nbins : 0u;
+  for (uint32_t b0 = threadIdx.x; b0 < a.nbins; b0 += blockDim.x) {
+    const uint32_t b = b0 + rot < a.nbins ? b0 + rot : b0 + rot - a.nbins;
     const unsigned long long pk = bins[b];
     const unsigned long long by = FIXED ? pk * a.fixed_len : byte_bins[b];
     if (!pk) continue;
