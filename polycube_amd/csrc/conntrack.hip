@@ -460,13 +460,27 @@ __device__ __forceinline__ int32_t outcome(const CtBatch &b, int32_t o0, int32_t
 
 // A packet's walk input in sorted order (64 B: one line): its record, key
 // bucket, batch index and stage-A outcomes (rule id << 1 | verdict per label).
-struct WalkRec {
+struct alignas(16) WalkRec {
   CtRec r;
   uint32_t key, idx;
   int32_t o0, o1, o2, o3;
   uint32_t pad[2];
 };
 static_assert(sizeof(WalkRec) == 64, "WalkRec is 64 bytes");
+
+// One record as four 16-byte loads (a field-by-field copy of the packed
+// struct issues ~20 narrow loads per record on the walk's critical path).
+typedef uint32_t ct_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ WalkRec load_rec(const WalkRec *p) {
+  const ct_u32x4 *s = reinterpret_cast<const ct_u32x4 *>(p);
+  union {
+    ct_u32x4 v[4];
+    WalkRec w;
+  } u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) u.v[k] = s[k];
+  return u.w;
+}
 
 __device__ __forceinline__ int32_t process(const CtBatch &b, const CtTable &t, Cache &c, const WalkRec &w) {
   const CtRec &r = w.r;
@@ -521,16 +535,16 @@ __global__ void ct_walk_kernel(CtBatch b, CtTable t, const WalkRec *wrec, int32_
   Cache c{};
   // two records in flight in named registers, A/B alternating (a register
   // move of an in-flight load would wait for it)
-  WalkRec A = wrec[q < last ? q : last];
-  WalkRec B = wrec[q + 1 < last ? q + 1 : last];
+  WalkRec A = load_rec(&wrec[q < last ? q : last]);
+  WalkRec B = load_rec(&wrec[q + 1 < last ? q + 1 : last]);
   for (;;) {
     if (q >= b.n || A.key != k || A.idx >= hi) break;
     sres[q] = process(b, t, c, A);
-    A = wrec[q + 2 < last ? q + 2 : last];
+    A = load_rec(&wrec[q + 2 < last ? q + 2 : last]);
     ++q;
     if (q >= b.n || B.key != k || B.idx >= hi) break;
     sres[q] = process(b, t, c, B);
-    B = wrec[q + 2 < last ? q + 2 : last];
+    B = load_rec(&wrec[q + 2 < last ? q + 2 : last]);
     ++q;
   }
   flush(c);
