@@ -19,6 +19,10 @@
 #include "conntrack.hpp"
 #include "pcn_ipt.h"
 
+#ifndef PCN_CT_FAST
+#define PCN_CT_FAST 1   // walk: straight-line step for established TCP / live UDP connections
+#endif
+
 namespace pcn {
 
 namespace {
@@ -491,6 +495,44 @@ __device__ __forceinline__ int32_t process(const CtBatch &b, const CtTable &t, C
   return o;
 }
 
+// The common step of a long run, without the general label/update code: a
+// TCP or UDP packet of the cached live connection, in its forward or reverse
+// direction.  TCP only while ESTABLISHED and without FIN: label ESTABLISHED
+// (label_of: RST or an established state), and an accepted packet refreshes
+// the ttl unless it carries RST (update's ST_EST branch).  UDP: label_of's
+// UDP_FORWARD / UDP_REVERSE and update's two live branches.  Returns false
+// (nothing done) for anything else, which then takes process().
+__device__ __forceinline__ bool fast_step(const CtBatch &b, const CtTable &t, Cache &c, const WalkRec &w,
+                                          int32_t &o) {
+  const CtRec &r = w.r;
+  if (!c.valid || !c.v.live || (r.kind != K_TCP && r.kind != K_UDP)) return false;
+  const bool fwd = c.v.rev == r.rev, rev = (c.v.rev ^ r.rev) == 3;
+  if (!(fwd || rev) || !same(c.k, Key{r.src, r.dst, r.sport, r.dport, r.proto})) return false;
+  if (r.kind == K_TCP) {
+    if (c.v.state != ST_EST || (r.flags & FIN)) return false;
+    o = outcome(b, w.o0, w.o1, w.o2, w.o3, r, ST_EST);
+    if ((o & 1) == PCN_IPT_ACCEPT) {
+      c.dirty = true;
+      if (!(r.flags & RST)) c.v.ttl = t.now + TCP_ESTABLISHED_T;
+    }
+    return true;
+  }
+  const bool nw = c.v.state == ST_NEW;
+  o = outcome(b, w.o0, w.o1, w.o2, w.o3, r, fwd && nw ? ST_NEW : ST_EST);
+  if ((o & 1) == PCN_IPT_ACCEPT) {
+    c.dirty = true;
+    c.v.ttl = t.now + (nw ? UDP_NEW_TIMEOUT : UDP_ESTABLISHED_TIMEOUT);
+    if (rev && nw) c.v.state = ST_EST;
+  }
+  return true;
+}
+
+__device__ __forceinline__ int32_t step(const CtBatch &b, const CtTable &t, Cache &c, const WalkRec &w) {
+  int32_t o;
+  if (PCN_CT_FAST && fast_step(b, t, c, w, o)) return o;
+  return process(b, t, c, w);
+}
+
 __device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, uint64_t i) {
   return l < b.nlab ? (b.a_rid[l * b.n + i] * 2) | b.a_verdict[l * b.n + i] : 0;
 }
@@ -539,11 +581,11 @@ __global__ void ct_walk_kernel(CtBatch b, CtTable t, const WalkRec *wrec, int32_
   WalkRec B = load_rec(&wrec[q + 1 < last ? q + 1 : last]);
   for (;;) {
     if (q >= b.n || A.key != k || A.idx >= hi) break;
-    sres[q] = process(b, t, c, A);
+    sres[q] = step(b, t, c, A);
     A = load_rec(&wrec[q + 2 < last ? q + 2 : last]);
     ++q;
     if (q >= b.n || B.key != k || B.idx >= hi) break;
-    sres[q] = process(b, t, c, B);
+    sres[q] = step(b, t, c, B);
     B = load_rec(&wrec[q + 2 < last ? q + 2 : last]);
     ++q;
   }

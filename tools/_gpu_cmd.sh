@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_BRANCH"
-B="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS"
-JIT=1 TAG=pmc_s9 bash tools/pmc.sh "FETCH_SIZE" "WRITE_SIZE" "$A" "$B" || exit $?
-python tools/pmc_summary.py gpurun_out/pmc_s9 --traffic --out gpurun_out/pmc_s9/summary.json | tail -40
+timeout -k 10 600 python -u -m pytest tests/test_gpu_conntrack.py tests/test_gpu_firewall.py -x -q --timeout 120 --timeout-method thread -k "not fuzz_parity" > gpurun_out/gpu_ct_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/gpu_ct_tests.log; [ $rc = 0 ] || { grep -E "Error|assert" gpurun_out/gpu_ct_tests.log | head; exit $rc; }
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-e2e --no-fw > gpurun_out/bench_ct.json 2> gpurun_out/bench_ct.err
+rc=$?; python -c "import json; d=json.load(open('gpurun_out/bench_ct.json')); print(d['value'], d['stateful_conntrack'])"; exit $rc
