@@ -317,7 +317,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       m = live >= 64 ? ~0ull : ((1ull << live) - 1);
       uint64_t sm[NS];
 #pragma unroll
-      for (int f = 0; f < NS; ++f) sm[f] = t.u64(lay.sf, 16 * (cls[f] * nsw + k));
+      for (int f = 0; f < NS; ++f) sm[f] = t.u64(lay.sf, 8 * (cls[f] * nsw + k));
 #pragma unroll
       for (int f = 0; f < NS; ++f) m &= sm[f];
     }
@@ -379,17 +379,17 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
 #pragma unroll
         for (int f = 0; f < NS; ++f) oc[f] = (packed[f / 2] >> (16 * (f & 1))) & 0xffff;
         // At a candidate word every field's summary bit is set, so a field is
-        // PARTIAL there iff its FULL bit is clear.  Straight-line on purpose:
-        // every index read, then every word read, issue back to back.  A FULL
-        // field reads POOL[0], the all-ones word (indexed PART: through the
-        // zero cell, index 0).
+        // PARTIAL there iff its PM bit is set; one 16-byte read gives PM and
+        // PBASE.  Straight-line on purpose: every record read, then every word
+        // read, issue back to back.  A FULL field reads POOL[0], the all-ones
+        // word (indexed PART: through the zero cell, index 0).
         uint32_t at[NS];   // LDS/image offset of each field's u64 word
 #pragma unroll
         for (int f = 0; f < NS; ++f) {
           const uint32_t rec = oc[f] * nsw + k;
-          const u32x4 r = t.u128(lay.sf, 16 * rec);
-          const uint64_t pm = (static_cast<uint64_t>(r.y) << 32 | r.x) & ~(static_cast<uint64_t>(r.w) << 32 | r.z);
-          const uint32_t j = t.u32(lay.pbase, 4 * rec) + static_cast<uint32_t>(__builtin_popcountll(pm & below));
+          const u32x4 r = t.u128(lay.pbase, 16 * rec);
+          const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;
+          const uint32_t j = r.z + static_cast<uint32_t>(__builtin_popcountll(pm & below));
           const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
           if (lay.part_direct) {
             at[f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));

@@ -17,9 +17,10 @@
 //     META slot: each maps its value to a small index and a table holds the
 //     class of the AND of their vectors;
 //   - per class and 64-word block: SUMM (bit w: word w of the class vector
-//     != 0), FULL (bit w: word w holds all of its rules) and PBASE, the start
-//     of the class's PARTIAL words (neither zero nor full) in PART, stored in
-//     word order (a partial word's index = PBASE + popcount(partial bits below));
+//     != 0), and the candidate record {PM, PBASE}: PM (bit w: word w is
+//     PARTIAL, neither zero nor holding all of its rules) and the start of the
+//     class's partial words in PART, stored in word order (a partial word's
+//     index = PBASE + popcount(PM bits below));
 //     PART holds the partial words themselves (PART_DIRECT, while the image
 //     stays small enough for LDS) or u16 (u32 when PART_WIDE) indices into
 //     POOL, the distinct partial words (at 1k rules ~7x fewer);
@@ -69,8 +70,10 @@ struct TableLayout {
   uint32_t flags_skip;     // flags index of a non-TCP packet (the module is skipped)
   uint32_t meta;           // u16[]: class of the meta slot at sum(index_f * meta_stride[f])
   uint32_t meta_stride[6]; // proto, flags, ct, sport, dport, iface (0: not a meta field)
-  uint32_t sf;             // u64x2[nvec][nsw]: {SUMM, FULL}
-  uint32_t pbase;          // u32[nvec][nsw]: first PART index of the class's block
+  uint32_t sf;             // u64[nvec][nsw]: SUMM (bit w: word w of the class vector != 0)
+  uint32_t pbase;          // {u64 PM, u32 PBASE, u32 0}[nvec][nsw]: PM bit w = word w partial,
+                           // PBASE = first PART index of the class's block; the candidate
+                           // tables start here (the LDS prefix limit when the image does not fit)
   uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
   uint32_t part_wide;
   uint32_t part_direct;    // PART holds the partial words themselves (u64), not POOL indices

@@ -483,23 +483,27 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     lay.meta = blob.add(meta);
     img.meta_entries = static_cast<uint32_t>(meta.size());
   }
-  // Per class and 64-word block: SUMM (bit w: word w != 0), FULL (bit w: word w
-  // holds every rule of its word) and the PART array of the remaining
-  // "partial" words, stored in word order from PBASE (rank = popcount below w).
+  // Per class and 64-word block: SUMM (bit w: word w != 0), read by every
+  // packet's summary AND, and the candidate record {PM, PBASE}: PM (bit w:
+  // word w is partial -- neither zero nor every rule of its word) and the
+  // start of the class's partial words in PART, stored in word order (rank =
+  // popcount of PM below w).  At a candidate word every field's SUMM bit is
+  // set, so PM alone tells partial from FULL there, and one 16-byte read
+  // serves a field of the candidate stage.
   const auto &vecs = pool.vecs();
   img.nvec = static_cast<uint32_t>(vecs.size());
   const size_t nrec = size_t(img.nvec) * img.nsw;
-  std::vector<uint64_t> sf(2 * nrec, 0), words{~uint64_t(0)};   // {SUMM, FULL} per record
-  std::vector<uint32_t> pbase(nrec, 0), part;
+  std::vector<uint64_t> summ(nrec, 0), words{~uint64_t(0)};
+  std::vector<uint32_t> cand(4 * nrec, 0), part;                 // {PM lo, PM hi, PBASE, 0} per record
   std::map<uint64_t, uint32_t> word_id{{~uint64_t(0), 0}};
   for (uint32_t v = 0; v < img.nvec; ++v) {
     for (uint32_t w = 0; w < img.nrw; ++w) {
       const size_t rec = size_t(v) * img.nsw + w / 64;
-      if (w % 64 == 0) pbase[rec] = static_cast<uint32_t>(part.size());
+      if (w % 64 == 0) cand[4 * rec + 2] = static_cast<uint32_t>(part.size());
       const uint64_t x = vecs[v][w];
-      if (x) sf[2 * rec] |= uint64_t(1) << (w % 64);
-      if (x == perm.valid[w]) sf[2 * rec + 1] |= uint64_t(1) << (w % 64);
-      else if (x) {
+      if (x) summ[rec] |= uint64_t(1) << (w % 64);
+      if (x && x != perm.valid[w]) {
+        cand[4 * rec + (w % 64) / 32] |= uint32_t(1) << (w % 32);
         auto it = word_id.emplace(x, static_cast<uint32_t>(words.size())).first;
         if (it->second == words.size()) words.push_back(x);
         part.push_back(it->second);
@@ -507,8 +511,8 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     }
   }
   img.part_words = static_cast<uint32_t>(part.size());
-  lay.sf = blob.add(sf);
-  lay.pbase = blob.add(pbase);
+  lay.sf = blob.add(summ);
+  lay.pbase = blob.add(cand);
   // Partial words stored directly (one dependent LDS read less per field in
   // the candidate stage) while the whole image stays within kDirectMaxBytes.
   const size_t direct_bytes = blob.bytes.size() + part.size() * 8 + perm.perm.size() * 2 + 4 * kAlign;

@@ -107,18 +107,17 @@ class ImageModel:
             m = (1 << 64) - 1 if live >= 64 else (1 << live) - 1
             recs = [c * self.nsw + k for c in cls]
             for r in recs:
-                m &= self.u64(L["sf"] + 16 * r)
+                m &= self.u64(L["sf"] + 8 * r)
             while m:
                 bit = (m & -m).bit_length() - 1
                 m &= m - 1
                 acc = (1 << 64) - 1
                 for r in recs:
-                    fm = self.u64(L["sf"] + 16 * r + 8)
-                    if fm >> bit & 1:
-                        continue
-                    part = self.u64(L["sf"] + 16 * r) & ~fm
+                    part = self.u64(L["pbase"] + 16 * r)        # PM: partial words
+                    if not part >> bit & 1:
+                        continue                                  # FULL at this word
                     rank = bin(part & ((1 << bit) - 1)).count("1")
-                    j = self.u32(L["pbase"] + 4 * r) + rank
+                    j = self.u32(L["pbase"] + 16 * r + 8) + rank
                     if L["part_direct"]:
                         acc &= self.u64(L["part"] + 8 * j)
                         continue
