@@ -51,6 +51,11 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 #ifndef PCN_FLUSH_ROT
 #define PCN_FLUSH_ROT 1  // per-workgroup rotation of the counter flush order
 #endif
+#ifndef PCN_CAND_PRIO
+#define PCN_CAND_PRIO 1  // s_setprio of a wave in the candidate stage (-1: leave it); a wave there
+                         // holds LDS state the others' memory waits do not need (A/B: -2 % / -4.5 %
+                         // at hit rate 0.5 / 1, profiles/r01_ab17_cand_prio.log)
+#endif
 #ifndef PCN_STAGE_FAST
 #define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
 #endif
@@ -434,7 +439,10 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
   uint32_t cls[NS];
   bool need = false;
   if (mine) need = chain_classes<LDS, NS>(ch, p, port, cls, verdict, rid);
+  // the wave gets issue priority while it deals candidates through LDS
+  if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(PCN_CAND_PRIO >= 0 ? PCN_CAND_PRIO : 0);
   const uint32_t best = chain_candidates<LDS, NS>(ch, need, cls, ws);
+  if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(0);
   if (need) verdict = chain_finish(ch, best, rid);
 }
 
