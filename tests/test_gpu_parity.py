@@ -380,3 +380,18 @@ def test_ingest_ring_parity(dev):
         ring.release(done)
     ring.close()
     assert_counters(o, ipt)
+
+
+@JIT
+def test_ragged_batch_sizes_fixed_stride(dev, jit):
+    """Batches that end inside a wave's 64-frame group and inside a workgroup's
+    row (the prefetch's clamped tail, lanes past n), from 1 frame up to more
+    than one grid stride, on the fixed-stride fast path."""
+    rs = synth.config_rules(3)
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=jit)
+    frames_all = synth.config_frames(3, 300_017, rs).reshape(-1)
+    for n in (1, 2, 63, 64, 65, 777, 1025, 4097, 65_553, 262_147, 300_017):
+        frames = frames_all[: n * 64]
+        assert_same(*run_both(o, ipt, dev, frames, n))
+    assert_counters(o, ipt)
+    assert_jit_used(ipt, jit)
