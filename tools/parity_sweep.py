@@ -1,0 +1,128 @@
+"""Randomised GPU-vs-oracle parity sweep (measurement/evidence tool, GPU box).
+
+Each trial draws a service (pcn-iptables, or pcn-firewall in one of its three
+conntrack modes), quirky rule sets for every chain, defaults, localip, a frame
+stride, edge-case frames, a direction, an attach point, optional per-frame
+labels and in_port, and whether chain programs run; it then compares verdicts,
+rule ids and every counter of the product library against the CPU oracle
+(tests/ helpers).  Runs trials until --seconds elapse and prints one JSON line
+per trial plus a summary; exits non-zero on the first mismatch.
+
+  python tools/parity_sweep.py --seconds 150 > gpurun_out/parity_sweep.log
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def trial(seed, torch, dev):
+    from oracle.ffi import Oracle
+    from polycube_amd import Firewall, Iptables, synth
+    from rulegen import PORTS, quirky_rules
+    rng = np.random.default_rng(seed)
+    fw_mode = int(rng.integers(-1, 3))           # -1: pcn-iptables, else firewall conntrack mode
+    jit = int(rng.choice([1, 1, -1]))
+    o = Oracle()
+    if fw_mode < 0:
+        ipt = Iptables(device=0, jit=jit)
+        chains = (0, 1, 2)
+        localip = [synth.ip_nbo(int(x)) for x in rng.integers(0, 2**32, size=int(rng.integers(0, 6)))]
+        localip += [synth.ip_nbo((10 << 24) | (k << 16) | k) for k in range(int(rng.integers(0, 4)))]
+        for name, idx in PORTS.items():
+            o.add_port(name, idx)
+            ipt.add_port(name, idx)
+        o.set_localip(localip)
+        ipt.set_localip(localip)
+    else:
+        ipt = Firewall(device=0, jit=jit)
+        o.set_service(1, fw_mode)
+        if fw_mode == 0:
+            ipt.conntrack = "OFF"
+        elif fw_mode == 1:
+            ipt.accept_established = "OFF"
+        chains = (1, 2)
+    ipt.interactive = False
+    nrules = {}
+    for c in chains:
+        rules = quirky_rules(int(rng.integers(0, 260)), seed * 7 + c, ct=fw_mode != 0, ifaces=fw_mode < 0)
+        if fw_mode >= 0:
+            for r in rules:
+                r.setdefault("action", "DROP")
+        if rng.random() < 0.15:
+            rules = []
+        d = "DROP" if rng.random() < 0.5 else "ACCEPT"
+        o.set_chain(c, rules, d)
+        if fw_mode < 0:
+            o.apply_accept_established(c)
+        ch = ipt.chain(c)
+        for r in rules:
+            ch.append(**r)
+        ch.default = d
+        ch.apply_rules()
+        nrules[c] = len(rules)
+    stride = int(rng.choice([64, 96, 128]))
+    n = int(rng.integers(1, 1 << 15))
+    frames, lens = synth.fuzz_frames(n, seed, synth.make_rules(64, seed, protos=(6, 17, 1)), stride=stride)
+    frames = frames.reshape(-1)
+    fixed = rng.random() < 0.4                    # fixed-length frames: the fixed-stride fast path
+    hook = int(rng.random() < 0.25) if not fixed else 0
+    direction = int(rng.integers(0, 2))
+    ct = rng.integers(0, 5, size=n).astype(np.uint8) if rng.random() < 0.4 else None
+    in_port = rng.choice(np.array([0, 1, 2, 3, 0xFFFF], np.uint16), size=n) if rng.random() < 0.5 else None
+    kw = dict(stride=stride, direction=direction, hook=hook)
+    if fixed:
+        kw["fixed_len"] = stride
+    v_o, r_o = o.classify(frames, n=n, lens=None if fixed else lens, in_port=in_port, ct_status=ct,
+                          nthreads=min(16, os.cpu_count() or 1), **kw)
+
+    def t(a, dt=None):
+        return None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(dt) if dt else a).to(dev)
+    v_g, r_g = ipt.classify(t(frames), n=n, lens=None if fixed else t(lens, np.int16), in_port=t(in_port, np.int16),
+                            ct_status=t(ct), **kw)
+    torch.cuda.synchronize()
+    v_g, r_g = v_g.cpu().numpy(), r_g.cpu().numpy()
+    bad = int(np.count_nonzero((v_o != v_g) | (r_o != r_g)))
+    ctr_ok = True
+    for c in chains:
+        a = o.read_counters(c, 8000)
+        b = ipt.chain(c).read_counters(8000)
+        ctr_ok &= tuple(a) == tuple(b)
+    info = ipt.jit_info()
+    ipt.close()
+    return {"seed": seed, "service": "iptables" if fw_mode < 0 else f"firewall/ct{fw_mode}", "jit": jit,
+            "chain_program": info["launches_jit"] > 0, "rules": nrules, "n": n, "stride": stride, "fixed": fixed,
+            "hook": hook, "direction": direction, "labels": ct is not None, "in_port": in_port is not None,
+            "mismatches": bad, "counters_equal": bool(ctr_ok)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=120)
+    ap.add_argument("--seed0", type=int, default=1000)
+    a = ap.parse_args()
+    import torch
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    k = 0
+    ok = 0
+    while time.time() - t0 < a.seconds:
+        r = trial(a.seed0 + k, torch, dev)
+        print(json.dumps(r), flush=True)
+        k += 1
+        if r["mismatches"] or not r["counters_equal"]:
+            print(json.dumps({"summary": "MISMATCH", "trials": k}), flush=True)
+            sys.exit(1)
+        ok += 1
+    print(json.dumps({"summary": "all equal", "trials": k, "seconds": round(time.time() - t0, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
