@@ -189,6 +189,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "PCN_BENCH_DEVICE" in os.environ:   # test hook: several ranks on one GPU (RCCL refuses that)
+        local = int(os.environ["PCN_BENCH_DEVICE"])
     if world > 1:
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
@@ -209,10 +211,22 @@ def main():
         fw.append(**r)
     fw.default = "DROP"
     fw.apply_rules()
+    collective = "RCCL all-gather of the per-rule counter blocks (pcn_ipt_sync_counters)"
+    use_rccl = world > 1
     if world > 1:
         uid = [Iptables.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ipt.comm_init(world, rank, uid[0])
+        err = ""
+        try:
+            ipt.comm_init(world, rank, uid[0])
+        except Exception as e:           # keep the scaling line, say how it was made
+            err = str(e)
+        ok = torch.tensor([0 if err else 1])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        use_rccl = bool(ok.item())
+        if not use_rccl:
+            collective = f"gloo all-reduce of the counter block on the host (RCCL init failed: {err[:160]})"
+            log(f"[rank {rank}] {collective}")
 
     t = time.perf_counter()
     offsets_host = lens_host = None
@@ -233,10 +247,19 @@ def main():
         ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=rid, offsets=offsets, lens=lens, stream=s_ptr,
                      hook=hook)
 
+    def exchange():
+        if world == 1:
+            return
+        if use_rccl:
+            ipt.sync_counters(s_ptr)
+        else:   # fallback: the same per-step exchange through the host
+            pk, by, dp, db = fw.read_counters(len(rules))
+            blk = torch.tensor([dp, db] + pk + by, dtype=torch.int64)
+            dist.all_reduce(blk)
+
     def step():
         classify()
-        if world > 1:
-            ipt.sync_counters(s_ptr)
+        exchange()
 
     for _ in range(args.warmup):
         step()
@@ -250,8 +273,7 @@ def main():
         ev[k][0].record(stream)
         classify()
         ev[k][1].record(stream)
-        if world > 1:
-            ipt.sync_counters(s_ptr)
+        exchange()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -291,7 +313,8 @@ def main():
             "data": "synthetic (seeded synth.config_rules(3) + make_headers; no captured traffic)",
             "config": {"workload": WORKLOADS[cfg] + (", TC hook" if hook else ""),
                        "rules": len(rules), "frames_per_gpu": n, "frame_bytes": 64,
-                       "parallelism": f"dp{world} (packet-index shards, RCCL counter all-gather)"},
+                       "parallelism": f"dp{world} (packet-index shards, RCCL counter all-gather)",
+                       "collective": collective if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kernel, "kernel_ms": round(kern_ms, 4),
