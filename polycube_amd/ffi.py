@@ -82,6 +82,8 @@ class CtInfo(C.Structure):
 
 
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
+ABI_VERSION = 3            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
+
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
     "pcn_ipt_last_error": (C.c_char_p, []),
@@ -161,6 +163,8 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
+        if h.pcn_ipt_abi_version() != ABI_VERSION:   # a stale build would mis-read the structs
+            raise LibraryMissing(f"{LIB_PATH} has ABI {h.pcn_ipt_abi_version()}, this binding expects {ABI_VERSION}: rebuild")
         _lib = h
     return _lib
 
