@@ -103,10 +103,69 @@ def trial(seed, torch, dev):
             "mismatches": bad, "counters_equal": bool(ctr_ok)}
 
 
+def stateful_trial(seed, torch, dev):
+    """The connection table on both sides: random service, chain with or
+    without conntrack rules, interleaved flows in 2-4 batches of random
+    direction; verdicts, rule ids, counters and the whole session table."""
+    from oracle.ffi import Oracle
+    from polycube_amd import Firewall, Iptables, synth
+    rng = np.random.default_rng(seed)
+    fw_mode = int(rng.choice([-1, 1, 2]))
+    now = 1_700_000_000_000_000_000 + int(rng.integers(0, 10**9))
+    rs = synth.config_rules(2, seed=seed)
+    base = [dict(r, action=r.get("action", "DROP")) for r in rs.rules()][: int(rng.integers(1, 128))]
+    ct_rules = [{"conntrack": "ESTABLISHED", "action": "ACCEPT"}, {"conntrack": "NEW", "action": "ACCEPT"},
+                {"conntrack": "INVALID", "action": "DROP"}]
+    rules = (ct_rules[int(rng.integers(0, 2)):] if rng.random() < 0.6 else []) + base
+    o = Oracle()
+    ipt = Iptables(device=0, jit=1) if fw_mode < 0 else Firewall(device=0, jit=1)
+    chain = 1
+    if fw_mode >= 0:
+        o.set_service(1, fw_mode)
+        if fw_mode == 1:
+            ipt.accept_established = "OFF"
+    ipt.interactive = False
+    d = "DROP" if rng.random() < 0.5 else "ACCEPT"
+    o.set_chain(chain, rules, d)
+    if fw_mode < 0:
+        o.apply_accept_established(chain)
+    ch = ipt.chain(chain)
+    for r in rules:
+        ch.append(**r)
+    ch.default = d
+    ch.apply_rules()
+    o.ct_enable()
+    o.ct_set_time(now)
+    ipt.ct_enable(16)
+    ipt.ct_set_time(now)
+    n = int(rng.integers(1000, 20000))
+    f, lens = synth.flow_traffic(n, int(rng.integers(10, 2000)), seed, stride=128, rs=rs, lens_mode="mixed",
+                                 p_noise=0.1, p_err=0.05)
+    cuts = sorted(set([0, n] + [int(x) for x in rng.integers(1, n, size=int(rng.integers(1, 4)))]))
+    bad = 0
+    for lo, hi in zip(cuts, cuts[1:]):
+        direction = int(rng.integers(0, 2))
+        fr = np.ascontiguousarray(f[lo * 128:hi * 128])
+        v_o, r_o = o.classify(fr, n=hi - lo, lens=lens[lo:hi], stride=128, fixed_len=128, direction=direction)
+        v_g, r_g = ipt.classify(torch.from_numpy(fr).to(dev), n=hi - lo,
+                                lens=torch.from_numpy(lens[lo:hi].view(np.int16)).to(dev), stride=128,
+                                fixed_len=128, direction=direction)
+        torch.cuda.synchronize()
+        bad += int(np.count_nonzero((v_o != v_g.cpu().numpy()) | (r_o != r_g.cpu().numpy())))
+    a, b = o.ct_dump(), ipt.ct_dump()
+    tables = len(a) == len(b) and all(np.array_equal(a[k], b[k]) for k in a.dtype.names)
+    ctr_ok = tuple(o.read_counters(chain, len(rules) + 1)) == tuple(ch.read_counters(len(rules) + 1))
+    ipt.close()
+    return {"seed": seed, "stateful": True, "service": "iptables" if fw_mode < 0 else f"firewall/ct{fw_mode}",
+            "rules": len(rules), "n": n, "batches": len(cuts) - 1, "live_entries": int(len(a)),
+            "mismatches": bad, "counters_equal": bool(ctr_ok and tables), "tables_equal": bool(tables)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--seed0", type=int, default=1000)
+    ap.add_argument("--stateful", action="store_true", help="connection-table trials")
     a = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -114,7 +173,7 @@ def main():
     k = 0
     ok = 0
     while time.time() - t0 < a.seconds:
-        r = trial(a.seed0 + k, torch, dev)
+        r = (stateful_trial if a.stateful else trial)(a.seed0 + k, torch, dev)
         print(json.dumps(r), flush=True)
         k += 1
         if r["mismatches"] or not r["counters_equal"]:
