@@ -166,13 +166,18 @@ def main():
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--seed0", type=int, default=1000)
     ap.add_argument("--stateful", action="store_true", help="connection-table trials")
+    ap.add_argument("--lib", default="", help="another build of the product library (A/B)")
+    ap.add_argument("--trials", type=int, default=0, help="stop after this many trials (0: --seconds)")
     a = ap.parse_args()
     import torch
+    if a.lib:
+        from polycube_amd import ffi
+        ffi.LIB_PATH = a.lib
     dev = torch.device("cuda", 0)
     t0 = time.time()
     k = 0
     ok = 0
-    while time.time() - t0 < a.seconds:
+    while time.time() - t0 < a.seconds and (not a.trials or k < a.trials):
         r = (stateful_trial if a.stateful else trial)(a.seed0 + k, torch, dev)
         print(json.dumps(r), flush=True)
         k += 1
