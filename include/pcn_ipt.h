@@ -366,6 +366,29 @@ int pcn_ipt_comm_init(pcn_ipt *ctx, int nranks, int rank, const uint8_t uid[128]
  * into the scope=1 view.  Stream-ordered. */
 int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream);
 
+/* Flow-affinity split for stateful conntrack on N GPUs.  Replaces the NIC's
+ * RSS queue choice that spreads traffic over the reference's per-CPU datapath
+ * (polycubed/src/extiface_xdp.cpp:178-200 runs handle_rx on the receiving
+ * CPU; the Parser's `packet` struct is per CPU, Iptables_Parser_dp.c:45).
+ * The owner of a frame is a hash of its unordered IPv4 address pair (for an
+ * ICMP error >= 70 B, of the quoted header's pair, whose connection it
+ * labels, Iptables_ConntrackLabel_dp.c:491-529); non-IPv4 and frames the
+ * Parser drops belong to rank 0.  All packets of one connection therefore
+ * meet one connection table, in batch order.  Uses the batch's frames,
+ * frames_bytes, offsets, lens, stride, fixed_len, in_port, const_in_port,
+ * hook and n; the other fields are ignored.  1 <= nranks <= 255.
+ *
+ * pcn_ipt_flow_owner: owner[i] (device, n bytes) for every frame.
+ * pcn_ipt_flow_split: this rank's frames in batch order: index[k] (the frame's
+ * position in the batch), offsets[k], lens[k] and, if in_port_out is not
+ * NULL, in_port_out[k] — device arrays of capacity n, ready to be passed as a
+ * pcn_ipt_batch's offsets/lens/in_port.  *n_out (host) = the number of owned
+ * frames; synchronises the stream to read it.  offsets are u32: a fixed-stride
+ * batch must end below 4 GiB. */
+int pcn_ipt_flow_owner(pcn_ipt *ctx, const pcn_ipt_batch *batch, uint32_t nranks, uint8_t *owner, void *stream);
+int pcn_ipt_flow_split(pcn_ipt *ctx, const pcn_ipt_batch *batch, uint32_t nranks, uint32_t rank, uint32_t *index,
+                       uint32_t *offsets, uint16_t *lens, uint16_t *in_port_out, uint64_t *n_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

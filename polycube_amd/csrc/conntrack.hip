@@ -855,4 +855,105 @@ int ct_ae_fixup(const CtBatch &b, void *stream) {
   return int(hipGetLastError());
 }
 
+// ---- flow-affinity split (pcn_ipt_flow_owner / pcn_ipt_flow_split) ---------
+// The GPU analogue of the NIC's RSS queue choice in front of the reference's
+// per-CPU datapath: every packet of a connection goes to one owner, so each
+// owner's connection table and Parser state (the per-CPU `packet` struct,
+// Iptables_Parser_dp.c:27-37, quirk Q4) see that connection's packets in
+// batch order.  The owner hashes the *unordered* IPv4 address pair, which is
+// the part of the conntrack key (ConntrackLabel_dp.c:200-228) that is the
+// packet's own for every kind: an ICMP error is owned by the connection it
+// quotes (its key, :491-529), so RELATED finds the table that holds it.
+namespace {
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t flow_owner_of(const CtBatch &b, uint64_t i, uint32_t nranks) {
+  uint32_t w[18], L;
+  load_window(b, i, w, L);
+  const Parsed p = parse(w, L, b.hook);
+  if (p.status != 2) return 0;                      // dropped by the Parser or not IPv4: no state
+  uint32_t a = p.src, c = p.dst;
+  const bool icmp_err = p.proto == 1 && p.L >= 70 && p.icmp != 0 && p.icmp != 8 && !(p.icmp >= 13 && p.icmp <= 18);
+  if (icmp_err) { a = p.isrc; c = p.idst; }
+  const uint32_t lo = a < c ? a : c, hi = a < c ? c : a;
+  const uint32_t h = fmix32(fmix32(lo ^ 0x9e3779b9u) ^ hi);
+  return static_cast<uint32_t>((uint64_t(h) * nranks) >> 32);
+}
+
+__global__ void flow_owner_kernel(CtBatch b, uint32_t nranks, uint8_t *owner) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < b.n; i += uint64_t(gridDim.x) * blockDim.x)
+    owner[i] = static_cast<uint8_t>(flow_owner_of(b, i, nranks));
+}
+
+__global__ void flow_flag_kernel(CtBatch b, uint32_t nranks, uint32_t rank, uint8_t *flag) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < b.n; i += uint64_t(gridDim.x) * blockDim.x)
+    flag[i] = flow_owner_of(b, i, nranks) == rank;
+}
+
+// Owned frames as an offsets/lens/in_port batch, in batch order.
+__global__ void flow_gather_kernel(CtBatch b, const uint16_t *in_port, uint16_t const_in_port, const uint32_t *index,
+                                   const uint32_t *count, uint32_t *offsets, uint16_t *lens, uint16_t *in_port_out) {
+  const uint32_t m = *count;
+  for (uint64_t k = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; k < m; k += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t i = index[k];
+    offsets[k] = b.offsets ? b.offsets[i] : static_cast<uint32_t>(uint64_t(i) * b.stride);
+    lens[k] = b.lens ? b.lens[i] : static_cast<uint16_t>(b.fixed_len);
+    if (in_port_out) in_port_out[k] = in_port ? in_port[i] : const_in_port;
+  }
+}
+
+}  // namespace
+
+int ct_flow_owner(const CtBatch &b, uint32_t nranks, uint8_t *owner, int num_cus, void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!b.n) return 0;
+  hipLaunchKernelGGL(flow_owner_kernel, dim3(grid_for(b.n, 256, num_cus)), dim3(256), 0, st, b, nranks, owner);
+  return int(hipGetLastError());
+}
+
+int ct_flow_split(const CtBatch &b, const uint16_t *in_port, uint16_t const_in_port, uint32_t nranks, uint32_t rank,
+                  uint32_t *index, uint32_t *offsets, uint16_t *lens, uint16_t *in_port_out, uint64_t *n_out,
+                  int num_cus, void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  *n_out = 0;
+  if (!b.n) return 0;
+  const int n = static_cast<int>(b.n);
+  size_t tb = 0;
+  CT_CHECK(hipcub::DeviceSelect::Flagged(nullptr, tb, hipcub::CountingInputIterator<uint32_t>(0),
+                                         static_cast<const uint8_t *>(nullptr), index,
+                                         static_cast<uint32_t *>(nullptr), n, st));
+  const size_t head = (b.n + 255) / 256 * 256;      // flags, then the selected count, then cub's temp
+  uint8_t *buf = nullptr;
+  CT_CHECK(hipMallocAsync(reinterpret_cast<void **>(&buf), head + 256 + tb, st));
+  uint8_t *flag = buf;
+  uint32_t *count = reinterpret_cast<uint32_t *>(buf + head);
+  void *temp = buf + head + 256;
+  const unsigned grid = grid_for(b.n, 256, num_cus);
+  hipLaunchKernelGGL(flow_flag_kernel, dim3(grid), dim3(256), 0, st, b, nranks, rank, flag);
+  int e = int(hipGetLastError());
+  if (e == hipSuccess)
+    e = int(hipcub::DeviceSelect::Flagged(temp, tb, hipcub::CountingInputIterator<uint32_t>(0), flag, index, count,
+                                          n, st));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(flow_gather_kernel, dim3(grid), dim3(256), 0, st, b, in_port, const_in_port, index, count,
+                       offsets, lens, in_port_out);
+    e = int(hipGetLastError());
+  }
+  uint32_t m = 0;
+  if (e == hipSuccess) e = int(hipMemcpyAsync(&m, count, 4, hipMemcpyDeviceToHost, st));
+  const int f = int(hipFreeAsync(buf, st));
+  if (e == hipSuccess) e = int(hipStreamSynchronize(st));
+  if (e == hipSuccess) e = f;
+  if (e == hipSuccess) *n_out = m;
+  return e;
+}
+
 }  // namespace pcn

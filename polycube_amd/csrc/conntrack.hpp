@@ -83,6 +83,15 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
 // before the chain runs.  rule_ids may be null.
 int ct_ae_fixup(const CtBatch &b, void *stream);
 
+// Flow-affinity split (pcn_ipt_flow_owner / pcn_ipt_flow_split): the owner
+// rank of every frame, from its unordered IPv4 address pair (an ICMP error's
+// quoted pair); the split compacts this rank's frames, in batch order, into
+// offsets/lens/in_port arrays and synchronises the stream for the count.
+int ct_flow_owner(const CtBatch &b, uint32_t nranks, uint8_t *owner, int num_cus, void *stream);
+int ct_flow_split(const CtBatch &b, const uint16_t *in_port, uint16_t const_in_port, uint32_t nranks, uint32_t rank,
+                  uint32_t *index, uint32_t *offsets, uint16_t *lens, uint16_t *in_port_out, uint64_t *n_out,
+                  int num_cus, void *stream);
+
 int ct_table_init(CtTable &t, uint32_t cap_log2);
 void ct_table_free(CtTable &t);
 

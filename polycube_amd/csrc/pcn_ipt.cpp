@@ -1253,5 +1253,47 @@ int pcn_fw_chain_update(pcn_ipt *ctx, int chain, uint32_t id, const pcn_ipt_rule
   });
 }
 
+
+static int flow_args(pcn_ipt *ctx, const pcn_ipt_batch *b, uint32_t nranks) {
+  if (!b) return fail(-EINVAL, "null batch");
+  if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
+  if (nranks < 1 || nranks > 255) return fail(-EINVAL, "nranks must be 1..255");
+  if (b->n && !b->frames) return fail(-EINVAL, "frames are required");
+  if (b->n > 0xffffffffull) return fail(-EINVAL, "at most 2^32-1 frames per batch");
+  if (b->hook != PCN_IPT_HOOK_XDP && b->hook != PCN_IPT_HOOK_TC) return fail(-EINVAL, "unknown hook");
+  return 0;
+}
+
+int pcn_ipt_flow_owner(pcn_ipt *ctx, const pcn_ipt_batch *b, uint32_t nranks, uint8_t *owner, void *stream) {
+  return guarded(ctx, [&] {
+    if (int rc = flow_args(ctx, b, nranks)) return rc;
+    if (b->n && !owner) return fail(-EINVAL, "owner is required");
+    device_guard(ctx);
+    const int e = ct_flow_owner(ct_batch(ctx, b, 0), nranks, owner, ctx->num_cus, stream);
+    if (e != hipSuccess) return fail(-EIO, std::string("flow owner: ") + hipGetErrorString(hipError_t(e)));
+    return 0;
+  });
+}
+
+int pcn_ipt_flow_split(pcn_ipt *ctx, const pcn_ipt_batch *b, uint32_t nranks, uint32_t rank, uint32_t *index,
+                       uint32_t *offsets, uint16_t *lens, uint16_t *in_port_out, uint64_t *n_out, void *stream) {
+  return guarded(ctx, [&] {
+    if (int rc = flow_args(ctx, b, nranks)) return rc;
+    if (rank >= nranks) return fail(-EINVAL, "rank must be < nranks");
+    if (!n_out) return fail(-EINVAL, "n_out is required");
+    *n_out = 0;
+    if (!b->n) return 0;
+    if (!index || !offsets || !lens) return fail(-EINVAL, "index, offsets and lens are required");
+    if (!b->offsets && (b->n - 1) * uint64_t(b->stride) > 0xffffffffull)
+      return fail(-EINVAL, "a fixed-stride batch must end below 4 GiB (offsets are u32)");
+    if (!b->lens && b->fixed_len > 0xffff) return fail(-EINVAL, "fixed_len must fit u16");
+    device_guard(ctx);
+    const int e = ct_flow_split(ct_batch(ctx, b, 0), b->in_port, b->const_in_port, nranks, rank, index, offsets,
+                                lens, in_port_out, n_out, ctx->num_cus, stream);
+    if (e != hipSuccess) return fail(-EIO, std::string("flow split: ") + hipGetErrorString(hipError_t(e)));
+    return 0;
+  });
+}
+
 }  // extern "C"
 

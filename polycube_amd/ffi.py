@@ -129,6 +129,9 @@ SIGNATURES = {
     "pcn_ipt_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "pcn_ipt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     "pcn_ipt_sync_counters": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pcn_ipt_flow_owner": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_uint32, C.c_void_p, C.c_void_p]),
+    "pcn_ipt_flow_split": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]),
     "pcn_ipt_ct_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pcn_ipt_ct_disable": (C.c_int, [C.c_void_p]),
     "pcn_ipt_ct_clear": (C.c_int, [C.c_void_p]),

@@ -291,6 +291,44 @@ class Iptables:
     def sync_counters(self, stream=None):
         _check(ffi.lib().pcn_ipt_sync_counters(self._h, stream))
 
+    # ---- flow-affinity split (stateful conntrack on N GPUs) ----
+    @staticmethod
+    def _frames_batch(frames, n, offsets, lens, stride, fixed_len, in_port, const_in_port, hook):
+        def p(t):
+            return None if t is None else t.data_ptr()
+        if n is None:
+            n = offsets.numel() if offsets is not None else frames.numel() // stride
+        return n, ffi.Batch(frames.data_ptr(), frames.numel(), p(offsets), p(lens), stride, fixed_len, p(in_port),
+                            const_in_port, INGRESS, hook, 0, None, n, None, None)
+
+    def flow_owner(self, frames, nranks, n=None, offsets=None, lens=None, stride=64, fixed_len=64, hook=XDP,
+                   stream=None):
+        """Owner rank of every frame (pcn_ipt_flow_owner): a uint8 tensor on the frames' device."""
+        import torch
+        n, b = self._frames_batch(frames, n, offsets, lens, stride, fixed_len, None, 1, hook)
+        owner = torch.empty(n, dtype=torch.uint8, device=frames.device)
+        s = stream if stream is not None else torch.cuda.current_stream(frames.device).cuda_stream
+        _check(ffi.lib().pcn_ipt_flow_owner(self._h, C.byref(b), nranks, owner.data_ptr(), s))
+        return owner
+
+    def flow_split(self, frames, nranks, rank, n=None, offsets=None, lens=None, stride=64, fixed_len=64,
+                   in_port=None, const_in_port=1, hook=XDP, stream=None):
+        """This rank's frames in batch order (pcn_ipt_flow_split): returns (index, offsets, lens,
+        in_port) tensors of the owned count, ready for classify(frames, offsets=, lens=, in_port=)."""
+        import torch
+        n, b = self._frames_batch(frames, n, offsets, lens, stride, fixed_len, in_port, const_in_port, hook)
+        dev = frames.device
+        index = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        offs = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        ls = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
+        ports = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
+        m = C.c_uint64(0)
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        _check(ffi.lib().pcn_ipt_flow_split(self._h, C.byref(b), nranks, rank, index.data_ptr(), offs.data_ptr(),
+                                            ls.data_ptr(), ports.data_ptr(), C.byref(m), s))
+        k = m.value
+        return index[:k], offs[:k], ls[:k], ports[:k]
+
 
 class IngestRing:
     """Pinned host slots feeding the GPU classifier (include/pcn_ipt.h, ring).
