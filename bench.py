@@ -131,8 +131,26 @@ def ct_rate(ipt, rs, n, dev, steps=5, warmup=2, flows=1 << 16, seed=0xC7):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     live = len(ipt.ct_dump())
+    # flow-affinity split (pcn_ipt_flow_split) of the same batch over 8 tables,
+    # and the owned share's stateful classify on a fresh table
+    ipt.ct_clear()
+    split = ipt.flow_split(frames, 8, 0, n=n, stride=64)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        split = ipt.flow_split(frames, 8, 0, n=n, stride=64)
+    split_ms = (time.perf_counter() - t0) / steps * 1e3
+    idx, offs, lens, ports = split
+    m = idx.numel()
+    ipt.classify(frames, n=m, verdicts=verdicts, offsets=offs, lens=lens, in_port=ports, stream=stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ipt.classify(frames, n=m, verdicts=verdicts, offsets=offs, lens=lens, in_port=ports, stream=stream)
+    torch.cuda.synchronize()
+    share_ms = (time.perf_counter() - t0) / steps * 1e3
     ipt.ct_disable()
-    return n * steps / el / 1e6, el / steps * 1e3, live
+    return n * steps / el / 1e6, el / steps * 1e3, live, {"split_ms": round(split_ms, 3), "share_frames": m,
+                                                           "share_ms": round(share_ms, 3)}
 
 
 def fw_rate(rules, frames, n, dev, s_ptr, jit, steps=20):
@@ -341,9 +359,12 @@ def main():
                 "what": "the same rules and frames through the pcn-firewall personality (pcn_ipt_set_service): "
                         "INGRESS chain, conntrack OFF"}
         if world == 1 and not args.no_ct and cfg == 3:
-            rate, ms, live = ct_rate(ipt, rs, n, dev)
+            rate, ms, live, shard = ct_rate(ipt, rs, n, dev)
             line["stateful_conntrack"] = {
                 "value": round(rate, 2), "unit": "Mpkt/s", "ms_per_step": round(ms, 3),
+                "flow_split_8": dict(shard, what="pcn_ipt_flow_split of the whole batch for rank 0 of 8 (split_ms, "
+                                                 "incl. its count read-back), then rank 0's owned frames through "
+                                                 "its own fresh connection table (share_ms)"),
                 "what": f"same chain with the connection table on (pcn_ipt_ct_enable): 2^{args.log2n} 64B frames of "
                         f"2^16 interleaved flows, labels from and updates to the HBM table in batch order "
                         f"({live} live entries after the run)"}

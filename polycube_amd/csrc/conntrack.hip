@@ -875,27 +875,74 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   return h;
 }
 
-__device__ __forceinline__ uint32_t flow_owner_of(const CtBatch &b, uint64_t i, uint32_t nranks) {
-  uint32_t w[18], L;
-  load_window(b, i, w, L);
-  const Parsed p = parse(w, L, b.hook);
-  if (p.status != 2) return 0;                      // dropped by the Parser or not IPv4: no state
-  uint32_t a = p.src, c = p.dst;
-  const bool icmp_err = p.proto == 1 && p.L >= 70 && p.icmp != 0 && p.icmp != 8 && !(p.icmp >= 13 && p.icmp <= 18);
-  if (icmp_err) { a = p.isrc; c = p.idst; }
+// Reads only the dwords the owner needs (bytes 12-35, and 52-63 of an ICMP
+// error), not parse()'s 72-byte window.  Same field rules as parse()
+// (Iptables_Parser_dp.c:94-153, the TC untag).  `vec`: the launch is a
+// 16-byte aligned fixed-stride batch whose first 48 bytes of every frame lie
+// inside the buffer, read as three 16-byte loads per lane (the scattered
+// dword loads run at ~2.4 TB/s on 64-byte frames, limited by requests).
+__device__ __forceinline__ uint32_t flow_owner_of(const CtBatch &b, uint64_t i, uint32_t nranks, bool vec) {
+  const uint64_t off = b.offsets ? b.offsets[i] : i * uint64_t(b.stride);
+  uint32_t L = b.lens ? b.lens[i] : b.fixed_len;
+  const uint64_t base = off & ~uint64_t(3);
+  const uint32_t sh = static_cast<uint32_t>(off & 3);
+  auto D = [&](uint32_t k) {
+    const uint64_t at = base + 4u * k;
+    return at + 4 <= b.frames_bytes ? *reinterpret_cast<const uint32_t *>(b.frames + at) : 0u;
+  };
+  uint32_t h12[12];
+  if (vec) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(b.frames + off);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint4 v = q[k];
+      h12[4 * k] = v.x; h12[4 * k + 1] = v.y; h12[4 * k + 2] = v.z; h12[4 * k + 3] = v.w;
+    }
+  }
+  uint32_t s = 0;
+  auto W = [&](uint32_t k) {
+    if (vec && k + s < 12) return h12[k + s];
+    return __builtin_amdgcn_alignbyte(D(k + s + 1), D(k + s), sh);
+  };
+  if (L < 14) return 0;
+  uint32_t et = ((W(3) & 0xff) << 8) | ((W(3) >> 8) & 0xff);
+  if (b.hook == PCN_IPT_HOOK_TC && (et == 0x8100 || et == 0x88A8)) {
+    if (L < 18) return 0;
+    s = 1;
+    L -= 4;
+    et = ((W(3) & 0xff) << 8) | ((W(3) >> 8) & 0xff);
+  }
+  if (et != 0x0800 || L < 34) return 0;            // not IPv4, or dropped by the Parser: no state
+  const uint32_t w5 = W(5), w7 = W(7);
+  const uint8_t proto = static_cast<uint8_t>(w5 >> 24);
+  if ((proto == 6 && L < 54) || (proto == 17 && L < 42)) return 0;
+  uint32_t a = (W(6) >> 16) | (w7 << 16), c = (w7 >> 16) | (W(8) << 16);
+  if (proto == 1 && L >= 70) {
+    const uint8_t icmp = static_cast<uint8_t>((W(8) >> 16) & 0xff);
+    if (icmp != 0 && icmp != 8 && !(icmp >= 13 && icmp <= 18)) {   // an error: its quoted pair
+      const uint32_t w14 = W(14);
+      a = (W(13) >> 16) | (w14 << 16);
+      c = (w14 >> 16) | (W(15) << 16);
+    }
+  }
   const uint32_t lo = a < c ? a : c, hi = a < c ? c : a;
   const uint32_t h = fmix32(fmix32(lo ^ 0x9e3779b9u) ^ hi);
   return static_cast<uint32_t>((uint64_t(h) * nranks) >> 32);
 }
 
-__global__ void flow_owner_kernel(CtBatch b, uint32_t nranks, uint8_t *owner) {
+__global__ void flow_owner_kernel(CtBatch b, uint32_t nranks, bool vec, uint8_t *owner) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < b.n; i += uint64_t(gridDim.x) * blockDim.x)
-    owner[i] = static_cast<uint8_t>(flow_owner_of(b, i, nranks));
+    owner[i] = static_cast<uint8_t>(flow_owner_of(b, i, nranks, vec));
 }
 
-__global__ void flow_flag_kernel(CtBatch b, uint32_t nranks, uint32_t rank, uint8_t *flag) {
+__global__ void flow_flag_kernel(CtBatch b, uint32_t nranks, uint32_t rank, bool vec, uint8_t *flag) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < b.n; i += uint64_t(gridDim.x) * blockDim.x)
-    flag[i] = flow_owner_of(b, i, nranks) == rank;
+    flag[i] = flow_owner_of(b, i, nranks, vec) == rank;
+}
+
+bool flow_vec(const CtBatch &b) {
+  return !b.offsets && b.stride % 16 == 0 && b.stride >= 48 && (reinterpret_cast<uintptr_t>(b.frames) % 16) == 0 &&
+         (b.n - 1) * uint64_t(b.stride) + 48 <= b.frames_bytes;
 }
 
 // Owned frames as an offsets/lens/in_port batch, in batch order.
@@ -915,7 +962,7 @@ __global__ void flow_gather_kernel(CtBatch b, const uint16_t *in_port, uint16_t 
 int ct_flow_owner(const CtBatch &b, uint32_t nranks, uint8_t *owner, int num_cus, void *stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!b.n) return 0;
-  hipLaunchKernelGGL(flow_owner_kernel, dim3(grid_for(b.n, 256, num_cus)), dim3(256), 0, st, b, nranks, owner);
+  hipLaunchKernelGGL(flow_owner_kernel, dim3(grid_for(b.n, 256, num_cus)), dim3(256), 0, st, b, nranks, flow_vec(b), owner);
   return int(hipGetLastError());
 }
 
@@ -937,7 +984,7 @@ int ct_flow_split(const CtBatch &b, const uint16_t *in_port, uint16_t const_in_p
   uint32_t *count = reinterpret_cast<uint32_t *>(buf + head);
   void *temp = buf + head + 256;
   const unsigned grid = grid_for(b.n, 256, num_cus);
-  hipLaunchKernelGGL(flow_flag_kernel, dim3(grid), dim3(256), 0, st, b, nranks, rank, flag);
+  hipLaunchKernelGGL(flow_flag_kernel, dim3(grid), dim3(256), 0, st, b, nranks, rank, flow_vec(b), flag);
   int e = int(hipGetLastError());
   if (e == hipSuccess)
     e = int(hipcub::DeviceSelect::Flagged(temp, tb, hipcub::CountingInputIterator<uint32_t>(0), flag, index, count,
