@@ -72,6 +72,19 @@ def test_ingest_ring_needs_a_device():
     ipt.close()
 
 
+def test_flow_split_needs_a_device_and_valid_ranks():
+    """pcn_ipt_flow_owner / pcn_ipt_flow_split argument checks (no GPU work is launched)."""
+    from polycube_amd import Iptables
+    ipt = Iptables(device=-1)
+    b = ffi.Batch(1, 64, None, None, 64, 64, None, 1, 0, 0, 0, None, 1, None, None)
+    m = C.c_uint64(7)
+    lib = ffi.lib()
+    assert lib.pcn_ipt_flow_owner(ipt._h, C.byref(b), 2, 1, None) == -19     # -ENODEV, no CPU fallback
+    assert lib.pcn_ipt_flow_split(ipt._h, C.byref(b), 2, 0, 1, 1, 1, None, C.byref(m), None) == -19
+    assert lib.pcn_ipt_flow_split(ipt._h, None, 2, 0, 1, 1, 1, None, C.byref(m), None) == -22
+    ipt.close()
+
+
 def test_null_context_is_an_error():
     assert ffi.lib().pcn_ipt_chain_flush(None, 0) < 0
     assert b"null" in ffi.lib().pcn_ipt_last_error()
