@@ -243,7 +243,8 @@ def main():
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         use_rccl = bool(ok.item())
         if not use_rccl:
-            collective = f"gloo all-reduce of the counter block on the host (RCCL init failed: {err[:160]})"
+            collective = (f"gloo all-reduce of the counter block on the host, timing stand-in: the sums are not "
+                          f"written back to the device counters (RCCL init failed: {err[:160]})")
             log(f"[rank {rank}] {collective}")
 
     t = time.perf_counter()
@@ -270,7 +271,7 @@ def main():
             return
         if use_rccl:
             ipt.sync_counters(s_ptr)
-        else:   # fallback: the same per-step exchange through the host
+        else:   # fallback, timing only: the same per-step exchange through the host, sums discarded
             pk, by, dp, db = fw.read_counters(len(rules))
             blk = torch.tensor([dp, db] + pk + by, dtype=torch.int64)
             dist.all_reduce(blk)
@@ -331,7 +332,9 @@ def main():
             "data": "synthetic (seeded synth.config_rules(3) + make_headers; no captured traffic)",
             "config": {"workload": WORKLOADS[cfg] + (", TC hook" if hook else ""),
                        "rules": len(rules), "frames_per_gpu": n, "frame_bytes": 64,
-                       "parallelism": f"dp{world} (packet-index shards, RCCL counter all-gather)",
+                       "parallelism": (f"dp{world} (packet-index shards, "
+                                       + ("RCCL counter all-gather)" if use_rccl else "host gloo counter all-reduce)")
+                                       if world > 1 else "dp1 (one packet shard, no exchange)"),
                        "collective": collective if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

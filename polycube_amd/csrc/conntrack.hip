@@ -681,10 +681,9 @@ __global__ void ae_move_kernel(CtBatch b) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   for (int c = 0; c < 3; ++c) {
     if (!((b.ae_mask >> c) & 1) || !b.ncounted[c]) continue;
-    b.ae_ctr[2 * c] += b.ctr[c][2];
-    b.ae_ctr[2 * c + 1] += b.ctr[c][3];
-    b.ctr[c][2] = 0;
-    b.ctr[c][3] = 0;
+    // atomic: a classify on another stream may be adding to rule 0 meanwhile
+    atomicAdd(&b.ae_ctr[2 * c], atomicExch(&b.ctr[c][2], 0ull));
+    atomicAdd(&b.ae_ctr[2 * c + 1], atomicExch(&b.ctr[c][3], 0ull));
   }
 }
 

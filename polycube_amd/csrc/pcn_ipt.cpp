@@ -145,6 +145,12 @@ struct pcn_ipt {
   unsigned long long *ctr_scratch = nullptr;   // [3][ctr_words]: stage-A counters (discarded)
   void *ct_buf = nullptr;                      // stage-A outcomes + a rule-id array
   size_t ct_buf_cap = 0;
+  // Stateful batches share ct_buf, the CtScratch buffers and the table, so
+  // they run one after another in submission order whatever stream each
+  // comes on: the next one's stage A waits for this event, recorded after
+  // the previous one's last conntrack kernel.
+  hipEvent_t ev_ct = nullptr;
+  bool ct_pending = false;
 };
 
 namespace pcn {
@@ -370,6 +376,7 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
     if (ctx->ev_staged) (void)hipEventDestroy(ctx->ev_staged);
     if (ctx->ev_gathered) (void)hipEventDestroy(ctx->ev_gathered);
+    if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
   }
   delete ctx;
 }
@@ -824,6 +831,8 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       hip_check(hipMalloc(&ctx->ct_buf, need), "hipMalloc(conntrack outcomes)");
       ctx->ct_buf_cap = need;
     }
+    // the previous stateful batch (any stream) must be done with the shared buffers and the table
+    if (ctx->ct_pending) hip_check(hipStreamWaitEvent(st, ctx->ev_ct, 0), "hipStreamWaitEvent(conntrack)");
     int32_t *a_rid = static_cast<int32_t *>(ctx->ct_buf);
     int32_t *rids = b->rule_ids ? b->rule_ids : a_rid + nlab * n;
     uint8_t *a_v = reinterpret_cast<uint8_t *>(a_rid + nlab * n + (b->rule_ids ? 0 : n));
@@ -844,6 +853,8 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     cb.rule_ids = rids;
     const int e = ct_run(cb, ctx->ct, *ctx->cts, ctx->num_cus, st);
     if (e != hipSuccess) return fail(-EIO, std::string("conntrack: ") + hipGetErrorString(hipError_t(e)));
+    hip_check(hipEventRecord(ctx->ev_ct, st), "hipEventRecord(conntrack)");
+    ctx->ct_pending = true;
     return 0;
   });
 }
@@ -1079,6 +1090,7 @@ int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2) {
       ctx->ct.now = now;
     }
     if (!ctx->cts) ctx->cts = ct_scratch_new();
+    if (!ctx->ev_ct) hip_check(hipEventCreateWithFlags(&ctx->ev_ct, hipEventDisableTiming), "hipEventCreate");
     ctx->ct_on = true;
     return 0;
   });

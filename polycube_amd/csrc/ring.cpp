@@ -179,7 +179,14 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   if (ok && b->use_offsets) ok = hipMemcpyAsync(s.d_offsets, s.h_offsets, 4 * n, hipMemcpyHostToDevice, st) == hipSuccess;
   if (ok && b->use_lens) ok = hipMemcpyAsync(s.d_lens, s.h_lens, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
   if (ok && b->use_in_port) ok = hipMemcpyAsync(s.d_in_port, s.h_in_port, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
-  if (!ok) return ring_fail(-EIO, "hipMemcpyAsync (H2D) failed");
+  // a failed submit leaves the slot kFilling (the caller may release and
+  // refill it): wait until nothing queued on the stream still reads it
+  auto quiesce = [&](int code, const std::string &msg) {
+    (void)hipStreamSynchronize(st);
+    (void)hipGetLastError();
+    return ring_fail(code, msg);
+  };
+  if (!ok) return quiesce(-EIO, "hipMemcpyAsync (H2D) failed");
   pcn_ipt_batch batch{};
   batch.frames = s.d_frames;
   batch.frames_bytes = bytes;
@@ -196,13 +203,13 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   batch.rule_ids = s.d_rule_ids;
   if (n) {
     const int rc = pcn_ipt_classify(r->ctx, &batch, st);
-    if (rc) return ring_fail(rc, std::string("classify: ") + pcn_ipt_last_error());
+    if (rc) return quiesce(rc, std::string("classify: ") + pcn_ipt_last_error());
   }
   // PCIe out: verdicts (and rule ids)
   ok = hipMemcpyAsync(s.h_verdicts, s.d_verdicts, n, hipMemcpyDeviceToHost, st) == hipSuccess;
   if (ok && s.d_rule_ids) ok = hipMemcpyAsync(s.h_rule_ids, s.d_rule_ids, 4 * n, hipMemcpyDeviceToHost, st) == hipSuccess;
   if (ok) ok = hipEventRecord(s.done, st) == hipSuccess;
-  if (!ok) return ring_fail(-EIO, "hipMemcpyAsync (D2H) / hipEventRecord failed");
+  if (!ok) return quiesce(-EIO, "hipMemcpyAsync (D2H) / hipEventRecord failed");
   s.n = n;
   s.state = kInFlight;
   r->inflight.push_back(slot);

@@ -72,8 +72,10 @@ def test_ingest_ring_needs_a_device():
     ipt.close()
 
 
-def test_flow_split_needs_a_device_and_valid_ranks():
-    """pcn_ipt_flow_owner / pcn_ipt_flow_split argument checks (no GPU work is launched)."""
+def test_flow_split_needs_a_device():
+    """pcn_ipt_flow_owner / pcn_ipt_flow_split without a device or batch (no GPU
+    work is launched).  The rank checks need a device context:
+    tests/test_gpu_flow_split.py::test_bad_ranks_are_refused."""
     from polycube_amd import Iptables
     ipt = Iptables(device=-1)
     b = ffi.Batch(1, 64, None, None, 64, 64, None, 1, 0, 0, 0, None, 1, None, None)

@@ -208,3 +208,35 @@ def test_full_table_drops_inserts_without_faulting(dev):
     info = ipt.ct_info()
     assert info["inserts_lost"] > 0
     assert 1000 < len(ipt.ct_dump()) <= 1024
+
+
+def test_ring_over_many_streams_keeps_batch_order(dev):
+    """A stateful context fed by the ingest ring, one stream per slot: the
+    batches share the connection table and the conntrack scratch, so each
+    one's stage A waits for the previous batch's last conntrack kernel.  Four
+    slots are submitted back to back with no wait between them; verdicts,
+    rule ids, counters and the session table equal one sequential oracle."""
+    rs = synth.config_rules(2)
+    rules = CT_RULES + rs.rules()
+    o, ipt = ct_pair({1: rules}, {1: "DROP"}, jit=1)
+    n_all, nb = 32000, 4
+    f, lens = synth.flow_traffic(n_all, 900, 17, rs=rs, lens_mode="mixed")
+    per = n_all // nb
+    ring = ipt.ring(slots=nb, slot_frames=per, slot_bytes=per * 128, streams=nb, rule_ids=True)
+    expect = {}
+    for k in range(nb):
+        slot, frames, _, lns, _ = ring.acquire()
+        lo, hi = k * per, (k + 1) * per
+        frames[:per * 128] = f[lo * 128:hi * 128]
+        lns[:per] = lens[lo:hi]
+        ring.submit(slot, per, stride=128, fixed_len=128, lens=True)
+        expect[slot] = o.classify(f[lo * 128:hi * 128], n=per, lens=lens[lo:hi], stride=128, fixed_len=128)
+    while expect:
+        done, v, r = ring.complete()
+        v_o, r_o = expect.pop(done)
+        assert_same(v_o, r_o, v.copy(), r.copy())
+        ring.release(done)
+    ring.close()
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_ae(o, ipt)
