@@ -422,110 +422,6 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
   return staged ? ws->best[lane] : kNoRule;
 }
 
-// ---- rule-chain stage, part 2, in place (per lane, wave-converged) ----
-// Each owner lane walks its own candidate words, PCN_CAND_UNROLL at a time:
-// the records of its classes are read once per summary block, then for up to
-// U candidates every field's word is read back to back and every PERM entry
-// after that, so a round costs two LDS round trips whatever U is (the dealt
-// stage costs seven: item write, item read, record, word, PERM, atomic, best).
-// A round runs while any lane of the wave still holds a candidate; a lane
-// without one in slot u reads POOL[0] and PERM[0] (broadcast, no conflict)
-// and ignores them.
-#ifndef PCN_CAND_INPLACE
-#define PCN_CAND_INPLACE 0
-#endif
-#ifndef PCN_CAND_UNROLL
-#define PCN_CAND_UNROLL 4   // largest round (2..4)
-#endif
-// One round of R candidates per lane, straight-line: every address first,
-// then every word read, then every PERM read, so the LDS reads of the round
-// are in flight together (a wave-uniform branch around a read would make the
-// compiler wait for it at the join).
-template <bool LDS, int NS, int R>
-__device__ __forceinline__ void cand_round(const Tab<LDS> &t, const TableLayout &lay, uint32_t k, uint64_t &m,
-                                           const uint64_t pm[NS], const uint32_t pb[NS], uint32_t &best) {
-  uint32_t bitu[R], at[R][NS];
-  bool has[R];
-#pragma unroll
-  for (int u = 0; u < R; ++u) {
-    has[u] = m != 0;
-    const uint32_t bit = has[u] ? static_cast<uint32_t>(__builtin_ctzll(m)) : 0u;
-    bitu[u] = bit;
-    m &= m - 1;
-    const uint64_t below = (1ull << bit) - 1;
-#pragma unroll
-    for (int f = 0; f < NS; ++f) {
-      const uint32_t j = pb[f] + static_cast<uint32_t>(__builtin_popcountll(pm[f] & below));
-      const uint32_t part_mask = has[u] ? 0u - static_cast<uint32_t>((pm[f] >> bit) & 1) : 0u;
-      if (lay.part_direct) {
-        at[u][f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));
-      } else {
-        const bool wide = lay.part_wide;
-        const uint32_t ia = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
-        at[u][f] = lay.pool + 8 * (wide ? t.u32(lay.part, ia - lay.part) : t.u16(lay.part, ia - lay.part));
-      }
-    }
-  }
-  uint64_t acc[R];
-#pragma unroll
-  for (int u = 0; u < R; ++u) {
-    acc[u] = ~0ull;
-#pragma unroll
-    for (int f = 0; f < NS; ++f) acc[u] &= t.u64(lay.pool, at[u][f] - lay.pool);
-  }
-  uint32_t e[R];
-#pragma unroll
-  for (int u = 0; u < R; ++u) {
-    const bool hit = has[u] && acc[u] != 0;
-    const uint32_t pi = hit ? (k * 64 + bitu[u]) * 63 + static_cast<uint32_t>(__builtin_ctzll(acc[u])) : 0u;
-    e[u] = t.u16(lay.perm, 2 * pi);
-    e[u] = hit ? e[u] : kNoRule;
-  }
-#pragma unroll
-  for (int u = 0; u < R; ++u) best = e[u] < best ? e[u] : best;
-}
-
-template <bool LDS, int NS>
-__device__ __forceinline__ uint32_t chain_candidates_inplace(const DevChain &ch, bool active, const uint32_t cls[NS]) {
-  if (__ballot(active) == 0) return kNoRule;
-  const Tab<LDS> t{ch.image, ch.lds_image, ch.lds_limit};
-  const TableLayout &lay = ch.lay;
-  const uint32_t nrw = ch.nrw, nsw = ch.nsw;
-  uint32_t best = kNoRule;
-  for (uint32_t k = 0; k < nsw; ++k) {
-    const uint32_t live = nrw - k * 64;
-    uint64_t m = 0;
-    if (active) {
-      m = live >= 64 ? ~0ull : ((1ull << live) - 1);
-      uint64_t sm[NS];
-#pragma unroll
-      for (int f = 0; f < NS; ++f) sm[f] = t.u64(lay.sf, 8 * (cls[f] * nsw + k));
-#pragma unroll
-      for (int f = 0; f < NS; ++f) m &= sm[f];
-    }
-    if (__ballot(m != 0) == 0) continue;
-    // this lane's candidate records {PM, PBASE} (lanes without a candidate read class 0's)
-    uint64_t pm[NS];
-    uint32_t pb[NS];
-#pragma unroll
-    for (int f = 0; f < NS; ++f) {
-      const u32x4 r = t.u128(lay.pbase, 16 * ((m ? cls[f] : 0u) * nsw + k));
-      pm[f] = static_cast<uint64_t>(r.y) << 32 | r.x;
-      pb[f] = r.z;
-    }
-    // rounds sized by the wave's largest remaining count (at most PCN_CAND_UNROLL)
-    for (;;) {
-      const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(m));
-      if (PCN_CAND_UNROLL >= 4 && __ballot(c >= 4)) cand_round<LDS, NS, 4>(t, lay, k, m, pm, pb, best);
-      else if (PCN_CAND_UNROLL >= 3 && __ballot(c >= 3)) cand_round<LDS, NS, 3>(t, lay, k, m, pm, pb, best);
-      else if (__ballot(c >= 2)) cand_round<LDS, NS, 2>(t, lay, k, m, pm, pb, best);
-      else if (__ballot(c >= 1)) cand_round<LDS, NS, 1>(t, lay, k, m, pm, pb, best);
-      else break;
-    }
-  }
-  return best;
-}
-
 // ---- rule-chain stage, part 3 (per lane) ----
 __device__ __forceinline__ uint32_t chain_finish(const DevChain &ch, uint32_t best, int32_t &rid) {
   if (best == kNoRule) { rid = PCN_IPT_RID_DEFAULT; return static_cast<uint32_t>(ch.default_action); }
@@ -545,8 +441,7 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
   if (mine) need = chain_classes<LDS, NS>(ch, p, port, cls, verdict, rid);
   // the wave gets issue priority while it deals candidates through LDS
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(PCN_CAND_PRIO >= 0 ? PCN_CAND_PRIO : 0);
-  const uint32_t best = PCN_CAND_INPLACE ? chain_candidates_inplace<LDS, NS>(ch, need, cls)
-                                         : chain_candidates<LDS, NS>(ch, need, cls, ws);
+  const uint32_t best = chain_candidates<LDS, NS>(ch, need, cls, ws);
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(0);
   if (need) verdict = chain_finish(ch, best, rid);
 }
