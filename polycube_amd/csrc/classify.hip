@@ -32,7 +32,8 @@
 extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 
 // Measurement-only ablation builds (tools/ablate.py; never the product .so):
-// 1 parse only, 2 + field lookups, 3 + summary AND, 4 full minus counters.
+// 1 parse only, 2 + field lookups, 3 + summary AND, 4 full minus counters,
+// 5 full minus the end-of-launch counter flush.
 #ifndef PCN_ABLATE
 #define PCN_ABLATE 0
 #endif
@@ -296,7 +297,8 @@ struct WaveScratch {
   u32x4 cls[64];         // each owner's classes
 #endif
 };
-static_assert(sizeof(WaveScratch) <= PCN_WAVE_LDS_BYTES, "scratch fits the per-wave region");
+static_assert(sizeof(WaveScratch) <= PCN_WAVE_SCRATCH_BYTES && PCN_WAVE_SCRATCH_BYTES <= PCN_WAVE_LDS_BYTES,
+              "scratch fits the per-wave region");
 
 // ---- rule-chain stage, part 2 (whole wave, converged) ----
 // Lanes with `active` AND their class summaries into a candidate-word mask.
@@ -807,6 +809,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       if (d == 0 || i + d * step < n_round) process(i + d * step, st[d]);
   }
   __syncthreads();
+  if (PCN_ABLATE == 5) return;
   // ---- flush the workgroup histogram ----
   // Workgroups finish together and all add into the same counters; each
   // starts at its own rotation of the bins so the global atomics of

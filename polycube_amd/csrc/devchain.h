@@ -45,6 +45,8 @@
 #endif
 #define PCN_WAVE_LDS_BYTES 3072     // per-wave LDS region: header transpose buffer (64 frames x 48 B),
                                     // reused as the candidate-stage scratch
+#define PCN_WAVE_SCRATCH_BYTES 1280 // the candidate-stage scratch alone: the whole region of a launch
+                                    // without the fixed-stride header transpose
 
 namespace pcn {
 
@@ -72,8 +74,11 @@ struct TableLayout {
   uint32_t meta_stride[6]; // proto, flags, ct, sport, dport, iface (0: not a meta field)
   uint32_t sf;             // u64[nvec][nsw]: SUMM (bit w: word w of the class vector != 0)
   uint32_t pbase;          // {u64 PM, u32 PBASE, u32 0}[nvec][nsw]: PM bit w = word w partial,
-                           // PBASE = first PART index of the class's block; the candidate
-                           // tables start here (the LDS prefix limit when the image does not fit)
+                           // PBASE = first PART index of the class's block.  With indexed
+                           // PART (large images) pbase and PART are the last two tables, so
+                           // [0, pbase) -- every table but those -- is the LDS prefix staged
+                           // when the whole image does not fit; direct images keep PART,
+                           // POOL and PERM after pbase
   uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
   uint32_t part_wide;
   uint32_t part_direct;    // PART holds the partial words themselves (u64), not POOL indices

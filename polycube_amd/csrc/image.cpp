@@ -512,27 +512,35 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
   }
   img.part_words = static_cast<uint32_t>(part.size());
   lay.sf = blob.add(summ);
-  lay.pbase = blob.add(cand);
   // Partial words stored directly (one dependent LDS read less per field in
   // the candidate stage) while the whole image stays within kDirectMaxBytes.
-  const size_t direct_bytes = blob.bytes.size() + part.size() * 8 + perm.perm.size() * 2 + 4 * kAlign;
+  const size_t direct_bytes = blob.bytes.size() + cand.size() * 4 + part.size() * 8 + perm.perm.size() * 2 +
+                              5 * kAlign;
   lay.part_direct = direct_bytes <= kDirectMaxBytes && !compact_images();
   lay.part_wide = !lay.part_direct && words.size() > 0xFFFF;
   if (lay.part_direct) {
+    lay.pbase = blob.add(cand);
     std::vector<uint64_t> direct(part.size());
     for (size_t k = 0; k < part.size(); ++k) direct[k] = words[part[k]];
     lay.part = blob.add(direct);
     words.resize(1);   // POOL[0] = all-ones: what a FULL field reads
-  } else if (lay.part_wide) {
-    lay.part = blob.add(part);
+    lay.pool = blob.add(words);
+    lay.zero = blob.add(std::vector<uint32_t>(4, 0));
+    lay.perm = blob.add(perm.perm);
   } else {
-    lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
+    // An image this size may not fit LDS whole: POOL, the zero cell and PERM
+    // go before the {PM, PBASE} records and PART, so the staged prefix
+    // [0, pbase) holds every table but those two (the candidate stage then
+    // makes two L2 reads per field, not four).
+    lay.pool = blob.add(words);
+    lay.zero = blob.add(std::vector<uint32_t>(4, 0));
+    lay.perm = blob.add(perm.perm);
+    lay.pbase = blob.add(cand);
+    if (lay.part_wide) lay.part = blob.add(part);
+    else lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
   }
-  lay.pool = blob.add(words);
-  lay.zero = blob.add(std::vector<uint32_t>(4, 0));
   img.pool_words = static_cast<uint32_t>(words.size());
   img.part_bytes = part.size() * (lay.part_direct ? 8 : lay.part_wide ? 4 : 2) + words.size() * 8;
-  lay.perm = blob.add(perm.perm);
   lay.bytes = static_cast<uint32_t>((blob.bytes.size() + kAlign - 1) / kAlign * kAlign);
   blob.bytes.resize(lay.bytes);
   img.tables = std::move(blob.bytes);

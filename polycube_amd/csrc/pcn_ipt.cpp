@@ -65,12 +65,13 @@ constexpr uint32_t kLdsBudget = PCN_DEBUG_LDS_BUDGET;  // gfx950 LDS per CU (one
 // Measurement knob (tools/ablate.py experiments): bytes per wave region
 // (default PCN_WAVE_LDS_BYTES; a kernel built without the header transpose
 // needs only its candidate scratch).
-uint32_t wave_region_bytes() {
+uint32_t wave_region_bytes(bool fixed) {
   static const uint32_t v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_WAVE_BYTES");
     return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : uint32_t(PCN_WAVE_LDS_BYTES);
   }();
-  return v;
+  // only the fixed-stride path transposes headers through the region
+  return fixed ? v : uint32_t(PCN_WAVE_SCRATCH_BYTES);
 }
 
 struct ImageSlot {
@@ -662,7 +663,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     // counter bins: u32 pkts, plus u32 bytes unless every frame has the same length
     const uint32_t bin_bytes = (fixed ? 4 : 8) * a.nbins;
     const uint32_t tail = (bin_bytes + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * wave_region_bytes();
+                          (PCN_BLOCK / 64) * wave_region_bytes(fixed);
     // whole images if they fit, else their per-packet prefix [0, pbase) (the
     // candidate-stage tables are then read from L2/HBM), else nothing
     uint32_t img_bytes = 0;
@@ -682,7 +683,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.bins_offset = kLdsDescBytes + img_bytes;
     a.lds_localip = a.bins_offset + (bin_bytes + 15) / 16 * 16;
     a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
-    a.wave_bytes = wave_region_bytes();
+    a.wave_bytes = wave_region_bytes(fixed);
     a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
@@ -891,7 +892,7 @@ int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
     d.lds_bins = d.ncounted <= kMaxLdsRuleBins ? 3 : -1;
     const uint32_t nbins = 3 + (d.lds_bins >= 0 ? d.ncounted : 0);
     const uint32_t tail = (nbins * 4 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * wave_region_bytes();
+                          (PCN_BLOCK / 64) * wave_region_bytes(true);
     d.lds_limit = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget   ? d.lay.bytes
                   : kLdsDescBytes + d.lay.pbase + tail <= kLdsBudget ? d.lay.pbase
                                                                      : 0;

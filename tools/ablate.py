@@ -43,9 +43,15 @@ def child(lib, hit, log2n, iters, cfg, jit):
                                   protos=(6, 17) if cfg == 3 else (17,))
         frames = torch.from_numpy(synth.build_frames(*cols).reshape(-1)).cuda()
     v = torch.empty(n, dtype=torch.uint8, device="cuda")
-    for _ in range(3):
-        ipt.classify(frames, n=n, verdicts=v, rule_ids=False, **kw)
-    torch.cuda.synchronize()
+    # clock settle (as bench.py): untimed launches for SETTLE seconds (default 0.5)
+    import time
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(16):
+            ipt.classify(frames, n=n, verdicts=v, rule_ids=False, **kw)
+        torch.cuda.synchronize()
+        if time.perf_counter() - t0 >= float(os.environ.get("SETTLE", "0.5")):
+            break
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
     for a, b in evs:
         a.record()
