@@ -119,15 +119,32 @@ __device__ __forceinline__ void load_fixed(const uint8_t *frame, Hdr &h) {
 
 // Unaligned frame start: 14 aligned dwords, each only if it lies inside the
 // buffer, then byte-shifted into the window.
+// A frame whose 16 dwords lie inside the buffer (every frame but the last
+// few) is read as four 16-byte loads from its dword-aligned start: global
+// loads need only dword alignment, and four requests per lane instead of
+// fourteen is what an IMIX batch of scattered headers is bound by.
+typedef uint32_t u32x4d __attribute__((ext_vector_type(4), aligned(4)));
+#ifndef PCN_GENERIC_X4
+#define PCN_GENERIC_X4 1
+#endif
 __device__ __forceinline__ void load_generic(const uint8_t *frames, uint64_t frames_bytes,
                                              uint64_t off, Hdr &h) {
   uint64_t base = off & ~uint64_t(3);
   uint32_t sh = static_cast<uint32_t>(off & 3);
-  uint32_t d[14];
+  uint32_t d[16];
+  if (PCN_GENERIC_X4 && base + 64 <= frames_bytes) {
+    const u32x4d *p = reinterpret_cast<const u32x4d *>(frames + base);
 #pragma unroll
-  for (int k = 0; k < 14; ++k) {
-    uint64_t at = base + 4u * k;
-    d[k] = (at + 4 <= frames_bytes) ? *reinterpret_cast<const uint32_t *>(frames + at) : 0u;
+    for (int q = 0; q < 4; ++q) {
+      const u32x4d v = __builtin_nontemporal_load(p + q);
+      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {
+      uint64_t at = base + 4u * k;
+      d[k] = (at + 4 <= frames_bytes) ? *reinterpret_cast<const uint32_t *>(frames + at) : 0u;
+    }
   }
 #pragma unroll
   for (int k = 0; k < 13; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
@@ -393,6 +410,11 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
         uint32_t at[NS];   // LDS/image offset of each field's u64 word
 #pragma unroll
         for (int f = 0; f < NS; ++f) {
+          if (lay.part_dense) {
+            const uint32_t cell = oc[f] * nrw + k * 64 + bit;
+            at[f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
+            continue;
+          }
           const uint32_t rec = oc[f] * nsw + k;
           const u32x4 r = t.u128(lay.pbase, 16 * rec);
           const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;

@@ -82,6 +82,10 @@ struct TableLayout {
   uint32_t part;           // u16[] (u32[] if part_wide): POOL index of each partial word
   uint32_t part_wide;
   uint32_t part_direct;    // PART holds the partial words themselves (u64), not POOL indices
+  uint32_t part_dense;     // PART is dense: u16 (u32 if part_wide) POOL index of every (class,
+                           // word), 0 where the word is FULL; no {PM, PBASE} records (pbase ==
+                           // part).  Used when the image is too large for LDS anyway: a
+                           // candidate field is then one L2 read instead of two
   uint32_t pool;           // u64[]: distinct partial words; POOL[0] is all-ones
   uint32_t zero;           // 16 zero bytes (the PART cell a FULL field reads: index 0)
   uint32_t perm;           // u16[nrw * 63]

@@ -20,6 +20,10 @@ constexpr uint32_t kHashMul = 0x9E3779B1u;
 constexpr size_t kMetaMaxEntries = 8192;   // key fields join the meta slot while its table stays this small
 constexpr size_t kMetaMaxClasses = 1024;   // ... and holds at most this many distinct vectors
 constexpr size_t kDirectMaxBytes = 96 * 1024;
+// Dense PART: when the image with records and indexed PART exceeds the LDS of
+// a CU (it is then read from L2 in part anyway), up to 4 MiB of L2 (one XCD's)
+constexpr size_t kDenseMinBytes = 160 * 1024;
+constexpr size_t kDenseMaxBytes = 4 * 1024 * 1024;
 constexpr uint32_t kIpWindowMax = 4;           // IP buckets read whole up to this many boundaries
 
 // Measurement knob (tools/ablate.py experiments): PCN_IPT_DEBUG_COMPACT=1
@@ -495,6 +499,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
   const size_t nrec = size_t(img.nvec) * img.nsw;
   std::vector<uint64_t> summ(nrec, 0), words{~uint64_t(0)};
   std::vector<uint32_t> cand(4 * nrec, 0), part;                 // {PM lo, PM hi, PBASE, 0} per record
+  std::vector<uint32_t> dense(size_t(img.nvec) * img.nrw, 0);     // POOL index per (class, word)
   std::map<uint64_t, uint32_t> word_id{{~uint64_t(0), 0}};
   for (uint32_t v = 0; v < img.nvec; ++v) {
     for (uint32_t w = 0; w < img.nrw; ++w) {
@@ -507,6 +512,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
         auto it = word_id.emplace(x, static_cast<uint32_t>(words.size())).first;
         if (it->second == words.size()) words.push_back(x);
         part.push_back(it->second);
+        dense[size_t(v) * img.nrw + w] = it->second;
       }
     }
   }
@@ -529,18 +535,30 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     lay.perm = blob.add(perm.perm);
   } else {
     // An image this size may not fit LDS whole: POOL, the zero cell and PERM
-    // go before the {PM, PBASE} records and PART, so the staged prefix
-    // [0, pbase) holds every table but those two (the candidate stage then
-    // makes two L2 reads per field, not four).
+    // go before the candidate tables, so the staged prefix [0, pbase) holds
+    // every table but those.  When the image with {PM, PBASE} records and
+    // indexed PART would exceed LDS anyway, PART is stored dense instead (a
+    // POOL index per class and word, larger but L2-resident), so a candidate
+    // field costs one L2 read rather than a record read and an index read.
     lay.pool = blob.add(words);
     lay.zero = blob.add(std::vector<uint32_t>(4, 0));
     lay.perm = blob.add(perm.perm);
-    lay.pbase = blob.add(cand);
-    if (lay.part_wide) lay.part = blob.add(part);
-    else lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
+    const size_t iw = lay.part_wide ? 4 : 2;
+    const size_t indexed_bytes = blob.bytes.size() + cand.size() * 4 + part.size() * iw + 2 * kAlign;
+    lay.part_dense = indexed_bytes > kDenseMinBytes && dense.size() * iw <= kDenseMaxBytes && !compact_images();
+    if (lay.part_dense) {
+      if (lay.part_wide) lay.part = blob.add(dense);
+      else lay.part = blob.add(std::vector<uint16_t>(dense.begin(), dense.end()));
+      lay.pbase = lay.part;
+    } else {
+      lay.pbase = blob.add(cand);
+      if (lay.part_wide) lay.part = blob.add(part);
+      else lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
+    }
   }
   img.pool_words = static_cast<uint32_t>(words.size());
-  img.part_bytes = part.size() * (lay.part_direct ? 8 : lay.part_wide ? 4 : 2) + words.size() * 8;
+  img.part_bytes = (lay.part_dense ? dense.size() : part.size()) * (lay.part_direct ? 8 : lay.part_wide ? 4 : 2) +
+                   words.size() * 8;
   lay.bytes = static_cast<uint32_t>((blob.bytes.size() + kAlign - 1) / kAlign * kAlign);
   blob.bytes.resize(lay.bytes);
   img.tables = std::move(blob.bytes);

@@ -15,7 +15,7 @@ LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_shift0", "ip_shift1", "ip_steps0", 
           "hash0", "hash1", "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "skip0", "skip1",
           "slot0", "slot1", "slot2", "nslots", "proto_idx", "flags_idx", "ct_idx", "flags_skip", "meta",
           "stride_proto", "stride_flags", "stride_ct", "stride_sport", "stride_dport", "stride_iface",
-          "sf", "pbase", "part", "part_wide", "part_direct", "pool", "zero", "perm"]
+          "sf", "pbase", "part", "part_wide", "part_direct", "part_dense", "pool", "zero", "perm"]
 MISS = 0xFFFF
 EMPTY = 0xFFFFFFFF
 
@@ -112,6 +112,12 @@ class ImageModel:
                 bit = (m & -m).bit_length() - 1
                 m &= m - 1
                 acc = (1 << 64) - 1
+                if L["part_dense"]:                               # POOL index per (class, word)
+                    for c in cls:
+                        cell = c * self.nrw + 64 * k + bit
+                        q = self.u32(L["part"] + 4 * cell) if L["part_wide"] else self.u16(L["part"] + 2 * cell)
+                        acc &= self.u64(L["pool"] + 8 * q)
+                    recs = []
                 for r in recs:
                     part = self.u64(L["pbase"] + 16 * r)        # PM: partial words
                     if not part >> bit & 1:

@@ -179,3 +179,27 @@ def test_image_meta_slot_with_ifaces_flags_conntrack(n_rules, n_ports, seed, man
                     int.from_bytes(bytes(row[36:38]), "big"), int(row[47]) if row[23] == 6 else 0,
                     int(in_port[i]), int(ct[i]))[0]
         assert got == rid[i], f"packet {i}: model {got} oracle {rid[i]}"
+
+
+def test_image_dense_part_config5():
+    """10k rules: the image exceeds LDS, so PART is stored dense (a POOL index
+    per class and word); the walk through it answers like the oracle."""
+    rs = synth.config_rules(5)
+    rules = rs.rules()
+    o = Oracle(10000, 10000)
+    o.set_chain(FORWARD, rules, "DROP")
+    ipt = Iptables(device=-1, max_rules=16384, max_counted_rules=10000)
+    ipt.interactive = False
+    ch = ipt.chain(FORWARD)
+    for r in rules:
+        ch.append(**r)
+    ch.default = "DROP"
+    ch.apply_rules()
+    model = ImageModel(ch)
+    assert model.lay["part_dense"] == 1 and model.lay["pbase"] == model.lay["part"]
+    cols = synth.make_headers(rs, 600, 0x5EED, hit_frac=0.8)
+    frames = synth.build_frames(*cols, frame_len=64)
+    _, rid = o.classify(frames, n=600, stride=64)
+    got = model_classify(model, frames, 600)
+    assert np.array_equal(got, rid)
+    assert (rid >= 0).sum() > 300

@@ -34,7 +34,7 @@ def layout_words():
     return n
 
 
-def spec_for(cfg):
+def spec_for(cfg, imix=False):
     from polycube_amd import Iptables, ffi, synth
     rs = synth.config_rules(cfg)
     ipt = Iptables(device=-1, max_rules=16384, max_counted_rules=10000)
@@ -56,9 +56,11 @@ def spec_for(cfg):
     from image_model import LAYOUT
     ns = lay[LAYOUT.index("nslots")]
     vals = ", ".join(f"{x}u" for x in lay)
-    return ("#pragma once\n#define PCN_JIT_FIXED true\n#define PCN_JIT_LDS true\n#define PCN_JIT_CH 1\n"
+    # --imix: the offsets/lens launch shape with the staged prefix [0, pbase) (config 5's)
+    limit = lay[LAYOUT.index("pbase")] if imix else lay[0]
+    return (f"#pragma once\n#define PCN_JIT_FIXED {'false' if imix else 'true'}\n#define PCN_JIT_LDS true\n#define PCN_JIT_CH 1\n"
             f"#define PCN_JIT_NS {ns}\n#define PCN_JIT_INPUTS 0\n#define PCN_JIT_CHAIN {{{vals}, nullptr, nullptr, {info['nrules']}u, {nrw}u, "
-            f"{nsw}u, {present}u, {info['nvec']}u, {all_cls}u, {ncounted}u, 10000u, 0, 0u, {lay[0]}u, {lds_bins}}}\n")
+            f"{nsw}u, {present}u, {info['nvec']}u, {all_cls}u, {ncounted}u, 10000u, 0, 0u, {limit}u, {lds_bins}}}\n")
 
 
 def main():
@@ -66,10 +68,11 @@ def main():
     ap.add_argument("--cfg", type=int, default=3)
     ap.add_argument("--defs", default="")
     ap.add_argument("--out", default="/tmp/pcn_jit.s")
+    ap.add_argument("--imix", action="store_true", help="offsets/lens launch shape (FIXED false, prefix staged)")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp()
     with open(os.path.join(tmp, "pcn_jit_spec.h"), "w") as fh:
-        fh.write(spec_for(a.cfg))
+        fh.write(spec_for(a.cfg, a.imix))
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", f"-I{ROOT}/include", f"-I{ROOT}/polycube_amd/csrc",
            f"-I{tmp}", "-DPCN_JIT", *a.defs.split(), "--offload-arch=gfx950", "-x", "hip", "--cuda-device-only",
            "-S", f"{ROOT}/polycube_amd/csrc/classify.hip", "-o", a.out, "-Rpass-analysis=kernel-resource-usage"]

@@ -12,7 +12,7 @@ k=0
 for grp in "$@"; do
   k=$((k+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$ROOT/gpurun_out/$TAG/p$k" -o run \
-    -- python3 "$ROOT/tools/ablate.py" --child --lib "${LIB:-}" --hit ${HIT:-0.5} --iters 5 --log2n 24 --jit ${JIT:--1} > "$ROOT/gpurun_out/$TAG/p$k.log" 2>&1
+    -- python3 "$ROOT/tools/ablate.py" --child --lib "${LIB:-}" --hit ${HIT:-0.5} --iters 5 --log2n ${LOG2N:-24} --cfg ${CFG:-3} --jit ${JIT:--1} > "$ROOT/gpurun_out/$TAG/p$k.log" 2>&1
   rc=$?
   echo "pass $k ($grp) rc=$rc"
   case $rc in 124|134|137|139) exit $rc;; esac
