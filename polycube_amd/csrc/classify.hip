@@ -33,15 +33,30 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 
 // Measurement-only ablation builds (tools/ablate.py; never the product .so):
 // 1 parse only, 2 + field lookups, 3 + summary AND, 4 full minus counters,
-// 5 full minus the end-of-launch counter flush.
+// 5 full minus the end-of-launch counter flush, 6 full minus the per-rule
+// counter bins, 7 per-rule bins by plain stores (wrong counts; cost of the atomic).
 #ifndef PCN_ABLATE
 #define PCN_ABLATE 0
 #endif
 #ifndef PCN_HDR_LDS
 #define PCN_HDR_LDS 1    // fixed stride: 1 coalesced chunks transposed through LDS, 0 per-lane strided loads
 #endif
-#ifndef PCN_PREFETCH
-#define PCN_PREFETCH 1   // frames per lane in flight ahead of the one being classified
+// Frames per lane in flight ahead of the one being classified.  Fixed
+// stride: 2 (A/B with settled clocks, config 3: -3 % kernel time at hit rate
+// 0.5, config 2: -2.5 %; profiles/r02_ab_prefetch*.log).  Offsets/lens
+// batches: 1 (their 13-dword windows cost more registers; depth 2 measured
+// +2 % on config 5).
+#ifndef PCN_PREFETCH_FIXED
+#define PCN_PREFETCH_FIXED 2
+#endif
+#ifndef PCN_PREFETCH_GENERIC
+#define PCN_PREFETCH_GENERIC 1
+#endif
+#ifdef PCN_PREFETCH      // one depth for both paths (measurement builds)
+#undef PCN_PREFETCH_FIXED
+#undef PCN_PREFETCH_GENERIC
+#define PCN_PREFETCH_FIXED PCN_PREFETCH
+#define PCN_PREFETCH_GENERIC PCN_PREFETCH
 #endif
 #ifndef PCN_FASTPATH
 #define PCN_FASTPATH 1   // wave fast path: all 64 frames plain IPv4 TCP/UDP -> straight-line parse
@@ -542,7 +557,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   const uint64_t last = a.n - 1;
   // in_port / ct_status ride along with the header: when the batch has none
   // the host points them at a zero cell with a zero index mask, so the loads
-  // stay unconditional too.  PCN_PREFETCH frames per lane are in flight.
+  // stay unconditional too.  PF frames per lane are in flight.
   // Fixed-stride frames are fetched coalesced: a wave's 64 frames are 192
   // 16-byte chunks (bytes 0..47 of each frame), chunk t = 64q + lane is loaded
   // by instruction q of that lane, and the chunks are transposed through a
@@ -568,7 +583,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   constexpr bool kLoadPort = !JIT || (kJitInputs & 1);
   constexpr bool kLoadCt = !JIT || (kJitInputs & 6);
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
-  Stage st[PCN_PREFETCH];
+  constexpr int PF = FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
+  Stage st[PF];
   auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
     if (FIXED && PCN_HDR_LDS) {
       uint64_t group = j - lane;                 // wave-uniform
@@ -602,7 +618,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     x.ct = kLoadCt ? a.ct_status[jc & a.ct_mask] : 0u;
   };
 #pragma unroll
-  for (int d = 0; d < PCN_PREFETCH; ++d) prefetch(st[d], first + d * step);
+  for (int d = 0; d < PF; ++d) prefetch(st[d], first + d * step);
   if (PCN_STAGE_FAST) stage_images();
   // pkts[nbins], then (variable lengths only) bytes[nbins]; with a fixed
   // length every bin's bytes are pkts * len at the flush
@@ -611,7 +627,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     reinterpret_cast<uint32_t *>(pcn_smem + a.lds_localip)[k] = a.localip[k];
   __syncthreads();
   // Stage d always holds the frames i with (i - first) / step == d (mod
-  // PCN_PREFETCH): the loop is unrolled PCN_PREFETCH times so no stage is
+  // PF): the loop is unrolled PF times so no stage is
   // ever copied (a register move of an in-flight load waits for it).
   auto process = [&](const uint64_t i, Stage &cur) {
     const bool valid = i < a.n;
@@ -649,7 +665,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
     uint32_t L = FIXED ? a.fixed_len : cur.L;
     const uint32_t cur_port = cur.port, cur_ct = cur.ct;
-    prefetch(cur, i + PCN_PREFETCH * step);
+    prefetch(cur, i + PF * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
     int32_t cchain = -1;    // chain whose counters this packet bumps
@@ -814,9 +830,11 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       if (CH < 3 ? c != CH : c == PCN_IPT_OUTPUT) continue;
       const DevChain &ch = CH < 3 ? run_ch : a.ch[c];
       if (valid && cchain == c && rid >= 0 && static_cast<uint32_t>(rid) < ch.ncounted) {
-        if (ch.lds_bins >= 0) {
+        if (PCN_ABLATE == 6) {
+        } else if (ch.lds_bins >= 0) {
           uint32_t b = static_cast<uint32_t>(ch.lds_bins) + static_cast<uint32_t>(rid);
-          atomicAdd(&bins[b], 1u);
+          if (PCN_ABLATE == 7) bins[b] = 1u;   // measurement: a plain store instead of the atomic
+          else atomicAdd(&bins[b], 1u);
           if (!FIXED) atomicAdd(&byte_bins[b], L);
         } else {
           atomicAdd(&ch.ctr[2 + 2 * rid], 1ull);
@@ -825,9 +843,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       }
     }
   };
-  for (uint64_t i = first; i < n_round; i += PCN_PREFETCH * step) {
+  for (uint64_t i = first; i < n_round; i += PF * step) {
 #pragma unroll
-    for (int d = 0; d < PCN_PREFETCH; ++d)
+    for (int d = 0; d < PF; ++d)
       if (d == 0 || i + d * step < n_round) process(i + d * step, st[d]);
   }
   __syncthreads();

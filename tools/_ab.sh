@@ -1,8 +1,5 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_dense.log 2>&1; rc=$?
-tail -3 gpurun_out/t_dense.log
-[ $rc = 0 ] || exit $rc
-timeout -k 10 600 python tools/ablate.py --cfg 5 --log2n 22 --variants "jit,jit4,jit" --hits 0.5 > gpurun_out/ab_dense.log 2>&1
-CFG5_HOOK=tc timeout -k 10 600 python tools/ablate.py --cfg 5 --log2n 22 --variants "jit" --hits 0.5 >> gpurun_out/ab_dense.log 2>&1
-cut -c1-170 gpurun_out/ab_dense.log
+timeout -k 10 900 python tools/ablate.py --cfg 5 --log2n 22 --variants "jit,jit:-DPCN_PREFETCH=2,jit,jit:-DPCN_PREFETCH=2" --hits 0.5 > gpurun_out/ab_pf5.log 2>&1
+timeout -k 10 900 python tools/ablate.py --cfg 2 --variants "jit,jit:-DPCN_PREFETCH=2,jit,jit:-DPCN_PREFETCH=2" --hits 0.5 >> gpurun_out/ab_pf5.log 2>&1
+cut -c1-170 gpurun_out/ab_pf5.log
