@@ -72,6 +72,14 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
                          // holds LDS state the others' memory waits do not need (A/B: -2 % / -4.5 %
                          // at hit rate 0.5 / 1, profiles/r01_ab17_cand_prio.log)
 #endif
+#ifndef PCN_HDR_NT
+#define PCN_HDR_NT 1     // header loads with the nontemporal hint (read once, never again)
+#endif
+template <typename T>
+__device__ __forceinline__ T hdr_load(const T *p) {
+  if (PCN_HDR_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
 #ifndef PCN_STAGE_FAST
 #define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
 #endif
@@ -151,7 +159,7 @@ __device__ __forceinline__ void load_generic(const uint8_t *frames, uint64_t fra
     const u32x4d *p = reinterpret_cast<const u32x4d *>(frames + base);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const u32x4d v = __builtin_nontemporal_load(p + q);
+      const u32x4d v = hdr_load(p + q);
       d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
     }
   } else {
@@ -595,13 +603,13 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         const uint8_t *gb = a.frames + group * a.stride;
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(gb + loff[q]));
+          x.c[q] = hdr_load(reinterpret_cast<const u32x4 *>(gb + loff[q]));
       } else {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           uint64_t f = group + cf[q];
           f = f < a.n ? f : last;
-          x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]));
+          x.c[q] = hdr_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]));
         }
       }
     } else if (FIXED) {
