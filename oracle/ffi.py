@@ -60,6 +60,9 @@ def lib():
         h.orc_set_accept_established.argtypes = [vp, C.c_int, C.c_int]
         h.orc_get_accept_established.argtypes = [vp, C.c_int]
         h.orc_read_accept_established.argtypes = [vp, C.c_int, u64p, u64p, C.c_int]
+        h.orc_set_horus.argtypes = [vp, C.c_int]
+        h.orc_horus_info.argtypes = [vp, u32p]
+        h.orc_read_horus_counters.argtypes = [vp, u64p, u64p, C.c_uint32, C.c_int]
         _lib = h
     return _lib
 
@@ -174,6 +177,21 @@ class Oracle:
         pk, by = C.c_uint64(), C.c_uint64()
         lib().orc_read_accept_established(self._h, chain, C.byref(pk), C.byref(by), int(flush))
         return pk.value, by.value
+
+    # ---- Horus (Iptables_Horus_dp.c) ----
+    def set_horus(self, on):
+        assert lib().orc_set_horus(self._h, int(on)) == 0
+
+    def horus_info(self):
+        out = (C.c_uint32 * 4)()
+        lib().orc_horus_info(self._h, out)
+        return {"enabled": out[0], "runtime": out[1], "entries": out[2], "fields": out[3]}
+
+    def read_horus_counters(self, n, flush=False):
+        pk = (C.c_uint64 * max(n, 1))()
+        by = (C.c_uint64 * max(n, 1))()
+        lib().orc_read_horus_counters(self._h, pk, by, n, int(flush))
+        return list(pk[:n]), list(by[:n])
 
     def export_map(self, chain, field, cap=70000):
         nrw = lib().orc_chain_nrw(self._h, chain)

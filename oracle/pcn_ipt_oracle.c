@@ -87,6 +87,13 @@ typedef struct {
 
 typedef struct { char name[64]; uint16_t index; } port_t;
 
+/* One Horus entry: the set fields of the key as the datapath's packed
+ * horusKey holds them (sk/dk: the port's two network-order bytes read as a
+ * little-endian u16, i.e. the htons() of modules/Horus.cpp:44-51), the
+ * HorusValue {action, ruleID} (defines.h:161-164). */
+#define HZ_MAX 2048                              /* HorusConst::MAX_RULE_SIZE_FOR_HORUS, defines.h:127 */
+typedef struct { uint32_t src, dst; uint8_t proto; uint16_t sk, dk; uint8_t action; uint32_t rule; } hzent_t;
+
 struct orc_ctx {
   int service;                           /* ORC_SVC_IPTABLES / ORC_SVC_FIREWALL */
   int fw_ct_mode;                        /* pcn-firewall conntrackMode (defines.h:56-58) */
@@ -100,6 +107,14 @@ struct orc_ctx {
   struct ctstate *ct;
   int ae[NCHAINS];                       /* accept_established_enabled_<chain>_ (Iptables.h) */
   uint64_t ae_pkts[NCHAINS], ae_bytes[NCHAINS]; /* pkts_/bytes_acceptestablished_<Chain> */
+  /* Horus (Iptables.h:183-188) */
+  int hz_enabled, hz_runtime;
+  uint32_t hz_fields; int hz_n;
+  hzent_t hz[HZ_MAX];
+  uint64_t hz_pkts[HZ_MAX], hz_bytes[HZ_MAX]; /* pkts_horus / bytes_horus (Horus_dp.c:77-78) */
+  /* the shared per-CPU `packet` struct's ports while conntrack is off (the
+   * Horus key reads them for packets the Parser wrote no ports for, Q4) */
+  uint16_t hz_stale[2];
 };
 
 /* ---------------- rule parsing ---------------- */
@@ -516,6 +531,7 @@ int orc_add_port(orc_ctx *c, const char *name, uint16_t index) {
   return 0;
 }
 
+static void horus_update(orc_ctx *c, int chain);
 int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n, int def) {
   if (chain < 0 || chain >= NCHAINS || (def != 0 && def != 1)) return -EINVAL;
   prule_t *pr = calloc((size_t)n + 1, sizeof(prule_t));
@@ -534,7 +550,108 @@ int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n, int 
   ch->def_pkts = dp; ch->def_bytes = db;
   memset(pk, 0, c->max_counted * 8); memset(by, 0, c->max_counted * 8);
   ch->rules = pr; ch->nrules = (int)n; ch->default_action = def;
-  return compile_chain(c, chain);
+  int rc = compile_chain(c, chain);
+  horus_update(c, chain);
+  return rc;
+}
+
+/* ---------------- Horus ---------------- */
+
+static inline uint16_t bswap16(uint16_t x) { return (uint16_t)(x >> 8 | x << 8); }
+
+/* Chain::fromRuleToHorusKeyValue + horusFromRulesToMap (Utils.cpp:537-630):
+ * the leading rules whose key sets the same fields as rule 0 (a /32 address,
+ * protocol, ports; anything else the rule matches on is not part of the key),
+ * up to the first rule with a conntrack match; std::map::insert keeps the
+ * first rule of a repeated key. */
+static void horus_build(orc_ctx *c) {
+  const ochain_t *in = &c->ch[ORC_INPUT];
+  uint32_t set_fields = 0;
+  hzent_t key;
+  memset(&key, 0, sizeof key);        /* one HorusRule reused for every rule (Utils.cpp:604) */
+  c->hz_n = 0;
+  for (int i = 0; i < in->nrules && i < HZ_MAX; i++) {
+    const prule_t *r = &in->rules[i];
+    if (r->ct_set) break;             /* fromRuleToHorusKeyValue returns false: stop */
+    uint32_t f = 0;
+    if (r->src_set && r->src.netmask == 32) { f |= ORC_HZ_SRCIP; key.src = r->src.ip; }
+    if (r->dst_set && r->dst.netmask == 32) { f |= ORC_HZ_DSTIP; key.dst = r->dst.ip; }
+    if (r->proto_set) { f |= ORC_HZ_L4PROTO; key.proto = (uint8_t)r->proto; }
+    if (r->sport_set) { f |= ORC_HZ_SRCPORT; key.sk = bswap16(r->sport); }
+    if (r->dport_set) { f |= ORC_HZ_DSTPORT; key.dk = bswap16(r->dport); }
+    key.action = r->action == 0 ? 0 : 1;
+    key.rule = (uint32_t)i;           /* rule->getId(): dense ids (Q12) */
+    if (i == 0) {
+      if (!f) break;
+      set_fields = f;
+    }
+    if (f != set_fields) break;
+    int dup = 0;
+    for (int k = 0; k < c->hz_n && !dup; k++) {
+      const hzent_t *e = &c->hz[k];
+      dup = e->src == key.src && e->dst == key.dst && e->proto == key.proto && e->sk == key.sk && e->dk == key.dk;
+    }
+    if (!dup) c->hz[c->hz_n++] = key;
+  }
+  c->hz_fields = set_fields;
+}
+
+/* Chain::updateChain's Horus part (Chain.cpp:505-592), run for every chain update */
+static void horus_update(orc_ctx *c, int chain) {
+  c->hz_runtime = 0;                  /* the old program goes, and its counters with it */
+  c->hz_n = 0;
+  c->hz_fields = 0;
+  memset(c->hz_pkts, 0, sizeof c->hz_pkts);
+  memset(c->hz_bytes, 0, sizeof c->hz_bytes);
+  if (chain != ORC_INPUT || !c->hz_enabled || c->service != ORC_SVC_IPTABLES) return;
+  /* MIN_RULE_SIZE_FOR_HORUS = 1 INPUT rule, FORWARD rule list empty */
+  if (c->ch[ORC_INPUT].nrules < 1 || c->ch[ORC_FORWARD].nrules != 0) return;
+  horus_build(c);
+  if (c->hz_n >= 1) c->hz_runtime = 1;
+}
+
+int orc_set_horus(orc_ctx *c, int on) {
+  if (c->service != ORC_SVC_IPTABLES) return -EINVAL;
+  c->hz_enabled = on != 0;
+  return 0;
+}
+
+int orc_horus_info(orc_ctx *c, uint32_t out[4]) {
+  out[0] = (uint32_t)c->hz_enabled; out[1] = (uint32_t)c->hz_runtime;
+  out[2] = (uint32_t)c->hz_n; out[3] = c->hz_fields;
+  return 0;
+}
+
+int orc_read_horus_counters(orc_ctx *c, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush) {
+  for (uint32_t i = 0; i < n; i++) {
+    const int ok = i < HZ_MAX;
+    if (pkts) pkts[i] = ok ? c->hz_pkts[i] : 0;
+    if (bytes) bytes[i] = ok ? c->hz_bytes[i] : 0;
+    if (ok && flush) { c->hz_pkts[i] = 0; c->hz_bytes[i] = 0; }   /* Horus::flushCounters */
+  }
+  return 0;
+}
+
+/* Iptables_Horus_dp.c:112-133: the packed horusKey of the per-CPU packet
+ * struct.  The Parser writes the naturally aligned struct (srcPort at bytes
+ * 10-11, dstPort at 12-13, byte 9 padding that nothing writes), and Horus
+ * reads it through a packed declaration (srcPort at 9-10, dstPort at 11-12):
+ * rs/rd are the Parser's srcPort/dstPort as stored (wire bytes 34-35, 36-37). */
+static const hzent_t *horus_lookup(const orc_ctx *c, uint32_t saddr, uint32_t daddr, uint8_t proto, uint16_t rs,
+                                   uint16_t rd) {
+  const uint32_t F = c->hz_fields;
+  const uint16_t sk = (uint16_t)((rs & 0xff) << 8);                /* bytes 9-10: [0, wire34] */
+  const uint16_t dk = (uint16_t)((rs >> 8) | ((rd & 0xff) << 8));  /* bytes 11-12: [wire35, wire36] */
+  for (int k = 0; k < c->hz_n; k++) {
+    const hzent_t *e = &c->hz[k];
+    if ((F & ORC_HZ_SRCIP) && e->src != saddr) continue;
+    if ((F & ORC_HZ_DSTIP) && e->dst != daddr) continue;
+    if ((F & ORC_HZ_L4PROTO) && e->proto != proto) continue;
+    if ((F & ORC_HZ_SRCPORT) && e->sk != sk) continue;
+    if ((F & ORC_HZ_DSTPORT) && e->dk != dk) continue;
+    return e;
+  }
+  return NULL;
 }
 
 int orc_set_service(orc_ctx *c, int service, int fw_ct_mode) {
@@ -590,6 +707,7 @@ typedef struct {        /* per-CPU counters (percpu arrays) */
   uint64_t *pkts[NCHAINS], *bytes[NCHAINS];
   uint64_t dpk[NCHAINS], dby[NCHAINS];
   uint64_t ae_pkts[NCHAINS], ae_bytes[NCHAINS];   /* pkts_/bytes_acceptestablished_<Chain> */
+  uint64_t *hz_pkts, *hz_bytes;                   /* pkts_horus / bytes_horus */
 } pcpu_t;
 
 static inline uint16_t be16(const uint8_t *p) { return (uint16_t)(p[0] << 8 | p[1]); }
@@ -900,7 +1018,7 @@ static inline int default_verdict(const ochain_t *ch, pcpu_t *pc, int chain, uin
 /* st != NULL: stateful conntrack (labels from and updates to st, one packet
  * at a time); else labels come from ct_in or an empty table. */
 static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, uint32_t L, uint16_t port,
-                        int ct_in, pcpu_t *pc, int32_t *rid, struct ctstate *st, int *label) {
+                        int ct_in, pcpu_t *pc, int32_t *rid, struct ctstate *st, int *label, uint16_t *hzp) {
   *rid = -2;
   *label = 255;
   /* TC hook: the receive path strips the outer 802.1Q / 802.1ad tag before
@@ -933,13 +1051,31 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     memcpy(&sport, f + 34, 2); memcpy(&dport, f + 36, 2);
     if (st) { st->sport = sport; st->dport = dport; }
   }
+  if (!st && hzp && (proto == 6 || proto == 17)) { hzp[0] = sport; hzp[1] = dport; }
   ctpkt_t cp;
   if (st) cp = (ctpkt_t){saddr, daddr, (uint8_t)proto, st->sport, st->dport, st->flags, st->seq, st->ack};
+  /* Horus (Parser_dp.c:145-147 -> Horus_dp.c:97-167), ingress only: the
+   * egress Parser's tail call lands on an empty program slot */
+  int pass_labeling = 0, chain = -1, ct;
+  if (dir == ORC_INGRESS && c->hz_runtime) {
+    uint16_t rs = sport, rd = dport;                       /* written by this packet */
+    if (proto != 6 && proto != 17) {                       /* stale (Q4) */
+      rs = st ? st->sport : hzp ? hzp[0] : 0;
+      rd = st ? st->dport : hzp ? hzp[1] : 0;
+    }
+    const hzent_t *e = horus_lookup(c, saddr, daddr, (uint8_t)proto, rs, rd);
+    if (e) {
+      pc->hz_pkts[e->rule] += 1; pc->hz_bytes[e->rule] += L;
+      *rid = ORC_RID_HORUS0 - (int32_t)e->rule;
+      if (e->action == 0) return RX_DROP;
+      pass_labeling = 1;                                   /* PASS_LABELING -> ConntrackLabel */
+      goto labeling;
+    }
+  }
   /* ports as the NBO u16 the eBPF hash keys hold; the maps store ntohs(port) */
   sport = (uint16_t)(sport >> 8 | sport << 8);
   dport = (uint16_t)(dport >> 8 | dport << 8);
 
-  int chain, ct;
   if (c->service == ORC_SVC_FIREWALL) {
     /* pcn-firewall: Firewall_Parser_dp.c:94-165 -> [ConntrackLabel, when the
      * conntrack mode is not DISABLED (modules/Parser.cpp:41-45)] ->
@@ -982,7 +1118,6 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     goto rules;
   }
   /* ChainSelector_dp.c:131-298 */
-  int pass_labeling = 0;
   if (dir == ORC_INGRESS) {
     const ochain_t *in = &c->ch[ORC_INPUT], *fw = &c->ch[ORC_FORWARD];
     if (in->default_action == 1 && fw->default_action == 1 && in->nrules == 0 &&
@@ -1001,6 +1136,7 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     if (c->ch[chain].default_action == 0) return RX_DROP; /* DROP_NO_LABELING */
     pass_labeling = 1;
   }
+labeling:
   if (st) {
     ct = ct_label(st, &cp, f, L);                    /* ConntrackLabel_dp.c:190-531 */
     if (ct < 0) return RX_DROP;
@@ -1107,6 +1243,7 @@ typedef struct {
   const orc_ctx *c; int dir; int hook; const uint8_t *frames; const uint32_t *offsets; const uint16_t *lens;
   uint32_t stride, fixed_len; const uint16_t *in_port; uint16_t const_port; const uint8_t *ct;
   uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc; struct ctstate *st; uint8_t *labels;
+  uint16_t *hzp;   /* stale ports for Horus keys while conntrack is off (NULL: not tracked) */
 } job_t;
 
 static void *run_job(void *arg) {
@@ -1118,7 +1255,7 @@ static void *run_job(void *arg) {
     int ct = j->ct ? j->ct[i] : -1;
     int32_t rid;
     int lab;
-    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st, &lab);
+    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st, &lab, j->hzp);
     if (j->labels) j->labels[i] = (uint8_t)lab;
     j->verdicts[i] = v == RX_DROP ? 0 : 1;
     if (j->rule_ids) j->rule_ids[i] = rid;
@@ -1140,6 +1277,11 @@ int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, co
                         uint64_t n, uint8_t *verdicts, int32_t *rule_ids, uint8_t *labels, int nthreads) {
   if (c->ct && ct_status) return -EINVAL;   /* labels come from the table */
   if (c->ct) nthreads = 1;                   /* one packet at a time, in batch order */
+  /* with horus on, the Parser's stale ports (read by Horus keys) are tracked
+   * from packet to packet: one packet at a time too.  They are tracked only
+   * while horus is on (or conntrack, which keeps its own): the GPU does the same. */
+  uint16_t *hzp = c->hz_enabled && !c->ct ? c->hz_stale : NULL;
+  if (hzp) nthreads = 1;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   job_t *jobs = calloc((size_t)nthreads, sizeof(job_t));
@@ -1148,11 +1290,13 @@ int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, co
     job_t *j = &jobs[t];
     *j = (job_t){c, dir, hook, frames, offsets, lens, stride, fixed_len, in_port, const_port, ct_status,
                  n * t / nthreads, n * (t + 1) / nthreads, verdicts, rule_ids,
-                 {{0}, {0}, {0}, {0}, {0}, {0}}, c->ct, labels};
+                 {{0}, {0}, {0}, {0}, {0}, {0}, NULL, NULL}, c->ct, labels, hzp};
     for (int k = 0; k < NCHAINS; k++) {
       j->pc.pkts[k] = calloc(c->max_counted, 8);
       j->pc.bytes[k] = calloc(c->max_counted, 8);
     }
+    j->pc.hz_pkts = calloc(HZ_MAX, 8);
+    j->pc.hz_bytes = calloc(HZ_MAX, 8);
   }
   for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, run_job, &jobs[t]);
   run_job(&jobs[0]);
@@ -1170,6 +1314,11 @@ int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, co
       c->ae_bytes[k] += jobs[t].pc.ae_bytes[k];
       free(jobs[t].pc.pkts[k]); free(jobs[t].pc.bytes[k]);
     }
+    for (int r = 0; r < HZ_MAX; r++) {
+      c->hz_pkts[r] += jobs[t].pc.hz_pkts[r];
+      c->hz_bytes[r] += jobs[t].pc.hz_bytes[r];
+    }
+    free(jobs[t].pc.hz_pkts); free(jobs[t].pc.hz_bytes);
   }
   free(jobs); free(th);
   return 0;

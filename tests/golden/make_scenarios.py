@@ -210,6 +210,21 @@ def scenarios():
         step([["flush", "FORWARD"], ["interactive", False]] + big + [["apply", "FORWARD"]], nping_udp(), "pass",
              counters={"chain": "FORWARD", "rule": 1, "pkts": 5}),
     ]})
+    # ---------------- local_test_horus1.sh ----------------
+    # `polycubectl pcn-iptables set horus=ON|OFF` only sets the flag
+    # (Iptables::setHorus); the next INPUT update builds the Horus program.
+    t = "src/services/pcn-iptables/test/local_test_horus1.sh"
+    out.append({"name": "local_test_horus1", "source": t, "steps": [
+        step([], ping_host(), "pass", f"{t}:16"),
+        step([P("INPUT", "ACCEPT"), P("OUTPUT", "ACCEPT")], ping_host(), "pass", f"{t}:21"),
+        step([P("INPUT", "DROP")], ping_host(), "fail", f"{t}:25"),
+        step([P("INPUT", "ACCEPT"), ["horus", "ON"]], ping_host(), "pass", f"{t}:31"),
+        step([A("INPUT", src=IP, action="DROP")], ping_host(), "fail", f"{t}:35"),
+        step([D("INPUT", src=IP, action="DROP")], ping_host(), "pass", f"{t}:41"),
+        step([["horus", "OFF"]], ping_host(), "pass", f"{t}:47"),
+        step([A("INPUT", src=IP, action="DROP")], ping_host(), "fail", f"{t}:51"),
+        step([D("INPUT", src=IP, action="DROP")], ping_host(), "pass", f"{t}:55"),
+    ]})
     return out
 
 

@@ -111,6 +111,9 @@ class OracleCube:
         if kind == "interactive":
             self.interactive = bool(op[1])
             return
+        if kind == "horus":                       # Iptables::setHorus: the flag only
+            self.o.set_horus(op[1] == "ON")
+            return
         c = op[1]
         if kind == "append":
             self.rules[c].append(op[2])
@@ -187,6 +190,9 @@ class GpuCube:
         kind = op[0]
         if kind == "interactive":
             self.ipt.interactive = bool(op[1])
+            return
+        if kind == "horus":
+            self.ipt.horus = op[1]
             return
         ch = self.ipt.chain(op[1])
         if kind == "append":
