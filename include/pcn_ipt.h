@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 3
+#define PCN_IPT_ABI_VERSION 4
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -315,6 +315,46 @@ int pcn_ipt_ct_get_info(pcn_ipt *ctx, pcn_ipt_ct_info *out);
 int pcn_ipt_set_accept_established(pcn_ipt *ctx, int chain, int on);
 int pcn_ipt_get_accept_established(pcn_ipt *ctx, int chain);
 int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, int flush);
+
+/* ---- Horus (pcn-iptables `horus` leaf, iptables.yang:112-118) ----------- */
+/* The exact-match prefilter of pcn-iptables, OFF by default (Iptables.h:185).
+ * pcn_ipt_set_horus only sets the flag (Iptables::setHorus, Iptables.cpp:
+ * 400-406).  Every chain update (verbs, apply, default change) drops the Horus
+ * table and its counters, and an INPUT update with horus on, INPUT rules and
+ * no FORWARD rules builds a new one (Chain::updateChain, Chain.cpp:505-592)
+ * from the leading INPUT rules that set the same key fields as rule 0: a /32
+ * source / destination, protocol, ports; the table ends at the first rule with
+ * another pattern or a conntrack match, and a repeated key keeps its first
+ * rule (Chain::horusFromRulesToMap, Utils.cpp:537-630).
+ * The datapath looks every parsed ingress IPv4 packet up after the Parser and
+ * before the ChainSelector (Iptables_Parser_dp.c:145-147), so forwarded
+ * traffic meets INPUT rules too.  A hit bumps the Horus counters of its rule
+ * and reports rule id PCN_IPT_RID_HORUS0 - <INPUT rule id>; DROP drops,
+ * ACCEPT continues as PASS_LABELING (ICMP length checks, labels, conntrack
+ * update, accept; Iptables_Horus_dp.c:136-161).  The key's ports are read as
+ * the reference reads them, through a packed struct laid over the aligned
+ * one the Parser writes: source port = [0, first source-port byte], destination
+ * port = [second source-port byte, first destination-port byte]; a packet the
+ * Parser writes no ports for (ICMP, GRE ...) keys on the ports the last TCP/UDP
+ * packet left (Q4), tracked from the moment horus is set (or, with conntrack
+ * on, by the connection table's own copy).  pcn_ipt_chain_stats adds (and
+ * flushes) the Horus counters of rule id k to rule k of whichever chain is
+ * read, as ChainStats::fetchCounters does (ChainStats.cpp:106-121).
+ * pcn-iptables only; pcn-firewall contexts refuse it. */
+#define PCN_IPT_RID_HORUS0 (-4096)
+#define PCN_IPT_HORUS_MAX 2048                       /* HorusConst::MAX_RULE_SIZE_FOR_HORUS */
+enum { PCN_IPT_HZ_SRCIP = 1, PCN_IPT_HZ_DSTIP = 2, PCN_IPT_HZ_L4PROTO = 4, PCN_IPT_HZ_SRCPORT = 8,
+       PCN_IPT_HZ_DSTPORT = 16 };
+typedef struct {
+  uint32_t enabled;          /* the horus leaf */
+  uint32_t runtime;          /* a Horus table is in place (horus_runtime_enabled_) */
+  uint32_t entries;          /* keys in the table */
+  uint32_t fields;           /* PCN_IPT_HZ_* set fields of the key */
+} pcn_ipt_horus_info;
+int pcn_ipt_set_horus(pcn_ipt *ctx, int on);
+int pcn_ipt_get_horus_info(pcn_ipt *ctx, pcn_ipt_horus_info *out);
+/* pkts_horus / bytes_horus[rule id] (Iptables_Horus_dp.c:77-90) */
+int pcn_ipt_read_horus_counters(pcn_ipt *ctx, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush);
 
 /* ---- pcn-firewall personality ------------------------------------------ */
 /* pcn-firewall (src/services/pcn-firewall) runs the same field modules,

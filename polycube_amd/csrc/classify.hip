@@ -159,7 +159,7 @@ __device__ __forceinline__ void load_generic(const uint8_t *frames, uint64_t fra
     const u32x4d *p = reinterpret_cast<const u32x4d *>(frames + base);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const u32x4d v = hdr_load(p + q);
+      const u32x4d v = __builtin_nontemporal_load(p + q);   // (a template would drop the 4-byte alignment)
       d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
     }
   } else {
@@ -238,6 +238,28 @@ __device__ __forceinline__ uint32_t key_class(const Tab<LDS> &t, uint32_t tab, u
   const bool m0 = e0 != PCN_HASH_EMPTY && (e0 >> 16) == key;
   const bool m1 = e1 != PCN_HASH_EMPTY && (e1 >> 16) == key;
   return m0 ? (e0 & 0xffff) : (m1 ? (e1 & 0xffff) : wild);
+}
+
+// Horus (Iptables_Horus_dp.c:112-133): the packed key of the per-CPU packet
+// struct.  pd = the Parser's srcPort/dstPort as stored (wire bytes 34-37 as
+// a little-endian dword); the packed struct reads bytes 9-10 / 11-12 of the
+// aligned one: [padding 0, first source-port byte] and [second source-port
+// byte, first destination-port byte].
+__device__ __forceinline__ bool horus_lookup(const LaunchArgs &a, uint32_t saddr, uint32_t daddr, uint32_t proto,
+                                             uint32_t pd, uint32_t &meta) {
+  const uint32_t F = a.horus_fields;
+  const uint32_t sk = (pd & 0xffu) << 8, dk = ((pd >> 8) & 0xffu) | (((pd >> 16) & 0xffu) << 8);
+  const uint32_t ks = (F & PCN_IPT_HZ_SRCIP) ? saddr : 0u, kd = (F & PCN_IPT_HZ_DSTIP) ? daddr : 0u;
+  const uint32_t kp = (F & PCN_IPT_HZ_L4PROTO) ? proto : 0u;
+  const uint32_t kports = ((F & PCN_IPT_HZ_SRCPORT) ? sk : 0u) | (((F & PCN_IPT_HZ_DSTPORT) ? dk : 0u) << 16);
+  uint32_t slot = horus_hash(ks, kd, kports, kp) & a.horus_mask;
+  for (uint32_t k = 0; k < a.horus_probes; ++k) {
+    const u32x4 e = *reinterpret_cast<const u32x4 *>(a.horus + 4 * slot);
+    if (!(e.w & kHorusUsed)) return false;
+    if (e.x == ks && e.y == kd && e.z == kports && (e.w & 0xffu) == kp) { meta = e.w; return true; }
+    slot = (slot + 1) & a.horus_mask;
+  }
+  return false;
 }
 
 struct Parsed {
@@ -574,7 +596,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   struct Stage {
     Hdr h;          // generic path
     u32x4 c[3];     // fixed path: this lane's three chunks
-    uint32_t L, port, ct;
+    uint32_t L, port, ct, stale;
   };
   const uint32_t lane = threadIdx.x & 63;
   // fixed path: frame within the wave's group, byte offset of the chunk, and
@@ -590,6 +612,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // per-frame side inputs a chain program knows it does not have are never loaded
   constexpr bool kLoadPort = !JIT || (kJitInputs & 1);
   constexpr bool kLoadCt = !JIT || (kJitInputs & 6);
+  constexpr bool kLoadStale = !JIT || (kJitInputs & 8);
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   constexpr int PF = FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
   Stage st[PF];
@@ -624,6 +647,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     const uint64_t jc = j < a.n ? j : last;
     x.port = kLoadPort ? a.in_port[jc & a.in_port_mask] : 0u;
     x.ct = kLoadCt ? a.ct_status[jc & a.ct_mask] : 0u;
+    x.stale = kLoadStale ? a.stale_ports[jc & a.stale_mask] : 0u;
   };
 #pragma unroll
   for (int d = 0; d < PF; ++d) prefetch(st[d], first + d * step);
@@ -670,9 +694,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       for (int k = 0; k < 13; ++k) asm volatile("" : "+v"(cur.h.w[k]));
       h = cur.h;
     }
-    asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
+    asm volatile("" : "+v"(cur.port), "+v"(cur.ct), "+v"(cur.stale));
     uint32_t L = FIXED ? a.fixed_len : cur.L;
-    const uint32_t cur_port = cur.port, cur_ct = cur.ct;
+    const uint32_t cur_port = cur.port, cur_ct = cur.ct, cur_stale = cur.stale;
     prefetch(cur, i + PF * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
@@ -766,20 +790,37 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         }
         if (done) chain = -1;
       } else if (!done) {
-        // ---- ChainSelector_dp.c:131-298 ----
         bool pass = false;
-        if (a.direction == PCN_IPT_INGRESS) {
-          if (a.allow_logic) pass = true;
-          else chain = (a.nlocal && localip_has(a, p.daddr)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
-        } else {
-          if (a.nlocal && localip_has(a, p.saddr)) chain = PCN_IPT_OUTPUT;
-          else { verdict = PCN_IPT_ACCEPT; done = true; }   // egress PASS
+        // ---- Horus (Parser_dp.c:145-147 -> Horus_dp.c:97-167), ingress ----
+        if (a.horus_fields && a.direction == PCN_IPT_INGRESS) {
+          const uint32_t pd = (p.proto == 6 || p.proto == 17) ? ((h.w[8] >> 16) | (h.w[9] << 16)) : cur_stale;
+          uint32_t meta;
+          if (horus_lookup(a, p.saddr, p.daddr, p.proto, pd, meta)) {
+            const uint32_t id = meta >> 16;
+            if (a.horus_ctr) {
+              atomicAdd(&a.horus_ctr[2 * id], 1ull);
+              atomicAdd(&a.horus_ctr[2 * id + 1], static_cast<unsigned long long>(L));
+            }
+            rid = PCN_IPT_RID_HORUS0 - static_cast<int32_t>(id);
+            if ((meta >> 8) & 1) pass = true;                 // ACCEPT: PASS_LABELING
+            else { verdict = PCN_IPT_DROP; done = true; }
+          }
         }
-        if (!done && chain >= 0 && ((a.empty_mask >> chain) & 1)) {
-          cchain = chain; rid = PCN_IPT_RID_DEFAULT;       // default counters
-          if ((a.drop_mask >> chain) & 1) { verdict = PCN_IPT_DROP; done = true; }
-          pass = true;
-          chain = -1;
+        // ---- ChainSelector_dp.c:131-298 ----
+        if (!done && !pass) {
+          if (a.direction == PCN_IPT_INGRESS) {
+            if (a.allow_logic) pass = true;
+            else chain = (a.nlocal && localip_has(a, p.daddr)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
+          } else {
+            if (a.nlocal && localip_has(a, p.saddr)) chain = PCN_IPT_OUTPUT;
+            else { verdict = PCN_IPT_ACCEPT; done = true; }   // egress PASS
+          }
+          if (!done && chain >= 0 && ((a.empty_mask >> chain) & 1)) {
+            cchain = chain; rid = PCN_IPT_RID_DEFAULT;       // default counters
+            if ((a.drop_mask >> chain) & 1) { verdict = PCN_IPT_DROP; done = true; }
+            pass = true;
+            chain = -1;
+          }
         }
         // ---- ConntrackLabel_dp.c:436-531 ICMP length checks ----
         uint32_t icmp_type = 0xffffffffu;

@@ -172,7 +172,13 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *
     bool pass = false;
     if (p.status == 2) {
       bool labeled = true;
-      if (b.fw) {
+      // a Horus hit (stage A found it: the same for every label) skips the
+      // ChainSelector: DROP is final, ACCEPT is PASS_LABELING (Horus_dp.c:150-160)
+      const bool horus = !b.fw && b.a_rid[i] <= PCN_IPT_RID_HORUS0;
+      if (horus) {
+        if (b.a_verdict[i] == PCN_IPT_ACCEPT) pass = true;
+        else labeled = false;
+      } else if (b.fw) {
         // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder
         // (Firewall_ChainForwarder_dp.c:20-42).  An empty chain goes to
         // DefaultAction after labelling, which stage A already resolved.
@@ -640,6 +646,14 @@ __global__ void ct_count_kernel(CtBatch b, const CtRec *rec) {
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const int32_t rid = b.rule_ids[i];
     const CtRec &r = rec[i];
+    if (rid <= PCN_IPT_RID_HORUS0) {                  // Horus_dp.c:80-90, counted at the lookup
+      if (b.horus_ctr) {
+        const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
+        atomicAdd(&b.horus_ctr[2 * id], 1ull);
+        atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(r.len));
+      }
+      continue;
+    }
     const uint32_t c = r.cinfo & 3;
     if (c == 3) continue;
     uint32_t bin;
@@ -718,6 +732,11 @@ struct CtScratch {
   WalkRec *wrec = nullptr;
   void *temp = nullptr;
   size_t temp_bytes = 0;
+  // ct_stale_ports alone (stateless batches): parse flags, scan, ports
+  uint32_t *zpp = nullptr, *zlast = nullptr, *zports = nullptr;
+  uint64_t zcap = 0;
+  void *ztemp = nullptr;
+  size_t ztemp_bytes = 0;
 };
 
 CtScratch *ct_scratch_new() { return new CtScratch(); }
@@ -728,7 +747,9 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
                   static_cast<void *>(s->hard_cnt), static_cast<void *>(s->rec), static_cast<void *>(s->wrec),
-                  static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp})
+                  static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
+                  static_cast<void *>(s->zpp), static_cast<void *>(s->zlast), static_cast<void *>(s->zports),
+                  s->ztemp})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -782,6 +803,48 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     if (s.temp) CT_CHECK(hipFree(s.temp));
     CT_CHECK(hipMalloc(&s.temp, need));
     s.temp_bytes = need;
+  }
+  return hipSuccess;
+}
+
+__global__ void stale_kernel(uint64_t n, const uint32_t *last, const uint32_t *pports, const uint32_t *carry,
+                             uint32_t *out) {
+  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += step)
+    out[i] = last[i] ? pports[last[i] - 1] : *carry;
+}
+
+int ct_stale_ports(const CtBatch &b, CtScratch &s, uint32_t *carry, bool update_carry, uint32_t *out, int num_cus,
+                   void *stream) {
+  if (b.n == 0) return hipSuccess;
+  if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (s.zcap < b.n) {
+    for (uint32_t **p : {&s.zpp, &s.zlast, &s.zports}) {
+      if (*p) CT_CHECK(hipFree(*p));
+      CT_CHECK(hipMalloc(p, b.n * 4));
+    }
+    s.zcap = b.n;
+  }
+  size_t need = 0;
+  CT_CHECK(hipcub::DeviceScan::InclusiveScan(nullptr, need, s.zpp, s.zlast, hipcub::Max(), int(b.n), st));
+  if (s.ztemp_bytes < need) {
+    if (s.ztemp) CT_CHECK(hipFree(s.ztemp));
+    CT_CHECK(hipMalloc(&s.ztemp, need));
+    s.ztemp_bytes = need;
+  }
+  const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
+  hipLaunchKernelGGL(ct_parse_kernel, dim3(grid), dim3(blk), 0, st, b, s.zpp, s.zports);
+  CT_CHECK(hipGetLastError());
+  size_t tb = s.ztemp_bytes;
+  CT_CHECK(hipcub::DeviceScan::InclusiveScan(s.ztemp, tb, s.zpp, s.zlast, hipcub::Max(), int(b.n), st));
+  if (out) {
+    hipLaunchKernelGGL(stale_kernel, dim3(grid), dim3(blk), 0, st, b.n, s.zlast, s.zports, carry, out);
+    CT_CHECK(hipGetLastError());
+  }
+  if (update_carry) {
+    hipLaunchKernelGGL(ct_carry_kernel, dim3(1), dim3(64), 0, st, b.n, s.zlast, s.zports, carry);
+    CT_CHECK(hipGetLastError());
   }
   return hipSuccess;
 }

@@ -59,6 +59,8 @@ struct CtBatch {
   unsigned long long *ctr[3];
   uint32_t ncounted[3];
   unsigned long long *ae_ctr; // [3][2] pkts, bytes
+  unsigned long long *horus_ctr;  // [PCN_IPT_HORUS_MAX][2] (null: Horus off); Horus hits are the
+                                  // packets with rule id <= PCN_IPT_RID_HORUS0 (stage A found them)
 };
 
 struct CtTable {
@@ -91,6 +93,13 @@ int ct_flow_owner(const CtBatch &b, uint32_t nranks, uint8_t *owner, int num_cus
 int ct_flow_split(const CtBatch &b, const uint16_t *in_port, uint16_t const_in_port, uint32_t nranks, uint32_t rank,
                   uint32_t *index, uint32_t *offsets, uint16_t *lens, uint16_t *in_port_out, uint64_t *n_out,
                   int num_cus, void *stream);
+
+// The ports the shared `packet` struct holds for every frame of a batch (Q4):
+// out[i] = the ports dword (wire bytes 34-37) of the last frame <= i the
+// Parser wrote ports for, else *carry.  update_carry: *carry becomes the
+// batch's last such frame's ports.  out may be null (carry update only).
+int ct_stale_ports(const CtBatch &b, CtScratch &s, uint32_t *carry, bool update_carry, uint32_t *out, int num_cus,
+                   void *stream);
 
 int ct_table_init(CtTable &t, uint32_t cap_log2);
 void ct_table_free(CtTable &t);

@@ -48,7 +48,28 @@
 #define PCN_WAVE_SCRATCH_BYTES 1280 // the candidate-stage scratch alone: the whole region of a launch
                                     // without the fixed-stride header transpose
 
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+#define PCN_HD __host__ __device__
+#else
+#define PCN_HD
+#endif
+
 namespace pcn {
+
+// Horus table (pcn_ipt.h): open addressing, 16 bytes per slot
+// {src, dst, ports = sk | dk << 16, meta = proto | action << 8 | 1 << 9 (used)
+// | rule id << 16}; fields outside the key's set fields are 0 in both the
+// slot and the packet's key.  sk / dk are the key's port bytes as the
+// reference's packed horusKey holds them, read as little-endian u16.
+constexpr uint32_t kHorusUsed = 1u << 9;
+PCN_HD inline uint32_t horus_hash(uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto) {
+  uint64_t h = ((uint64_t(src) << 32) | dst) * 0x9E3779B97F4A7C15ull;
+  h ^= ((uint64_t(ports) << 8) | proto) * 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 32;
+  return static_cast<uint32_t>(h);
+}
 
 // Byte offsets inside a table image (all 16-byte aligned).
 struct TableLayout {
@@ -141,6 +162,16 @@ struct LaunchArgs {
   uint32_t fw;                   // 0: pcn-iptables dispatch; else pcn-firewall, PCN_FW_LAUNCH_*
   int32_t fast_chain;            // >= 0: every IPv4 TCP/UDP frame selects this chain (no localip,
                                  // allow logic or empty chain involved); -1: no wave fast path
+  // Horus (ingress pcn-iptables launches only; horus_fields == 0: off)
+  const uint32_t *horus;         // 4 u32 per slot
+  uint32_t horus_mask;           // slots - 1
+  uint32_t horus_probes;         // longest probe sequence of a stored key
+  uint32_t horus_fields;         // PCN_IPT_HZ_* set fields of the key
+  uint32_t has_stale;            // per-frame stale ports given (the key has port fields)
+  unsigned long long *horus_ctr; // [PCN_IPT_HORUS_MAX][2] pkts, bytes; null: not counted (stage A)
+  const uint32_t *stale_ports;   // per frame: the ports dword (wire bytes 34-37) of the last TCP/UDP
+                                 // packet before it (Q4); the zero cell with mask 0 when absent
+  uint64_t stale_mask;
 };
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)

@@ -152,6 +152,15 @@ struct pcn_ipt {
   // the previous one's last conntrack kernel.
   hipEvent_t ev_ct = nullptr;
   bool ct_pending = false;
+  // Horus (pcn_ipt.h): the flag, the table in place and its counters
+  bool hz_enabled = false, hz_runtime = false;
+  uint32_t hz_fields = 0, hz_entries = 0, hz_mask = 0, hz_probes = 0;
+  uint32_t *d_horus = nullptr;                 // 4 u32 per slot
+  size_t d_horus_cap = 0;
+  unsigned long long *d_hz_ctr = nullptr;      // [PCN_IPT_HORUS_MAX][2]
+  uint32_t *d_hz_carry = nullptr;              // the Parser's stale ports while conntrack is off
+  uint32_t *d_stale = nullptr;                 // per-frame stale ports of the batch being classified
+  size_t stale_cap = 0;
 };
 
 namespace pcn {
@@ -229,6 +238,19 @@ void fetch_stats(pcn_ipt *ctx, int chain) {
     cs.stats[id].second += buf[3 + 2 * id];
   }
   hip_check(hipMemset(cs.ctr + 2, 0, 2 * size_t(n) * 8), "hipMemset(counters)");
+  // while a Horus table is in place, rule k of the chain read also takes (and
+  // flushes) Horus's counters of rule id k, whichever chain it is
+  // (ChainStats.cpp:106-121)
+  if (ctx->hz_runtime && !cs.stats.empty()) {
+    const size_t m = std::min<size_t>(cs.stats.size(), PCN_IPT_HORUS_MAX);
+    std::vector<unsigned long long> hz(2 * m);
+    hip_check(hipMemcpy(hz.data(), ctx->d_hz_ctr, hz.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(horus counters)");
+    for (size_t id = 0; id < m; ++id) {
+      cs.stats[id].first += hz[2 * id];
+      cs.stats[id].second += hz[2 * id + 1];
+    }
+    hip_check(hipMemset(ctx->d_hz_ctr, 0, hz.size() * 8), "hipMemset(horus counters)");
+  }
   // rule 0 of an accept-established chain also takes (and flushes) the
   // accept-established counters (ChainStats.cpp:64-103)
   if (ctx->ae[chain] && !cs.stats.empty()) {
@@ -257,9 +279,96 @@ void apply_ae(pcn_ipt *ctx, int chain) {
   else for (int c = chain; c < PCN_IPT_NCHAINS; ++c) ctx->ae[c] = false;
 }
 
+// Chain::fromRuleToHorusKeyValue + horusFromRulesToMap (Utils.cpp:537-630):
+// the leading INPUT rules that set the same key fields as rule 0 (a /32
+// address, protocol, ports), up to the first conntrack rule; a repeated key
+// keeps its first rule (std::map::insert).
+struct HorusEntry {
+  uint32_t src, dst, ports, meta;   // devchain.h slot layout
+};
+std::vector<HorusEntry> horus_entries(const std::vector<Rule> &rules, uint32_t &fields) {
+  std::vector<HorusEntry> out;
+  uint32_t set_fields = 0;
+  HorusEntry key{0, 0, 0, 0};
+  uint8_t proto = 0;
+  for (size_t i = 0; i < rules.size() && i < PCN_IPT_HORUS_MAX; ++i) {
+    const Rule &r = rules[i];
+    if (r.conntrack) break;
+    uint32_t f = 0;
+    if (r.src && r.src->len == 32) { f |= PCN_IPT_HZ_SRCIP; key.src = r.src->ip; }
+    if (r.dst && r.dst->len == 32) { f |= PCN_IPT_HZ_DSTIP; key.dst = r.dst->ip; }
+    if (r.l4proto) { f |= PCN_IPT_HZ_L4PROTO; proto = *r.l4proto; }
+    // ports: htons(port) as the packed key holds it (modules/Horus.cpp:44-51), read as a LE u16
+    auto be = [](uint16_t x) { return static_cast<uint32_t>(((x & 0xff) << 8) | (x >> 8)); };
+    if (r.sport) { f |= PCN_IPT_HZ_SRCPORT; key.ports = (key.ports & 0xffff0000u) | be(*r.sport); }
+    if (r.dport) { f |= PCN_IPT_HZ_DSTPORT; key.ports = (key.ports & 0xffffu) | (be(*r.dport) << 16); }
+    if (i == 0) {
+      if (!f) break;
+      set_fields = f;
+    }
+    if (f != set_fields) break;
+    HorusEntry e{(f & PCN_IPT_HZ_SRCIP) ? key.src : 0u, (f & PCN_IPT_HZ_DSTIP) ? key.dst : 0u,
+                 ((f & PCN_IPT_HZ_SRCPORT) ? (key.ports & 0xffffu) : 0u) |
+                     ((f & PCN_IPT_HZ_DSTPORT) ? (key.ports & 0xffff0000u) : 0u),
+                 ((f & PCN_IPT_HZ_L4PROTO) ? proto : 0u) | (r.action == PCN_IPT_ACCEPT ? 0x100u : 0u) |
+                     kHorusUsed | (static_cast<uint32_t>(i) << 16)};
+    bool dup = false;
+    for (const HorusEntry &x : out)
+      dup = dup || (x.src == e.src && x.dst == e.dst && x.ports == e.ports && (x.meta & 0xff) == (e.meta & 0xff));
+    if (!dup) out.push_back(e);
+  }
+  fields = set_fields;
+  return out;
+}
+
+// Chain::updateChain's Horus part (Chain.cpp:505-592), after every chain
+// update: the old table and its counters go; an INPUT update with horus on,
+// INPUT rules and an empty FORWARD rule list builds a new one.
+void horus_update(pcn_ipt *ctx, int chain) {
+  ctx->hz_runtime = false;
+  ctx->hz_entries = ctx->hz_fields = 0;
+  if (ctx->has_device) {
+    device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    hip_check(hipMemset(ctx->d_hz_ctr, 0, PCN_IPT_HORUS_MAX * 16), "hipMemset(horus counters)");
+  }
+  if (chain != PCN_IPT_INPUT || !ctx->hz_enabled || ctx->service != PCN_IPT_SERVICE_IPTABLES) return;
+  if (ctx->chains[PCN_IPT_INPUT].rules.empty() || !ctx->chains[PCN_IPT_FORWARD].rules.empty()) return;
+  uint32_t fields = 0;
+  const std::vector<HorusEntry> ents = horus_entries(ctx->chains[PCN_IPT_INPUT].rules, fields);
+  if (ents.empty()) return;
+  // open addressing at load <= 1/2, linear probing; the kernel probes at most `probes` slots
+  uint32_t size = 16;
+  while (size < 2 * ents.size()) size <<= 1;
+  std::vector<HorusEntry> tab(size, HorusEntry{0, 0, 0, 0});
+  uint32_t probes = 1;
+  for (const HorusEntry &e : ents) {
+    uint32_t slot = horus_hash(e.src, e.dst, e.ports, e.meta & 0xff) & (size - 1), k = 1;
+    while (tab[slot].meta & kHorusUsed) { slot = (slot + 1) & (size - 1); ++k; }
+    tab[slot] = e;
+    probes = std::max(probes, k);
+  }
+  if (ctx->has_device) {
+    const size_t bytes = size_t(size) * sizeof(HorusEntry);
+    if (ctx->d_horus_cap < bytes) {
+      if (ctx->d_horus) hip_check(hipFree(ctx->d_horus), "hipFree");
+      ctx->d_horus = nullptr;
+      hip_check(hipMalloc(&ctx->d_horus, bytes), "hipMalloc(horus table)");
+      ctx->d_horus_cap = bytes;
+    }
+    hip_check(hipMemcpy(ctx->d_horus, tab.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(horus table)");
+  }
+  ctx->hz_fields = fields;
+  ctx->hz_entries = static_cast<uint32_t>(ents.size());
+  ctx->hz_mask = size - 1;
+  ctx->hz_probes = probes;
+  ctx->hz_runtime = true;
+}
+
 void update_chain(pcn_ipt *ctx, int chain) {       // Chain::updateChain
   ChainState &cs = ctx->chains[chain];
   load_tables(ctx, chain, compile_chain(cs.rules, chain, cs.default_action, ctx->ports));
+  horus_update(ctx, chain);
 }
 
 bool valid_chain(int c) { return c >= 0 && c < PCN_IPT_NCHAINS; }
@@ -334,6 +443,10 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
       const uint8_t labels[4] = {0, 1, 2, 3};
       hip_check(hipMemcpy(ctx->d_labels, labels, 4, hipMemcpyHostToDevice), "hipMemcpy(labels)");
       hip_check(hipMalloc(&ctx->ctr_scratch, 3 * ctx->ctr_words * 8), "hipMalloc(scratch counters)");
+      hip_check(hipMalloc(&ctx->d_hz_ctr, PCN_IPT_HORUS_MAX * 16), "hipMalloc(horus counters)");
+      hip_check(hipMemset(ctx->d_hz_ctr, 0, PCN_IPT_HORUS_MAX * 16), "hipMemset(horus counters)");
+      hip_check(hipMalloc(&ctx->d_hz_carry, 64), "hipMalloc(horus carry)");
+      hip_check(hipMemset(ctx->d_hz_carry, 0, 64), "hipMemset(horus carry)");
       for (auto &cs : ctx->chains) {
         hip_check(hipMalloc(&cs.ctr, ctx->ctr_words * 8), "hipMalloc(counters)");
         hip_check(hipMemset(cs.ctr, 0, ctx->ctr_words * 8), "hipMemset(counters)");
@@ -378,6 +491,9 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     if (ctx->ev_staged) (void)hipEventDestroy(ctx->ev_staged);
     if (ctx->ev_gathered) (void)hipEventDestroy(ctx->ev_gathered);
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
+    for (void *p : {static_cast<void *>(ctx->d_horus), static_cast<void *>(ctx->d_hz_ctr),
+                    static_cast<void *>(ctx->d_hz_carry), static_cast<void *>(ctx->d_stale)})
+      if (p) (void)hipFree(p);
   }
   delete ctx;
 }
@@ -559,6 +675,7 @@ int pcn_ipt_load_chain(pcn_ipt *ctx, int chain, const pcn_ipt_tables *t) {
       }
     }
     load_tables(ctx, chain, std::move(ct));
+    horus_update(ctx, -1);     // an update without rules: no Horus table (Chain.cpp:505)
     return 0;
   });
 }
@@ -598,7 +715,7 @@ struct StageA {
   int32_t *rule_ids;
 };
 
-int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa) {
+int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa, const uint32_t *stale) {
   {
     if (!b) return fail(-EINVAL, "null batch");
     if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
@@ -724,6 +841,22 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.count_mask = b->direction == PCN_IPT_INGRESS
                        ? (1u << PCN_IPT_FORWARD) | (has_local && !firewall ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
+    // Horus: ingress pcn-iptables launches while a table is in place
+    a.stale_ports = reinterpret_cast<const uint32_t *>(ctx->d_zero);
+    a.stale_mask = 0;
+    if (ctx->hz_runtime && !firewall && b->direction == PCN_IPT_INGRESS) {
+      a.horus = ctx->d_horus;
+      a.horus_mask = ctx->hz_mask;
+      a.horus_probes = ctx->hz_probes;
+      a.horus_fields = ctx->hz_fields;
+      a.horus_ctr = sa ? nullptr : ctx->d_hz_ctr;     // stage A: ct_count counts the final outcome
+      a.fast_chain = -1;                               // the lookup lives in the general path
+      if (stale) {
+        a.stale_ports = stale;
+        a.stale_mask = ~uint64_t(0);
+        a.has_stale = 1;
+      }
+    }
     // slot count of the chain program (the generic kernel always runs 6)
     const int ns = ch < 3 ? static_cast<int>(a.ch[ch].lay.nslots) : 6;
     // chain program for this launch shape (jit.hpp), when enabled and ready
@@ -735,7 +868,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.lds = a.lds_images_bytes > 0;
       shape.ch = ch;
       shape.ns = ns;
-      shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0);
+      shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0);
       DevChain key = a.ch[ch];
       key.image = nullptr;
       key.ctr = nullptr;
@@ -784,6 +917,7 @@ CtBatch ct_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, uint32_t ae_mask) {
   }
   cb.ae_mask = ae_mask;
   cb.ae_ctr = ctx->d_ae;
+  cb.horus_ctr = ctx->hz_runtime ? ctx->d_hz_ctr : nullptr;
   cb.verdicts = b->verdicts;
   cb.rule_ids = b->rule_ids;
   return cb;
@@ -809,20 +943,54 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
     const bool firewall = ctx->service == PCN_IPT_SERVICE_FIREWALL;
+    const bool stateful = ctx->ct_on && !(firewall && ctx->fw_ct_mode == PCN_FW_CT_DISABLED);
+    // Horus keys read the Parser's stale ports (Q4): tracked from batch to
+    // batch while horus is set (the connection table keeps its own copy)
+    const bool track = ctx->hz_enabled && !firewall;
+    const bool want_stale = ctx->hz_runtime && b->direction == PCN_IPT_INGRESS &&
+                            (ctx->hz_fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT));
+    const bool serial = stateful || (track && !stateful);
+    if (serial && (!b->frames || !b->verdicts)) return fail(-EINVAL, "frames and verdicts are required");
+    device_guard(ctx);
+    // batches that share the context's conntrack / stale-port state run one
+    // after another in submission order, whatever stream each comes on
+    if (serial && ctx->ct_pending) hip_check(hipStreamWaitEvent(st, ctx->ev_ct, 0), "hipStreamWaitEvent(serial)");
+    const uint32_t *stale = nullptr;
+    if (track && (want_stale || !stateful)) {
+      if (!ctx->cts) ctx->cts = ct_scratch_new();
+      if (want_stale && ctx->stale_cap < b->n) {
+        if (ctx->d_stale) hip_check(hipFree(ctx->d_stale), "hipFree");
+        ctx->d_stale = nullptr;
+        hip_check(hipMalloc(&ctx->d_stale, b->n * 4), "hipMalloc(stale ports)");
+        ctx->stale_cap = b->n;
+      }
+      // with the connection table on, its own copy (read here, advanced by ct_run)
+      uint32_t *carry = stateful ? ctx->ct.carry : ctx->d_hz_carry;
+      const int e = ct_stale_ports(ct_batch(ctx, b, 0), *ctx->cts, carry, !stateful, want_stale ? ctx->d_stale : nullptr,
+                                   ctx->num_cus, st);
+      if (e != hipSuccess) return fail(-EIO, std::string("stale ports: ") + hipGetErrorString(hipError_t(e)));
+      stale = want_stale ? ctx->d_stale : nullptr;
+    }
+    if (!ctx->ev_ct && serial) hip_check(hipEventCreateWithFlags(&ctx->ev_ct, hipEventDisableTiming), "hipEventCreate");
+    auto mark = [&]() {
+      if (!serial) return 0;
+      hip_check(hipEventRecord(ctx->ev_ct, st), "hipEventRecord(serial)");
+      ctx->ct_pending = true;
+      return 0;
+    };
     // pcn-firewall with conntrack DISABLED: no labels and no table updates
     // (Firewall_ConntrackTableUpdate_dp.c:136-138), whatever the table holds
-    if (!ctx->ct_on || (firewall && ctx->fw_ct_mode == PCN_FW_CT_DISABLED)) {
-      int rc = launch_batch(ctx, b, stream, nullptr);
-      if (rc || !ae_mask) return rc;
+    if (!stateful) {
+      int rc = launch_batch(ctx, b, stream, nullptr, stale);
+      if (rc) return rc;
+      if (!ae_mask) return mark();
       device_guard(ctx);
       const int e = ct_ae_fixup(ct_batch(ctx, b, ae_mask), st);
       if (e != hipSuccess) return fail(-EIO, std::string("accept-established fixup: ") + hipGetErrorString(hipError_t(e)));
-      return 0;
+      return mark();
     }
     // stateful: stage A (one classify run per label that can change the outcome), then conntrack.hpp B-E
     if (b->ct_status) return fail(-EINVAL, "stateful conntrack labels packets from its table: ct_status must be NULL");
-    if (!b->frames || !b->verdicts) return fail(-EINVAL, "frames and verdicts are required");
-    device_guard(ctx);
     const uint32_t nlab = ct_rules ? 4 : 1;
     const size_t n = b->n;
     const size_t need = nlab * n * 5 + (b->rule_ids ? 0 : n * 4) + 64;
@@ -832,14 +1000,12 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       hip_check(hipMalloc(&ctx->ct_buf, need), "hipMalloc(conntrack outcomes)");
       ctx->ct_buf_cap = need;
     }
-    // the previous stateful batch (any stream) must be done with the shared buffers and the table
-    if (ctx->ct_pending) hip_check(hipStreamWaitEvent(st, ctx->ev_ct, 0), "hipStreamWaitEvent(conntrack)");
     int32_t *a_rid = static_cast<int32_t *>(ctx->ct_buf);
     int32_t *rids = b->rule_ids ? b->rule_ids : a_rid + nlab * n;
     uint8_t *a_v = reinterpret_cast<uint8_t *>(a_rid + nlab * n + (b->rule_ids ? 0 : n));
     for (uint32_t l = 0; l < nlab; ++l) {
       StageA sa{ctx->d_labels + l, a_v + l * n, a_rid + l * n};
-      int rc = launch_batch(ctx, b, stream, &sa);
+      int rc = launch_batch(ctx, b, stream, &sa, stale);
       if (rc) return rc;
     }
     // pcn-firewall AUTOMATIC: ESTABLISHED packets are accepted before the chain
@@ -854,9 +1020,7 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     cb.rule_ids = rids;
     const int e = ct_run(cb, ctx->ct, *ctx->cts, ctx->num_cus, st);
     if (e != hipSuccess) return fail(-EIO, std::string("conntrack: ") + hipGetErrorString(hipError_t(e)));
-    hip_check(hipEventRecord(ctx->ev_ct, st), "hipEventRecord(conntrack)");
-    ctx->ct_pending = true;
-    return 0;
+    return mark();
   });
 }
 
@@ -1091,7 +1255,6 @@ int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2) {
       ctx->ct.now = now;
     }
     if (!ctx->cts) ctx->cts = ct_scratch_new();
-    if (!ctx->ev_ct) hip_check(hipEventCreateWithFlags(&ctx->ev_ct, hipEventDisableTiming), "hipEventCreate");
     ctx->ct_on = true;
     return 0;
   });
@@ -1197,6 +1360,45 @@ int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uin
     }
     if (pkts) *pkts = v[0];
     if (bytes) *bytes = v[1];
+    return 0;
+  });
+}
+
+// ---- Horus ---------------------------------------------------------------
+
+int pcn_ipt_set_horus(pcn_ipt *ctx, int on) {
+  return guarded(ctx, [&] {
+    if (ctx->service != PCN_IPT_SERVICE_IPTABLES) return fail(-EINVAL, "horus is a pcn-iptables setting");
+    // Iptables::setHorus (Iptables.cpp:400-406): the flag; the next chain update acts on it
+    ctx->hz_enabled = on != 0;
+    return 0;
+  });
+}
+
+int pcn_ipt_get_horus_info(pcn_ipt *ctx, pcn_ipt_horus_info *out) {
+  return guarded(ctx, [&] {
+    if (!out) return fail(-EINVAL, "null output");
+    out->enabled = ctx->hz_enabled;
+    out->runtime = ctx->hz_runtime;
+    out->entries = ctx->hz_entries;
+    out->fields = ctx->hz_fields;
+    return 0;
+  });
+}
+
+int pcn_ipt_read_horus_counters(pcn_ipt *ctx, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush) {
+  return guarded(ctx, [&] {
+    std::vector<unsigned long long> v(2 * size_t(PCN_IPT_HORUS_MAX), 0);
+    if (ctx->has_device) {
+      device_guard(ctx);
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      hip_check(hipMemcpy(v.data(), ctx->d_hz_ctr, v.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(horus counters)");
+      if (flush) hip_check(hipMemset(ctx->d_hz_ctr, 0, v.size() * 8), "hipMemset(horus counters)");
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      if (pkts) pkts[i] = i < PCN_IPT_HORUS_MAX ? v[2 * size_t(i)] : 0;
+      if (bytes) bytes[i] = i < PCN_IPT_HORUS_MAX ? v[2 * size_t(i) + 1] : 0;
+    }
     return 0;
   });
 }

@@ -208,6 +208,29 @@ class Iptables:
     def load_chain(self, chain, tables):
         _check(ffi.lib().pcn_ipt_load_chain(self._h, chain, C.byref(tables)))
 
+    # ---- Horus (the `horus` leaf, iptables.yang:112-118) ----
+    @property
+    def horus(self):
+        """"ON" / "OFF" (Iptables::getHorus); setting it takes effect at the next chain update."""
+        return "ON" if self.horus_info()["enabled"] else "OFF"
+
+    @horus.setter
+    def horus(self, v):
+        on = v if isinstance(v, bool) else str(v).upper() == "ON"
+        _check(ffi.lib().pcn_ipt_set_horus(self._h, int(on)))
+
+    def horus_info(self):
+        out = ffi.HorusInfo()
+        _check(ffi.lib().pcn_ipt_get_horus_info(self._h, C.byref(out)))
+        return {k: getattr(out, k) for k, _ in ffi.HorusInfo._fields_}
+
+    def read_horus_counters(self, n, flush=False):
+        """pkts_horus / bytes_horus of rule ids 0..n-1 (lists)."""
+        pk = (C.c_uint64 * max(n, 1))()
+        by = (C.c_uint64 * max(n, 1))()
+        _check(ffi.lib().pcn_ipt_read_horus_counters(self._h, pk, by, n, int(flush)))
+        return list(pk[:n]), list(by[:n])
+
     # ---- datapath (device pointers; torch tensors accepted for convenience) ----
     def classify_ptrs(self, frames, frames_bytes, n, verdicts, rule_ids=None, offsets=None,
                       lens=None, stride=64, fixed_len=64, in_port=None, const_in_port=1,

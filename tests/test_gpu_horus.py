@@ -1,0 +1,231 @@
+"""Horus on the GPU against the CPU oracle (`pytest -m gpu`).
+
+Bit-exact on verdicts, rule ids (a Horus hit reports PCN_IPT_RID_HORUS0 -
+rule id), the chains' counters and the Horus counters, with the Parser's
+stale ports carried from packet to packet and batch to batch, through the
+generic kernel and the chain programs, stateless and with the connection
+table.  The semantics restated are listed in tests/test_oracle_horus.py."""
+import numpy as np
+import pytest
+
+from helpers import ip_host, ip_nbo, probe_frames
+from oracle.ffi import Oracle
+from test_gpu_conntrack import NOW, assert_tables
+from test_gpu_parity import JIT, assert_counters, assert_same
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+RID_HORUS0 = -4096
+HOST = "10.10.0.10"
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def setup(input_rules, forward=(), output=(), defaults=None, jit=0, ct=False):
+    """Oracle and GPU cube with horus on; INPUT is updated last, so its update builds the table."""
+    from polycube_amd import Iptables
+    d = {0: "ACCEPT", 1: "DROP", 2: "ACCEPT"}
+    d.update(defaults or {})
+    o = Oracle()
+    ipt = Iptables(device=0, jit=jit)
+    o.set_localip([ip_nbo(HOST)])
+    ipt.set_localip([ip_nbo(HOST)])
+    o.set_horus(True)
+    ipt.horus = "ON"
+    ipt.interactive = False
+    for c, rules in ((1, forward), (2, output), (0, input_rules)):
+        o.set_chain(c, list(rules), d[c])
+        ch = ipt.chain(c)
+        for r in rules:
+            ch.append(**r)
+        ch.default = d[c]
+        ch.apply_rules()
+    assert o.horus_info() == ipt.horus_info()
+    if ct:
+        o.ct_enable()
+        o.ct_set_time(NOW)
+        ipt.ct_enable(14)
+        ipt.ct_set_time(NOW)
+    return o, ipt
+
+
+PROTO = {"TCP": 6, "UDP": 17, "ICMP": 1, "GRE": 47}
+
+
+def rule_packets(rng, r):
+    """Packets whose packed Horus key is rule r's: source port 0x<s>?? when the
+    rule has sport s (< 256), and [.., d >> 8] [d & 0xff, ..] around the
+    source/destination port boundary for dport d.  A rule for a protocol
+    without ports gets a UDP packet first that leaves the ports behind (Q4)."""
+    b34 = r["sport"] & 0xff if "sport" in r else int(rng.integers(0, 256))
+    b35 = r["dport"] >> 8 if "dport" in r else int(rng.integers(0, 256))
+    b36 = r["dport"] & 0xff if "dport" in r else int(rng.integers(0, 256))
+    sport, dport = (b34 << 8) | b35, (b36 << 8) | int(rng.integers(0, 256))
+    proto = PROTO[r["l4proto"]] if "l4proto" in r else int(rng.choice([6, 17]))
+    base = {"dir": "ingress", "port": 1, "src": r.get("src", "8.8.4.4").split("/")[0],
+            "dst": r.get("dst", HOST).split("/")[0], "proto": proto,
+            "sport": sport, "dport": dport, "flags": 0x10, "icmp_type": 8,
+            "len": {6: 74, 17: 64, 1: 98, 47: 64}[proto]}
+    if proto in (6, 17):
+        return [base]
+    lead = dict(base, proto=17, src="8.8.4.4", len=64)
+    return [lead, base]
+
+
+def traffic(rng, n, addrs, ports, rules=()):
+    """Packets from/to the rules' addresses (or random ones), TCP/UDP/ICMP/GRE,
+    to the host or forwarded, ports drawn so the packed-key byte quirk
+    (source port 0x??pp, destination port 0xqq??) sometimes matches; a share
+    built to hit a rule's key exactly (rule_packets)."""
+    pk = []
+    while len(pk) < n:
+        if rules and rng.random() < 0.25:
+            pk.extend(rule_packets(rng, rules[int(rng.integers(0, len(rules)))]))
+            continue
+        proto = int(rng.choice([6, 17, 17, 1, 47]))
+        src = addrs[rng.integers(0, len(addrs))] if rng.random() < 0.7 else \
+            ".".join(str(int(x)) for x in rng.integers(1, 255, 4))
+        dst = HOST if rng.random() < 0.5 else addrs[rng.integers(0, len(addrs))]
+        if rng.random() < 0.6 and ports:
+            a, b = ports[rng.integers(0, len(ports))]       # key bytes wanted at wire 35/36 (or 34)
+            sport = (int(rng.integers(0, 256)) << 8) | a if rng.random() < 0.5 else (a << 8) | int(rng.integers(0, 256))
+            dport = (b << 8) | int(rng.integers(0, 256))
+        else:
+            sport, dport = int(rng.integers(0, 65536)), int(rng.integers(0, 65536))
+        length = {6: 74, 17: 64, 1: 98, 47: 64}[proto]
+        if proto == 1 and rng.random() < 0.2:
+            length = int(rng.choice([40, 66, 70]))
+        pk.append({"dir": "ingress", "port": 1, "src": src, "dst": dst, "proto": proto, "sport": sport,
+                   "dport": dport, "flags": int(rng.choice([0x02, 0x10, 0x12, 0x11])),
+                   "icmp_type": int(rng.choice([0, 3, 8, 11])), "len": length})
+    return pk
+
+
+def run(o, ipt, dev, packets, direction=0):
+    f, lens, ports, _ = probe_frames(packets)
+    n = len(packets)
+    v_o, r_o = o.classify(f, n=n, lens=lens, stride=128, in_port=ports, direction=direction)
+    v_g, r_g = ipt.classify(torch.from_numpy(f).to(dev), n=n, lens=torch.from_numpy(lens.view(np.int16)).to(dev),
+                            stride=128, fixed_len=128, in_port=torch.from_numpy(ports.view(np.int16)).to(dev),
+                            direction=direction)
+    torch.cuda.synchronize()
+    return v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy()
+
+
+def assert_horus_counters(o, ipt, n=64):
+    assert o.read_horus_counters(n) == ipt.read_horus_counters(n)
+
+
+ADDRS = ["1.1.1.1", "2.2.2.2", "3.3.3.3", "4.4.4.4", "5.5.5.5", HOST]
+
+
+def rule_sets():
+    a = ADDRS
+    return {
+        "src": [{"src": a[0], "action": "DROP"}, {"src": a[1], "action": "ACCEPT"}, {"src": a[2], "action": "DROP"},
+                {"src": a[1], "action": "DROP"}, {"src": "7.0.0.0/8", "action": "DROP"},
+                {"src": a[3], "l4proto": "UDP", "action": "ACCEPT"}],
+        "proto_ports": [{"l4proto": "TCP", "dport": 0x5000 | 0x21, "action": "DROP"},
+                        {"l4proto": "UDP", "dport": 0x3100 | 0x07, "action": "ACCEPT"},
+                        {"l4proto": "ICMP", "dport": 0x1100 | 0x09, "action": "DROP"},
+                        {"l4proto": "GRE", "dport": 0x2200 | 0x41, "action": "ACCEPT"},
+                        {"src": a[4], "action": "DROP"}],
+        "five": [{"src": a[k], "dst": HOST, "l4proto": p, "sport": s, "dport": d, "action": act}
+                 for k, (p, s, d, act) in enumerate([("TCP", 0x33, 0x4455, "DROP"), ("UDP", 0x12, 0x7001, "ACCEPT"),
+                                                     ("TCP", 0x90, 0x0a0b, "ACCEPT"), ("ICMP", 0x05, 0x6060, "DROP")])]
+                + [{"dst": HOST, "action": "DROP"}],
+    }
+
+
+def key_ports(rules):
+    """(wire byte 34 or 35, wire byte 36) pairs that make packets match the rules' packed port keys."""
+    out = []
+    for r in rules:
+        if "dport" in r:
+            out.append((r["dport"] >> 8, r["dport"] & 0xff))
+        if "sport" in r and r["sport"] < 256:
+            out.append((r["sport"], r.get("dport", 0) >> 8))
+    return out
+
+
+@JIT
+@pytest.mark.parametrize("kind", ["src", "proto_ports", "five"])
+def test_horus_parity_across_batches(dev, jit, kind):
+    rules = rule_sets()[kind]
+    rng = np.random.default_rng(len(kind))
+    o, ipt = setup(rules, output=[{"dst": ADDRS[0], "action": "DROP"}], jit=jit)
+    info = ipt.horus_info()
+    assert info["runtime"] == 1 and info["entries"] >= 3
+    ports = key_ports(rules)
+    hits = 0
+    for k in range(4):
+        pk = traffic(rng, 3000 + 777 * k, ADDRS, ports, rules)
+        v_o, r_o, v_g, r_g = run(o, ipt, dev, pk)
+        assert_same(v_o, r_o, v_g, r_g)
+        hits += int((r_o <= RID_HORUS0).sum())
+        # egress batches move the shared struct's ports too
+        pk = traffic(rng, 500, ADDRS, ports)
+        for p in pk:
+            p["dir"], p["src"] = "egress", HOST
+        v_o, r_o, v_g, r_g = run(o, ipt, dev, pk, direction=1)
+        assert_same(v_o, r_o, v_g, r_g)
+    assert hits > 500
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_horus_counters(o, ipt)
+
+
+def test_horus_with_connection_table(dev):
+    """Stateful: Horus hits bypass the ChainSelector; an ACCEPT hit is
+    labelled and updates the table like PASS_LABELING, a DROP hit does
+    neither; verdicts, rule ids, counters, Horus counters and the table."""
+    rules = rule_sets()["five"][:4] + [{"conntrack": "ESTABLISHED", "action": "ACCEPT"}]
+    rules = [dict(r, dport=r["dport"], sport=r["sport"]) for r in rules[:4]] + rules[4:]
+    rng = np.random.default_rng(5)
+    o, ipt = setup(rules, jit=1, ct=True)
+    ports = key_ports(rules)
+    for k in range(3):
+        pk = traffic(rng, 2500, ADDRS, ports, rules[:4])
+        v_o, r_o, v_g, r_g = run(o, ipt, dev, pk)
+        assert_same(v_o, r_o, v_g, r_g)
+        assert (r_o <= RID_HORUS0).sum() > 200
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_horus_counters(o, ipt)
+
+
+def test_chain_stats_take_the_horus_counters(dev):
+    """pcn_ipt_chain_stats folds Horus's counters of rule id k into rule k of
+    the chain read (ChainStats.cpp:106-121), and flushes them."""
+    rules = [{"src": ADDRS[0], "action": "DROP"}, {"src": ADDRS[1], "action": "ACCEPT"}]
+    o, ipt = setup(rules)
+    pk = [{"dir": "ingress", "port": 1, "src": ADDRS[k % 3], "dst": HOST, "proto": 17, "sport": 1, "dport": 2,
+           "flags": 0, "len": 64 + k % 3} for k in range(30)]
+    v_o, r_o, v_g, r_g = run(o, ipt, dev, pk)
+    assert_same(v_o, r_o, v_g, r_g)
+    hp, hb = ipt.read_horus_counters(2)
+    assert hp == [10, 10]
+    st = ipt.chain("INPUT").stats()
+    assert [x[1] for x in st[:2]] == [10, 10] and [x[2] for x in st[:2]] == hb
+    assert ipt.read_horus_counters(2)[0] == [0, 0]
+
+
+def test_turning_horus_off_takes_effect_at_the_next_update(dev):
+    rules = [{"src": ADDRS[1], "action": "ACCEPT"}]
+    o, ipt = setup(rules)
+    fwd = [{"dir": "ingress", "port": 1, "src": ADDRS[1], "dst": "9.9.9.9", "proto": 17, "sport": 1, "dport": 2,
+            "flags": 0, "len": 64}]
+    assert run(o, ipt, dev, fwd)[2][0] == 1              # Horus ACCEPT beats FORWARD's default DROP
+    ipt.horus = "OFF"
+    o.set_horus(False)
+    assert run(o, ipt, dev, fwd)[2][0] == 1              # still in place
+    ipt.chain("INPUT").apply_rules()
+    o.set_chain(0, rules, "ACCEPT")
+    v_o, r_o, v_g, r_g = run(o, ipt, dev, fwd)
+    assert_same(v_o, r_o, v_g, r_g)
+    assert v_g[0] == 0 and ipt.horus_info()["runtime"] == 0

@@ -198,3 +198,46 @@ def test_horus_with_conntrack_accepts_through_pass_labeling():
     assert list(v) == [1, 0] and list(r) == [RID_HORUS0, RID_HORUS0 - 1]
     tab = o.ct_dump()
     assert len(tab) == 1 and tab[0]["l4proto"] == 17
+
+
+def test_product_control_plane_matches_the_oracle():
+    """The library's Horus bookkeeping (pcn_ipt.cpp horus_update, on a
+    device-less context: no GPU work) follows the same chain-update sequence
+    as the oracle: the same table size, key fields and on/off state after
+    every step of random rule edits, flag flips and default changes."""
+    from polycube_amd import Iptables
+    rng = np.random.default_rng(3)
+    o, ipt = Oracle(), Iptables(device=-1)
+    rules = {0: [], 1: [], 2: []}
+    pool = [{"src": A, "action": "DROP"}, {"src": B, "action": "ACCEPT"}, {"src": C, "dport": 80, "action": "DROP"},
+            {"src": "9.0.0.0/8", "action": "DROP"}, {"dst": HOST, "l4proto": "UDP", "action": "ACCEPT"},
+            {"conntrack": "NEW", "action": "ACCEPT"}, {"src": A, "action": "ACCEPT"}]
+    for step in range(300):
+        k = rng.integers(0, 10)
+        if k == 0:
+            on = bool(rng.random() < 0.7)
+            o.set_horus(on)
+            ipt.horus = on
+            continue
+        c = int(rng.choice([0] * 8 + [1, 2]))
+        if c == 1 and rules[1]:
+            k = 7                                 # FORWARD rules stop Horus: delete them again soon
+        if k <= 6 or not rules[c]:
+            r = pool[int(rng.integers(0, len(pool)))]
+            rules[c].append(r)
+            ipt.chain(c).append(**r)
+        elif k <= 8:
+            i = int(rng.integers(0, len(rules[c])))
+            rules[c].pop(i)
+            ipt.chain(c).delete(i)
+        else:
+            d = "DROP" if rng.integers(0, 2) else "ACCEPT"
+            if ipt.chain(c).default == (0 if d == "DROP" else 1):
+                continue                          # Chain::setDefault to the same action: no update
+            ipt.chain(c).default = d
+        o.set_chain(c, rules[c], ipt.chain(c).default)
+        a, b = o.horus_info(), ipt.horus_info()
+        assert a == b, (step, a, b)
+        seen_on = locals().get("seen_on", 0) + a["runtime"]
+    assert seen_on > 20
+    ipt.close()

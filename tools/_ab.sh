@@ -1,4 +1,8 @@
 set -u
 mkdir -p gpurun_out
-JIT=1 TAG=pmc_r02 bash tools/pmc.sh "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" || exit 1
-python3 tools/pmc_summary.py gpurun_out/pmc_r02 --out gpurun_out/pmc_r02/summary.json
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_horus.py > gpurun_out/t_horus.log 2>&1; rc=$?
+grep -E "PASS|FAIL|Error|assert|passed|failed" gpurun_out/t_horus.log | head -40
+[ $rc = 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_all.log 2>&1; rc=$?
+tail -5 gpurun_out/t_all.log
+exit $rc
