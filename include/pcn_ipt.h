@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 4
+#define PCN_IPT_ABI_VERSION 5
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -340,21 +340,37 @@ int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uin
  * on, by the connection table's own copy).  pcn_ipt_chain_stats adds (and
  * flushes) the Horus counters of rule id k to rule k of whichever chain is
  * read, as ChainStats::fetchCounters does (ChainStats.cpp:106-121).
- * pcn-iptables only; pcn-firewall contexts refuse it. */
+ *
+ * pcn-firewall has Horus on from the start, with no knob (Firewall.h:337;
+ * pcn_ipt_set_horus turns it off anyway, an extension).  Each chain has its
+ * own program (Chain::updateChain, pcn-firewall Chain.cpp:232-306), rebuilt by
+ * every update of that chain that leaves it with rules -- not by a default
+ * change, which reloads only DefaultAction (:60-82) -- with the same rule
+ * (pcn-firewall Utils.cpp:483-577).  Its Parser calls it for both directions
+ * (Firewall_Parser_dp.c:154-157), and there the key holds the ports as stored
+ * (both sides packed).  The program keeps the conntrack setting it was built
+ * with (modules/Horus.cpp:135-139): built with conntrack on, an ACCEPT hit is
+ * PASS_LABELING (labels, table update, accept); built with it off, RX_OK.
+ * While conntrack is off its ConntrackLabel program does not exist
+ * (Firewall.cpp:163-171), so every tail call Horus makes into it fails: a miss
+ * drops, and so does an ACCEPT hit of a program built with conntrack on.
+ * `chain` names the program: PCN_IPT_INPUT (pcn-iptables), PCN_FW_INGRESS /
+ * PCN_FW_EGRESS (pcn-firewall). */
 #define PCN_IPT_RID_HORUS0 (-4096)
 #define PCN_IPT_HORUS_MAX 2048                       /* HorusConst::MAX_RULE_SIZE_FOR_HORUS */
 enum { PCN_IPT_HZ_SRCIP = 1, PCN_IPT_HZ_DSTIP = 2, PCN_IPT_HZ_L4PROTO = 4, PCN_IPT_HZ_SRCPORT = 8,
        PCN_IPT_HZ_DSTPORT = 16 };
 typedef struct {
-  uint32_t enabled;          /* the horus leaf */
-  uint32_t runtime;          /* a Horus table is in place (horus_runtime_enabled_) */
+  uint32_t enabled;          /* the horus leaf (pcn-firewall: horus_enabled) */
+  uint32_t runtime;          /* a Horus program is in place (horus_runtime_enabled_) */
   uint32_t entries;          /* keys in the table */
   uint32_t fields;           /* PCN_IPT_HZ_* set fields of the key */
+  uint32_t conntrack;        /* pcn-firewall: the program was built with conntrack on */
 } pcn_ipt_horus_info;
 int pcn_ipt_set_horus(pcn_ipt *ctx, int on);
-int pcn_ipt_get_horus_info(pcn_ipt *ctx, pcn_ipt_horus_info *out);
-/* pkts_horus / bytes_horus[rule id] (Iptables_Horus_dp.c:77-90) */
-int pcn_ipt_read_horus_counters(pcn_ipt *ctx, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush);
+int pcn_ipt_get_horus_info(pcn_ipt *ctx, int chain, pcn_ipt_horus_info *out);
+/* pkts_horus / bytes_horus[rule id] (Iptables_Horus_dp.c:77-90, Firewall_Horus_dp.c:82-95) */
+int pcn_ipt_read_horus_counters(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush);
 
 /* ---- pcn-firewall personality ------------------------------------------ */
 /* pcn-firewall (src/services/pcn-firewall) runs the same field modules,

@@ -61,8 +61,9 @@ def lib():
         h.orc_get_accept_established.argtypes = [vp, C.c_int]
         h.orc_read_accept_established.argtypes = [vp, C.c_int, u64p, u64p, C.c_int]
         h.orc_set_horus.argtypes = [vp, C.c_int]
-        h.orc_horus_info.argtypes = [vp, u32p]
-        h.orc_read_horus_counters.argtypes = [vp, u64p, u64p, C.c_uint32, C.c_int]
+        h.orc_horus_info.argtypes = [vp, C.c_int, u32p]
+        h.orc_read_horus_counters.argtypes = [vp, C.c_int, u64p, u64p, C.c_uint32, C.c_int]
+        h.orc_set_default.argtypes = [vp, C.c_int, C.c_int]
         _lib = h
     return _lib
 
@@ -178,19 +179,25 @@ class Oracle:
         lib().orc_read_accept_established(self._h, chain, C.byref(pk), C.byref(by), int(flush))
         return pk.value, by.value
 
-    # ---- Horus (Iptables_Horus_dp.c) ----
+    def set_default(self, chain, default):
+        """pcn-firewall Chain::setDefault: the default action alone, no chain update."""
+        d = {"DROP": 0, "ACCEPT": 1}[default.upper()] if isinstance(default, str) else int(default)
+        assert lib().orc_set_default(self._h, chain, d) == 0
+
+    # ---- Horus (Iptables_Horus_dp.c, Firewall_Horus_dp.c) ----
     def set_horus(self, on):
         assert lib().orc_set_horus(self._h, int(on)) == 0
 
-    def horus_info(self):
-        out = (C.c_uint32 * 4)()
-        lib().orc_horus_info(self._h, out)
-        return {"enabled": out[0], "runtime": out[1], "entries": out[2], "fields": out[3]}
+    def horus_info(self, chain=0):
+        """chain: 0 (pcn-iptables INPUT), 1 / 2 (pcn-firewall INGRESS / EGRESS)."""
+        out = (C.c_uint32 * 5)()
+        assert lib().orc_horus_info(self._h, chain, out) == 0
+        return {"enabled": out[0], "runtime": out[1], "entries": out[2], "fields": out[3], "conntrack": out[4]}
 
-    def read_horus_counters(self, n, flush=False):
+    def read_horus_counters(self, n, flush=False, chain=0):
         pk = (C.c_uint64 * max(n, 1))()
         by = (C.c_uint64 * max(n, 1))()
-        lib().orc_read_horus_counters(self._h, pk, by, n, int(flush))
+        assert lib().orc_read_horus_counters(self._h, chain, pk, by, n, int(flush)) == 0
         return list(pk[:n]), list(by[:n])
 
     def export_map(self, chain, field, cap=70000):

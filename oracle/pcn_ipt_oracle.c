@@ -93,6 +93,15 @@ typedef struct { char name[64]; uint16_t index; } port_t;
  * HorusValue {action, ruleID} (defines.h:161-164). */
 #define HZ_MAX 2048                              /* HorusConst::MAX_RULE_SIZE_FOR_HORUS, defines.h:127 */
 typedef struct { uint32_t src, dst; uint8_t proto; uint16_t sk, dk; uint8_t action; uint32_t rule; } hzent_t;
+/* One Horus program: pcn-iptables has one (ingress, from INPUT); pcn-firewall
+ * one per chain (INGRESS / EGRESS, Firewall.h:333-340). */
+typedef struct {
+  int runtime;                               /* horus_runtime_enabled_ */
+  int ct;                                    /* pcn-firewall: _CONNTRACK_ENABLED when it was built */
+  uint32_t fields; int n;
+  hzent_t ent[HZ_MAX];
+  uint64_t pkts[HZ_MAX], bytes[HZ_MAX];      /* pkts_horus / bytes_horus (Horus_dp.c:77-78) */
+} hzprog_t;
 
 struct orc_ctx {
   int service;                           /* ORC_SVC_IPTABLES / ORC_SVC_FIREWALL */
@@ -107,11 +116,9 @@ struct orc_ctx {
   struct ctstate *ct;
   int ae[NCHAINS];                       /* accept_established_enabled_<chain>_ (Iptables.h) */
   uint64_t ae_pkts[NCHAINS], ae_bytes[NCHAINS]; /* pkts_/bytes_acceptestablished_<Chain> */
-  /* Horus (Iptables.h:183-188) */
-  int hz_enabled, hz_runtime;
-  uint32_t hz_fields; int hz_n;
-  hzent_t hz[HZ_MAX];
-  uint64_t hz_pkts[HZ_MAX], hz_bytes[HZ_MAX]; /* pkts_horus / bytes_horus (Horus_dp.c:77-78) */
+  /* Horus (Iptables.h:183-188; pcn-firewall Firewall.h:333-340) */
+  int hz_enabled;
+  hzprog_t hz[2];                            /* [0] iptables INPUT / firewall INGRESS, [1] firewall EGRESS */
   /* the shared per-CPU `packet` struct's ports while conntrack is off (the
    * Horus key reads them for packets the Parser wrote no ports for, Q4) */
   uint16_t hz_stale[2];
@@ -559,17 +566,17 @@ int orc_set_chain(orc_ctx *c, int chain, const orc_rule *rules, uint32_t n, int 
 
 static inline uint16_t bswap16(uint16_t x) { return (uint16_t)(x >> 8 | x << 8); }
 
-/* Chain::fromRuleToHorusKeyValue + horusFromRulesToMap (Utils.cpp:537-630):
- * the leading rules whose key sets the same fields as rule 0 (a /32 address,
+/* Chain::fromRuleToHorusKeyValue + horusFromRulesToMap (pcn-iptables
+ * Utils.cpp:537-630; pcn-firewall Utils.cpp:483-577, the same rule): the
+ * leading rules whose key sets the same fields as rule 0 (a /32 address,
  * protocol, ports; anything else the rule matches on is not part of the key),
  * up to the first rule with a conntrack match; std::map::insert keeps the
  * first rule of a repeated key. */
-static void horus_build(orc_ctx *c) {
-  const ochain_t *in = &c->ch[ORC_INPUT];
+static void horus_build(const ochain_t *in, hzprog_t *h) {
   uint32_t set_fields = 0;
   hzent_t key;
   memset(&key, 0, sizeof key);        /* one HorusRule reused for every rule (Utils.cpp:604) */
-  c->hz_n = 0;
+  h->n = 0;
   for (int i = 0; i < in->nrules && i < HZ_MAX; i++) {
     const prule_t *r = &in->rules[i];
     if (r->ct_set) break;             /* fromRuleToHorusKeyValue returns false: stop */
@@ -587,63 +594,113 @@ static void horus_build(orc_ctx *c) {
     }
     if (f != set_fields) break;
     int dup = 0;
-    for (int k = 0; k < c->hz_n && !dup; k++) {
-      const hzent_t *e = &c->hz[k];
+    for (int k = 0; k < h->n && !dup; k++) {
+      const hzent_t *e = &h->ent[k];
       dup = e->src == key.src && e->dst == key.dst && e->proto == key.proto && e->sk == key.sk && e->dk == key.dk;
     }
-    if (!dup) c->hz[c->hz_n++] = key;
+    if (!dup) h->ent[h->n++] = key;
   }
-  c->hz_fields = set_fields;
+  h->fields = set_fields;
 }
 
-/* Chain::updateChain's Horus part (Chain.cpp:505-592), run for every chain update */
+/* The Horus program a chain's updates rebuild: pcn-iptables INPUT -> [0];
+ * pcn-firewall INGRESS (FORWARD slot) -> [0], EGRESS (OUTPUT slot) -> [1]. */
+static int horus_slot(const orc_ctx *c, int chain) {
+  if (c->service == ORC_SVC_FIREWALL) return chain == ORC_FORWARD ? 0 : chain == ORC_OUTPUT ? 1 : -1;
+  return chain == ORC_INPUT ? 0 : -1;
+}
+
+/* The Horus program a batch's Parser calls: pcn-iptables ingress only (the
+ * egress Parser's tail call lands on an empty program slot); pcn-firewall the
+ * direction's own. */
+static hzprog_t *horus_of_batch(orc_ctx *c, int dir) {
+  hzprog_t *h = c->service == ORC_SVC_FIREWALL ? &c->hz[dir == ORC_INGRESS ? 0 : 1]
+                                               : dir == ORC_INGRESS ? &c->hz[0] : NULL;
+  return h && h->runtime ? h : NULL;
+}
+
+static void horus_reset(hzprog_t *h) {
+  h->runtime = 0;                     /* the old program goes, and its counters with it */
+  h->n = 0;
+  h->fields = 0;
+  memset(h->pkts, 0, sizeof h->pkts);
+  memset(h->bytes, 0, sizeof h->bytes);
+}
+
+/* Chain::updateChain's Horus part, run for every chain update.
+ * pcn-iptables (Chain.cpp:505-592): any update drops the program; an INPUT
+ * update with horus on, >= 1 INPUT rule (MIN_RULE_SIZE_FOR_HORUS) and an empty
+ * FORWARD rule list builds a new one.
+ * pcn-firewall (Chain.cpp:232-306): an update of INGRESS / EGRESS rebuilds that
+ * chain's own program when horus is on (always: Firewall.h:337) and the chain
+ * has >= 1 rule, and the program keeps the conntrack setting it was compiled
+ * with (modules/Horus.cpp:135-139; setConntrack does not reload it,
+ * Firewall.cpp:151-191). */
 static void horus_update(orc_ctx *c, int chain) {
-  c->hz_runtime = 0;                  /* the old program goes, and its counters with it */
-  c->hz_n = 0;
-  c->hz_fields = 0;
-  memset(c->hz_pkts, 0, sizeof c->hz_pkts);
-  memset(c->hz_bytes, 0, sizeof c->hz_bytes);
-  if (chain != ORC_INPUT || !c->hz_enabled || c->service != ORC_SVC_IPTABLES) return;
-  /* MIN_RULE_SIZE_FOR_HORUS = 1 INPUT rule, FORWARD rule list empty */
+  if (c->service == ORC_SVC_FIREWALL) {
+    const int k = horus_slot(c, chain);
+    if (k < 0) return;
+    hzprog_t *h = &c->hz[k];
+    horus_reset(h);
+    if (!c->hz_enabled || c->ch[chain].nrules < 1) return;
+    horus_build(&c->ch[chain], h);
+    h->ct = c->fw_ct_mode != FW_CT_DISABLED;
+    if (h->n >= 1) h->runtime = 1;
+    return;
+  }
+  hzprog_t *h = &c->hz[0];
+  horus_reset(h);
+  if (chain != ORC_INPUT || !c->hz_enabled) return;
   if (c->ch[ORC_INPUT].nrules < 1 || c->ch[ORC_FORWARD].nrules != 0) return;
-  horus_build(c);
-  if (c->hz_n >= 1) c->hz_runtime = 1;
+  horus_build(&c->ch[ORC_INPUT], h);
+  if (h->n >= 1) h->runtime = 1;
 }
 
 int orc_set_horus(orc_ctx *c, int on) {
-  if (c->service != ORC_SVC_IPTABLES) return -EINVAL;
   c->hz_enabled = on != 0;
   return 0;
 }
 
-int orc_horus_info(orc_ctx *c, uint32_t out[4]) {
-  out[0] = (uint32_t)c->hz_enabled; out[1] = (uint32_t)c->hz_runtime;
-  out[2] = (uint32_t)c->hz_n; out[3] = c->hz_fields;
+int orc_horus_info(orc_ctx *c, int chain, uint32_t out[5]) {
+  const int k = horus_slot(c, chain);
+  if (k < 0) return -EINVAL;
+  const hzprog_t *h = &c->hz[k];
+  out[0] = (uint32_t)c->hz_enabled; out[1] = (uint32_t)h->runtime;
+  out[2] = (uint32_t)h->n; out[3] = h->fields; out[4] = (uint32_t)(h->runtime && h->ct);
   return 0;
 }
 
-int orc_read_horus_counters(orc_ctx *c, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush) {
+int orc_read_horus_counters(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush) {
+  const int k = horus_slot(c, chain);
+  if (k < 0) return -EINVAL;
+  hzprog_t *h = &c->hz[k];
   for (uint32_t i = 0; i < n; i++) {
     const int ok = i < HZ_MAX;
-    if (pkts) pkts[i] = ok ? c->hz_pkts[i] : 0;
-    if (bytes) bytes[i] = ok ? c->hz_bytes[i] : 0;
-    if (ok && flush) { c->hz_pkts[i] = 0; c->hz_bytes[i] = 0; }   /* Horus::flushCounters */
+    if (pkts) pkts[i] = ok ? h->pkts[i] : 0;
+    if (bytes) bytes[i] = ok ? h->bytes[i] : 0;
+    if (ok && flush) { h->pkts[i] = 0; h->bytes[i] = 0; }   /* Horus::flushCounters */
   }
   return 0;
 }
 
-/* Iptables_Horus_dp.c:112-133: the packed horusKey of the per-CPU packet
- * struct.  The Parser writes the naturally aligned struct (srcPort at bytes
- * 10-11, dstPort at 12-13, byte 9 padding that nothing writes), and Horus
- * reads it through a packed declaration (srcPort at 9-10, dstPort at 11-12):
- * rs/rd are the Parser's srcPort/dstPort as stored (wire bytes 34-35, 36-37). */
-static const hzent_t *horus_lookup(const orc_ctx *c, uint32_t saddr, uint32_t daddr, uint8_t proto, uint16_t rs,
-                                   uint16_t rd) {
-  const uint32_t F = c->hz_fields;
-  const uint16_t sk = (uint16_t)((rs & 0xff) << 8);                /* bytes 9-10: [0, wire34] */
-  const uint16_t dk = (uint16_t)((rs >> 8) | ((rd & 0xff) << 8));  /* bytes 11-12: [wire35, wire36] */
-  for (int k = 0; k < c->hz_n; k++) {
-    const hzent_t *e = &c->hz[k];
+/* The Horus key of the per-CPU packet struct; rs/rd are the Parser's
+ * srcPort/dstPort as stored (wire bytes 34-35, 36-37).
+ * pcn-iptables (Iptables_Horus_dp.c:112-133): the Parser writes the naturally
+ * aligned struct (srcPort at bytes 10-11, dstPort at 12-13, byte 9 padding
+ * that nothing writes), and Horus reads it through a packed declaration
+ * (srcPort at 9-10, dstPort at 11-12).
+ * pcn-firewall (Firewall_Horus_dp.c:112-133): both sides declare the struct
+ * packed (Firewall_Parser_dp.c:32-43), so the key holds the ports as stored. */
+static const hzent_t *horus_lookup(const orc_ctx *c, const hzprog_t *h, uint32_t saddr, uint32_t daddr,
+                                   uint8_t proto, uint16_t rs, uint16_t rd) {
+  const uint32_t F = h->fields;
+  uint16_t sk = rs, dk = rd;
+  if (c->service != ORC_SVC_FIREWALL) {
+    sk = (uint16_t)((rs & 0xff) << 8);                /* bytes 9-10: [0, wire34] */
+    dk = (uint16_t)((rs >> 8) | ((rd & 0xff) << 8));  /* bytes 11-12: [wire35, wire36] */
+  }
+  for (int k = 0; k < h->n; k++) {
+    const hzent_t *e = &h->ent[k];
     if ((F & ORC_HZ_SRCIP) && e->src != saddr) continue;
     if ((F & ORC_HZ_DSTIP) && e->dst != daddr) continue;
     if ((F & ORC_HZ_L4PROTO) && e->proto != proto) continue;
@@ -654,9 +711,21 @@ static const hzent_t *horus_lookup(const orc_ctx *c, uint32_t saddr, uint32_t da
   return NULL;
 }
 
+/* pcn-firewall Chain::setDefault (Chain.cpp:60-82): only the DefaultAction
+ * program is reloaded -- no Chain::updateChain, so the rule modules, their
+ * counters and the Horus program stay as they are. */
+int orc_set_default(orc_ctx *c, int chain, int def) {
+  if (chain < 0 || chain >= NCHAINS || (def != 0 && def != 1)) return -EINVAL;
+  c->ch[chain].default_action = def;
+  return 0;
+}
+
 int orc_set_service(orc_ctx *c, int service, int fw_ct_mode) {
   if (service != ORC_SVC_IPTABLES && service != ORC_SVC_FIREWALL) return -EINVAL;
   if (fw_ct_mode < FW_CT_DISABLED || fw_ct_mode > FW_CT_AUTOMATIC) return -EINVAL;
+  /* pcn-firewall's horus_enabled is true from the start and has no knob
+   * (Firewall.h:337); pcn-iptables' leaf is OFF by default (Iptables.h:185) */
+  if (service != c->service) c->hz_enabled = service == ORC_SVC_FIREWALL;
   c->service = service;
   c->fw_ct_mode = fw_ct_mode;
   return 0;
@@ -1018,7 +1087,8 @@ static inline int default_verdict(const ochain_t *ch, pcpu_t *pc, int chain, uin
 /* st != NULL: stateful conntrack (labels from and updates to st, one packet
  * at a time); else labels come from ct_in or an empty table. */
 static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, uint32_t L, uint16_t port,
-                        int ct_in, pcpu_t *pc, int32_t *rid, struct ctstate *st, int *label, uint16_t *hzp) {
+                        int ct_in, pcpu_t *pc, int32_t *rid, struct ctstate *st, int *label, uint16_t *hzp,
+                        const hzprog_t *hz) {
   *rid = -2;
   *label = 255;
   /* TC hook: the receive path strips the outer 802.1Q / 802.1ad tag before
@@ -1054,22 +1124,35 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
   if (!st && hzp && (proto == 6 || proto == 17)) { hzp[0] = sport; hzp[1] = dport; }
   ctpkt_t cp;
   if (st) cp = (ctpkt_t){saddr, daddr, (uint8_t)proto, st->sport, st->dport, st->flags, st->seq, st->ack};
-  /* Horus (Parser_dp.c:145-147 -> Horus_dp.c:97-167), ingress only: the
-   * egress Parser's tail call lands on an empty program slot */
+  /* Horus (pcn-iptables Parser_dp.c:145-147 -> Horus_dp.c:97-167, ingress
+   * only: the egress Parser's tail call lands on an empty program slot;
+   * pcn-firewall Firewall_Parser_dp.c:154-157 -> Firewall_Horus_dp.c:97-175,
+   * each direction its own).  hz: the batch's program in place, or NULL. */
   int pass_labeling = 0, chain = -1, ct;
-  if (dir == ORC_INGRESS && c->hz_runtime) {
+  const int fwsvc = c->service == ORC_SVC_FIREWALL;
+  if (hz) {
     uint16_t rs = sport, rd = dport;                       /* written by this packet */
     if (proto != 6 && proto != 17) {                       /* stale (Q4) */
       rs = st ? st->sport : hzp ? hzp[0] : 0;
       rd = st ? st->dport : hzp ? hzp[1] : 0;
     }
-    const hzent_t *e = horus_lookup(c, saddr, daddr, (uint8_t)proto, rs, rd);
+    const hzent_t *e = horus_lookup(c, hz, saddr, daddr, (uint8_t)proto, rs, rd);
     if (e) {
       pc->hz_pkts[e->rule] += 1; pc->hz_bytes[e->rule] += L;
       *rid = ORC_RID_HORUS0 - (int32_t)e->rule;
       if (e->action == 0) return RX_DROP;
       pass_labeling = 1;                                   /* PASS_LABELING -> ConntrackLabel */
-      goto labeling;
+      if (!fwsvc) goto labeling;
+      /* pcn-firewall, compiled with conntrack off: RX_OK (Firewall_Horus_dp.c:162-164);
+       * with it on, PASS_LABELING tail-calls ConntrackLabel (:157-161), which
+       * setConntrack(OFF) has deleted since (Firewall.cpp:163-171): the tail
+       * call fails and the program returns RX_DROP */
+      if (!hz->ct) return RX_OK;
+      if (c->fw_ct_mode == FW_CT_DISABLED) return RX_DROP;
+    } else if (fwsvc && c->fw_ct_mode == FW_CT_DISABLED) {
+      /* a miss always tail-calls ConntrackLabel (Firewall_Horus_dp.c:170-174):
+       * with conntrack off that program does not exist, so RX_DROP */
+      return RX_DROP;
     }
   }
   /* ports as the NBO u16 the eBPF hash keys hold; the maps store ntohs(port) */
@@ -1099,6 +1182,12 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
         ct = ct_in >= 0 ? ct_in : ct_label_empty(proto, flags, icmp_type);
       }
       *label = ct;
+      /* PASS_LABELING (a Horus ACCEPT) -> ConntrackTableUpdate -> RX_OK in
+       * both modes (Firewall_ConntrackLabel_dp.c:463-489) */
+      if (pass_labeling) {
+        if (st) ct_update(st, &cp, f, ct);
+        return RX_OK;
+      }
       /* _CONNTRACK_MODE == 2 (AUTOMATIC): ESTABLISHED -> ConntrackTableUpdate
        * -> RX_OK, before any chain and without counters
        * (Firewall_ConntrackLabel_dp.c:474-478) */
@@ -1244,6 +1333,7 @@ typedef struct {
   uint32_t stride, fixed_len; const uint16_t *in_port; uint16_t const_port; const uint8_t *ct;
   uint64_t lo, hi; uint8_t *verdicts; int32_t *rule_ids; pcpu_t pc; struct ctstate *st; uint8_t *labels;
   uint16_t *hzp;   /* stale ports for Horus keys while conntrack is off (NULL: not tracked) */
+  const hzprog_t *hz;   /* the batch's Horus program, or NULL */
 } job_t;
 
 static void *run_job(void *arg) {
@@ -1255,7 +1345,7 @@ static void *run_job(void *arg) {
     int ct = j->ct ? j->ct[i] : -1;
     int32_t rid;
     int lab;
-    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st, &lab, j->hzp);
+    int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st, &lab, j->hzp, j->hz);
     if (j->labels) j->labels[i] = (uint8_t)lab;
     j->verdicts[i] = v == RX_DROP ? 0 : 1;
     if (j->rule_ids) j->rule_ids[i] = rid;
@@ -1282,6 +1372,7 @@ int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, co
    * while horus is on (or conntrack, which keeps its own): the GPU does the same. */
   uint16_t *hzp = c->hz_enabled && !c->ct ? c->hz_stale : NULL;
   if (hzp) nthreads = 1;
+  hzprog_t *hz = horus_of_batch(c, dir);
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   job_t *jobs = calloc((size_t)nthreads, sizeof(job_t));
@@ -1290,7 +1381,7 @@ int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, co
     job_t *j = &jobs[t];
     *j = (job_t){c, dir, hook, frames, offsets, lens, stride, fixed_len, in_port, const_port, ct_status,
                  n * t / nthreads, n * (t + 1) / nthreads, verdicts, rule_ids,
-                 {{0}, {0}, {0}, {0}, {0}, {0}, NULL, NULL}, c->ct, labels, hzp};
+                 {{0}, {0}, {0}, {0}, {0}, {0}, NULL, NULL}, c->ct, labels, hzp, hz};
     for (int k = 0; k < NCHAINS; k++) {
       j->pc.pkts[k] = calloc(c->max_counted, 8);
       j->pc.bytes[k] = calloc(c->max_counted, 8);
@@ -1314,9 +1405,9 @@ int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, co
       c->ae_bytes[k] += jobs[t].pc.ae_bytes[k];
       free(jobs[t].pc.pkts[k]); free(jobs[t].pc.bytes[k]);
     }
-    for (int r = 0; r < HZ_MAX; r++) {
-      c->hz_pkts[r] += jobs[t].pc.hz_pkts[r];
-      c->hz_bytes[r] += jobs[t].pc.hz_bytes[r];
+    for (int r = 0; hz && r < HZ_MAX; r++) {
+      hz->pkts[r] += jobs[t].pc.hz_pkts[r];
+      hz->bytes[r] += jobs[t].pc.hz_bytes[r];
     }
     free(jobs[t].pc.hz_pkts); free(jobs[t].pc.hz_bytes);
   }

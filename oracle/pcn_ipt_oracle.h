@@ -73,20 +73,29 @@ int orc_classify(orc_ctx *c, int direction, int hook, const uint8_t *frames,
                  uint32_t fixed_len, const uint16_t *in_port,
                  uint16_t const_port, const uint8_t *ct_status, uint64_t n,
                  uint8_t *verdicts, int32_t *rule_ids, int nthreads);
-/* Horus (pcn-iptables `horus` leaf, iptables.yang:112-118; OFF by default,
- * Iptables.h:185).  orc_set_horus only sets the flag (Iptables::setHorus,
- * Iptables.cpp:400-406); like Chain::updateChain (Chain.cpp:505-592) every
- * orc_set_chain drops the Horus program and its counters, and an INPUT update
- * with horus on, INPUT rules and an empty FORWARD chain builds a new one from
- * the leading INPUT rules that set the same fields (Utils.cpp:537-630).  A hit
- * reports rule id ORC_RID_HORUS0 - <rule id> and counts into the Horus
- * counters (Iptables_Horus_dp.c:80-90, 136-161). */
+/* Horus.  pcn-iptables: the `horus` leaf (iptables.yang:112-118, OFF by
+ * default, Iptables.h:185); orc_set_horus only sets the flag
+ * (Iptables::setHorus, Iptables.cpp:400-406); like Chain::updateChain
+ * (Chain.cpp:505-592) every orc_set_chain drops the Horus program and its
+ * counters, and an INPUT update with horus on, INPUT rules and an empty
+ * FORWARD chain builds a new one from the leading INPUT rules that set the
+ * same fields (Utils.cpp:537-630).  pcn-firewall: on from the start with no
+ * knob (Firewall.h:337; orc_set_horus still turns it off, for tests), one
+ * program per chain, rebuilt by that chain's orc_set_chain (Chain.cpp:232-306)
+ * and keeping the conntrack setting it was built with.  A hit reports rule id
+ * ORC_RID_HORUS0 - <rule id> and counts into the program's counters
+ * (Iptables_Horus_dp.c:80-90, 136-161; Firewall_Horus_dp.c:85-95, 137-167).
+ * `chain` names the program: ORC_INPUT for pcn-iptables, ORC_FORWARD
+ * (INGRESS) / ORC_OUTPUT (EGRESS) for pcn-firewall. */
 #define ORC_RID_HORUS0 (-4096)
 enum { ORC_HZ_SRCIP = 1, ORC_HZ_DSTIP = 2, ORC_HZ_L4PROTO = 4, ORC_HZ_SRCPORT = 8, ORC_HZ_DSTPORT = 16 };
 int orc_set_horus(orc_ctx *c, int on);
-/* out[0] enabled, out[1] runtime enabled, out[2] entries, out[3] set fields (ORC_HZ_*) */
-int orc_horus_info(orc_ctx *c, uint32_t out[4]);
-int orc_read_horus_counters(orc_ctx *c, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush);
+/* out[0] enabled, out[1] runtime enabled, out[2] entries, out[3] set fields
+ * (ORC_HZ_*), out[4] pcn-firewall: built with conntrack on */
+int orc_horus_info(orc_ctx *c, int chain, uint32_t out[5]);
+int orc_read_horus_counters(orc_ctx *c, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush);
+/* pcn-firewall Chain::setDefault: the default action alone (no chain update) */
+int orc_set_default(orc_ctx *c, int chain, int default_action);
 
 /* orc_classify that also reports each packet's connection label (0..3, the
  * connStatus the field modules see), or 255 when the packet was decided

@@ -240,15 +240,19 @@ __device__ __forceinline__ uint32_t key_class(const Tab<LDS> &t, uint32_t tab, u
   return m0 ? (e0 & 0xffff) : (m1 ? (e1 & 0xffff) : wild);
 }
 
-// Horus (Iptables_Horus_dp.c:112-133): the packed key of the per-CPU packet
-// struct.  pd = the Parser's srcPort/dstPort as stored (wire bytes 34-37 as
-// a little-endian dword); the packed struct reads bytes 9-10 / 11-12 of the
-// aligned one: [padding 0, first source-port byte] and [second source-port
-// byte, first destination-port byte].
+// Horus: the key of the per-CPU packet struct.  pd = the Parser's
+// srcPort/dstPort as stored (wire bytes 34-37 as a little-endian dword).
+// pcn-iptables (Iptables_Horus_dp.c:112-133): the packed struct reads bytes
+// 9-10 / 11-12 of the aligned one: [padding 0, first source-port byte] and
+// [second source-port byte, first destination-port byte].  pcn-firewall
+// (kHzNatural, Firewall_Horus_dp.c:112-133): packed on both sides, the ports
+// as stored.
 __device__ __forceinline__ bool horus_lookup(const LaunchArgs &a, uint32_t saddr, uint32_t daddr, uint32_t proto,
                                              uint32_t pd, uint32_t &meta) {
   const uint32_t F = a.horus_fields;
-  const uint32_t sk = (pd & 0xffu) << 8, dk = ((pd >> 8) & 0xffu) | (((pd >> 16) & 0xffu) << 8);
+  const bool nat = a.horus_flags & kHzNatural;
+  const uint32_t sk = nat ? (pd & 0xffffu) : (pd & 0xffu) << 8;
+  const uint32_t dk = nat ? (pd >> 16) : ((pd >> 8) & 0xffu) | (((pd >> 16) & 0xffu) << 8);
   const uint32_t ks = (F & PCN_IPT_HZ_SRCIP) ? saddr : 0u, kd = (F & PCN_IPT_HZ_DSTIP) ? daddr : 0u;
   const uint32_t kp = (F & PCN_IPT_HZ_L4PROTO) ? proto : 0u;
   const uint32_t kports = ((F & PCN_IPT_HZ_SRCPORT) ? sk : 0u) | (((F & PCN_IPT_HZ_DSTPORT) ? dk : 0u) << 16);
@@ -613,6 +617,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   constexpr bool kLoadPort = !JIT || (kJitInputs & 1);
   constexpr bool kLoadCt = !JIT || (kJitInputs & 6);
   constexpr bool kLoadStale = !JIT || (kJitInputs & 8);
+  constexpr bool kHorus = !JIT || (kJitInputs & 16);   // a Horus program is in place
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   constexpr int PF = FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
   Stage st[PF];
@@ -773,10 +778,34 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         // written (per-CPU zero: NEW).
         chain = a.direction == PCN_IPT_INGRESS ? PCN_IPT_FORWARD : PCN_IPT_OUTPUT;
         p.ct = a.has_ct ? cur_ct : 0u;
-        if (a.fw != PCN_FW_LAUNCH_CT_OFF) {
+        // ---- Horus (Firewall_Parser_dp.c:154-157 -> Firewall_Horus_dp.c:97-175) ----
+        bool pass = false;
+        if (kHorus && a.horus_fields) {
+          const uint32_t pd = (p.proto == 6 || p.proto == 17) ? ((h.w[8] >> 16) | (h.w[9] << 16)) : cur_stale;
+          uint32_t meta;
+          if (horus_lookup(a, p.saddr, p.daddr, p.proto, pd, meta)) {
+            const uint32_t id = meta >> 16;
+            if (a.horus_ctr) {
+              atomicAdd(&a.horus_ctr[2 * id], 1ull);
+              atomicAdd(&a.horus_ctr[2 * id + 1], static_cast<unsigned long long>(L));
+            }
+            rid = PCN_IPT_RID_HORUS0 - static_cast<int32_t>(id);
+            done = true;
+            if (!((meta >> 8) & 1)) verdict = PCN_IPT_DROP;
+            else if (a.horus_flags & kHzAcceptFinal) verdict = PCN_IPT_ACCEPT;
+            else if (a.horus_flags & kHzAcceptDrops) verdict = PCN_IPT_DROP;
+            else { pass = true; done = false; }           // PASS_LABELING -> ConntrackLabel
+          } else if (a.horus_flags & kHzMissDrops) {
+            verdict = PCN_IPT_DROP; done = true;
+          }
+        }
+        if (!done && a.fw != PCN_FW_LAUNCH_CT_OFF) {
           uint32_t icmp_type;
           if (icmp_drop(p, h, L, icmp_type)) { verdict = PCN_IPT_DROP; done = true; }
           else if (!a.has_ct) p.ct = empty_table_label(p, icmp_type);
+          // PASS_LABELING -> ConntrackTableUpdate -> RX_OK in both modes
+          // (Firewall_ConntrackLabel_dp.c:463-489)
+          if (!done && pass) { verdict = PCN_IPT_ACCEPT; done = true; }
           // AUTOMATIC: ESTABLISHED -> ConntrackTableUpdate -> RX_OK before the
           // chain, uncounted (Firewall_ConntrackLabel_dp.c:474-478)
           if (!done && a.fw == PCN_FW_LAUNCH_CT_AUTO && p.ct == 1) {
@@ -792,7 +821,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       } else if (!done) {
         bool pass = false;
         // ---- Horus (Parser_dp.c:145-147 -> Horus_dp.c:97-167), ingress ----
-        if (a.horus_fields && a.direction == PCN_IPT_INGRESS) {
+        if (kHorus && a.horus_fields) {
           const uint32_t pd = (p.proto == 6 || p.proto == 17) ? ((h.w[8] >> 16) | (h.w[9] << 16)) : cur_stale;
           uint32_t meta;
           if (horus_lookup(a, p.saddr, p.daddr, p.proto, pd, meta)) {

@@ -173,10 +173,12 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *
     if (p.status == 2) {
       bool labeled = true;
       // a Horus hit (stage A found it: the same for every label) skips the
-      // ChainSelector: DROP is final, ACCEPT is PASS_LABELING (Horus_dp.c:150-160)
-      const bool horus = !b.fw && b.a_rid[i] <= PCN_IPT_RID_HORUS0;
+      // ChainSelector / ChainForwarder: DROP is final, ACCEPT is PASS_LABELING
+      // (Horus_dp.c:150-160; Firewall_Horus_dp.c:151-161), or final for a
+      // pcn-firewall program built with conntrack off (:162-164)
+      const bool horus = b.a_rid[i] <= PCN_IPT_RID_HORUS0;
       if (horus) {
-        if (b.a_verdict[i] == PCN_IPT_ACCEPT) pass = true;
+        if (b.a_verdict[i] == PCN_IPT_ACCEPT && !b.horus_final) pass = true;
         else labeled = false;
       } else if (b.fw) {
         // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder
@@ -735,6 +737,7 @@ struct CtScratch {
   // ct_stale_ports alone (stateless batches): parse flags, scan, ports
   uint32_t *zpp = nullptr, *zlast = nullptr, *zports = nullptr;
   uint64_t zcap = 0;
+  unsigned long long *zfound = nullptr;   // the carry-only path: 1 + the last port-writing frame
   void *ztemp = nullptr;
   size_t ztemp_bytes = 0;
 };
@@ -749,7 +752,7 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->hard_cnt), static_cast<void *>(s->rec), static_cast<void *>(s->wrec),
                   static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
                   static_cast<void *>(s->zpp), static_cast<void *>(s->zlast), static_cast<void *>(s->zports),
-                  s->ztemp})
+                  s->ztemp, static_cast<void *>(s->zfound)})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -807,6 +810,47 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
   return hipSuccess;
 }
 
+// The carry alone: the ports of the batch's last frame that wrote them.
+// Workgroup g takes the g-th block of frames counting from the end and stops
+// once a later block has found one, so a batch that ends in TCP/UDP costs one
+// wave of blocks, not a pass over the batch.  found = 1 + that frame's index.
+__global__ void tail_ports_kernel(CtBatch b, unsigned long long *found) {
+  __shared__ uint32_t best;
+  __shared__ int stop;
+  const uint64_t B = blockDim.x;
+  for (uint64_t blk = blockIdx.x; blk * B < b.n; blk += gridDim.x) {
+    const uint64_t hi = b.n - blk * B;                     // this block: frames [hi - B, hi)
+    if (threadIdx.x == 0) {
+      best = 0;
+      stop = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > hi;
+    }
+    __syncthreads();
+    if (stop) return;                                      // uniform: a later frame has them
+    if (threadIdx.x < hi) {
+      const uint64_t i = hi - 1 - threadIdx.x;
+      uint32_t w[18], L;
+      load_window(b, i, w, L);
+      const Parsed p = parse(w, L, b.hook);
+      if (p.status == 2 && p.ports_ok) atomicMax(&best, static_cast<uint32_t>(B - threadIdx.x));
+    }
+    __syncthreads();
+    const uint32_t got = best;                             // B - t of the latest frame t
+    if (got) {
+      if (threadIdx.x == 0) atomicMax(found, static_cast<unsigned long long>(hi - (B - got)));
+      return;
+    }
+    __syncthreads();                                       // best / stop are rewritten next round
+  }
+}
+
+__global__ void tail_carry_kernel(CtBatch b, const unsigned long long *found, uint32_t *carry) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || !*found) return;
+  uint32_t w[18], L;
+  load_window(b, *found - 1, w, L);
+  const Parsed p = parse(w, L, b.hook);
+  *carry = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
+}
+
 __global__ void stale_kernel(uint64_t n, const uint32_t *last, const uint32_t *pports, const uint32_t *carry,
                              uint32_t *out) {
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
@@ -819,6 +863,18 @@ int ct_stale_ports(const CtBatch &b, CtScratch &s, uint32_t *carry, bool update_
   if (b.n == 0) return hipSuccess;
   if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!out) {
+    if (!update_carry) return hipSuccess;
+    if (!s.zfound) CT_CHECK(hipMalloc(&s.zfound, 64));
+    CT_CHECK(hipMemsetAsync(s.zfound, 0, 8, st));
+    const unsigned blk = 256;
+    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>((b.n + blk - 1) / blk, uint64_t(num_cus) * 4));
+    hipLaunchKernelGGL(tail_ports_kernel, dim3(grid), dim3(blk), 0, st, b, s.zfound);
+    CT_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(tail_carry_kernel, dim3(1), dim3(64), 0, st, b, s.zfound, carry);
+    CT_CHECK(hipGetLastError());
+    return hipSuccess;
+  }
   if (s.zcap < b.n) {
     for (uint32_t **p : {&s.zpp, &s.zlast, &s.zports}) {
       if (*p) CT_CHECK(hipFree(*p));

@@ -61,6 +61,8 @@ struct CtBatch {
   unsigned long long *ae_ctr; // [3][2] pkts, bytes
   unsigned long long *horus_ctr;  // [PCN_IPT_HORUS_MAX][2] (null: Horus off); Horus hits are the
                                   // packets with rule id <= PCN_IPT_RID_HORUS0 (stage A found them)
+  uint32_t horus_final;       // pcn-firewall program built with conntrack off: an ACCEPT hit is RX_OK,
+                              // unlabelled (Firewall_Horus_dp.c:162-164)
 };
 
 struct CtTable {

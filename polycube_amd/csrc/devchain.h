@@ -62,6 +62,11 @@ namespace pcn {
 // slot and the packet's key.  sk / dk are the key's port bytes as the
 // reference's packed horusKey holds them, read as little-endian u16.
 constexpr uint32_t kHorusUsed = 1u << 9;
+// LaunchArgs::horus_flags (0: pcn-iptables)
+constexpr uint32_t kHzNatural = 1;       // pcn-firewall: the key holds the ports as stored (packed on both sides)
+constexpr uint32_t kHzAcceptFinal = 2;   // ACCEPT hit -> RX_OK (program built with conntrack off)
+constexpr uint32_t kHzAcceptDrops = 4;   // ACCEPT hit -> RX_DROP (PASS_LABELING into a deleted ConntrackLabel)
+constexpr uint32_t kHzMissDrops = 8;     // miss -> RX_DROP (the tail call into a deleted ConntrackLabel)
 PCN_HD inline uint32_t horus_hash(uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto) {
   uint64_t h = ((uint64_t(src) << 32) | dst) * 0x9E3779B97F4A7C15ull;
   h ^= ((uint64_t(ports) << 8) | proto) * 0xC2B2AE3D27D4EB4Full;
@@ -162,8 +167,9 @@ struct LaunchArgs {
   uint32_t fw;                   // 0: pcn-iptables dispatch; else pcn-firewall, PCN_FW_LAUNCH_*
   int32_t fast_chain;            // >= 0: every IPv4 TCP/UDP frame selects this chain (no localip,
                                  // allow logic or empty chain involved); -1: no wave fast path
-  // Horus (ingress pcn-iptables launches only; horus_fields == 0: off)
+  // Horus (the program the batch's Parser calls; horus_fields == 0: off)
   const uint32_t *horus;         // 4 u32 per slot
+  uint32_t horus_flags;          // kHz*
   uint32_t horus_mask;           // slots - 1
   uint32_t horus_probes;         // longest probe sequence of a stored key
   uint32_t horus_fields;         // PCN_IPT_HZ_* set fields of the key

@@ -110,6 +110,17 @@ struct ChainState {
   std::string jit_spec;
 };
 
+// One Horus program (pcn_ipt.h): pcn-iptables has one (ingress, built from
+// INPUT); pcn-firewall one per chain (Firewall.h:333-340).
+struct HorusProg {
+  bool runtime = false;                        // horus_runtime_enabled_
+  bool ct = false;                             // pcn-firewall: _CONNTRACK_ENABLED when built
+  uint32_t fields = 0, entries = 0, mask = 0, probes = 0;
+  uint32_t *d_tab = nullptr;                   // 4 u32 per slot
+  size_t cap = 0;
+  unsigned long long *d_ctr = nullptr;         // [PCN_IPT_HORUS_MAX][2]
+};
+
 }  // namespace
 
 struct pcn_ipt {
@@ -152,12 +163,10 @@ struct pcn_ipt {
   // the previous one's last conntrack kernel.
   hipEvent_t ev_ct = nullptr;
   bool ct_pending = false;
-  // Horus (pcn_ipt.h): the flag, the table in place and its counters
-  bool hz_enabled = false, hz_runtime = false;
-  uint32_t hz_fields = 0, hz_entries = 0, hz_mask = 0, hz_probes = 0;
-  uint32_t *d_horus = nullptr;                 // 4 u32 per slot
-  size_t d_horus_cap = 0;
-  unsigned long long *d_hz_ctr = nullptr;      // [PCN_IPT_HORUS_MAX][2]
+  // Horus (pcn_ipt.h): the flag and the programs in place with their counters:
+  // [0] pcn-iptables INPUT / pcn-firewall INGRESS, [1] pcn-firewall EGRESS
+  bool hz_enabled = false;
+  HorusProg hz[2];
   uint32_t *d_hz_carry = nullptr;              // the Parser's stale ports while conntrack is off
   uint32_t *d_stale = nullptr;                 // per-frame stale ports of the batch being classified
   size_t stale_cap = 0;
@@ -222,6 +231,29 @@ void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
   cs.tables = std::move(tables);
 }
 
+// The Horus program a chain's updates rebuild: pcn-iptables INPUT -> [0];
+// pcn-firewall INGRESS (FORWARD slot) -> [0], EGRESS (OUTPUT slot) -> [1].
+int horus_slot(const pcn_ipt *ctx, int chain) {
+  if (ctx->service == PCN_IPT_SERVICE_FIREWALL) return chain == PCN_IPT_FORWARD ? 0 : chain == PCN_IPT_OUTPUT ? 1 : -1;
+  return chain == PCN_IPT_INPUT ? 0 : -1;
+}
+
+// The program whose counters a chain's stats take.
+HorusProg *horus_stats_prog(pcn_ipt *ctx, int chain) {
+  if (ctx->service != PCN_IPT_SERVICE_FIREWALL) return &ctx->hz[0];
+  const int k = horus_slot(ctx, chain);
+  return k < 0 ? nullptr : &ctx->hz[k];
+}
+
+// The program a batch's Parser calls, if one is in place: pcn-iptables
+// ingress only (the egress Parser's tail call lands on an empty slot);
+// pcn-firewall the direction's own.
+const HorusProg *horus_of_batch(const pcn_ipt *ctx, int direction) {
+  const HorusProg *h = ctx->service == PCN_IPT_SERVICE_FIREWALL ? &ctx->hz[direction == PCN_IPT_INGRESS ? 0 : 1]
+                       : direction == PCN_IPT_INGRESS ? &ctx->hz[0] : nullptr;
+  return h && h->runtime ? h : nullptr;
+}
+
 // ChainStats::fetchCounters for every rule (read-and-flush into host totals),
 // i.e. Chain::getStatsList (Chain.cpp:961-976) without the DEFAULT row.
 void fetch_stats(pcn_ipt *ctx, int chain) {
@@ -238,18 +270,20 @@ void fetch_stats(pcn_ipt *ctx, int chain) {
     cs.stats[id].second += buf[3 + 2 * id];
   }
   hip_check(hipMemset(cs.ctr + 2, 0, 2 * size_t(n) * 8), "hipMemset(counters)");
-  // while a Horus table is in place, rule k of the chain read also takes (and
-  // flushes) Horus's counters of rule id k, whichever chain it is
-  // (ChainStats.cpp:106-121)
-  if (ctx->hz_runtime && !cs.stats.empty()) {
+  // while a Horus program is in place, rule k of the chain read also takes
+  // (and flushes) its counters of rule id k: pcn-iptables' one program
+  // whichever chain is read (ChainStats.cpp:106-121), pcn-firewall's the
+  // chain's own (pcn-firewall ChainStats.cpp:127-143)
+  const HorusProg *hp = horus_stats_prog(ctx, chain);
+  if (hp && hp->runtime && !cs.stats.empty()) {
     const size_t m = std::min<size_t>(cs.stats.size(), PCN_IPT_HORUS_MAX);
     std::vector<unsigned long long> hz(2 * m);
-    hip_check(hipMemcpy(hz.data(), ctx->d_hz_ctr, hz.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(horus counters)");
+    hip_check(hipMemcpy(hz.data(), hp->d_ctr, hz.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(horus counters)");
     for (size_t id = 0; id < m; ++id) {
       cs.stats[id].first += hz[2 * id];
       cs.stats[id].second += hz[2 * id + 1];
     }
-    hip_check(hipMemset(ctx->d_hz_ctr, 0, hz.size() * 8), "hipMemset(horus counters)");
+    hip_check(hipMemset(hp->d_ctr, 0, hz.size() * 8), "hipMemset(horus counters)");
   }
   // rule 0 of an accept-established chain also takes (and flushes) the
   // accept-established counters (ChainStats.cpp:64-103)
@@ -279,10 +313,11 @@ void apply_ae(pcn_ipt *ctx, int chain) {
   else for (int c = chain; c < PCN_IPT_NCHAINS; ++c) ctx->ae[c] = false;
 }
 
-// Chain::fromRuleToHorusKeyValue + horusFromRulesToMap (Utils.cpp:537-630):
-// the leading INPUT rules that set the same key fields as rule 0 (a /32
-// address, protocol, ports), up to the first conntrack rule; a repeated key
-// keeps its first rule (std::map::insert).
+// Chain::fromRuleToHorusKeyValue + horusFromRulesToMap (pcn-iptables
+// Utils.cpp:537-630, pcn-firewall Utils.cpp:483-577): the leading rules that
+// set the same key fields as rule 0 (a /32 address, protocol, ports), up to
+// the first conntrack rule; a repeated key keeps its first rule
+// (std::map::insert).
 struct HorusEntry {
   uint32_t src, dst, ports, meta;   // devchain.h slot layout
 };
@@ -321,23 +356,18 @@ std::vector<HorusEntry> horus_entries(const std::vector<Rule> &rules, uint32_t &
   return out;
 }
 
-// Chain::updateChain's Horus part (Chain.cpp:505-592), after every chain
-// update: the old table and its counters go; an INPUT update with horus on,
-// INPUT rules and an empty FORWARD rule list builds a new one.
-void horus_update(pcn_ipt *ctx, int chain) {
-  ctx->hz_runtime = false;
-  ctx->hz_entries = ctx->hz_fields = 0;
+// Drop a program (and its counters), then, with entries, build its table:
+// open addressing at load <= 1/2, linear probing; the kernel probes at most
+// `probes` slots.
+void horus_set(pcn_ipt *ctx, HorusProg &h, const std::vector<HorusEntry> &ents, uint32_t fields) {
+  h.runtime = false;
+  h.entries = h.fields = 0;
   if (ctx->has_device) {
     device_guard(ctx);
     hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    hip_check(hipMemset(ctx->d_hz_ctr, 0, PCN_IPT_HORUS_MAX * 16), "hipMemset(horus counters)");
+    hip_check(hipMemset(h.d_ctr, 0, PCN_IPT_HORUS_MAX * 16), "hipMemset(horus counters)");
   }
-  if (chain != PCN_IPT_INPUT || !ctx->hz_enabled || ctx->service != PCN_IPT_SERVICE_IPTABLES) return;
-  if (ctx->chains[PCN_IPT_INPUT].rules.empty() || !ctx->chains[PCN_IPT_FORWARD].rules.empty()) return;
-  uint32_t fields = 0;
-  const std::vector<HorusEntry> ents = horus_entries(ctx->chains[PCN_IPT_INPUT].rules, fields);
   if (ents.empty()) return;
-  // open addressing at load <= 1/2, linear probing; the kernel probes at most `probes` slots
   uint32_t size = 16;
   while (size < 2 * ents.size()) size <<= 1;
   std::vector<HorusEntry> tab(size, HorusEntry{0, 0, 0, 0});
@@ -350,25 +380,49 @@ void horus_update(pcn_ipt *ctx, int chain) {
   }
   if (ctx->has_device) {
     const size_t bytes = size_t(size) * sizeof(HorusEntry);
-    if (ctx->d_horus_cap < bytes) {
-      if (ctx->d_horus) hip_check(hipFree(ctx->d_horus), "hipFree");
-      ctx->d_horus = nullptr;
-      hip_check(hipMalloc(&ctx->d_horus, bytes), "hipMalloc(horus table)");
-      ctx->d_horus_cap = bytes;
+    if (h.cap < bytes) {
+      if (h.d_tab) hip_check(hipFree(h.d_tab), "hipFree");
+      h.d_tab = nullptr;
+      hip_check(hipMalloc(&h.d_tab, bytes), "hipMalloc(horus table)");
+      h.cap = bytes;
     }
-    hip_check(hipMemcpy(ctx->d_horus, tab.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(horus table)");
+    hip_check(hipMemcpy(h.d_tab, tab.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(horus table)");
   }
-  ctx->hz_fields = fields;
-  ctx->hz_entries = static_cast<uint32_t>(ents.size());
-  ctx->hz_mask = size - 1;
-  ctx->hz_probes = probes;
-  ctx->hz_runtime = true;
+  h.fields = fields;
+  h.entries = static_cast<uint32_t>(ents.size());
+  h.mask = size - 1;
+  h.probes = probes;
+  h.runtime = true;
 }
 
-void update_chain(pcn_ipt *ctx, int chain) {       // Chain::updateChain
+// Chain::updateChain's Horus part, after every update of `chain` (build =
+// false: the chain's rules are not known, pcn_ipt_load_chain).
+// pcn-iptables (Chain.cpp:505-592): any update drops the program; an INPUT
+// update with horus on, INPUT rules and an empty FORWARD rule list builds a
+// new one.  pcn-firewall (Chain.cpp:232-306): an INGRESS / EGRESS update
+// rebuilds that chain's own program when horus is on and the chain has rules;
+// the program keeps the conntrack setting it was compiled with
+// (modules/Horus.cpp:135-139; setConntrack does not reload it).
+void horus_update(pcn_ipt *ctx, int chain, bool build = true) {
+  const bool firewall = ctx->service == PCN_IPT_SERVICE_FIREWALL;
+  const int k = firewall ? horus_slot(ctx, chain) : 0;
+  if (k < 0) return;
+  HorusProg &h = ctx->hz[k];
+  uint32_t fields = 0;
+  std::vector<HorusEntry> ents;
+  const bool want = build && ctx->hz_enabled &&
+                    (firewall ? !ctx->chains[chain].rules.empty()
+                              : chain == PCN_IPT_INPUT && !ctx->chains[PCN_IPT_INPUT].rules.empty() &&
+                                    ctx->chains[PCN_IPT_FORWARD].rules.empty());
+  if (want) ents = horus_entries(ctx->chains[chain].rules, fields);
+  horus_set(ctx, h, ents, fields);
+  h.ct = firewall && ctx->fw_ct_mode != PCN_FW_CT_DISABLED;
+}
+
+void update_chain(pcn_ipt *ctx, int chain, bool horus = true) {   // Chain::updateChain
   ChainState &cs = ctx->chains[chain];
   load_tables(ctx, chain, compile_chain(cs.rules, chain, cs.default_action, ctx->ports));
-  horus_update(ctx, chain);
+  if (horus) horus_update(ctx, chain);
 }
 
 bool valid_chain(int c) { return c >= 0 && c < PCN_IPT_NCHAINS; }
@@ -443,8 +497,10 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
       const uint8_t labels[4] = {0, 1, 2, 3};
       hip_check(hipMemcpy(ctx->d_labels, labels, 4, hipMemcpyHostToDevice), "hipMemcpy(labels)");
       hip_check(hipMalloc(&ctx->ctr_scratch, 3 * ctx->ctr_words * 8), "hipMalloc(scratch counters)");
-      hip_check(hipMalloc(&ctx->d_hz_ctr, PCN_IPT_HORUS_MAX * 16), "hipMalloc(horus counters)");
-      hip_check(hipMemset(ctx->d_hz_ctr, 0, PCN_IPT_HORUS_MAX * 16), "hipMemset(horus counters)");
+      for (HorusProg &h : ctx->hz) {
+        hip_check(hipMalloc(&h.d_ctr, PCN_IPT_HORUS_MAX * 16), "hipMalloc(horus counters)");
+        hip_check(hipMemset(h.d_ctr, 0, PCN_IPT_HORUS_MAX * 16), "hipMemset(horus counters)");
+      }
       hip_check(hipMalloc(&ctx->d_hz_carry, 64), "hipMalloc(horus carry)");
       hip_check(hipMemset(ctx->d_hz_carry, 0, 64), "hipMemset(horus carry)");
       for (auto &cs : ctx->chains) {
@@ -491,7 +547,8 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     if (ctx->ev_staged) (void)hipEventDestroy(ctx->ev_staged);
     if (ctx->ev_gathered) (void)hipEventDestroy(ctx->ev_gathered);
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
-    for (void *p : {static_cast<void *>(ctx->d_horus), static_cast<void *>(ctx->d_hz_ctr),
+    for (void *p : {static_cast<void *>(ctx->hz[0].d_tab), static_cast<void *>(ctx->hz[0].d_ctr),
+                    static_cast<void *>(ctx->hz[1].d_tab), static_cast<void *>(ctx->hz[1].d_ctr),
                     static_cast<void *>(ctx->d_hz_carry), static_cast<void *>(ctx->d_stale)})
       if (p) (void)hipFree(p);
   }
@@ -616,9 +673,11 @@ int pcn_ipt_chain_set_default(pcn_ipt *ctx, int chain, int action) {
     if (cs.default_action == action) return 0;
     cs.default_action = action;
     // Chain::setDefault -> reloadChain: the programs are rebuilt from the
-    // current rule list with the new default action.
+    // current rule list with the new default action.  pcn-firewall reloads only
+    // its DefaultAction program (pcn-firewall Chain.cpp:60-82): no chain
+    // update, so its Horus program stays in place.
     fetch_stats(ctx, chain);
-    update_chain(ctx, chain);
+    update_chain(ctx, chain, ctx->service != PCN_IPT_SERVICE_FIREWALL);
     return 0;
   });
 }
@@ -675,7 +734,7 @@ int pcn_ipt_load_chain(pcn_ipt *ctx, int chain, const pcn_ipt_tables *t) {
       }
     }
     load_tables(ctx, chain, std::move(ct));
-    horus_update(ctx, -1);     // an update without rules: no Horus table (Chain.cpp:505)
+    horus_update(ctx, chain, false);   // an update without rules: no Horus program (Chain.cpp:505)
     return 0;
   });
 }
@@ -841,15 +900,21 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.count_mask = b->direction == PCN_IPT_INGRESS
                        ? (1u << PCN_IPT_FORWARD) | (has_local && !firewall ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
-    // Horus: ingress pcn-iptables launches while a table is in place
+    // Horus: the program the batch's Parser calls, while one is in place
     a.stale_ports = reinterpret_cast<const uint32_t *>(ctx->d_zero);
     a.stale_mask = 0;
-    if (ctx->hz_runtime && !firewall && b->direction == PCN_IPT_INGRESS) {
-      a.horus = ctx->d_horus;
-      a.horus_mask = ctx->hz_mask;
-      a.horus_probes = ctx->hz_probes;
-      a.horus_fields = ctx->hz_fields;
-      a.horus_ctr = sa ? nullptr : ctx->d_hz_ctr;     // stage A: ct_count counts the final outcome
+    if (const HorusProg *hz = horus_of_batch(ctx, b->direction)) {
+      a.horus = hz->d_tab;
+      a.horus_mask = hz->mask;
+      a.horus_probes = hz->probes;
+      a.horus_fields = hz->fields;
+      a.horus_ctr = sa ? nullptr : hz->d_ctr;         // stage A: ct_count counts the final outcome
+      if (firewall) {
+        a.horus_flags = kHzNatural;
+        if (!hz->ct) a.horus_flags |= kHzAcceptFinal;                        // Firewall_Horus_dp.c:162-164
+        else if (ctx->fw_ct_mode == PCN_FW_CT_DISABLED) a.horus_flags |= kHzAcceptDrops;
+        if (ctx->fw_ct_mode == PCN_FW_CT_DISABLED) a.horus_flags |= kHzMissDrops;   // :170-174
+      }
       a.fast_chain = -1;                               // the lookup lives in the general path
       if (stale) {
         a.stale_ports = stale;
@@ -868,7 +933,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.lds = a.lds_images_bytes > 0;
       shape.ch = ch;
       shape.ns = ns;
-      shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0);
+      shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0) |
+                     (a.horus_fields ? 16 : 0);
       DevChain key = a.ch[ch];
       key.image = nullptr;
       key.ctr = nullptr;
@@ -917,7 +983,9 @@ CtBatch ct_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, uint32_t ae_mask) {
   }
   cb.ae_mask = ae_mask;
   cb.ae_ctr = ctx->d_ae;
-  cb.horus_ctr = ctx->hz_runtime ? ctx->d_hz_ctr : nullptr;
+  const HorusProg *hz = horus_of_batch(ctx, b->direction);
+  cb.horus_ctr = hz ? hz->d_ctr : nullptr;
+  cb.horus_final = hz && cb.fw && !hz->ct;          // pcn-firewall built with conntrack off: ACCEPT is RX_OK
   cb.verdicts = b->verdicts;
   cb.rule_ids = b->rule_ids;
   return cb;
@@ -945,11 +1013,13 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     const bool firewall = ctx->service == PCN_IPT_SERVICE_FIREWALL;
     const bool stateful = ctx->ct_on && !(firewall && ctx->fw_ct_mode == PCN_FW_CT_DISABLED);
     // Horus keys read the Parser's stale ports (Q4): tracked from batch to
-    // batch while horus is set (the connection table keeps its own copy)
-    const bool track = ctx->hz_enabled && !firewall;
-    const bool want_stale = ctx->hz_runtime && b->direction == PCN_IPT_INGRESS &&
-                            (ctx->hz_fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT));
-    const bool serial = stateful || (track && !stateful);
+    // batch while horus is set, in the connection table's own copy while it is
+    // on (advanced by ct_run in stateful batches, here otherwise: pcn-firewall
+    // with conntrack DISABLED still parses into the same struct)
+    const bool track = ctx->hz_enabled || (ctx->ct_on && !stateful);
+    const HorusProg *hz = horus_of_batch(ctx, b->direction);
+    const bool want_stale = hz && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT));
+    const bool serial = stateful || track;
     if (serial && (!b->frames || !b->verdicts)) return fail(-EINVAL, "frames and verdicts are required");
     device_guard(ctx);
     // batches that share the context's conntrack / stale-port state run one
@@ -964,8 +1034,8 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
         hip_check(hipMalloc(&ctx->d_stale, b->n * 4), "hipMalloc(stale ports)");
         ctx->stale_cap = b->n;
       }
-      // with the connection table on, its own copy (read here, advanced by ct_run)
-      uint32_t *carry = stateful ? ctx->ct.carry : ctx->d_hz_carry;
+      // with the connection table on, its own copy (advanced by ct_run when stateful)
+      uint32_t *carry = ctx->ct_on ? ctx->ct.carry : ctx->d_hz_carry;
       const int e = ct_stale_ports(ct_batch(ctx, b, 0), *ctx->cts, carry, !stateful, want_stale ? ctx->d_stale : nullptr,
                                    ctx->num_cus, st);
       if (e != hipSuccess) return fail(-EIO, std::string("stale ports: ") + hipGetErrorString(hipError_t(e)));
@@ -1157,6 +1227,11 @@ int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain) {
       // pcn-firewall also flushes the DefaultAction counters (pcn-firewall Chain.cpp:154-155)
       const size_t from = ctx->service == PCN_IPT_SERVICE_FIREWALL ? 0 : 2;
       hip_check(hipMemset(cs.ctr + from, 0, (ctx->ctr_words - from) * 8), "hipMemset(counters)");
+      // ... and the chain's Horus counters of its rule ids (pcn-firewall Chain.cpp:139-152)
+      const int k = horus_slot(ctx, chain);
+      if (ctx->service == PCN_IPT_SERVICE_FIREWALL && k >= 0 && ctx->hz[k].runtime)
+        hip_check(hipMemset(ctx->hz[k].d_ctr, 0,
+                            std::min<size_t>(cs.rules.size(), PCN_IPT_HORUS_MAX) * 16), "hipMemset(horus counters)");
     }
     cs.stats.assign(cs.rules.size(), {0, 0});     // counters_.clear()
     return 0;
@@ -1368,32 +1443,38 @@ int pcn_ipt_read_accept_established(pcn_ipt *ctx, int chain, uint64_t *pkts, uin
 
 int pcn_ipt_set_horus(pcn_ipt *ctx, int on) {
   return guarded(ctx, [&] {
-    if (ctx->service != PCN_IPT_SERVICE_IPTABLES) return fail(-EINVAL, "horus is a pcn-iptables setting");
-    // Iptables::setHorus (Iptables.cpp:400-406): the flag; the next chain update acts on it
+    // Iptables::setHorus (Iptables.cpp:400-406): the flag; the next chain
+    // update acts on it.  (pcn-firewall has no such knob: on from the start.)
     ctx->hz_enabled = on != 0;
     return 0;
   });
 }
 
-int pcn_ipt_get_horus_info(pcn_ipt *ctx, pcn_ipt_horus_info *out) {
+int pcn_ipt_get_horus_info(pcn_ipt *ctx, int chain, pcn_ipt_horus_info *out) {
   return guarded(ctx, [&] {
     if (!out) return fail(-EINVAL, "null output");
+    const int k = horus_slot(ctx, chain);
+    if (k < 0) return fail(-EINVAL, "no Horus program for this chain");
+    const HorusProg &h = ctx->hz[k];
     out->enabled = ctx->hz_enabled;
-    out->runtime = ctx->hz_runtime;
-    out->entries = ctx->hz_entries;
-    out->fields = ctx->hz_fields;
+    out->runtime = h.runtime;
+    out->entries = h.entries;
+    out->fields = h.fields;
+    out->conntrack = h.runtime && h.ct;
     return 0;
   });
 }
 
-int pcn_ipt_read_horus_counters(pcn_ipt *ctx, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush) {
+int pcn_ipt_read_horus_counters(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *bytes, uint32_t n, int flush) {
   return guarded(ctx, [&] {
+    const int k = horus_slot(ctx, chain);
+    if (k < 0) return fail(-EINVAL, "no Horus program for this chain");
     std::vector<unsigned long long> v(2 * size_t(PCN_IPT_HORUS_MAX), 0);
     if (ctx->has_device) {
       device_guard(ctx);
       hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-      hip_check(hipMemcpy(v.data(), ctx->d_hz_ctr, v.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(horus counters)");
-      if (flush) hip_check(hipMemset(ctx->d_hz_ctr, 0, v.size() * 8), "hipMemset(horus counters)");
+      hip_check(hipMemcpy(v.data(), ctx->hz[k].d_ctr, v.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(horus counters)");
+      if (flush) hip_check(hipMemset(ctx->hz[k].d_ctr, 0, v.size() * 8), "hipMemset(horus counters)");
     }
     for (uint32_t i = 0; i < n; ++i) {
       if (pkts) pkts[i] = i < PCN_IPT_HORUS_MAX ? v[2 * size_t(i)] : 0;
@@ -1415,6 +1496,10 @@ int pcn_ipt_set_service(pcn_ipt *ctx, int service) {
     ctx->service = service;
     ctx->fw_ct_mode = PCN_FW_CT_AUTOMATIC;            // Firewall.h:323
     for (bool &on : ctx->ae) on = false;
+    // pcn-firewall's horus_enabled is true from the start (Firewall.h:337);
+    // pcn-iptables' leaf is OFF by default (Iptables.h:185)
+    ctx->hz_enabled = service == PCN_IPT_SERVICE_FIREWALL;
+    for (HorusProg &h : ctx->hz) horus_set(ctx, h, {}, 0);
     return 0;
   });
 }

@@ -82,11 +82,12 @@ class CtInfo(C.Structure):
 
 
 class HorusInfo(C.Structure):
-    _fields_ = [("enabled", C.c_uint32), ("runtime", C.c_uint32), ("entries", C.c_uint32), ("fields", C.c_uint32)]
+    _fields_ = [("enabled", C.c_uint32), ("runtime", C.c_uint32), ("entries", C.c_uint32), ("fields", C.c_uint32),
+                ("conntrack", C.c_uint32)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
-ABI_VERSION = 4            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
+ABI_VERSION = 5            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
 
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
@@ -131,8 +132,8 @@ SIGNATURES = {
                                         C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.POINTER(C.c_int32))]),
     "pcn_ipt_ring_release": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pcn_ipt_set_horus": (C.c_int, [C.c_void_p, C.c_int]),
-    "pcn_ipt_get_horus_info": (C.c_int, [C.c_void_p, C.POINTER(HorusInfo)]),
-    "pcn_ipt_read_horus_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+    "pcn_ipt_get_horus_info": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(HorusInfo)]),
+    "pcn_ipt_read_horus_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                               C.c_uint32, C.c_int]),
     "pcn_ipt_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "pcn_ipt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),

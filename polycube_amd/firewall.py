@@ -94,6 +94,14 @@ class Firewall(Iptables):
     def chain(self, name):
         return self.chains[name.upper()] if isinstance(name, str) else FwChain(self, name)
 
+    _HORUS_CHAIN = INGRESS_CHAIN
+
+    def _horus_chain(self, chain):
+        """Horus programs are per chain here (INGRESS / EGRESS; Firewall.h:333-340)."""
+        if chain is None:
+            return self._HORUS_CHAIN
+        return _FW_CHAINS[chain.upper()] if isinstance(chain, str) else int(chain)
+
     @property
     def conntrack_mode(self):
         return _check(ffi.lib().pcn_fw_get_conntrack_mode(self._h))

@@ -209,6 +209,8 @@ class Iptables:
         _check(ffi.lib().pcn_ipt_load_chain(self._h, chain, C.byref(tables)))
 
     # ---- Horus (the `horus` leaf, iptables.yang:112-118) ----
+    _HORUS_CHAIN = 0           # the chain whose program horus_info() / read_horus_counters() name by default
+
     @property
     def horus(self):
         """"ON" / "OFF" (Iptables::getHorus); setting it takes effect at the next chain update."""
@@ -219,16 +221,22 @@ class Iptables:
         on = v if isinstance(v, bool) else str(v).upper() == "ON"
         _check(ffi.lib().pcn_ipt_set_horus(self._h, int(on)))
 
-    def horus_info(self):
+    def _horus_chain(self, chain):
+        if chain is None:
+            return self._HORUS_CHAIN
+        return _CHAIN_NAMES[chain.upper()] if isinstance(chain, str) else int(chain)
+
+    def horus_info(self, chain=None):
+        """The Horus program of `chain` (pcn-iptables: INPUT)."""
         out = ffi.HorusInfo()
-        _check(ffi.lib().pcn_ipt_get_horus_info(self._h, C.byref(out)))
+        _check(ffi.lib().pcn_ipt_get_horus_info(self._h, self._horus_chain(chain), C.byref(out)))
         return {k: getattr(out, k) for k, _ in ffi.HorusInfo._fields_}
 
-    def read_horus_counters(self, n, flush=False):
+    def read_horus_counters(self, n, flush=False, chain=None):
         """pkts_horus / bytes_horus of rule ids 0..n-1 (lists)."""
         pk = (C.c_uint64 * max(n, 1))()
         by = (C.c_uint64 * max(n, 1))()
-        _check(ffi.lib().pcn_ipt_read_horus_counters(self._h, pk, by, n, int(flush)))
+        _check(ffi.lib().pcn_ipt_read_horus_counters(self._h, self._horus_chain(chain), pk, by, n, int(flush)))
         return list(pk[:n]), list(by[:n])
 
     # ---- datapath (device pointers; torch tensors accepted for convenience) ----

@@ -291,10 +291,13 @@ class OracleFwCube:
     def _fetch(self, c):                      # Chain::getStatsList
         n = len(self.rules[c])
         pk, by, _, _ = self.o.read_counters(FW_CHAINS[c], n, flush=True)
+        # the chain's Horus counters of each rule id too (ChainStats.cpp:127-143;
+        # zero whenever no program is in place: every rebuild starts them at 0)
+        hp, hb = self.o.read_horus_counters(n, flush=True, chain=FW_CHAINS[c])
         st = self.stats[c]
         st.extend([[0, 0]] * (n - len(st)))
         for i in range(n):
-            st[i] = [st[i][0] + pk[i], st[i][1] + by[i]]
+            st[i] = [st[i][0] + pk[i] + hp[i], st[i][1] + by[i] + hb[i]]
 
     def _check_rule(self, r):
         if "action" not in r:
@@ -324,10 +327,10 @@ class OracleFwCube:
             return
         c = op[1]
         rules, st = self.rules[c], self.stats[c]
-        if kind == "default":
+        if kind == "default":                 # Chain::setDefault: no chain update (Chain.cpp:60-82)
             self.default[c] = op[2]
             self._fetch(c)
-            self._apply(c)
+            self.o.set_default(FW_CHAINS[c], op[2])
             return
         if kind == "reset_counters":
             self._fetch(c)

@@ -229,3 +229,144 @@ def test_turning_horus_off_takes_effect_at_the_next_update(dev):
     v_o, r_o, v_g, r_g = run(o, ipt, dev, fwd)
     assert_same(v_o, r_o, v_g, r_g)
     assert v_g[0] == 0 and ipt.horus_info()["runtime"] == 0
+
+
+# ---- pcn-firewall: one program per chain, natural port key, conntrack compiled in ----
+FW_IN, FW_EG = 1, 2
+
+
+def fw_rule_packets(rng, r, direction):
+    """Packets whose key is rule r's (pcn-firewall: the ports as on the wire).
+    A rule for a protocol without ports gets a UDP packet first that leaves
+    its ports behind (Q4)."""
+    proto = PROTO[r["l4proto"]] if "l4proto" in r else int(rng.choice([6, 17]))
+    sport = r.get("sport", int(rng.integers(0, 65536)))
+    dport = r.get("dport", int(rng.integers(0, 65536)))
+    src = r.get("src", ADDRS[int(rng.integers(0, 5))]).split("/")[0]
+    dst = r.get("dst", HOST).split("/")[0]
+    base = {"dir": direction, "port": 1, "src": src, "dst": dst, "proto": proto, "sport": sport, "dport": dport,
+            "flags": int(rng.choice([0x02, 0x10, 0x12])), "icmp_type": 8,
+            "len": {6: 74, 17: 64, 1: 98, 47: 64}[proto]}
+    if proto in (6, 17):
+        return [base]
+    return [dict(base, proto=17, src="8.8.4.4", len=64), base]
+
+
+def fw_traffic(rng, n, rules, direction):
+    ports = [r[k] for r in rules for k in ("sport", "dport") if k in r] or [80]
+    pk = []
+    while len(pk) < n:
+        if rules and rng.random() < 0.3:
+            pk.extend(fw_rule_packets(rng, rules[int(rng.integers(0, len(rules)))], direction))
+            continue
+        proto = int(rng.choice([6, 17, 17, 1, 47]))
+        a = ADDRS[rng.integers(0, len(ADDRS))] if rng.random() < 0.7 else \
+            ".".join(str(int(x)) for x in rng.integers(1, 255, 4))
+        b = HOST if rng.random() < 0.6 else ADDRS[rng.integers(0, len(ADDRS))]
+        src, dst = (a, b) if direction == "ingress" else (b, a)
+        pick = lambda: int(rng.choice(ports)) if rng.random() < 0.4 else int(rng.integers(0, 65536))  # noqa: E731
+        length = {6: 74, 17: 64, 1: 98, 47: 64}[proto]
+        if proto == 1 and rng.random() < 0.2:
+            length = int(rng.choice([40, 66, 70]))
+        pk.append({"dir": direction, "port": 1, "src": src, "dst": dst, "proto": proto, "sport": pick(),
+                   "dport": pick(), "flags": int(rng.choice([0x02, 0x10, 0x12, 0x11])),
+                   "icmp_type": int(rng.choice([0, 3, 8, 11])), "len": length})
+    return pk
+
+
+FW_EGRESS_RULES = [{"dst": ADDRS[0], "l4proto": "UDP", "action": "ACCEPT"},
+                   {"dst": ADDRS[1], "l4proto": "UDP", "action": "DROP"},
+                   {"dst": ADDRS[2], "l4proto": "TCP", "action": "ACCEPT"},
+                   {"dst": ADDRS[3], "l4proto": "ICMP", "action": "DROP"}]
+
+
+def fw_setup(ingress, egress, jit, stateful, defaults=("DROP", "ACCEPT")):
+    from polycube_amd import Firewall
+    o = Oracle()
+    o.set_service(1, 2)
+    f = Firewall(device=0, jit=jit)
+    if stateful:
+        o.ct_enable()
+        o.ct_set_time(NOW)
+        f.ct_enable(14)
+        f.ct_set_time(NOW)
+    for c, name, rules, d in ((FW_IN, "INGRESS", ingress, defaults[0]), (FW_EG, "EGRESS", egress, defaults[1])):
+        ch = f.chain(name)
+        ch.default = d
+        for r in rules:
+            ch.append(**r)
+        o.set_chain(c, list(rules), d)
+        assert o.horus_info(c) == f.horus_info(name)
+    return o, f
+
+
+def fw_mode(o, f, mode):
+    """0 DISABLED / 1 MANUAL / 2 AUTOMATIC on both (Firewall.cpp:112-191)."""
+    if mode == 0:
+        f.conntrack = "OFF"
+    else:
+        f.conntrack = "ON"
+        f.accept_established = "ON" if mode == 2 else "OFF"
+    o.set_service(1, mode)
+    assert f.conntrack_mode == mode
+
+
+def fw_compare(o, f, dev, pk, direction):
+    v_o, r_o, v_g, r_g = run(o, f, dev, pk, direction=direction)
+    assert_same(v_o, r_o, v_g, r_g)
+    return int((r_o <= RID_HORUS0).sum())
+
+
+@JIT
+@pytest.mark.parametrize("stateful", [False, True], ids=["stateless", "table"])
+@pytest.mark.parametrize("kind", ["src", "proto_ports", "five"])
+def test_firewall_horus_parity_across_modes(dev, jit, kind, stateful):
+    """Both chains' programs, every conntrack mode switch the REST API allows
+    and a rebuild while conntrack is off (ACCEPT hits then final, misses
+    dropped while it stays off): verdicts, rule ids, the chains' and the Horus
+    counters, and the session table."""
+    ingress = rule_sets()[kind]
+    rng = np.random.default_rng(7 + len(kind) + 10 * stateful)
+    o, f = fw_setup(ingress, FW_EGRESS_RULES, jit, stateful)
+    assert f.horus_info("INGRESS")["runtime"] == 1 and f.horus_info("EGRESS")["entries"] == 4
+    hits = 0
+    for k, mode in enumerate([2, 1, 0, "rebuild", 0, 1, 2]):
+        if mode == "rebuild":          # two INGRESS updates while conntrack is off: built without it
+            f.chain("INGRESS").append(src="6.6.6.6", action="DROP")
+            f.chain("INGRESS").delete(len(ingress))
+            o.set_chain(FW_IN, list(ingress), "DROP")
+            assert f.horus_info("INGRESS") == o.horus_info(FW_IN) and o.horus_info(FW_IN)["conntrack"] == 0
+            continue
+        fw_mode(o, f, mode)
+        hits += fw_compare(o, f, dev, fw_traffic(rng, 1500 + 300 * k, ingress, "ingress"), 0)
+        hits += fw_compare(o, f, dev, fw_traffic(rng, 700, FW_EGRESS_RULES, "egress"), 1)
+    assert hits > 800
+    assert_counters(o, f, chains=(FW_IN, FW_EG), n=len(ingress) + 1)
+    for c, name in ((FW_IN, "INGRESS"), (FW_EG, "EGRESS")):
+        assert o.read_horus_counters(64, chain=c) == f.read_horus_counters(64, chain=name)
+    if stateful:
+        assert_tables(o, f)
+    f.close()
+
+
+def test_firewall_chain_stats_fold_their_own_program(dev):
+    """pcn-firewall ChainStats::fetchCounters: each chain takes its own
+    program's counters (ChainStats.cpp:127-143); reset_counters flushes them
+    (Chain.cpp:139-152); a default change keeps the program (Chain.cpp:60-82)."""
+    o, f = fw_setup([{"src": ADDRS[0], "action": "ACCEPT"}], [{"dst": ADDRS[0], "action": "ACCEPT"}], -1, False)
+    fw_compare(o, f, dev, [pkt_fw(ADDRS[0], HOST, "ingress")] * 3, 0)
+    fw_compare(o, f, dev, [pkt_fw(HOST, ADDRS[0], "egress")] * 2, 1)
+    f.chain("INGRESS").default = "ACCEPT"
+    assert f.horus_info("INGRESS")["runtime"] == 1
+    assert [x[1] for x in f.chain("INGRESS").stats()[:1]] == [3]
+    assert [x[1] for x in f.chain("EGRESS").stats()[:1]] == [2]
+    fw_compare(o, f, dev, [pkt_fw(HOST, ADDRS[0], "egress")] * 4, 1)
+    f.chain("EGRESS").reset_counters()
+    assert f.read_horus_counters(1, chain="EGRESS")[0] == [0]
+    assert [x[1] for x in f.chain("EGRESS").stats()[:1]] == [0]
+    f.close()
+
+
+def pkt_fw(src, dst, direction, proto=17):
+    return {"dir": direction, "port": 1, "src": src, "dst": dst, "proto": proto, "sport": 1, "dport": 2,
+            "flags": 0, "len": 64}

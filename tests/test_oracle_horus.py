@@ -57,7 +57,7 @@ def test_forwarded_traffic_meets_input_rules():
     PASS_LABELING), although FORWARD's default is DROP."""
     rules = [{"src": A, "action": "DROP"}, {"src": B, "action": "ACCEPT"}]
     o = cube(rules)
-    assert o.horus_info() == {"enabled": 1, "runtime": 1, "entries": 2, "fields": 1}
+    assert o.horus_info() == {"enabled": 1, "runtime": 1, "entries": 2, "fields": 1, "conntrack": 0}
     pk = [pkt(A, "9.9.9.9"), pkt(B, "9.9.9.9"), pkt(C, "9.9.9.9"), pkt(B, HOST, length=80)]
     v, r = run(o, pk)
     assert list(v) == [0, 1, 0, 1]
