@@ -266,6 +266,33 @@ __device__ __forceinline__ bool horus_lookup(const LaunchArgs &a, uint32_t saddr
   return false;
 }
 
+// Fused stale ports: one published word per 64-frame group,
+// {epoch:24 | status:2 | ports:32} (an old epoch: not published yet).
+constexpr uint32_t kStaleLocal = 1;       // the group's last TCP/UDP frame's ports
+constexpr uint32_t kStaleInclusive = 2;   // no TCP/UDP frame in the group: the ports before it
+constexpr uint32_t kStaleNone = 3;        // no TCP/UDP frame in the group, the ports before it not known
+__device__ __forceinline__ uint64_t stale_word(uint32_t epoch, uint32_t status, uint32_t ports) {
+  return (static_cast<uint64_t>(epoch) << 40) | (static_cast<uint64_t>(status) << 32) | ports;
+}
+// The ports the last TCP/UDP frame before group g left: walk back through the
+// published groups (waiting for one not yet published: it belongs to a
+// workgroup that started earlier), else the carry of the previous batches.
+__device__ uint32_t stale_lookback(const LaunchArgs &a, uint64_t g) {
+  g = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g >> 32))) << 32) |
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g));
+  while (g > 0) {
+    --g;
+    uint64_t d;
+    for (;;) {
+      d = __hip_atomic_load(&a.stale_desc[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((d >> 40) == a.stale_epoch) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (((d >> 32) & 3) != kStaleNone) return static_cast<uint32_t>(d);
+  }
+  return *a.stale_carry;
+}
+
 struct Parsed {
   uint32_t saddr, daddr;       // NBO as loaded
   uint32_t proto, sport, dport, flags;
@@ -581,9 +608,34 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   if (!PCN_STAGE_FAST) stage_images();
   uint32_t *const byte_bins = bins + a.nbins;
   const uint32_t const_port = a.const_in_port;
-  const uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t n_round = (a.n + step - 1) / step * step;   // uniform trip count per wave
+#ifndef PCN_DBG_HZ
+#define PCN_DBG_HZ 0     // measurement only: 1 = no stale-port tracking, 2 = no Horus lookups
+#endif
+  // The Parser's stale ports (Q4) for Horus keys, computed here (has_stale):
+  // each workgroup takes a contiguous chunk of the batch, in the order the
+  // workgroups start (a counter), and every 64-frame group publishes the
+  // ports of its last TCP/UDP frame; a frame that needs the ports of an
+  // earlier group looks back through the published groups.  A workgroup only
+  // ever waits on groups of workgroups that started before it, so the waits
+  // always resolve.
+  constexpr bool kStale = (!JIT || (kJitInputs & 8)) && PCN_DBG_HZ != 1;
+  constexpr bool kHorus = (!JIT || (kJitInputs & 16)) && PCN_DBG_HZ != 2;   // a Horus program is in place
+  const bool chunked = kStale && a.has_stale;
+  uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint64_t n_round = (a.n + step - 1) / step * step;   // uniform trip count per wave
+  if (chunked) {
+    uint32_t *slot = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);   // zeroed after the prologue
+    if (threadIdx.x == 0) *slot = atomicAdd(a.chunk_ctr, 1u);
+    __syncthreads();
+    const uint64_t b = *slot;
+    __syncthreads();
+    const uint64_t lo = b * a.chunk_frames, hi = lo + a.chunk_frames;
+    const uint64_t nr = (a.n + blockDim.x - 1) / blockDim.x * blockDim.x;
+    first = lo + threadIdx.x;
+    step = blockDim.x;
+    n_round = hi < nr ? hi : nr;
+  }
   // software pipeline: the next frame's header is in flight while this one is classified
   // The prefetch is unconditional (the index is clamped to the last frame):
   // a conditional load merges into a phi the compiler can only resolve with
@@ -600,7 +652,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   struct Stage {
     Hdr h;          // generic path
     u32x4 c[3];     // fixed path: this lane's three chunks
-    uint32_t L, port, ct, stale;
+    uint32_t L, port, ct;
   };
   const uint32_t lane = threadIdx.x & 63;
   // fixed path: frame within the wave's group, byte offset of the chunk, and
@@ -616,8 +668,6 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // per-frame side inputs a chain program knows it does not have are never loaded
   constexpr bool kLoadPort = !JIT || (kJitInputs & 1);
   constexpr bool kLoadCt = !JIT || (kJitInputs & 6);
-  constexpr bool kLoadStale = !JIT || (kJitInputs & 8);
-  constexpr bool kHorus = !JIT || (kJitInputs & 16);   // a Horus program is in place
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   constexpr int PF = FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
   Stage st[PF];
@@ -652,7 +702,6 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     const uint64_t jc = j < a.n ? j : last;
     x.port = kLoadPort ? a.in_port[jc & a.in_port_mask] : 0u;
     x.ct = kLoadCt ? a.ct_status[jc & a.ct_mask] : 0u;
-    x.stale = kLoadStale ? a.stale_ports[jc & a.stale_mask] : 0u;
   };
 #pragma unroll
   for (int d = 0; d < PF; ++d) prefetch(st[d], first + d * step);
@@ -699,9 +748,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       for (int k = 0; k < 13; ++k) asm volatile("" : "+v"(cur.h.w[k]));
       h = cur.h;
     }
-    asm volatile("" : "+v"(cur.port), "+v"(cur.ct), "+v"(cur.stale));
+    asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
     uint32_t L = FIXED ? a.fixed_len : cur.L;
-    const uint32_t cur_port = cur.port, cur_ct = cur.ct, cur_stale = cur.stale;
+    const uint32_t cur_port = cur.port, cur_ct = cur.ct;
     prefetch(cur, i + PF * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
@@ -714,6 +763,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // has a chain every such frame selects, the Parser / ChainSelector /
     // ConntrackLabel steps below reduce to straight-line field extraction.
     bool fast = false;
+    bool gen = false;       // general path: the Parser ran (done: decided there)
+    bool done = true;
     if (PCN_FASTPATH && FIXED && a.fast_chain >= 0) {
       const uint32_t pr = h.w[5] >> 24;
       const bool plain = valid && (h.w[3] & 0xffff) == 0x0008 &&
@@ -750,7 +801,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         }
       }
       // ---- Parser_dp.c:94-153 ----
-      bool done = true;
+      gen = true;
       if (L < 14 || untag_drop) verdict = PCN_IPT_DROP;
       else if ((h.w[3] & 0xffff) != 0x0008) verdict = PCN_IPT_ACCEPT;   // ethertype != 0x0800
       else if (L < 34) verdict = PCN_IPT_DROP;
@@ -768,6 +819,31 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         p.sport = bswap16u(h.w[8] >> 16);
         p.dport = bswap16u(h.w[9] & 0xffff);
       }
+    }
+    // ---- the Parser's srcPort/dstPort as stored (wire bytes 34-37), stale
+    // for a packet it writes none for (Q4): Horus keys read them ----
+    const uint32_t own_pd = (h.w[8] >> 16) | (h.w[9] << 16);
+    uint32_t stale = 0;
+    if (chunked) {
+      const bool wrote = fast ? valid : gen && !done && (p.proto == 6 || p.proto == 17);
+      const bool need = gen && !done && p.proto != 6 && p.proto != 17;
+      const uint64_t wm = __ballot(wrote);
+      const uint64_t g = (a.gbase + i) >> 6;              // the wave's group (64-aligned frames)
+      const uint32_t last_pd = __shfl(own_pd, wm ? 63 - __builtin_clzll(wm) : 0);
+      if (lane == 0)
+        __hip_atomic_store(&a.stale_desc[g], stale_word(a.stale_epoch, wm ? kStaleLocal : kStaleNone, last_pd),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t before = wm & ((1ull << lane) - 1);
+      stale = __shfl(own_pd, before ? 63 - __builtin_clzll(before) : 0);
+      if (__ballot(need && !before)) {
+        const uint32_t cin = stale_lookback(a, g);
+        if (!before) stale = cin;
+        if (!wm && lane == 0)
+          __hip_atomic_store(&a.stale_desc[g], stale_word(a.stale_epoch, kStaleInclusive, cin),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (gen) {
       if (!done && a.fw) {
         // ---- pcn-firewall: Parser -> [ConntrackLabel] -> ChainForwarder ----
         // (Firewall_Parser_dp.c:94-165, Firewall_ChainForwarder_dp.c:20-42):
@@ -781,15 +857,10 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         // ---- Horus (Firewall_Parser_dp.c:154-157 -> Firewall_Horus_dp.c:97-175) ----
         bool pass = false;
         if (kHorus && a.horus_fields) {
-          const uint32_t pd = (p.proto == 6 || p.proto == 17) ? ((h.w[8] >> 16) | (h.w[9] << 16)) : cur_stale;
+          const uint32_t pd = (p.proto == 6 || p.proto == 17) ? own_pd : stale;
           uint32_t meta;
-          if (horus_lookup(a, p.saddr, p.daddr, p.proto, pd, meta)) {
-            const uint32_t id = meta >> 16;
-            if (a.horus_ctr) {
-              atomicAdd(&a.horus_ctr[2 * id], 1ull);
-              atomicAdd(&a.horus_ctr[2 * id + 1], static_cast<unsigned long long>(L));
-            }
-            rid = PCN_IPT_RID_HORUS0 - static_cast<int32_t>(id);
+          if (horus_lookup(a, p.saddr, p.daddr, p.proto, pd, meta)) {   // counted with the rule bins
+            rid = PCN_IPT_RID_HORUS0 - static_cast<int32_t>(meta >> 16);
             done = true;
             if (!((meta >> 8) & 1)) verdict = PCN_IPT_DROP;
             else if (a.horus_flags & kHzAcceptFinal) verdict = PCN_IPT_ACCEPT;
@@ -822,15 +893,10 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         bool pass = false;
         // ---- Horus (Parser_dp.c:145-147 -> Horus_dp.c:97-167), ingress ----
         if (kHorus && a.horus_fields) {
-          const uint32_t pd = (p.proto == 6 || p.proto == 17) ? ((h.w[8] >> 16) | (h.w[9] << 16)) : cur_stale;
+          const uint32_t pd = (p.proto == 6 || p.proto == 17) ? own_pd : stale;
           uint32_t meta;
-          if (horus_lookup(a, p.saddr, p.daddr, p.proto, pd, meta)) {
-            const uint32_t id = meta >> 16;
-            if (a.horus_ctr) {
-              atomicAdd(&a.horus_ctr[2 * id], 1ull);
-              atomicAdd(&a.horus_ctr[2 * id + 1], static_cast<unsigned long long>(L));
-            }
-            rid = PCN_IPT_RID_HORUS0 - static_cast<int32_t>(id);
+          if (horus_lookup(a, p.saddr, p.daddr, p.proto, pd, meta)) {   // counted with the rule bins
+            rid = PCN_IPT_RID_HORUS0 - static_cast<int32_t>(meta >> 16);
             if ((meta >> 8) & 1) pass = true;                 // ACCEPT: PASS_LABELING
             else { verdict = PCN_IPT_DROP; done = true; }
           }
@@ -885,6 +951,36 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     }
     // ---- counters ----
     if (PCN_ABLATE == 4) return;
+    // Horus hits (Horus_dp.c:80-90): LDS bins, or one global atomic pair per
+    // distinct rule id of the wave
+    if (kHorus && a.horus_ctr) {
+      const bool hz = valid && rid <= PCN_IPT_RID_HORUS0;
+      if (__ballot(hz)) {
+        const uint32_t id = hz ? static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid) : 0u;
+        if (a.hz_bins >= 0) {
+          if (hz) {
+            atomicAdd(&bins[a.hz_bins + id], 1u);
+            if (!FIXED) atomicAdd(&byte_bins[a.hz_bins + id], L);
+          }
+        } else {
+          bool left = hz;
+          while (__ballot(left)) {
+            const uint32_t lead = static_cast<uint32_t>(__builtin_ctzll(__ballot(left)));
+            const uint32_t lid = __shfl(id, lead);
+            const bool mine = left && id == lid;
+            const uint64_t mm = __ballot(mine);
+            uint32_t by = mine ? L : 0u;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) by += __shfl_xor(by, o);
+            if (lane == lead) {
+              atomicAdd(&a.horus_ctr[2 * lid], static_cast<unsigned long long>(__builtin_popcountll(mm)));
+              atomicAdd(&a.horus_ctr[2 * lid + 1], static_cast<unsigned long long>(by));
+            }
+            left = left && !mine;
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       if (!((a.count_mask >> c) & 1)) continue;   // chain unreachable in this launch
@@ -949,6 +1045,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
             b < static_cast<uint32_t>(ch.lds_bins) + ch.ncounted)
           dst = ch.ctr + 2 + 2 * (b - static_cast<uint32_t>(ch.lds_bins));
       }
+      if (a.hz_bins >= 0 && b >= static_cast<uint32_t>(a.hz_bins) && a.horus_ctr)
+        dst = a.horus_ctr + 2 * (b - static_cast<uint32_t>(a.hz_bins));
       if (!dst) continue;
     }
     atomicAdd(dst, pk);
@@ -1017,6 +1115,12 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
   for (uint64_t base = 0; base < a.n; base += chunk) {
     LaunchArgs c = a;
     c.n = a.n - base < chunk ? a.n - base : chunk;
+    if (a.has_stale) {   // contiguous chunks per workgroup, claimed in start order
+      c.gbase = base;
+      c.chunk_frames = (c.n + uint64_t(grid) * kBlock - 1) / (uint64_t(grid) * kBlock) * kBlock;
+      const hipError_t e = hipMemsetAsync(a.chunk_ctr, 0, 4, stream);
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
     if (base) {
       if (!a.offsets) { c.frames = a.frames + base * a.stride; c.frames_bytes = a.frames_bytes - base * a.stride; }
       else c.offsets = a.offsets + base;

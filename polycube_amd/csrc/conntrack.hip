@@ -69,10 +69,19 @@ __device__ __forceinline__ void load_window(const CtBatch &b, uint64_t i, uint32
   const uint64_t base = off & ~uint64_t(3);
   const uint32_t sh = static_cast<uint32_t>(off & 3);
   uint32_t d[19];
+  if (base + 76 <= b.frames_bytes) {
+    // the whole window inside the buffer: unconditional loads, which the
+    // compiler merges into 16-byte ones (the per-dword bound checks kept each
+    // of them a separate, branch-guarded dword load)
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(b.frames + base);
 #pragma unroll
-  for (int k = 0; k < 19; ++k) {
-    const uint64_t at = base + 4u * k;
-    d[k] = at + 4 <= b.frames_bytes ? *reinterpret_cast<const uint32_t *>(b.frames + at) : 0u;
+    for (int k = 0; k < 19; ++k) d[k] = p[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 19; ++k) {
+      const uint64_t at = base + 4u * k;
+      d[k] = at + 4 <= b.frames_bytes ? *reinterpret_cast<const uint32_t *>(b.frames + at) : 0u;
+    }
   }
 #pragma unroll
   for (int k = 0; k < 18; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
@@ -640,8 +649,9 @@ constexpr uint64_t kCountChunk = 65536;       // packets per workgroup: u32 byte
 
 __global__ void ct_count_kernel(CtBatch b, const CtRec *rec) {
   constexpr uint32_t per = 2 + kLdsRules;
-  __shared__ uint32_t pk[3 * per], by[3 * per];
-  for (uint32_t k = threadIdx.x; k < 3 * per; k += blockDim.x) { pk[k] = 0; by[k] = 0; }
+  // groups 0-2: the chains; group 3: Horus rule ids (bins 2..)
+  __shared__ uint32_t pk[4 * per], by[4 * per];
+  for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) { pk[k] = 0; by[k] = 0; }
   __syncthreads();
   const uint64_t lo = uint64_t(blockIdx.x) * kCountChunk;
   const uint64_t hi = lo + kCountChunk < b.n ? lo + kCountChunk : b.n;
@@ -649,10 +659,14 @@ __global__ void ct_count_kernel(CtBatch b, const CtRec *rec) {
     const int32_t rid = b.rule_ids[i];
     const CtRec &r = rec[i];
     if (rid <= PCN_IPT_RID_HORUS0) {                  // Horus_dp.c:80-90, counted at the lookup
-      if (b.horus_ctr) {
-        const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
+      if (!b.horus_ctr) continue;
+      const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
+      if (id >= kLdsRules) {
         atomicAdd(&b.horus_ctr[2 * id], 1ull);
         atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(r.len));
+      } else {
+        atomicAdd(&pk[3 * per + 2 + id], 1u);
+        atomicAdd(&by[3 * per + 2 + id], uint32_t(r.len));
       }
       continue;
     }
@@ -678,11 +692,12 @@ __global__ void ct_count_kernel(CtBatch b, const CtRec *rec) {
     atomicAdd(&by[c * per + bin], uint32_t(r.len));
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < 3 * per; k += blockDim.x) {
+  for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) {
     if (!pk[k]) continue;
     const uint32_t c = k / per, bin = k % per;
     unsigned long long *dp, *db;
-    if (bin == 0) { dp = &b.ctr[c][0]; db = &b.ctr[c][1]; }
+    if (c == 3) { dp = &b.horus_ctr[2 * (bin - 2)]; db = &b.horus_ctr[2 * (bin - 2) + 1]; }
+    else if (bin == 0) { dp = &b.ctr[c][0]; db = &b.ctr[c][1]; }
     else if (bin == 1) { dp = &b.ae_ctr[2 * c]; db = &b.ae_ctr[2 * c + 1]; }
     else { dp = &b.ctr[c][2 + 2 * (bin - 2)]; db = &b.ctr[c][3 + 2 * (bin - 2)]; }
     atomicAdd(dp, static_cast<unsigned long long>(pk[k]));
@@ -734,12 +749,8 @@ struct CtScratch {
   WalkRec *wrec = nullptr;
   void *temp = nullptr;
   size_t temp_bytes = 0;
-  // ct_stale_ports alone (stateless batches): parse flags, scan, ports
-  uint32_t *zpp = nullptr, *zlast = nullptr, *zports = nullptr;
-  uint64_t zcap = 0;
-  unsigned long long *zfound = nullptr;   // the carry-only path: 1 + the last port-writing frame
-  void *ztemp = nullptr;
-  size_t ztemp_bytes = 0;
+  // ct_advance_carry: 1 + the batch's last port-writing frame
+  unsigned long long *zfound = nullptr;
 };
 
 CtScratch *ct_scratch_new() { return new CtScratch(); }
@@ -751,8 +762,7 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
                   static_cast<void *>(s->hard_cnt), static_cast<void *>(s->rec), static_cast<void *>(s->wrec),
                   static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
-                  static_cast<void *>(s->zpp), static_cast<void *>(s->zlast), static_cast<void *>(s->zports),
-                  s->ztemp, static_cast<void *>(s->zfound)})
+                  static_cast<void *>(s->zfound)})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -851,57 +861,17 @@ __global__ void tail_carry_kernel(CtBatch b, const unsigned long long *found, ui
   *carry = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
 }
 
-__global__ void stale_kernel(uint64_t n, const uint32_t *last, const uint32_t *pports, const uint32_t *carry,
-                             uint32_t *out) {
-  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += step)
-    out[i] = last[i] ? pports[last[i] - 1] : *carry;
-}
-
-int ct_stale_ports(const CtBatch &b, CtScratch &s, uint32_t *carry, bool update_carry, uint32_t *out, int num_cus,
-                   void *stream) {
+int ct_advance_carry(const CtBatch &b, CtScratch &s, uint32_t *carry, int num_cus, void *stream) {
   if (b.n == 0) return hipSuccess;
-  if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (!out) {
-    if (!update_carry) return hipSuccess;
-    if (!s.zfound) CT_CHECK(hipMalloc(&s.zfound, 64));
-    CT_CHECK(hipMemsetAsync(s.zfound, 0, 8, st));
-    const unsigned blk = 256;
-    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>((b.n + blk - 1) / blk, uint64_t(num_cus) * 4));
-    hipLaunchKernelGGL(tail_ports_kernel, dim3(grid), dim3(blk), 0, st, b, s.zfound);
-    CT_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(tail_carry_kernel, dim3(1), dim3(64), 0, st, b, s.zfound, carry);
-    CT_CHECK(hipGetLastError());
-    return hipSuccess;
-  }
-  if (s.zcap < b.n) {
-    for (uint32_t **p : {&s.zpp, &s.zlast, &s.zports}) {
-      if (*p) CT_CHECK(hipFree(*p));
-      CT_CHECK(hipMalloc(p, b.n * 4));
-    }
-    s.zcap = b.n;
-  }
-  size_t need = 0;
-  CT_CHECK(hipcub::DeviceScan::InclusiveScan(nullptr, need, s.zpp, s.zlast, hipcub::Max(), int(b.n), st));
-  if (s.ztemp_bytes < need) {
-    if (s.ztemp) CT_CHECK(hipFree(s.ztemp));
-    CT_CHECK(hipMalloc(&s.ztemp, need));
-    s.ztemp_bytes = need;
-  }
-  const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
-  hipLaunchKernelGGL(ct_parse_kernel, dim3(grid), dim3(blk), 0, st, b, s.zpp, s.zports);
+  if (!s.zfound) CT_CHECK(hipMalloc(&s.zfound, 64));
+  CT_CHECK(hipMemsetAsync(s.zfound, 0, 8, st));
+  const unsigned blk = 256;
+  const unsigned grid = static_cast<unsigned>(std::min<uint64_t>((b.n + blk - 1) / blk, uint64_t(num_cus) * 4));
+  hipLaunchKernelGGL(tail_ports_kernel, dim3(grid), dim3(blk), 0, st, b, s.zfound);
   CT_CHECK(hipGetLastError());
-  size_t tb = s.ztemp_bytes;
-  CT_CHECK(hipcub::DeviceScan::InclusiveScan(s.ztemp, tb, s.zpp, s.zlast, hipcub::Max(), int(b.n), st));
-  if (out) {
-    hipLaunchKernelGGL(stale_kernel, dim3(grid), dim3(blk), 0, st, b.n, s.zlast, s.zports, carry, out);
-    CT_CHECK(hipGetLastError());
-  }
-  if (update_carry) {
-    hipLaunchKernelGGL(ct_carry_kernel, dim3(1), dim3(64), 0, st, b.n, s.zlast, s.zports, carry);
-    CT_CHECK(hipGetLastError());
-  }
+  hipLaunchKernelGGL(tail_carry_kernel, dim3(1), dim3(64), 0, st, b, s.zfound, carry);
+  CT_CHECK(hipGetLastError());
   return hipSuccess;
 }
 

@@ -96,12 +96,11 @@ int ct_flow_split(const CtBatch &b, const uint16_t *in_port, uint16_t const_in_p
                   uint32_t *index, uint32_t *offsets, uint16_t *lens, uint16_t *in_port_out, uint64_t *n_out,
                   int num_cus, void *stream);
 
-// The ports the shared `packet` struct holds for every frame of a batch (Q4):
-// out[i] = the ports dword (wire bytes 34-37) of the last frame <= i the
-// Parser wrote ports for, else *carry.  update_carry: *carry becomes the
-// batch's last such frame's ports.  out may be null (carry update only).
-int ct_stale_ports(const CtBatch &b, CtScratch &s, uint32_t *carry, bool update_carry, uint32_t *out, int num_cus,
-                   void *stream);
+// The ports the shared `packet` struct holds after a batch (Q4): *carry
+// becomes the ports dword (wire bytes 34-37) of the batch's last frame the
+// Parser wrote ports for, if any.  (Within a batch the classify kernel
+// computes them itself, classify.hip stale_lookback.)
+int ct_advance_carry(const CtBatch &b, CtScratch &s, uint32_t *carry, int num_cus, void *stream);
 
 int ct_table_init(CtTable &t, uint32_t cap_log2);
 void ct_table_free(CtTable &t);

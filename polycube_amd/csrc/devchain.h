@@ -173,11 +173,16 @@ struct LaunchArgs {
   uint32_t horus_mask;           // slots - 1
   uint32_t horus_probes;         // longest probe sequence of a stored key
   uint32_t horus_fields;         // PCN_IPT_HZ_* set fields of the key
-  uint32_t has_stale;            // per-frame stale ports given (the key has port fields)
+  uint32_t has_stale;            // the key has port fields: stale ports computed in the kernel
+                                 // (classify.hip stale_lookback; chunked workgroup order)
   unsigned long long *horus_ctr; // [PCN_IPT_HORUS_MAX][2] pkts, bytes; null: not counted (stage A)
-  const uint32_t *stale_ports;   // per frame: the ports dword (wire bytes 34-37) of the last TCP/UDP
-                                 // packet before it (Q4); the zero cell with mask 0 when absent
-  uint64_t stale_mask;
+  int32_t hz_bins;               // first LDS counter bin of the Horus rule ids; -1 => wave-aggregated global atomics
+  uint64_t *stale_desc;          // per 64-frame group of the batch: the published word (stale_word)
+  const uint32_t *stale_carry;   // ports dword (wire bytes 34-37) the previous batches left (Q4)
+  uint32_t *chunk_ctr;           // workgroup start counter (zeroed before each launch)
+  uint64_t chunk_frames;         // frames per workgroup (a multiple of the block size)
+  uint64_t gbase;                // batch index of this launch's frame 0 (a multiple of 64)
+  uint32_t stale_epoch;          // this batch's publication epoch (24 bits, never 0)
 };
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)

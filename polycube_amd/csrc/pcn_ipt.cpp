@@ -116,6 +116,7 @@ struct HorusProg {
   bool runtime = false;                        // horus_runtime_enabled_
   bool ct = false;                             // pcn-firewall: _CONNTRACK_ENABLED when built
   uint32_t fields = 0, entries = 0, mask = 0, probes = 0;
+  uint32_t nids = 0;                           // 1 + the largest rule id in the table
   uint32_t *d_tab = nullptr;                   // 4 u32 per slot
   size_t cap = 0;
   unsigned long long *d_ctr = nullptr;         // [PCN_IPT_HORUS_MAX][2]
@@ -168,8 +169,11 @@ struct pcn_ipt {
   bool hz_enabled = false;
   HorusProg hz[2];
   uint32_t *d_hz_carry = nullptr;              // the Parser's stale ports while conntrack is off
-  uint32_t *d_stale = nullptr;                 // per-frame stale ports of the batch being classified
-  size_t stale_cap = 0;
+  // the classify kernel's stale-port groups (classify.hip stale_lookback)
+  uint64_t *d_stale_desc = nullptr;            // one word per 64-frame group
+  size_t stale_groups = 0;
+  uint32_t stale_epoch = 0;                    // bumped per launch (24 bits)
+  uint32_t *d_chunk_ctr = nullptr;
 };
 
 namespace pcn {
@@ -361,7 +365,7 @@ std::vector<HorusEntry> horus_entries(const std::vector<Rule> &rules, uint32_t &
 // `probes` slots.
 void horus_set(pcn_ipt *ctx, HorusProg &h, const std::vector<HorusEntry> &ents, uint32_t fields) {
   h.runtime = false;
-  h.entries = h.fields = 0;
+  h.entries = h.fields = h.nids = 0;
   if (ctx->has_device) {
     device_guard(ctx);
     hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -373,6 +377,7 @@ void horus_set(pcn_ipt *ctx, HorusProg &h, const std::vector<HorusEntry> &ents, 
   std::vector<HorusEntry> tab(size, HorusEntry{0, 0, 0, 0});
   uint32_t probes = 1;
   for (const HorusEntry &e : ents) {
+    h.nids = std::max(h.nids, (e.meta >> 16) + 1);
     uint32_t slot = horus_hash(e.src, e.dst, e.ports, e.meta & 0xff) & (size - 1), k = 1;
     while (tab[slot].meta & kHorusUsed) { slot = (slot + 1) & (size - 1); ++k; }
     tab[slot] = e;
@@ -549,7 +554,8 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
     for (void *p : {static_cast<void *>(ctx->hz[0].d_tab), static_cast<void *>(ctx->hz[0].d_ctr),
                     static_cast<void *>(ctx->hz[1].d_tab), static_cast<void *>(ctx->hz[1].d_ctr),
-                    static_cast<void *>(ctx->d_hz_carry), static_cast<void *>(ctx->d_stale)})
+                    static_cast<void *>(ctx->d_hz_carry), static_cast<void *>(ctx->d_stale_desc),
+                    static_cast<void *>(ctx->d_chunk_ctr)})
       if (p) (void)hipFree(p);
   }
   delete ctx;
@@ -774,7 +780,7 @@ struct StageA {
   int32_t *rule_ids;
 };
 
-int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa, const uint32_t *stale) {
+int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa, const uint32_t *carry) {
   {
     if (!b) return fail(-EINVAL, "null batch");
     if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
@@ -828,6 +834,14 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       uint32_t nc = a.ch[c].ncounted;
       if (nc && base - 3 + nc <= kMaxLdsRuleBins) { a.ch[c].lds_bins = static_cast<int32_t>(base); base += nc; }
       else a.ch[c].lds_bins = -1;
+    }
+    // Horus hits count into the same workgroup histogram (a hot key would
+    // otherwise serialize on one global address)
+    const HorusProg *hzb = horus_of_batch(ctx, b->direction);
+    a.hz_bins = -1;
+    if (hzb && !sa && base - 3 + hzb->nids <= kMaxLdsRuleBins) {
+      a.hz_bins = static_cast<int32_t>(base);
+      base += hzb->nids;
     }
     // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
     // (TC frames may carry a VLAN tag: the 52-byte window of the generic path)
@@ -901,8 +915,6 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
                        ? (1u << PCN_IPT_FORWARD) | (has_local && !firewall ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
     // Horus: the program the batch's Parser calls, while one is in place
-    a.stale_ports = reinterpret_cast<const uint32_t *>(ctx->d_zero);
-    a.stale_mask = 0;
     if (const HorusProg *hz = horus_of_batch(ctx, b->direction)) {
       a.horus = hz->d_tab;
       a.horus_mask = hz->mask;
@@ -916,10 +928,28 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
         if (ctx->fw_ct_mode == PCN_FW_CT_DISABLED) a.horus_flags |= kHzMissDrops;   // :170-174
       }
       a.fast_chain = -1;                               // the lookup lives in the general path
-      if (stale) {
-        a.stale_ports = stale;
-        a.stale_mask = ~uint64_t(0);
+      if (carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) {
+        // the key reads ports: stale ones (Q4) computed in the kernel
+        const size_t groups = b->n / 64 + 1;
+        if (ctx->stale_groups < groups) {
+          if (ctx->d_stale_desc) hip_check(hipFree(ctx->d_stale_desc), "hipFree");
+          ctx->d_stale_desc = nullptr;
+          hip_check(hipMalloc(&ctx->d_stale_desc, groups * 8), "hipMalloc(stale groups)");
+          hip_check(hipMemset(ctx->d_stale_desc, 0, groups * 8), "hipMemset(stale groups)");
+          ctx->stale_groups = groups;
+          ctx->stale_epoch = 0;
+        }
+        if (!ctx->d_chunk_ctr) hip_check(hipMalloc(&ctx->d_chunk_ctr, 64), "hipMalloc(chunk counter)");
+        if (++ctx->stale_epoch >= (1u << 24)) {       // words of an old epoch must never match
+          hip_check(hipMemsetAsync(ctx->d_stale_desc, 0, ctx->stale_groups * 8, static_cast<hipStream_t>(stream)),
+                    "hipMemset(stale groups)");
+          ctx->stale_epoch = 1;
+        }
         a.has_stale = 1;
+        a.stale_desc = ctx->d_stale_desc;
+        a.stale_carry = carry;
+        a.chunk_ctr = ctx->d_chunk_ctr;
+        a.stale_epoch = ctx->stale_epoch;
       }
     }
     // slot count of the chain program (the generic kernel always runs 6)
@@ -1025,22 +1055,17 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     // batches that share the context's conntrack / stale-port state run one
     // after another in submission order, whatever stream each comes on
     if (serial && ctx->ct_pending) hip_check(hipStreamWaitEvent(st, ctx->ev_ct, 0), "hipStreamWaitEvent(serial)");
-    const uint32_t *stale = nullptr;
-    if (track && (want_stale || !stateful)) {
+    // with the connection table on, its own copy (advanced by ct_run when stateful)
+    uint32_t *carry = ctx->ct_on ? ctx->ct.carry : ctx->d_hz_carry;
+    const uint32_t *stale = track && want_stale ? carry : nullptr;
+    // the carry after this batch: the ports its last TCP/UDP frame left
+    auto advance_carry = [&]() -> int {
+      if (!track || stateful) return 0;
       if (!ctx->cts) ctx->cts = ct_scratch_new();
-      if (want_stale && ctx->stale_cap < b->n) {
-        if (ctx->d_stale) hip_check(hipFree(ctx->d_stale), "hipFree");
-        ctx->d_stale = nullptr;
-        hip_check(hipMalloc(&ctx->d_stale, b->n * 4), "hipMalloc(stale ports)");
-        ctx->stale_cap = b->n;
-      }
-      // with the connection table on, its own copy (advanced by ct_run when stateful)
-      uint32_t *carry = ctx->ct_on ? ctx->ct.carry : ctx->d_hz_carry;
-      const int e = ct_stale_ports(ct_batch(ctx, b, 0), *ctx->cts, carry, !stateful, want_stale ? ctx->d_stale : nullptr,
-                                   ctx->num_cus, st);
+      const int e = ct_advance_carry(ct_batch(ctx, b, 0), *ctx->cts, carry, ctx->num_cus, st);
       if (e != hipSuccess) return fail(-EIO, std::string("stale ports: ") + hipGetErrorString(hipError_t(e)));
-      stale = want_stale ? ctx->d_stale : nullptr;
-    }
+      return 0;
+    };
     if (!ctx->ev_ct && serial) hip_check(hipEventCreateWithFlags(&ctx->ev_ct, hipEventDisableTiming), "hipEventCreate");
     auto mark = [&]() {
       if (!serial) return 0;
@@ -1052,6 +1077,7 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     // (Firewall_ConntrackTableUpdate_dp.c:136-138), whatever the table holds
     if (!stateful) {
       int rc = launch_batch(ctx, b, stream, nullptr, stale);
+      if (!rc) rc = advance_carry();
       if (rc) return rc;
       if (!ae_mask) return mark();
       device_guard(ctx);

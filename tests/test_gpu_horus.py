@@ -370,3 +370,81 @@ def test_firewall_chain_stats_fold_their_own_program(dev):
 def pkt_fw(src, dst, direction, proto=17):
     return {"dir": direction, "port": 1, "src": src, "dst": dst, "proto": proto, "sport": 1, "dport": 2,
             "flags": 0, "len": 64}
+
+
+def run_fixed(o, ipt, dev, packets, direction=0):
+    """Fixed stride and length (the bench's launch shape: the FIXED kernel path)."""
+    f, _, ports, _ = probe_frames(packets)
+    n = len(packets)
+    v_o, r_o = o.classify(f, n=n, stride=128, fixed_len=64, in_port=ports, direction=direction)
+    v_g, r_g = ipt.classify(torch.from_numpy(f).to(dev), n=n, stride=128, fixed_len=64,
+                            in_port=torch.from_numpy(ports.view(np.int16)).to(dev), direction=direction)
+    torch.cuda.synchronize()
+    return v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy()
+
+
+@JIT
+@pytest.mark.parametrize("fixed", [False, True], ids=["lens", "fixed"])
+@pytest.mark.parametrize("nrules", [2, 1100], ids=["lds_bins", "global_fallback"])
+def test_horus_counters_hot_key(dev, jit, nrules, fixed):
+    """A hot key (most packets hit one rule id) through both counting paths:
+    the workgroup LDS bins, and -- when the chain's rule bins leave no room
+    (1100 INPUT rule bins + 1100 Horus ids > 2048) -- one global atomic pair
+    per distinct id of a wave.  Counters exact against the oracle."""
+    rules = [{"l4proto": "UDP", "dport": 1000 + i, "action": "DROP" if i % 2 else "ACCEPT"} for i in range(nrules)]
+    o, ipt = setup(rules, jit=jit)
+    assert ipt.horus_info()["entries"] == nrules
+    rng = np.random.default_rng(nrules)
+    for k in range(3):
+        n = 6000
+        pick = np.where(rng.random(n) < 0.8, 0, rng.integers(0, nrules, n))
+        pk = []
+        for j in pick:
+            p = rule_packets(rng, rules[int(j)])[0]
+            p["dst"] = HOST if rng.random() < 0.5 else "9.9.9.9"
+            p["len"] = int(rng.choice([64, 74, 128]))
+            pk.append(p)
+        v_o, r_o, v_g, r_g = (run_fixed if fixed else run)(o, ipt, dev, pk)
+        assert_same(v_o, r_o, v_g, r_g)
+        assert (r_o == RID_HORUS0).sum() > 3000
+    assert o.read_horus_counters(nrules) == ipt.read_horus_counters(nrules)
+    assert_counters(o, ipt, n=nrules + 1)
+
+
+@JIT
+@pytest.mark.parametrize("fixed", [False, True], ids=["lens", "fixed"])
+def test_stale_ports_across_long_runs(dev, jit, fixed):
+    """The in-kernel stale ports (classify.hip stale_lookback) where a frame's
+    last TCP/UDP predecessor is many 64-frame groups back, or in an earlier
+    batch: long ICMP runs, an all-ICMP batch, runs ending at group edges."""
+    rules = [{"l4proto": "ICMP", "dport": 0x1100 | 0x09, "action": "DROP"},
+             {"l4proto": "ICMP", "dport": 0x2200 | 0x41, "action": "ACCEPT"},
+             {"l4proto": "UDP", "dport": 0x3100 | 0x07, "action": "DROP"}]
+    o, ipt = setup(rules, jit=jit)
+    rng = np.random.default_rng(17)
+    go = run_fixed if fixed else run
+
+    def icmp():
+        return {"dir": "ingress", "port": 1, "src": "8.8.8.8", "dst": HOST, "proto": 1, "sport": 0, "dport": 0,
+                "flags": 0, "icmp_type": 8, "len": 98}
+
+    def lead(r):                     # the UDP packet rule_packets puts before an ICMP rule's packet
+        return rule_packets(rng, r)[0]
+
+    batches = []
+    b = [lead(rules[0])] + [icmp() for _ in range(3000)] + [lead(rules[1])] + [icmp() for _ in range(127)]
+    batches.append(b)                                  # a 47-group run, then a run ending on a group edge
+    batches.append([icmp() for _ in range(2000)])      # all ICMP: the carry of the previous batch
+    mixed = []
+    for k in range(60):
+        mixed += [lead(rules[k % 2])] + [icmp() for _ in range(int(rng.integers(0, 200)))]
+    batches.append(mixed)
+    hits = 0
+    for pk in batches:
+        for p in pk:
+            p["len"] = 98 if p["proto"] == 1 else 64
+        v_o, r_o, v_g, r_g = go(o, ipt, dev, pk)
+        assert_same(v_o, r_o, v_g, r_g)
+        hits += int((r_o <= RID_HORUS0).sum())
+    assert hits > 4000
+    assert o.read_horus_counters(3) == ipt.read_horus_counters(3)

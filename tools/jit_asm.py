@@ -34,7 +34,7 @@ def layout_words():
     return n
 
 
-def spec_for(cfg, imix=False):
+def spec_for(cfg, imix=False, inputs=0):
     from polycube_amd import Iptables, ffi, synth
     rs = synth.config_rules(cfg)
     ipt = Iptables(device=-1, max_rules=16384, max_counted_rules=10000)
@@ -59,7 +59,7 @@ def spec_for(cfg, imix=False):
     # --imix: the offsets/lens launch shape with the staged prefix [0, pbase) (config 5's)
     limit = lay[LAYOUT.index("pbase")] if imix else lay[0]
     return (f"#pragma once\n#define PCN_JIT_FIXED {'false' if imix else 'true'}\n#define PCN_JIT_LDS true\n#define PCN_JIT_CH 1\n"
-            f"#define PCN_JIT_NS {ns}\n#define PCN_JIT_INPUTS 0\n#define PCN_JIT_CHAIN {{{vals}, nullptr, nullptr, {info['nrules']}u, {nrw}u, "
+            f"#define PCN_JIT_NS {ns}\n#define PCN_JIT_INPUTS {inputs}\n#define PCN_JIT_CHAIN {{{vals}, nullptr, nullptr, {info['nrules']}u, {nrw}u, "
             f"{nsw}u, {present}u, {info['nvec']}u, {all_cls}u, {ncounted}u, 10000u, 0, 0u, {limit}u, {lds_bins}}}\n")
 
 
@@ -69,10 +69,11 @@ def main():
     ap.add_argument("--defs", default="")
     ap.add_argument("--out", default="/tmp/pcn_jit.s")
     ap.add_argument("--imix", action="store_true", help="offsets/lens launch shape (FIXED false, prefix staged)")
+    ap.add_argument("--inputs", type=int, default=0, help="PCN_JIT_INPUTS (8: stale ports, 16: Horus table)")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp()
     with open(os.path.join(tmp, "pcn_jit_spec.h"), "w") as fh:
-        fh.write(spec_for(a.cfg, a.imix))
+        fh.write(spec_for(a.cfg, a.imix, a.inputs))
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", f"-I{ROOT}/include", f"-I{ROOT}/polycube_amd/csrc",
            f"-I{tmp}", "-DPCN_JIT", *a.defs.split(), "--offload-arch=gfx950", "-x", "hip", "--cuda-device-only",
            "-S", f"{ROOT}/polycube_amd/csrc/classify.hip", "-o", a.out, "-Rpass-analysis=kernel-resource-usage"]
