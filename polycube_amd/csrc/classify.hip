@@ -383,6 +383,22 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
 #ifndef PCN_ITEM_CLS
 #define PCN_ITEM_CLS 1   // 1: candidates carry their owner's classes; 0: owners stage class rows
 #endif
+#ifndef PCN_REC_PIN
+#define PCN_REC_PIN 0    // 1: candidate records all issued before the first is used (A/B: 1.6 % slower, profiles/r02_ab_recpin.log)
+#endif
+// An empty asm that takes every register of r: the loads that produce them
+// are all issued before it, and each stays live until it.
+template <int N>
+__device__ __forceinline__ void pin_regs(u32x4 (&r)[N]) {
+  static_assert(N >= 1 && N <= 6, "slot count");
+  if constexpr (N == 1) asm volatile("" : "+v"(r[0]));
+  else if constexpr (N == 2) asm volatile("" : "+v"(r[0]), "+v"(r[1]));
+  else if constexpr (N == 3) asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]));
+  else if constexpr (N == 4) asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]));
+  else if constexpr (N == 5) asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]));
+  else asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]));
+}
+
 struct WaveScratch {
   u32x4 item[64];        // (owner lane << 8 | candidate bit, the owner's classes as u16 pairs)
   uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
@@ -484,6 +500,15 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
         // read, issue back to back.  A FULL field reads POOL[0], the all-ones
         // word (indexed PART: through the zero cell, index 0).
         uint32_t at[NS];   // LDS/image offset of each field's u64 word
+        u32x4 recs[NS];
+        if (!lay.part_dense) {
+          // all NS records in flight together: one LDS round trip (left to
+          // itself the compiler recycles two record registers and waits
+          // between pairs)
+#pragma unroll
+          for (int f = 0; f < NS; ++f) recs[f] = t.u128(lay.pbase, 16 * (oc[f] * nsw + k));
+          if (PCN_REC_PIN) pin_regs<NS>(recs);
+        }
 #pragma unroll
         for (int f = 0; f < NS; ++f) {
           if (lay.part_dense) {
@@ -491,8 +516,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
             at[f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
             continue;
           }
-          const uint32_t rec = oc[f] * nsw + k;
-          const u32x4 r = t.u128(lay.pbase, 16 * rec);
+          const u32x4 r = recs[f];
           const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;
           const uint32_t j = r.z + static_cast<uint32_t>(__builtin_popcountll(pm & below));
           const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
