@@ -1,0 +1,55 @@
+"""Stateful conntrack batches for profiling (GPU box only).
+
+  python tools/ct_probe.py [--log2n 24] [--flows 65536] [--steps 3]
+  rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU ... --kernel-trace -- python3 tools/ct_probe.py
+
+Builds the bench's stateful leg (config-3 rules, synth.flow_traffic frames)
+and prints the wall time per batch and the per-kernel split from HIP events
+around the whole classify call.
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from polycube_amd import Iptables, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log2n", type=int, default=24)
+    ap.add_argument("--flows", type=int, default=1 << 16)
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rs = synth.config_rules(3)
+    ipt = Iptables(device=0, jit=1)
+    ipt.interactive = False
+    fw = ipt.chain("FORWARD")
+    for r in rs.rules():
+        fw.append(**r)
+    fw.default = "DROP"
+    fw.apply_rules()
+    n = 1 << a.log2n
+    f, _ = synth.flow_traffic(n, a.flows, 0xC7, stride=64, rs=rs)
+    frames = torch.from_numpy(f).to(dev)
+    v = torch.empty(n, dtype=torch.uint8, device=dev)
+    ipt.ct_enable(20)
+    ipt.ct_set_time(1_700_000_000 * 10**9)
+    ipt.classify(frames, n=n, verdicts=v)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ipt.classify(frames, n=n, verdicts=v)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / a.steps * 1e3
+    print(f"{ms:.3f} ms per batch of 2^{a.log2n}, {a.flows} flows: {n / ms / 1e3:.1f} Mpkt/s, "
+          f"{len(ipt.ct_dump())} live entries", flush=True)
+    ipt.close()
+
+
+if __name__ == "__main__":
+    main()
