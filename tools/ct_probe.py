@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--log2n", type=int, default=24)
     ap.add_argument("--flows", type=int, default=1 << 16)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--p-icmp", type=float, default=0.1)
+    ap.add_argument("--p-err", type=float, default=0.02)
+    ap.add_argument("--p-noise", type=float, default=0.05)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rs = synth.config_rules(3)
@@ -34,7 +37,8 @@ def main():
     fw.default = "DROP"
     fw.apply_rules()
     n = 1 << a.log2n
-    f, _ = synth.flow_traffic(n, a.flows, 0xC7, stride=64, rs=rs)
+    f, _ = synth.flow_traffic(n, a.flows, 0xC7, stride=64, rs=rs, p_icmp=a.p_icmp, p_err=a.p_err,
+                              p_noise=a.p_noise)
     frames = torch.from_numpy(f).to(dev)
     v = torch.empty(n, dtype=torch.uint8, device=dev)
     ipt.ct_enable(20)
