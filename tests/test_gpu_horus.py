@@ -448,3 +448,39 @@ def test_stale_ports_across_long_runs(dev, jit, fixed):
         hits += int((r_o <= RID_HORUS0).sum())
     assert hits > 4000
     assert o.read_horus_counters(3) == ipt.read_horus_counters(3)
+
+
+def test_stale_ports_across_a_split_launch(dev):
+    """A batch with per-frame lengths longer than one launch holds (the u32
+    histogram bound splits it, classify.hip launch_classify): the stale-port
+    groups of the second launch look back into the first one's
+    (LaunchArgs::gbase).  2^24 + 2^17 frames, an ICMP run across the split,
+    bit-exact against the oracle on every frame."""
+    from polycube_amd import synth
+    rules = [{"l4proto": "ICMP", "dport": 0x1100 | 0x09, "action": "DROP"},
+             {"l4proto": "UDP", "dport": 0x3100 | 0x07, "action": "DROP"}]
+    o, ipt = setup(rules, jit=1)
+    n = (1 << 24) + (1 << 17)
+    rng = np.random.default_rng(23)
+    proto = np.where(rng.random(n) < 0.2, 1, 17).astype(np.int32)
+    split = 65536 * 256                                    # frames per launch at 64 B per frame, 256 CUs
+    lo = split - 5000
+    proto[lo:split + 3000] = 1                             # one run across the split (any CU count up to 256)
+    sport = rng.integers(0, 65536, n).astype(np.int32)
+    dport = rng.integers(0, 65536, n).astype(np.int32)
+    key = rng.random(n) < 0.3                              # UDP frames carrying the ICMP rule's key bytes
+    sport = np.where(key, (sport & 0xff00) | 0x11, sport)
+    dport = np.where(key, (0x09 << 8) | (dport & 0xff), dport)
+    sport[lo - 1], dport[lo - 1], proto[lo - 1] = 0x0011, 0x0900, 17
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = np.full(n, ip_host(HOST), np.uint32)
+    f = synth.build_frames(src, dst, proto, sport, dport, np.zeros(n, np.int32), frame_len=64,
+                           icmp_type=np.full(n, 8, np.int32)).reshape(-1)
+    lens = np.full(n, 64, np.uint16)
+    v_o, r_o = o.classify(f, n=n, lens=lens, stride=64)
+    v_g, r_g = ipt.classify(torch.from_numpy(f).to(dev), n=n, lens=torch.from_numpy(lens.view(np.int16)).to(dev),
+                            stride=64)
+    torch.cuda.synchronize()
+    assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
+    assert (r_o[lo:split + 3000] == RID_HORUS0).all()
+    assert o.read_horus_counters(2) == ipt.read_horus_counters(2)
