@@ -271,42 +271,12 @@ __global__ void ct_carry_kernel(uint64_t n, const uint32_t *last, const uint32_t
 }
 
 // ---- the table ----------------------------------------------------------
+typedef uint32_t ct_u32x4 __attribute__((ext_vector_type(4)));
 struct Key {
   uint32_t src, dst;
   uint16_t sport, dport;
   uint8_t proto;
 };
-
-__device__ __forceinline__ bool same(const Key &a, const Key &b) {
-  return a.src == b.src && a.dst == b.dst && a.sport == b.sport && a.dport == b.dport && a.proto == b.proto;
-}
-
-// The slot holding `k` (live or deleted), or null; with claim, an empty slot
-// is taken for it.  One lane owns each key in a launch, so a slot another
-// lane is claiming (tag 2) never holds ours.
-__device__ CtSlot *table_slot(const CtTable &t, const Key &k, bool claim) {
-  const uint64_t mask = (uint64_t(1) << t.cap_log2) - 1;
-  uint64_t s = key_hash(k.src, k.dst, k.proto, k.sport, k.dport) >> 7;
-  for (uint64_t probe = 0; probe <= mask; ++probe, ++s) {
-    CtSlot *e = &t.slots[s & mask];
-    uint32_t tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (tag == 0) {
-      if (!claim) return nullptr;
-      if (atomicCAS(&e->tag, 0u, 2u) == 0u) {
-        e->src = k.src; e->dst = k.dst; e->sport = k.sport; e->dport = k.dport; e->proto = k.proto;
-        e->valid = 0;
-        __hip_atomic_store(&e->tag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        return e;
-      }
-      tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tag != 1) continue;
-    if (e->src == k.src && e->dst == k.dst && e->sport == k.sport && e->dport == k.dport && e->proto == k.proto)
-      return e;
-  }
-  if (claim) atomicAdd(&t.stats[0], 1ull);          // table full: the insert is lost
-  return nullptr;
-}
 
 // A connection's value (ct_v) while a walking lane owns it, in registers.
 // Everything below passes values, never addresses of locals, so the lane's
@@ -317,6 +287,56 @@ struct Ent {
   uint8_t state, rev, live;
 };
 
+// A slot is two 16-byte halves: {tag, src, dst, sport | dport << 16} and
+// {ttl, seq, proto | valid << 8 | state << 16 | rev << 24}; each is read or
+// written with one access (field-by-field accesses were six dependent loads
+// per probe).
+__device__ __forceinline__ ct_u32x4 slot_half(const CtSlot *e, int h) {
+  return reinterpret_cast<const ct_u32x4 *>(e)[h];
+}
+__device__ __forceinline__ Ent slot_value(const ct_u32x4 hi) {
+  return Ent{static_cast<unsigned long long>(hi.y) << 32 | hi.x, hi.z, static_cast<uint8_t>(hi.w >> 16),
+             static_cast<uint8_t>(hi.w >> 24), static_cast<uint8_t>((hi.w >> 8) & 0xff)};
+}
+
+__device__ __forceinline__ bool same(const Key &a, const Key &b) {
+  return a.src == b.src && a.dst == b.dst && a.sport == b.sport && a.dport == b.dport && a.proto == b.proto;
+}
+
+// The slot holding `k` (live or deleted), or null; with claim, an empty slot
+// is taken for it.  One lane owns each key in a launch, so a slot another
+// lane is claiming (tag 2) never holds ours.  Also returns the slot's value
+// (a claimed slot: not live), by value so the caller's copy stays in registers.
+struct SlotRef {
+  CtSlot *e;
+  Ent v;
+};
+__device__ SlotRef table_slot(const CtTable &t, const Key &k, bool claim) {
+  const uint64_t mask = (uint64_t(1) << t.cap_log2) - 1;
+  uint64_t s = key_hash(k.src, k.dst, k.proto, k.sport, k.dport) >> 7;
+  for (uint64_t probe = 0; probe <= mask; ++probe, ++s) {
+    CtSlot *e = &t.slots[s & mask];
+    uint32_t tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tag == 0) {
+      if (!claim) return SlotRef{nullptr, Ent{}};
+      if (atomicCAS(&e->tag, 0u, 2u) == 0u) {
+        e->src = k.src; e->dst = k.dst; e->sport = k.sport; e->dport = k.dport; e->proto = k.proto;
+        e->valid = 0;
+        __hip_atomic_store(&e->tag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return SlotRef{e, Ent{}};
+      }
+      tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tag != 1) continue;
+    const ct_u32x4 lo = slot_half(e, 0), hi = slot_half(e, 1);   // ordered after the acquire
+    if (lo.y == k.src && lo.z == k.dst && lo.w == (uint32_t(k.sport) | uint32_t(k.dport) << 16) &&
+        (hi.w & 0xff) == k.proto)
+      return SlotRef{e, slot_value(hi)};
+  }
+  if (claim) atomicAdd(&t.stats[0], 1ull);          // table full: the insert is lost
+  return SlotRef{nullptr, Ent{}};
+}
+
 struct Cache {              // the key a walking lane last touched, its slot and value
   Key k;
   CtSlot *e;                // slot holding k (live or deleted), or null
@@ -325,8 +345,13 @@ struct Cache {              // the key a walking lane last touched, its slot and
 };
 
 __device__ __forceinline__ void flush(Cache &c) {
-  if (c.dirty && c.e) {
-    c.e->ttl = c.v.ttl; c.e->seq = c.v.seq; c.e->state = c.v.state; c.e->rev = c.v.rev; c.e->valid = c.v.live;
+  if (c.dirty && c.e) {     // the value half in one store (proto is the key's)
+    ct_u32x4 hi;
+    hi.x = static_cast<uint32_t>(c.v.ttl);
+    hi.y = static_cast<uint32_t>(c.v.ttl >> 32);
+    hi.z = c.v.seq;
+    hi.w = uint32_t(c.k.proto) | uint32_t(c.v.live) << 8 | uint32_t(c.v.state) << 16 | uint32_t(c.v.rev) << 24;
+    reinterpret_cast<ct_u32x4 *>(c.e)[1] = hi;
   }
   c.dirty = false;
 }
@@ -336,9 +361,9 @@ __device__ __forceinline__ bool lookup(const CtTable &t, Cache &c, const Key &k)
   if (!c.valid || !same(c.k, k)) {
     flush(c);
     c.k = k;
-    c.e = table_slot(t, k, false);
-    c.v = Ent{};
-    if (c.e) { c.v.ttl = c.e->ttl; c.v.seq = c.e->seq; c.v.state = c.e->state; c.v.rev = c.e->rev; c.v.live = c.e->valid; }
+    const SlotRef r = table_slot(t, k, false);
+    c.e = r.e;
+    c.v = r.v;
     c.valid = true;
   }
   return c.v.live;
@@ -349,7 +374,7 @@ __device__ __forceinline__ void put(const CtTable &t, Cache &c, unsigned long lo
                                    uint8_t rev, bool noexist) {
   if (c.v.live && noexist) return;
   if (!c.e) {
-    c.e = table_slot(t, c.k, true);
+    c.e = table_slot(t, c.k, true).e;
     if (!c.e) return;
   }
   c.v = Ent{ttl, seq, state, rev, 1};
@@ -491,7 +516,6 @@ static_assert(sizeof(WalkRec) == 64, "WalkRec is 64 bytes");
 
 // One record as four 16-byte loads (a field-by-field copy of the packed
 // struct issues ~20 narrow loads per record on the walk's critical path).
-typedef uint32_t ct_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ WalkRec load_rec(const WalkRec *p) {
   const ct_u32x4 *s = reinterpret_cast<const ct_u32x4 *>(p);
   union {
@@ -556,6 +580,11 @@ __device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, ui
 
 // After the sort: walk records in sorted order (each walking lane then reads
 // consecutive lines) and the list of run heads.
+#ifndef PCN_CT_LONG_RUN
+#define PCN_CT_LONG_RUN 512
+#endif
+constexpr uint64_t kLongRun = PCN_CT_LONG_RUN;   // a run at least this long gets a whole wave
+
 __global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *skeys, const uint32_t *sidx,
                                  WalkRec *wrec, uint32_t *heads, uint32_t *nheads, uint32_t sentinel) {
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
@@ -573,7 +602,12 @@ __global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *sk
     w.o3 = pack_outcome(b, 3, i);
     w.pad[0] = w.pad[1] = 0;
     wrec[q] = w;
-    if (q == 0 || skeys[q - 1] != k) heads[atomicAdd(nheads, 1u)] = static_cast<uint32_t>(q);
+    if (q == 0 || skeys[q - 1] != k) {
+      // runs longer than kLongRun from the front of `heads` (one wave each),
+      // the rest from the back (one lane each)
+      if (q + kLongRun < b.n && skeys[q + kLongRun] == k) heads[atomicAdd(&nheads[0], 1u)] = static_cast<uint32_t>(q);
+      else heads[b.n - 1 - atomicAdd(&nheads[1], 1u)] = static_cast<uint32_t>(q);
+    }
   }
 }
 
@@ -583,11 +617,57 @@ __global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *sk
 // (the heaviest flow of the batch) times the per-packet cost of one lane
 // (~0.9 us measured: instruction-bound, the wave executes the union of its
 // lanes' paths); 4 records in flight measured the same.
+// A long run (one wave): the wave stages the run's next 64 records in LDS
+// with one coalesced load while lane 0 walks the previous 64 out of LDS, so
+// the walking lane waits on LDS, not on a memory round trip per step.
+__device__ void walk_long(const CtBatch &b, const CtTable &t, const WalkRec *wrec, int32_t *sres, uint32_t p,
+                          uint32_t *cursor_j, uint64_t hi, int first) {
+  __shared__ WalkRec buf[2][64];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t k = wrec[p].key;
+  uint64_t q = first ? p : *cursor_j;
+  const uint64_t last = b.n - 1;
+  Cache c{};
+  uint64_t base = q;
+  buf[0][lane] = load_rec(&wrec[base + lane < last ? base + lane : last]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  int cur = 0;
+  for (;;) {
+    const WalkRec nx = load_rec(&wrec[base + 64 + lane < last ? base + 64 + lane : last]);
+    uint32_t done = 0;
+    if (lane == 0) {
+      for (int u = 0; u < 64; ++u) {
+        const WalkRec w = buf[cur][u];
+        if (q >= b.n || w.key != k || w.idx >= hi) { done = 1; break; }
+        sres[q] = step(b, t, c, w);
+        ++q;
+      }
+      if (done) {
+        flush(c);
+        *cursor_j = static_cast<uint32_t>(q);
+      }
+    }
+    __syncthreads();
+    done = __shfl(done, 0);
+    if (done) return;
+    base += 64;
+    buf[cur ^ 1][lane] = nx;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
 __global__ void ct_walk_kernel(CtBatch b, CtTable t, const WalkRec *wrec, int32_t *sres, const uint32_t *heads,
-                               const uint32_t *nheads, uint32_t *cursor, uint64_t hi, int first) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= *nheads) return;
-  const uint32_t p = heads[j];
+                               uint32_t nlong, uint32_t nshort, uint32_t *cursor, uint64_t hi, int first) {
+  if (blockIdx.x < nlong) {                     // 64-thread blocks: one wave per long run
+    walk_long(b, t, wrec, sres, heads[blockIdx.x], &cursor[blockIdx.x], hi, first);
+    return;
+  }
+  const uint32_t j = nlong + (blockIdx.x - nlong) * blockDim.x + threadIdx.x;
+  if (j >= nlong + nshort) return;
+  const uint32_t p = heads[b.n - nshort + (j - nlong)];
   const uint32_t k = wrec[p].key;
   uint64_t q = first ? p : cursor[j];
   const uint64_t last = b.n - 1;
@@ -804,7 +884,7 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     CT_CHECK(hipMalloc(&s.rec, n * sizeof(CtRec)));
     if (s.wrec) CT_CHECK(hipFree(s.wrec));
     CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
-    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1] run heads
+    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1] long runs, [2] other runs
     s.cap = n;
   }
   size_t need_scan = 0, need_sort = 0;
@@ -897,26 +977,26 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   tb = s.temp_bytes;
   CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
                                               st));
-  CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 4, st));
+  CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 8, st));
   hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.rec, s.keys2, s.idx2, s.wrec,
                      s.heads, s.hard_cnt + 1, sentinel);
   CT_CHECK(hipGetLastError());
-  uint32_t cnt[2] = {0, 0};
-  CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, 8, hipMemcpyDeviceToHost, st));
+  uint32_t cnt[3] = {0, 0, 0};
+  CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, 12, hipMemcpyDeviceToHost, st));
   CT_CHECK(hipStreamSynchronize(st));
-  const uint32_t nhard = cnt[0], nheads = cnt[1];
+  const uint32_t nhard = cnt[0], nlong = cnt[1], nshort = cnt[2], nheads = nlong + nshort;
   std::vector<uint32_t> hard(nhard);
   if (nhard) {
     CT_CHECK(hipMemcpy(hard.data(), s.hard_list, nhard * 4ull, hipMemcpyDeviceToHost));
     std::sort(hard.begin(), hard.end());
   }
-  const unsigned wblk = 64, wgrid = (nheads + wblk - 1) / wblk;
+  const unsigned wblk = 64, wgrid = nlong + (nshort + wblk - 1) / wblk;
   int first = 1;
   for (size_t h = 0; h <= hard.size(); ++h) {
     const uint64_t hi = h < hard.size() ? hard[h] : b.n;
     if (nheads) {
       hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(wblk), 0, st, b, t, s.wrec, s.sres, s.heads,
-                         s.hard_cnt + 1, s.cursor, hi, first);
+                         nlong, nshort, s.cursor, hi, first);
       CT_CHECK(hipGetLastError());
     }
     first = 0;
