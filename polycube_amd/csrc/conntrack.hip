@@ -370,10 +370,14 @@ __device__ __forceinline__ bool lookup(const CtTable &t, Cache &c, const Key &k)
 }
 
 // connections.update (noexist = false) / .insert (BPF_NOEXIST) of the cached key
+// kSpec: a wave's lane evaluating a record against a broadcast copy of the
+// connection (walk_long): a put that would claim a slot clears c.valid instead.
+template <bool kSpec = false>
 __device__ __forceinline__ void put(const CtTable &t, Cache &c, unsigned long long ttl, uint8_t state, uint32_t seq,
                                    uint8_t rev, bool noexist) {
   if (c.v.live && noexist) return;
   if (!c.e) {
+    if (kSpec) { c.valid = false; return; }
     c.e = table_slot(t, c.k, true).e;
     if (!c.e) return;
   }
@@ -425,7 +429,8 @@ __device__ int label_of(const CtRec &r, bool live, const Ent &e) {
 
 // ConntrackTableUpdate_dp.c:141-655 for an accepted packet with label l; the
 // cached key is the packet's own.
-__device__ void update(const CtTable &t, Cache &c, const CtRec &r, int l) {
+template <bool kSpec = false>
+__device__ __forceinline__ void update(const CtTable &t, Cache &c, const CtRec &r, int l) {
   if (l == ST_INV) return;
   const unsigned long long now = t.now;
   const bool live = c.v.live;
@@ -472,7 +477,7 @@ __device__ void update(const CtTable &t, Cache &c, const CtRec &r, int l) {
       }
       if (s != ST_TIME_WAIT || l != ST_NEW) return;   // TIME_WAIT + NEW: goto TCP_MISS
     }
-    if (syn_only(r.flags)) put(t, c, now + TCP_SYN_SENT_T, ST_SYN_SENT, r.seq + HEX_BE_ONE, r.rev, false);
+    if (syn_only(r.flags)) put<kSpec>(t, c, now + TCP_SYN_SENT_T, ST_SYN_SENT, r.seq + HEX_BE_ONE, r.rev, false);
     return;
   }
   if (r.kind == K_UDP) {
@@ -482,10 +487,10 @@ __device__ void update(const CtTable &t, Cache &c, const CtRec &r, int l) {
       else e.ttl = now + UDP_ESTABLISHED_TIMEOUT;
       return;
     }
-    put(t, c, now + UDP_NEW_TIMEOUT, ST_NEW, 0, r.rev, true);
+    put<kSpec>(t, c, now + UDP_NEW_TIMEOUT, ST_NEW, 0, r.rev, true);
     return;
   }
-  if (r.kind == K_ECHO) { put(t, c, now + ICMP_TIMEOUT, ST_NEW, 0, r.rev, true); return; }
+  if (r.kind == K_ECHO) { put<kSpec>(t, c, now + ICMP_TIMEOUT, ST_NEW, 0, r.rev, true); return; }
   if (r.kind == K_REPLY || r.kind == K_HARD) {
     if (live) e.live = 0;                          // connections.delete
   }
@@ -585,29 +590,48 @@ __device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, ui
 #endif
 constexpr uint64_t kLongRun = PCN_CT_LONG_RUN;   // a run at least this long gets a whole wave
 
+// Run heads are appended with one atomic per wave and list (a run head per
+// flow from every lane on one counter serialised ~2^20 atomics at 2^20 flows).
+__device__ __forceinline__ void append_heads(uint32_t *heads, uint32_t *ctr, bool mine, uint32_t q, bool back,
+                                             uint64_t n) {
+  const uint64_t m = __ballot(mine);
+  if (!m) return;
+  const uint32_t lane = __lane_id();
+  const uint32_t leader = static_cast<uint32_t>(__builtin_ctzll(m));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, static_cast<uint32_t>(__popcll(m)));
+  base = __shfl(base, static_cast<int>(leader));
+  const uint32_t pos = base + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1)));
+  if (mine) heads[back ? n - 1 - pos : pos] = q;
+}
+
 __global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *skeys, const uint32_t *sidx,
                                  WalkRec *wrec, uint32_t *heads, uint32_t *nheads, uint32_t sentinel) {
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < b.n; q += step) {
-    const uint32_t k = skeys[q];
-    if (k == sentinel) continue;
-    const uint32_t i = sidx[q];
-    WalkRec w;
-    w.r = rec[i];
-    w.key = k;
-    w.idx = i;
-    w.o0 = pack_outcome(b, 0, i);
-    w.o1 = pack_outcome(b, 1, i);
-    w.o2 = pack_outcome(b, 2, i);
-    w.o3 = pack_outcome(b, 3, i);
-    w.pad[0] = w.pad[1] = 0;
-    wrec[q] = w;
-    if (q == 0 || skeys[q - 1] != k) {
-      // runs longer than kLongRun from the front of `heads` (one wave each),
-      // the rest from the back (one lane each)
-      if (q + kLongRun < b.n && skeys[q + kLongRun] == k) heads[atomicAdd(&nheads[0], 1u)] = static_cast<uint32_t>(q);
-      else heads[b.n - 1 - atomicAdd(&nheads[1], 1u)] = static_cast<uint32_t>(q);
+  // wave-uniform trip count (the head appends ballot across the wave)
+  for (uint64_t q0 = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); q0 < b.n; q0 += step) {
+    const uint64_t q = q0 + __lane_id();
+    const uint32_t k = q < b.n ? skeys[q] : sentinel;
+    bool head = false, lng = false;
+    if (k != sentinel) {
+      const uint32_t i = sidx[q];
+      WalkRec w;
+      w.r = rec[i];
+      w.key = k;
+      w.idx = i;
+      w.o0 = pack_outcome(b, 0, i);
+      w.o1 = pack_outcome(b, 1, i);
+      w.o2 = pack_outcome(b, 2, i);
+      w.o3 = pack_outcome(b, 3, i);
+      w.pad[0] = w.pad[1] = 0;
+      wrec[q] = w;
+      head = q == 0 || skeys[q - 1] != k;
+      lng = head && q + kLongRun < b.n && skeys[q + kLongRun] == k;
     }
+    // runs longer than kLongRun from the front of `heads` (one wave each),
+    // the rest from the back (one lane each)
+    append_heads(heads, &nheads[0], lng, static_cast<uint32_t>(q), false, b.n);
+    append_heads(heads, &nheads[1], head && !lng, static_cast<uint32_t>(q), true, b.n);
   }
 }
 
@@ -618,40 +642,109 @@ __global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *sk
 // (~0.9 us measured: instruction-bound, the wave executes the union of its
 // lanes' paths); 4 records in flight measured the same.
 // A long run (one wave): the wave stages the run's next 64 records in LDS
-// with one coalesced load while lane 0 walks the previous 64 out of LDS, so
-// the walking lane waits on LDS, not on a memory round trip per step.
+// with one coalesced load while it walks the previous 64.  The walk of a
+// chunk is parallel where the reference's order cannot matter: in a round,
+// every lane takes its record's full label -> outcome -> update against the
+// connection as it stands (lane 0's cache, broadcast).  The leading records
+// that leave the connection as it is (an established flow's data, packets of
+// a half-closed or deleted flow that change nothing, a ttl already set to the
+// value they would set) all have their outcome at once.  The first record
+// that changes the connection is also right (it saw the state before it) and
+// its result becomes the cache; only a record that needs the table itself (a
+// slot to claim, another key of the bucket) takes step() on lane 0.  The next
+// round starts after that record, so a chunk costs one round per change.
 __device__ void walk_long(const CtBatch &b, const CtTable &t, const WalkRec *wrec, int32_t *sres, uint32_t p,
                           uint32_t *cursor_j, uint64_t hi, int first) {
   __shared__ WalkRec buf[2][64];
   const uint32_t lane = threadIdx.x;
   const uint32_t k = wrec[p].key;
-  uint64_t q = first ? p : *cursor_j;
+  const uint64_t q0 = first ? p : *cursor_j;
   const uint64_t last = b.n - 1;
   Cache c{};
-  uint64_t base = q;
+  uint64_t base = q0;
   buf[0][lane] = load_rec(&wrec[base + lane < last ? base + lane : last]);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   int cur = 0;
   for (;;) {
     const WalkRec nx = load_rec(&wrec[base + 64 + lane < last ? base + 64 + lane : last]);
-    uint32_t done = 0;
-    if (lane == 0) {
-      for (int u = 0; u < 64; ++u) {
-        const WalkRec w = buf[cur][u];
-        if (q >= b.n || w.key != k || w.idx >= hi) { done = 1; break; }
-        sres[q] = step(b, t, c, w);
-        ++q;
+    const WalkRec w = buf[cur][lane];
+    const CtRec &r = w.r;
+    const bool inrun = base + lane < b.n && w.key == k && w.idx < hi;
+    const uint64_t rm = __ballot(inrun);           // the run's records: a prefix of the chunk
+    const uint32_t m = rm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~rm));
+    uint32_t u0 = 0;
+    while (u0 < m) {
+      // lane 0's cached connection, to every lane
+      const uint32_t sv = __shfl(c.valid ? 1u | (c.v.live ? 2u : 0u) | (c.e ? 4u : 0u) : 0u, 0);
+      const uint32_t ks = __shfl(c.k.src, 0), kd = __shfl(c.k.dst, 0);
+      const uint32_t kp = __shfl(uint32_t(c.k.sport) | uint32_t(c.k.dport) << 16, 0);
+      const uint32_t kx = __shfl(uint32_t(c.k.proto) | uint32_t(c.v.state) << 8 | uint32_t(c.v.rev) << 16, 0);
+      const uint32_t tl = __shfl(static_cast<uint32_t>(c.v.ttl), 0), th = __shfl(static_cast<uint32_t>(c.v.ttl >> 32), 0);
+      const uint32_t sq = __shfl(c.v.seq, 0);
+      // every lane of the round: the full label -> outcome -> update of its
+      // record against that state, on a private copy.  cls 0: leaves the
+      // connection as it is (the ttl it sets is the one it has); 1: changes it
+      // (the round's last record: the next round starts from its result);
+      // 2: needs the table itself (another key of the bucket, a slot to claim,
+      // no cached key yet) and takes step() on lane 0.
+      int cls = 2;
+      int32_t o = 0;
+      Cache cc{};
+      if (lane >= u0 && lane < m && (sv & 1) && r.src == ks && r.dst == kd &&
+          (uint32_t(r.sport) | uint32_t(r.dport) << 16) == kp && r.proto == (kx & 0xff)) {
+        cc.k = Key{ks, kd, static_cast<uint16_t>(kp), static_cast<uint16_t>(kp >> 16), static_cast<uint8_t>(kx)};
+        cc.e = (sv & 4) ? t.slots : nullptr;          // never dereferenced under kSpec
+        cc.v = Ent{uint64_t(th) << 32 | tl, sq, static_cast<uint8_t>(kx >> 8), static_cast<uint8_t>(kx >> 16),
+                   static_cast<uint8_t>((sv >> 1) & 1)};
+        cc.valid = true;
+        cc.dirty = false;
+        const int l = label_of(r, cc.v.live, cc.v);
+        o = outcome(b, w.o0, w.o1, w.o2, w.o3, r, l);
+        if ((o & 1) == PCN_IPT_ACCEPT && l >= 0 && r.kind != K_ERR) update<true>(t, cc, r, l);
+        cls = !cc.valid ? 2
+              : (cc.v.ttl == (uint64_t(th) << 32 | tl) && cc.v.seq == sq && cc.v.state == ((kx >> 8) & 0xff) &&
+                 cc.v.rev == ((kx >> 16) & 0xff) && cc.v.live == ((sv >> 1) & 1))
+                  ? 0 : 1;
       }
-      if (done) {
-        flush(c);
-        *cursor_j = static_cast<uint32_t>(q);
+      const uint64_t em = __ballot(cls == 0) >> u0;
+      const uint32_t cnt = em == ~0ull >> u0 ? 64u - u0 : static_cast<uint32_t>(__builtin_ctzll(~em));
+      const uint32_t end = u0 + cnt < m ? u0 + cnt : m;
+      const bool mine = lane >= u0 && lane < end;
+      if (mine) sres[base + lane] = o;
+      const bool anyd = __ballot(mine && cls == 0 && cc.dirty) != 0;
+      if (lane == 0 && anyd) c.dirty = true;
+      u0 = end;
+      if (u0 < m) {
+        const int ecls = __shfl(cls, u0);
+        if (ecls == 1) {                              // the changing record: its result is the new state
+          if (lane == u0) sres[base + lane] = o;
+          const uint32_t nl = __shfl(static_cast<uint32_t>(cc.v.ttl), u0);
+          const uint32_t nh = __shfl(static_cast<uint32_t>(cc.v.ttl >> 32), u0);
+          const uint32_t ns = __shfl(cc.v.seq, u0);
+          const uint32_t nf = __shfl(uint32_t(cc.v.state) | uint32_t(cc.v.rev) << 8 | uint32_t(cc.v.live) << 16 |
+                                         uint32_t(cc.dirty) << 24, u0);
+          if (lane == 0) {
+            c.v = Ent{uint64_t(nh) << 32 | nl, ns, static_cast<uint8_t>(nf), static_cast<uint8_t>(nf >> 8),
+                      static_cast<uint8_t>(nf >> 16)};
+            if (nf >> 24) c.dirty = true;
+          }
+        } else {                                      // the record that needs the table: the full step
+          const WalkRec x = buf[cur][u0];
+          if (lane == 0) sres[base + u0] = step(b, t, c, x);
+        }
+        ++u0;
       }
     }
-    __syncthreads();
-    done = __shfl(done, 0);
-    if (done) return;
+    if (m < 64) {                                     // the run (or this round of it) ends here
+      if (lane == 0) {
+        flush(c);
+        *cursor_j = static_cast<uint32_t>(base + m);
+      }
+      return;
+    }
     base += 64;
+    __syncthreads();
     buf[cur ^ 1][lane] = nx;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();

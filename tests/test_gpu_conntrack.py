@@ -200,6 +200,40 @@ def test_headline_size_flows_parity(dev):
     assert_counters(o, ipt, n=1001)
 
 
+@pytest.mark.parametrize("p_icmp", [0.0, 0.1])
+def test_long_runs_walk_a_wave_each(dev, p_icmp):
+    """Keys with >= PCN_CT_LONG_RUN (512) packets in one batch get a whole wave
+    (conntrack.hip walk_long: records staged in LDS 64 at a time, eligible
+    segments labelled in parallel); interleaved with many short flows, TCP
+    noise (INVALID paths, FIN/RST) and, with ICMP, echo replies that split the
+    batch into segments.  Bit-exact vs the oracle across batches."""
+    rs = synth.config_rules(2)
+    rules = CT_RULES + rs.rules()
+    o, ipt = ct_pair({1: rules}, {1: "DROP"}, jit=1)
+    rng = np.random.default_rng(31)
+    n_long, n_short = 48000, 16000
+    fl, _ = synth.flow_traffic(n_long, 12, 31, stride=64, rs=rs, p_icmp=p_icmp, p_noise=0.03, p_err=0.0)
+    fs, _ = synth.flow_traffic(n_short, 2000, 32, stride=64, rs=rs, p_icmp=p_icmp, p_noise=0.05)
+    n = n_long + n_short
+    slot = np.zeros(n, bool)
+    slot[rng.choice(n, size=n_short, replace=False)] = True
+    nb = np.empty((n, 64), np.uint8)
+    nb[~slot] = fl.reshape(n_long, 64)
+    nb[slot] = fs.reshape(n_short, 64)
+    # the long flows do give runs past the 512 threshold inside one batch
+    ip = nb[:30000, 26:34].view(">u4")
+    pt = nb[:30000, 34:38].view(">u2")
+    key = np.stack([ip.min(1), ip.max(1), pt.min(1), pt.max(1), nb[:30000, 23]], 1).astype(np.int64)
+    _, cnt = np.unique(key, axis=0, return_counts=True)
+    assert (cnt >= 1000).sum() >= 5, np.sort(cnt)[-12:]
+    for lo, hi in ((0, 30000), (30000, 30001), (30001, n)):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, nb[lo:hi].reshape(-1), hi - lo, stride=64)
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_ae(o, ipt)
+
+
 def test_full_table_drops_inserts_without_faulting(dev):
     o, ipt = ct_pair({1: []}, {1: "ACCEPT"}, cap_log2=10)
     f, _ = synth.flow_traffic(20000, 5000, 8, stride=64, p_icmp=0.0, p_noise=0.0)
