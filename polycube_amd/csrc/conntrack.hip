@@ -38,6 +38,8 @@ constexpr unsigned long long UDP_ESTABLISHED_TIMEOUT = 180000000000ull, UDP_NEW_
                              TCP_SYN_SENT_T = 120000000000ull, TCP_SYN_RECV_T = 60000000000ull,
                              TCP_LAST_ACK_T = 30000000000ull, TCP_FIN_WAIT_T = 120000000000ull;
 
+typedef uint32_t ct_u32x4 __attribute__((ext_vector_type(4)));
+
 // Per-packet record written by ct_prep (32 B).
 struct CtRec {
   uint32_t src, dst;       // table key: the packet's own (ordered), or the quoted header's for K_ERR
@@ -151,6 +153,46 @@ __device__ __forceinline__ uint64_t key_hash(uint32_t src, uint32_t dst, uint8_t
   return h ^ (h >> 32);
 }
 
+// A packet's walk input (64 B: one line): its record, key bucket, batch index
+// and stage-A outcomes (rule id << 1 | verdict per label).  ct_prep writes
+// them in batch order (coalesced reads of the stage-A outcomes), ct_gather
+// moves them into sorted order with one 64-byte read each.
+struct alignas(16) WalkRec {
+  CtRec r;
+  uint32_t key, idx;
+  int32_t o0, o1, o2, o3;
+  uint32_t pad[2];
+};
+static_assert(sizeof(WalkRec) == 64, "WalkRec is 64 bytes");
+
+// One record as four 16-byte loads (a field-by-field copy of the packed
+// struct issues ~20 narrow loads per record on the walk's critical path).
+__device__ __forceinline__ WalkRec load_rec(const WalkRec *p) {
+  const ct_u32x4 *s = reinterpret_cast<const ct_u32x4 *>(p);
+  union {
+    ct_u32x4 v[4];
+    WalkRec w;
+  } u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) u.v[k] = s[k];
+  return u.w;
+}
+
+__device__ __forceinline__ void store_rec(WalkRec *p, const WalkRec &w) {
+  union {
+    ct_u32x4 v[4];
+    WalkRec w;
+  } u;
+  u.w = w;
+  ct_u32x4 *d = reinterpret_cast<ct_u32x4 *>(p);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = u.v[k];
+}
+
+__device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, uint64_t i) {
+  return l < b.nlab ? (b.a_rid[l * b.n + i] * 2) | b.a_verdict[l * b.n + i] : 0;
+}
+
 __global__ void ct_parse_kernel(CtBatch b, uint32_t *pp, uint32_t *pports) {
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
   for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < b.n; i += step) {
@@ -166,7 +208,7 @@ __global__ void ct_parse_kernel(CtBatch b, uint32_t *pp, uint32_t *pports) {
 // Chain selection (ChainSelector_dp.c:131-298), the conntrack key and kind;
 // packets that need no table access get their final outcome here.
 __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *pports, const uint32_t *carry,
-                               CtRec *rec, uint32_t *keys, uint32_t *idx, uint32_t kbits, uint32_t *hard_cnt,
+                               WalkRec *brec, uint32_t *keys, uint32_t *idx, uint32_t kbits, uint32_t *hard_cnt,
                                uint32_t *hard_list) {
   const uint32_t sentinel = (1u << kbits) - 1;
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
@@ -251,11 +293,21 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *
       }
     }
     r.cinfo = static_cast<uint8_t>((chain & 3) | (pass ? 4 : 0));
-    rec[i] = r;
     idx[i] = static_cast<uint32_t>(i);
     const bool member = r.kind >= K_TCP && r.kind <= K_ERR;
-    keys[i] = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
-                     : sentinel;
+    const uint32_t key = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
+                                : sentinel;
+    keys[i] = key;
+    WalkRec wr;
+    wr.r = r;
+    wr.key = key;
+    wr.idx = static_cast<uint32_t>(i);
+    wr.o0 = pack_outcome(b, 0, i);
+    wr.o1 = pack_outcome(b, 1, i);
+    wr.o2 = pack_outcome(b, 2, i);
+    wr.o3 = pack_outcome(b, 3, i);
+    wr.pad[0] = wr.pad[1] = 0;
+    store_rec(&brec[i], wr);
     if (r.kind == K_HARD) hard_list[atomicAdd(hard_cnt, 1u)] = static_cast<uint32_t>(i);
     if (!member && r.kind != K_HARD) {
       // no table access: the outcome of label INVALID (K_INV) or of any label
@@ -271,7 +323,6 @@ __global__ void ct_carry_kernel(uint64_t n, const uint32_t *last, const uint32_t
 }
 
 // ---- the table ----------------------------------------------------------
-typedef uint32_t ct_u32x4 __attribute__((ext_vector_type(4)));
 struct Key {
   uint32_t src, dst;
   uint16_t sport, dport;
@@ -307,28 +358,41 @@ __device__ __forceinline__ bool same(const Key &a, const Key &b) {
 // is taken for it.  One lane owns each key in a launch, so a slot another
 // lane is claiming (tag 2) never holds ours.  Also returns the slot's value
 // (a claimed slot: not live), by value so the caller's copy stays in registers.
+//
+// The tag loads are relaxed: an agent-scope acquire on gfx950 invalidates the
+// CU's L1 and the XCD's L2 after every probe (buffer_inv sc1), which cost the
+// whole walk dearly under lookup-heavy traffic (millions of one-packet keys).
+// Nothing here needs it: within a launch, a slot another lane publishes holds
+// another key, and a slot's key half only ever goes from zeros to its key, so
+// a stale read of it is zeros and can only mismatch -- except for the all-zero
+// key (an ICMP error quoting proto 0 between 0.0.0.0 and itself), which takes
+// the acquire and a re-read before it may match.  For the same reason the
+// publishing store is relaxed (a release is an L2 write-back per insert).
+// Earlier launches' slots are visible through the kernel boundary.
 struct SlotRef {
   CtSlot *e;
   Ent v;
 };
 __device__ SlotRef table_slot(const CtTable &t, const Key &k, bool claim) {
   const uint64_t mask = (uint64_t(1) << t.cap_log2) - 1;
+  const bool zero_key = (k.src | k.dst | k.sport | k.dport | k.proto) == 0;
   uint64_t s = key_hash(k.src, k.dst, k.proto, k.sport, k.dport) >> 7;
   for (uint64_t probe = 0; probe <= mask; ++probe, ++s) {
     CtSlot *e = &t.slots[s & mask];
-    uint32_t tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t tag = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tag == 0) {
       if (!claim) return SlotRef{nullptr, Ent{}};
       if (atomicCAS(&e->tag, 0u, 2u) == 0u) {
         e->src = k.src; e->dst = k.dst; e->sport = k.sport; e->dport = k.dport; e->proto = k.proto;
         e->valid = 0;
-        __hip_atomic_store(&e->tag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&e->tag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return SlotRef{e, Ent{}};
       }
-      tag = __hip_atomic_load(&e->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      tag = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tag != 1) continue;
-    const ct_u32x4 lo = slot_half(e, 0), hi = slot_half(e, 1);   // ordered after the acquire
+    if (zero_key) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const ct_u32x4 lo = slot_half(e, 0), hi = slot_half(e, 1);
     if (lo.y == k.src && lo.z == k.dst && lo.w == (uint32_t(k.sport) | uint32_t(k.dport) << 16) &&
         (hi.w & 0xff) == k.proto)
       return SlotRef{e, slot_value(hi)};
@@ -509,29 +573,6 @@ __device__ __forceinline__ int32_t outcome(const CtBatch &b, int32_t o0, int32_t
   return l == 0 ? o0 : l == 1 ? o1 : l == 2 ? o2 : o3;
 }
 
-// A packet's walk input in sorted order (64 B: one line): its record, key
-// bucket, batch index and stage-A outcomes (rule id << 1 | verdict per label).
-struct alignas(16) WalkRec {
-  CtRec r;
-  uint32_t key, idx;
-  int32_t o0, o1, o2, o3;
-  uint32_t pad[2];
-};
-static_assert(sizeof(WalkRec) == 64, "WalkRec is 64 bytes");
-
-// One record as four 16-byte loads (a field-by-field copy of the packed
-// struct issues ~20 narrow loads per record on the walk's critical path).
-__device__ __forceinline__ WalkRec load_rec(const WalkRec *p) {
-  const ct_u32x4 *s = reinterpret_cast<const ct_u32x4 *>(p);
-  union {
-    ct_u32x4 v[4];
-    WalkRec w;
-  } u;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) u.v[k] = s[k];
-  return u.w;
-}
-
 __device__ __forceinline__ int32_t process(const CtBatch &b, const CtTable &t, Cache &c, const WalkRec &w) {
   const CtRec &r = w.r;
   const bool live = lookup(t, c, Key{r.src, r.dst, r.sport, r.dport, r.proto});
@@ -579,10 +620,6 @@ __device__ __forceinline__ int32_t step(const CtBatch &b, const CtTable &t, Cach
   return process(b, t, c, w);
 }
 
-__device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, uint64_t i) {
-  return l < b.nlab ? (b.a_rid[l * b.n + i] * 2) | b.a_verdict[l * b.n + i] : 0;
-}
-
 // After the sort: walk records in sorted order (each walking lane then reads
 // consecutive lines) and the list of run heads.
 #ifndef PCN_CT_LONG_RUN
@@ -605,7 +642,7 @@ __device__ __forceinline__ void append_heads(uint32_t *heads, uint32_t *ctr, boo
   if (mine) heads[back ? n - 1 - pos : pos] = q;
 }
 
-__global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *skeys, const uint32_t *sidx,
+__global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t *skeys, const uint32_t *sidx,
                                  WalkRec *wrec, uint32_t *heads, uint32_t *nheads, uint32_t sentinel) {
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
   // wave-uniform trip count (the head appends ballot across the wave)
@@ -614,17 +651,7 @@ __global__ void ct_gather_kernel(CtBatch b, const CtRec *rec, const uint32_t *sk
     const uint32_t k = q < b.n ? skeys[q] : sentinel;
     bool head = false, lng = false;
     if (k != sentinel) {
-      const uint32_t i = sidx[q];
-      WalkRec w;
-      w.r = rec[i];
-      w.key = k;
-      w.idx = i;
-      w.o0 = pack_outcome(b, 0, i);
-      w.o1 = pack_outcome(b, 1, i);
-      w.o2 = pack_outcome(b, 2, i);
-      w.o3 = pack_outcome(b, 3, i);
-      w.pad[0] = w.pad[1] = 0;
-      wrec[q] = w;
+      store_rec(&wrec[q], load_rec(&brec[sidx[q]]));
       head = q == 0 || skeys[q - 1] != k;
       lng = head && q + kLongRun < b.n && skeys[q + kLongRun] == k;
     }
@@ -797,9 +824,9 @@ __global__ void ct_scatter_kernel(CtBatch b, const uint32_t *skeys, const uint32
 
 // An echo reply long enough to quote a header (ConntrackLabel_dp.c:450-531):
 // its own key decides ESTABLISHED; otherwise ICMP_MISS reads the quoted key.
-__global__ void ct_hard_kernel(CtBatch b, CtTable t, const CtRec *rec, uint32_t i) {
+__global__ void ct_hard_kernel(CtBatch b, CtTable t, const WalkRec *brec, uint32_t i) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const CtRec r = rec[i];
+  const CtRec r = brec[i].r;
   Cache c2{};
   const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
   const bool quoted = lookup(t, c2, q);            // read-only
@@ -820,7 +847,7 @@ constexpr uint32_t kCountBlock = 1024;
 constexpr uint32_t kLdsRules = 1024;          // LDS bins per chain; rules above use global atomics
 constexpr uint64_t kCountChunk = 65536;       // packets per workgroup: u32 byte bins cannot wrap
 
-__global__ void ct_count_kernel(CtBatch b, const CtRec *rec) {
+__global__ void ct_count_kernel(CtBatch b, const WalkRec *brec) {
   constexpr uint32_t per = 2 + kLdsRules;
   // groups 0-2: the chains; group 3: Horus rule ids (bins 2..)
   __shared__ uint32_t pk[4 * per], by[4 * per];
@@ -830,7 +857,7 @@ __global__ void ct_count_kernel(CtBatch b, const CtRec *rec) {
   const uint64_t hi = lo + kCountChunk < b.n ? lo + kCountChunk : b.n;
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const int32_t rid = b.rule_ids[i];
-    const CtRec &r = rec[i];
+    const CtRec &r = brec[i].r;
     if (rid <= PCN_IPT_RID_HORUS0) {                  // Horus_dp.c:80-90, counted at the lookup
       if (!b.horus_ctr) continue;
       const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
@@ -918,7 +945,7 @@ struct CtScratch {
   uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *hard_cnt = nullptr;
   uint32_t *heads = nullptr;
   int32_t *sres = nullptr;
-  CtRec *rec = nullptr;
+  WalkRec *brec = nullptr;   // batch order
   WalkRec *wrec = nullptr;
   void *temp = nullptr;
   size_t temp_bytes = 0;
@@ -933,7 +960,7 @@ void ct_scratch_free(CtScratch *s) {
   for (void *p : {static_cast<void *>(s->pp), static_cast<void *>(s->last), static_cast<void *>(s->pports),
                   static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
-                  static_cast<void *>(s->hard_cnt), static_cast<void *>(s->rec), static_cast<void *>(s->wrec),
+                  static_cast<void *>(s->hard_cnt), static_cast<void *>(s->brec), static_cast<void *>(s->wrec),
                   static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
                   static_cast<void *>(s->zfound)})
     if (p) (void)hipFree(p);
@@ -973,8 +1000,8 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, n * 4));
     }
-    if (s.rec) CT_CHECK(hipFree(s.rec));
-    CT_CHECK(hipMalloc(&s.rec, n * sizeof(CtRec)));
+    if (s.brec) CT_CHECK(hipFree(s.brec));
+    CT_CHECK(hipMalloc(&s.brec, n * sizeof(WalkRec)));
     if (s.wrec) CT_CHECK(hipFree(s.wrec));
     CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
     if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1] long runs, [2] other runs
@@ -1062,7 +1089,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   size_t tb = s.temp_bytes;
   CT_CHECK(hipcub::DeviceScan::InclusiveScan(s.temp, tb, s.pp, s.last, hipcub::Max(), int(b.n), st));
   CT_CHECK(hipMemsetAsync(s.hard_cnt, 0, 4, st));
-  hipLaunchKernelGGL(ct_prep_kernel, dim3(grid), dim3(blk), 0, st, b, s.last, s.pports, t.carry, s.rec, s.keys,
+  hipLaunchKernelGGL(ct_prep_kernel, dim3(grid), dim3(blk), 0, st, b, s.last, s.pports, t.carry, s.brec, s.keys,
                      s.idx, kbits, s.hard_cnt, s.hard_list);
   CT_CHECK(hipGetLastError());
   hipLaunchKernelGGL(ct_carry_kernel, dim3(1), dim3(64), 0, st, b.n, s.last, s.pports, t.carry);
@@ -1071,7 +1098,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
                                               st));
   CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 8, st));
-  hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.rec, s.keys2, s.idx2, s.wrec,
+  hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec,
                      s.heads, s.hard_cnt + 1, sentinel);
   CT_CHECK(hipGetLastError());
   uint32_t cnt[3] = {0, 0, 0};
@@ -1094,14 +1121,14 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
     }
     first = 0;
     if (h < hard.size()) {
-      hipLaunchKernelGGL(ct_hard_kernel, dim3(1), dim3(64), 0, st, b, t, s.rec, hard[h]);
+      hipLaunchKernelGGL(ct_hard_kernel, dim3(1), dim3(64), 0, st, b, t, s.brec, hard[h]);
       CT_CHECK(hipGetLastError());
     }
   }
   hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
   CT_CHECK(hipGetLastError());
   const unsigned cgrid = static_cast<unsigned>((b.n + kCountChunk - 1) / kCountChunk);
-  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.rec);
+  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.brec);
   CT_CHECK(hipGetLastError());
   return hipSuccess;
 }
