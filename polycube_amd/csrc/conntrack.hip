@@ -627,38 +627,78 @@ __device__ __forceinline__ int32_t step(const CtBatch &b, const CtTable &t, Cach
 #endif
 constexpr uint64_t kLongRun = PCN_CT_LONG_RUN;   // a run at least this long gets a whole wave
 
-// Run heads are appended with one atomic per wave and list (a run head per
-// flow from every lane on one counter serialised ~2^20 atomics at 2^20 flows).
-__device__ __forceinline__ void append_heads(uint32_t *heads, uint32_t *ctr, bool mine, uint32_t q, bool back,
-                                             uint64_t n) {
-  const uint64_t m = __ballot(mine);
-  if (!m) return;
-  const uint32_t lane = __lane_id();
-  const uint32_t leader = static_cast<uint32_t>(__builtin_ctzll(m));
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(ctr, static_cast<uint32_t>(__popcll(m)));
-  base = __shfl(base, static_cast<int>(leader));
-  const uint32_t pos = base + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1)));
-  if (mine) heads[back ? n - 1 - pos : pos] = q;
+// Run heads by length class, so a wave's lanes walk runs of about the same
+// length (a wave takes as long as its longest run: with a million one-packet
+// keys mixed in, 2^16 flows of ~256 packets were spread over 30 K waves
+// instead of 1 K).  Class 0: >= kLongRun packets (one wave each); classes
+// 1-4: [64, kLongRun), [8, 64), [2, 8), 1 (one lane each).  A class whose runs
+// have at least L packets has at most n / L heads, which fixes its region of
+// `heads` (kHeadsCap(n) entries in all).
+constexpr uint32_t kRunClasses = 5;
+__host__ __device__ constexpr uint64_t class_cap(uint64_t n, uint32_t c) {
+  return c == 0 ? n / kLongRun + 1 : c == 1 ? n / 64 + 1 : c == 2 ? n / 8 + 1 : c == 3 ? n / 2 + 1 : n;
+}
+__host__ __device__ constexpr uint64_t class_off(uint64_t n, uint32_t c) {
+  return c == 0 ? 0 : class_off(n, c - 1) + class_cap(n, c - 1);
+}
+__host__ __device__ constexpr uint64_t heads_cap(uint64_t n) { return class_off(n, kRunClasses); }
+
+// The run class of sorted position q (kRunClasses: not a run head).
+__device__ __forceinline__ uint32_t run_class(const uint32_t *skeys, uint64_t n, uint64_t q, uint32_t sentinel) {
+  if (q >= n) return kRunClasses;
+  const uint32_t k = skeys[q];
+  if (k == sentinel || (q > 0 && skeys[q - 1] == k)) return kRunClasses;
+  auto longer = [&](uint64_t d) { return q + d < n && skeys[q + d] == k; };   // more than d packets
+  return longer(kLongRun) ? 0 : longer(63) ? 1 : longer(7) ? 2 : longer(1) ? 3 : 4;
 }
 
 __global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t *skeys, const uint32_t *sidx,
-                                 WalkRec *wrec, uint32_t *heads, uint32_t *nheads, uint32_t sentinel) {
+                                 WalkRec *wrec, uint32_t sentinel) {
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
-  // wave-uniform trip count (the head appends ballot across the wave)
-  for (uint64_t q0 = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); q0 < b.n; q0 += step) {
-    const uint64_t q = q0 + __lane_id();
-    const uint32_t k = q < b.n ? skeys[q] : sentinel;
-    bool head = false, lng = false;
-    if (k != sentinel) {
-      store_rec(&wrec[q], load_rec(&brec[sidx[q]]));
-      head = q == 0 || skeys[q - 1] != k;
-      lng = head && q + kLongRun < b.n && skeys[q + kLongRun] == k;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < b.n; q += step)
+    if (skeys[q] != sentinel) store_rec(&wrec[q], load_rec(&brec[sidx[q]]));
+}
+
+// The run heads of each class.  A workgroup takes a contiguous range of the
+// sorted keys, counts its heads per class, reserves its places with one
+// global atomic per class, then writes them (LDS atomics per wave and class).
+// (Per-wave global atomics on the five counters serialised: 2-6 ms a batch.)
+__global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads, uint32_t *nheads,
+                                uint32_t sentinel) {
+  __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
+  const uint64_t per = ((n + gridDim.x - 1) / gridDim.x + blockDim.x - 1) / blockDim.x * blockDim.x;
+  const uint64_t lo = uint64_t(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
+  if (threadIdx.x < kRunClasses) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t mine[kRunClasses] = {};
+  for (uint64_t q = lo + threadIdx.x; q < hi; q += blockDim.x) {
+    const uint32_t c = run_class(skeys, n, q, sentinel);
+#pragma unroll
+    for (uint32_t k = 0; k < kRunClasses; ++k) mine[k] += c == k;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kRunClasses; ++k)
+    if (mine[k]) atomicAdd(&cnt[k], mine[k]);
+  __syncthreads();
+  if (threadIdx.x < kRunClasses) {
+    base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&nheads[threadIdx.x], cnt[threadIdx.x]) : 0u;
+    cnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const uint32_t lane = __lane_id();
+  for (uint64_t q0 = lo + (threadIdx.x & ~63u); q0 < hi; q0 += blockDim.x) {   // wave-uniform
+    const uint64_t q = q0 + lane;
+    const uint32_t c = q < hi ? run_class(skeys, n, q, sentinel) : kRunClasses;
+#pragma unroll
+    for (uint32_t k = 0; k < kRunClasses; ++k) {
+      const uint64_t m = __ballot(c == k);
+      if (!m) continue;
+      const uint32_t leader = static_cast<uint32_t>(__builtin_ctzll(m));
+      uint32_t at = 0;
+      if (lane == leader) at = atomicAdd(&cnt[k], static_cast<uint32_t>(__popcll(m)));
+      at = __shfl(at, static_cast<int>(leader));
+      if (c == k) heads[class_off(n, k) + base[k] + at + __popcll(m & ((1ull << lane) - 1))] = static_cast<uint32_t>(q);
     }
-    // runs longer than kLongRun from the front of `heads` (one wave each),
-    // the rest from the back (one lane each)
-    append_heads(heads, &nheads[0], lng, static_cast<uint32_t>(q), false, b.n);
-    append_heads(heads, &nheads[1], head && !lng, static_cast<uint32_t>(q), true, b.n);
   }
 }
 
@@ -779,15 +819,23 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const WalkRec *wre
   }
 }
 
+struct WalkPlan {
+  uint32_t cnt[kRunClasses];       // runs per class
+  uint32_t blk0[kRunClasses + 1];  // first block of each class
+};
+
 __global__ void ct_walk_kernel(CtBatch b, CtTable t, const WalkRec *wrec, int32_t *sres, const uint32_t *heads,
-                               uint32_t nlong, uint32_t nshort, uint32_t *cursor, uint64_t hi, int first) {
-  if (blockIdx.x < nlong) {                     // 64-thread blocks: one wave per long run
+                               WalkPlan plan, uint32_t *cursor, uint64_t hi, int first) {
+  if (blockIdx.x < plan.blk0[1]) {             // 64-thread blocks: one wave per long run
     walk_long(b, t, wrec, sres, heads[blockIdx.x], &cursor[blockIdx.x], hi, first);
     return;
   }
-  const uint32_t j = nlong + (blockIdx.x - nlong) * blockDim.x + threadIdx.x;
-  if (j >= nlong + nshort) return;
-  const uint32_t p = heads[b.n - nshort + (j - nlong)];
+  uint32_t cls = 1;
+  while (cls + 1 < kRunClasses && blockIdx.x >= plan.blk0[cls + 1]) ++cls;
+  const uint32_t jj = (blockIdx.x - plan.blk0[cls]) * blockDim.x + threadIdx.x;
+  if (jj >= plan.cnt[cls]) return;
+  const uint64_t j = class_off(b.n, cls) + jj;
+  const uint32_t p = heads[j];
   const uint32_t k = wrec[p].key;
   uint64_t q = first ? p : cursor[j];
   const uint64_t last = b.n - 1;
@@ -995,16 +1043,20 @@ void ct_table_free(CtTable &t) {
 
 static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
   if (s.cap < n) {
-    for (uint32_t **p : {&s.pp, &s.last, &s.pports, &s.keys, &s.keys2, &s.idx, &s.idx2, &s.cursor, &s.hard_list,
-                         &s.heads, reinterpret_cast<uint32_t **>(&s.sres)}) {
+    for (uint32_t **p : {&s.pp, &s.last, &s.pports, &s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list,
+                         reinterpret_cast<uint32_t **>(&s.sres)}) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, n * 4));
+    }
+    for (uint32_t **p : {&s.cursor, &s.heads}) {
+      if (*p) CT_CHECK(hipFree(*p));
+      CT_CHECK(hipMalloc(p, heads_cap(n) * 4));
     }
     if (s.brec) CT_CHECK(hipFree(s.brec));
     CT_CHECK(hipMalloc(&s.brec, n * sizeof(WalkRec)));
     if (s.wrec) CT_CHECK(hipFree(s.wrec));
     CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
-    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1] long runs, [2] other runs
+    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1..5] runs per class
     s.cap = n;
   }
   size_t need_scan = 0, need_sort = 0;
@@ -1097,26 +1149,36 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   tb = s.temp_bytes;
   CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
                                               st));
-  CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 8, st));
-  hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec,
-                     s.heads, s.hard_cnt + 1, sentinel);
+  CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 4 * kRunClasses, st));
+  hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec, sentinel);
   CT_CHECK(hipGetLastError());
-  uint32_t cnt[3] = {0, 0, 0};
-  CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, 12, hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 4,
+                                                                                   (b.n + blk - 1) / blk))),
+                     dim3(blk), 0, st, b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel);
+  CT_CHECK(hipGetLastError());
+  uint32_t cnt[1 + kRunClasses] = {};
+  CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
   CT_CHECK(hipStreamSynchronize(st));
-  const uint32_t nhard = cnt[0], nlong = cnt[1], nshort = cnt[2], nheads = nlong + nshort;
+  const uint32_t nhard = cnt[0];
   std::vector<uint32_t> hard(nhard);
   if (nhard) {
     CT_CHECK(hipMemcpy(hard.data(), s.hard_list, nhard * 4ull, hipMemcpyDeviceToHost));
     std::sort(hard.begin(), hard.end());
   }
-  const unsigned wblk = 64, wgrid = nlong + (nshort + wblk - 1) / wblk;
+  const unsigned wblk = 64;
+  WalkPlan plan{};
+  plan.blk0[0] = 0;
+  for (uint32_t c = 0; c < kRunClasses; ++c) {
+    plan.cnt[c] = cnt[1 + c];
+    plan.blk0[c + 1] = plan.blk0[c] + (c == 0 ? plan.cnt[c] : (plan.cnt[c] + wblk - 1) / wblk);
+  }
+  const unsigned wgrid = plan.blk0[kRunClasses];
   int first = 1;
   for (size_t h = 0; h <= hard.size(); ++h) {
     const uint64_t hi = h < hard.size() ? hard[h] : b.n;
-    if (nheads) {
-      hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(wblk), 0, st, b, t, s.wrec, s.sres, s.heads,
-                         nlong, nshort, s.cursor, hi, first);
+    if (wgrid) {
+      hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(wblk), 0, st, b, t, s.wrec, s.sres, s.heads, plan,
+                         s.cursor, hi, first);
       CT_CHECK(hipGetLastError());
     }
     first = 0;
