@@ -193,29 +193,71 @@ __device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, ui
   return l < b.nlab ? (b.a_rid[l * b.n + i] * 2) | b.a_verdict[l * b.n + i] : 0;
 }
 
-__global__ void ct_parse_kernel(CtBatch b, uint32_t *pp, uint32_t *pports) {
-  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < b.n; i += step) {
-    uint32_t w[18], L;
-    load_window(b, i, w, L);
-    const Parsed p = parse(w, L, b.hook);
-    const bool ok = p.status == 2 && p.ports_ok;
-    pp[i] = ok ? static_cast<uint32_t>(i + 1) : 0u;
-    pports[i] = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
+// The Parser's stale ports (Q4) inside ct_prep, without a pass of its own:
+// workgroups claim contiguous chunks of the batch in start order, every
+// 64-frame group publishes the ports of its last TCP/UDP frame (or that it
+// has none), and a frame that needs the ports of an earlier group looks back
+// through the published words, {1:24 | status:2 | ports:32} (0: not yet).
+// A group only waits on lower groups, whose waves are running or done, so the
+// waits resolve.  (Was ct_parse + a max-scan + ct_carry: 0.32 ms a batch.)
+constexpr uint32_t kPrepChunk = 4096;                        // frames per claimed chunk
+constexpr unsigned long long kStLocal = 1, kStIncl = 2, kStNone = 3;
+__device__ __forceinline__ unsigned long long ports_word(unsigned long long st, uint32_t ports) {
+  return (1ull << 40) | (st << 32) | ports;
+}
+__device__ uint32_t ports_lookback(const unsigned long long *desc, uint64_t g, const uint32_t *carry) {
+  while (g > 0) {
+    --g;
+    unsigned long long d;
+    for (;;) {
+      d = __hip_atomic_load(&desc[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d >> 40) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (((d >> 32) & 3) != kStNone) return static_cast<uint32_t>(d);
   }
+  return *carry;
 }
 
 // Chain selection (ChainSelector_dp.c:131-298), the conntrack key and kind;
 // packets that need no table access get their final outcome here.
-__global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *pports, const uint32_t *carry,
-                               WalkRec *brec, uint32_t *keys, uint32_t *idx, uint32_t kbits, uint32_t *hard_cnt,
-                               uint32_t *hard_list) {
+__global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, uint32_t *keys, uint32_t *idx,
+                               uint32_t kbits, uint32_t *hard_cnt, uint32_t *hard_list, unsigned long long *desc,
+                               uint32_t *chunk_ctr) {
   const uint32_t sentinel = (1u << kbits) - 1;
-  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < b.n; i += step) {
+  const uint32_t lane = __lane_id();
+  __shared__ uint32_t chunk;
+  for (;;) {
+    if (threadIdx.x == 0) chunk = atomicAdd(chunk_ctr, 1u);
+    __syncthreads();
+    const uint64_t lo = uint64_t(chunk) * kPrepChunk;
+    __syncthreads();                                      // everyone has read `chunk`
+    if (lo >= b.n) return;
+    const uint64_t hi = lo + kPrepChunk < b.n ? lo + kPrepChunk : b.n;
+  for (uint64_t i0 = lo + (threadIdx.x & ~63u); i0 < hi; i0 += blockDim.x) {   // one 64-frame group per wave
+    const uint64_t i = i0 + lane;
+    const bool valid = i < hi;
     uint32_t w[18], L;
-    load_window(b, i, w, L);
+    load_window(b, valid ? i : hi - 1, w, L);
     const Parsed p = parse(w, L, b.hook);
+    // ---- the shared `packet` struct's ports as this frame sees them ----
+    const uint32_t own = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
+    const bool wrote = valid && p.status == 2 && p.ports_ok;
+    const uint64_t wm = __ballot(wrote);
+    const uint64_t g = i0 >> 6;
+    const uint32_t last_pd = __shfl(own, wm ? 63 - __builtin_clzll(wm) : 0);
+    if (lane == 0)
+      __hip_atomic_store(&desc[g], ports_word(wm ? kStLocal : kStNone, last_pd), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t before = wm & ((1ull << lane) - 1);
+    uint32_t stale = __shfl(own, before ? 63 - __builtin_clzll(before) : 0);
+    if (__ballot(valid && p.status == 2 && !p.ports_ok && !before)) {
+      const uint32_t cin = ports_lookback(desc, g, carry);
+      if (!before) stale = cin;
+      if (!wm && lane == 0)
+        __hip_atomic_store(&desc[g], ports_word(kStIncl, cin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!valid) continue;
     CtRec r{};
     r.len = static_cast<uint16_t>(p.L);
     r.kind = K_NONE;
@@ -250,10 +292,7 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *
       }
       if (labeled) {
         // the shared `packet` struct: ports stale for anything but TCP/UDP (Q4)
-        uint32_t ports;
-        if (p.ports_ok) ports = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
-        else if (i > 0 && last[i - 1]) ports = pports[last[i - 1] - 1];
-        else ports = *carry;
+        const uint32_t ports = p.ports_ok ? own : stale;
         const uint16_t sp = static_cast<uint16_t>(ports & 0xffff), dp = static_cast<uint16_t>(ports >> 16);
         // ConntrackLabel_dp.c:200-228
         uint8_t ipRev, portRev;
@@ -316,11 +355,9 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *last, const uint32_t *
       b.rule_ids[i] = b.a_rid[l * b.n + i];
     }
   }
+  }
 }
 
-__global__ void ct_carry_kernel(uint64_t n, const uint32_t *last, const uint32_t *pports, uint32_t *carry) {
-  if (threadIdx.x == 0 && blockIdx.x == 0 && last[n - 1]) *carry = pports[last[n - 1] - 1];
-}
 
 // ---- the table ----------------------------------------------------------
 struct Key {
@@ -989,7 +1026,8 @@ unsigned grid_for(uint64_t n, unsigned block, int num_cus) {
 
 struct CtScratch {
   uint64_t cap = 0;
-  uint32_t *pp = nullptr, *last = nullptr, *pports = nullptr, *keys = nullptr, *keys2 = nullptr;
+  unsigned long long *pdesc = nullptr;   // ct_prep: the ports word of every 64-frame group
+  uint32_t *keys = nullptr, *keys2 = nullptr;
   uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *hard_cnt = nullptr;
   uint32_t *heads = nullptr;
   int32_t *sres = nullptr;
@@ -1005,7 +1043,7 @@ CtScratch *ct_scratch_new() { return new CtScratch(); }
 
 void ct_scratch_free(CtScratch *s) {
   if (!s) return;
-  for (void *p : {static_cast<void *>(s->pp), static_cast<void *>(s->last), static_cast<void *>(s->pports),
+  for (void *p : {static_cast<void *>(s->pdesc),
                   static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
                   static_cast<void *>(s->hard_cnt), static_cast<void *>(s->brec), static_cast<void *>(s->wrec),
@@ -1043,7 +1081,7 @@ void ct_table_free(CtTable &t) {
 
 static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
   if (s.cap < n) {
-    for (uint32_t **p : {&s.pp, &s.last, &s.pports, &s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list,
+    for (uint32_t **p : {&s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list,
                          reinterpret_cast<uint32_t **>(&s.sres)}) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, n * 4));
@@ -1052,18 +1090,19 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, heads_cap(n) * 4));
     }
+    if (s.pdesc) CT_CHECK(hipFree(s.pdesc));
+    CT_CHECK(hipMalloc(&s.pdesc, (n / 64 + 2) * 8));
     if (s.brec) CT_CHECK(hipFree(s.brec));
     CT_CHECK(hipMalloc(&s.brec, n * sizeof(WalkRec)));
     if (s.wrec) CT_CHECK(hipFree(s.wrec));
     CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
-    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1..5] runs per class
+    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1..5] runs per class,
+                                                              // [8] ct_prep's chunk counter
     s.cap = n;
   }
-  size_t need_scan = 0, need_sort = 0;
-  CT_CHECK(hipcub::DeviceScan::InclusiveScan(nullptr, need_scan, s.pp, s.last, hipcub::Max(), int(n), st));
-  CT_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, need_sort, s.keys, s.keys2, s.idx, s.idx2, int(n), 0,
+  size_t need = 0;
+  CT_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, s.keys, s.keys2, s.idx, s.idx2, int(n), 0,
                                               int(kbits), st));
-  const size_t need = std::max(need_scan, need_sort);
   if (s.temp_bytes < need) {
     if (s.temp) CT_CHECK(hipFree(s.temp));
     CT_CHECK(hipMalloc(&s.temp, need));
@@ -1136,16 +1175,15 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint32_t sentinel = (1u << kbits) - 1;
   CT_CHECK(grow(s, b.n, kbits, st));
   const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
-  hipLaunchKernelGGL(ct_parse_kernel, dim3(grid), dim3(blk), 0, st, b, s.pp, s.pports);
-  CT_CHECK(hipGetLastError());
-  size_t tb = s.temp_bytes;
-  CT_CHECK(hipcub::DeviceScan::InclusiveScan(s.temp, tb, s.pp, s.last, hipcub::Max(), int(b.n), st));
   CT_CHECK(hipMemsetAsync(s.hard_cnt, 0, 4, st));
-  hipLaunchKernelGGL(ct_prep_kernel, dim3(grid), dim3(blk), 0, st, b, s.last, s.pports, t.carry, s.brec, s.keys,
-                     s.idx, kbits, s.hard_cnt, s.hard_list);
+  CT_CHECK(hipMemsetAsync(s.hard_cnt + 8, 0, 4, st));
+  CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
+  const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + kPrepChunk - 1) / kPrepChunk));
+  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(blk), 0, st, b, t.carry, s.brec, s.keys, s.idx, kbits,
+                     s.hard_cnt, s.hard_list, s.pdesc, s.hard_cnt + 8);
   CT_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(ct_carry_kernel, dim3(1), dim3(64), 0, st, b.n, s.last, s.pports, t.carry);
-  CT_CHECK(hipGetLastError());
+  CT_CHECK(ct_advance_carry(b, s, t.carry, num_cus, stream));
+  size_t tb;
   tb = s.temp_bytes;
   CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
                                               st));

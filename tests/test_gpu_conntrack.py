@@ -234,6 +234,31 @@ def test_long_runs_walk_a_wave_each(dev, p_icmp):
     assert_ae(o, ipt)
 
 
+def test_errors_quoting_the_all_zero_key_among_inserts(dev):
+    """ICMP errors quoting proto 0 between 0.0.0.0 and itself, ports 0: the one
+    key a stale (zero) read of a slot claimed in the same launch could match,
+    so conntrack.hip's table_slot re-reads it after an acquire.  Interleaved
+    with a fresh table's worth of inserts, it stays a miss (INVALID) as in the
+    oracle."""
+    o, ipt = ct_pair({1: [{"conntrack": "RELATED", "action": "ACCEPT"},
+                          {"conntrack": "INVALID", "action": "DROP"}]}, {1: "ACCEPT"}, cap_log2=12)
+    rng = np.random.default_rng(17)
+    n = 24000
+    f, _ = synth.flow_traffic(n, 3000, 17, stride=128, p_icmp=0.0, p_err=0.0)
+    nb = f.reshape(n, 128)
+    err = rng.random(n) < 0.1
+    nb[err, 23] = 1
+    nb[err, 34] = 3                                   # destination unreachable
+    zero = np.zeros(n, np.int64)
+    synth.set_icmp_inner(nb, err, zero, zero, zero, zero, zero)
+    for lo, hi in ((0, 12000), (12000, n)):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, nb[lo:hi].reshape(-1), hi - lo)
+        assert_same(v_o, r_o, v_g, r_g)
+        assert (r_o[err[lo:hi]] == 1).all()          # INVALID -> DROP rule
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=3)
+
+
 def test_full_table_drops_inserts_without_faulting(dev):
     o, ipt = ct_pair({1: []}, {1: "ACCEPT"}, cap_log2=10)
     f, _ = synth.flow_traffic(20000, 5000, 8, stride=64, p_icmp=0.0, p_noise=0.0)
