@@ -676,17 +676,20 @@ __host__ __device__ constexpr uint64_t class_cap(uint64_t n, uint32_t c) {
   return c == 0 ? n / kLongRun + 1 : c == 1 ? n / 64 + 1 : c == 2 ? n / 8 + 1 : c == 3 ? n / 2 + 1 : n;
 }
 __host__ __device__ constexpr uint64_t class_off(uint64_t n, uint32_t c) {
-  return c == 0 ? 0 : class_off(n, c - 1) + class_cap(n, c - 1);
+  uint64_t off = 0;
+  for (uint32_t k = 0; k < c; ++k) off += class_cap(n, k);
+  return off;
 }
 __host__ __device__ constexpr uint64_t heads_cap(uint64_t n) { return class_off(n, kRunClasses); }
 
-// The run class of sorted position q (kRunClasses: not a run head).
+// The run class of sorted position q (kRunClasses: not a run head).  All six
+// key reads are issued unconditionally so they are in flight together.
 __device__ __forceinline__ uint32_t run_class(const uint32_t *skeys, uint64_t n, uint64_t q, uint32_t sentinel) {
-  if (q >= n) return kRunClasses;
-  const uint32_t k = skeys[q];
-  if (k == sentinel || (q > 0 && skeys[q - 1] == k)) return kRunClasses;
-  auto longer = [&](uint64_t d) { return q + d < n && skeys[q + d] == k; };   // more than d packets
-  return longer(kLongRun) ? 0 : longer(63) ? 1 : longer(7) ? 2 : longer(1) ? 3 : 4;
+  auto at = [&](uint64_t j) { return j < n ? skeys[j] : 0xffffffffu; };   // never a key: kbits <= 30
+  const uint32_t k = at(q), km = q ? at(q - 1) : 0xffffffffu;
+  const uint32_t k1 = at(q + 1), k7 = at(q + 7), k63 = at(q + 63), kl = at(q + kLongRun);
+  if (q >= n || k == sentinel || km == k) return kRunClasses;
+  return kl == k ? 0 : k63 == k ? 1 : k7 == k ? 2 : k1 == k ? 3 : 4;   // more than 512 / 63 / 7 / 1 packets
 }
 
 __global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t *skeys, const uint32_t *sidx,
@@ -696,22 +699,28 @@ __global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t 
     if (skeys[q] != sentinel) store_rec(&wrec[q], load_rec(&brec[sidx[q]]));
 }
 
-// The run heads of each class.  A workgroup takes a contiguous range of the
-// sorted keys, counts its heads per class, reserves its places with one
-// global atomic per class, then writes them (LDS atomics per wave and class).
-// (Per-wave global atomics on the five counters serialised: 2-6 ms a batch.)
+// The run heads of each class.  A workgroup takes a contiguous range of
+// kHeadsPer x blockDim sorted keys, counts its heads per class (eight
+// classifications' key reads in flight per lane), reserves its places with
+// one global atomic per class, then classifies again (from L2) and writes the
+// heads (LDS atomics per wave and class).  Per-wave
+// global atomics on the five counters serialised (2-6 ms a batch), and a
+// dependent key read per class probe left the kernel latency-bound.
+constexpr uint32_t kHeadsPer = 64;
 __global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads, uint32_t *nheads,
                                 uint32_t sentinel) {
   __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
-  const uint64_t per = ((n + gridDim.x - 1) / gridDim.x + blockDim.x - 1) / blockDim.x * blockDim.x;
-  const uint64_t lo = uint64_t(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
+  const uint64_t lo = uint64_t(blockIdx.x) * kHeadsPer * blockDim.x;
   if (threadIdx.x < kRunClasses) cnt[threadIdx.x] = 0;
   __syncthreads();
   uint32_t mine[kRunClasses] = {};
-  for (uint64_t q = lo + threadIdx.x; q < hi; q += blockDim.x) {
-    const uint32_t c = run_class(skeys, n, q, sentinel);
+  for (uint32_t j = 0; j < kHeadsPer; j += 8) {
 #pragma unroll
-    for (uint32_t k = 0; k < kRunClasses; ++k) mine[k] += c == k;
+    for (uint32_t u = 0; u < 8; ++u) {
+      const uint32_t c = run_class(skeys, n, lo + uint64_t(j + u) * blockDim.x + threadIdx.x, sentinel);
+#pragma unroll
+      for (uint32_t k = 0; k < kRunClasses; ++k) mine[k] += c == k;
+    }
   }
 #pragma unroll
   for (uint32_t k = 0; k < kRunClasses; ++k)
@@ -723,9 +732,9 @@ __global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *hea
   }
   __syncthreads();
   const uint32_t lane = __lane_id();
-  for (uint64_t q0 = lo + (threadIdx.x & ~63u); q0 < hi; q0 += blockDim.x) {   // wave-uniform
-    const uint64_t q = q0 + lane;
-    const uint32_t c = q < hi ? run_class(skeys, n, q, sentinel) : kRunClasses;
+  for (uint32_t it = 0; it < kHeadsPer; ++it) {                 // the keys are in L2 now
+    const uint64_t q = lo + uint64_t(it) * blockDim.x + threadIdx.x;
+    const uint32_t c = run_class(skeys, n, q, sentinel);
 #pragma unroll
     for (uint32_t k = 0; k < kRunClasses; ++k) {
       const uint64_t m = __ballot(c == k);
@@ -1190,8 +1199,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 4 * kRunClasses, st));
   hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec, sentinel);
   CT_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 4,
-                                                                                   (b.n + blk - 1) / blk))),
+  hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + kHeadsPer * blk - 1) / (kHeadsPer * blk))),
                      dim3(blk), 0, st, b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel);
   CT_CHECK(hipGetLastError());
   uint32_t cnt[1 + kRunClasses] = {};
