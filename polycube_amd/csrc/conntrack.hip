@@ -766,21 +766,34 @@ __global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *hea
 // its result becomes the cache; only a record that needs the table itself (a
 // slot to claim, another key of the bucket) takes step() on lane 0.  The next
 // round starts after that record, so a chunk costs one round per change.
-__device__ void walk_long(const CtBatch &b, const CtTable &t, const WalkRec *wrec, int32_t *sres, uint32_t p,
+#ifndef PCN_CT_GATHER
+// 0: the walk reads each record from batch order through the sorted index
+// (a dependent load, but no gather pass: -0.4..-0.6 ms a batch, the walk
+// +0.3 ms); 1: ct_gather copies the records into sorted order first
+#define PCN_CT_GATHER 0
+#endif
+struct RecSrc {
+  const WalkRec *rec;     // sorted order (gathered) or batch order
+  const uint32_t *sidx;   // sorted position -> batch index (PCN_CT_GATHER 0)
+  __device__ __forceinline__ WalkRec at(uint64_t q) const { return load_rec(&rec[PCN_CT_GATHER ? q : sidx[q]]); }
+  __device__ __forceinline__ uint32_t key(uint64_t q) const { return rec[PCN_CT_GATHER ? q : sidx[q]].key; }
+};
+
+__device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec, int32_t *sres, uint32_t p,
                           uint32_t *cursor_j, uint64_t hi, int first) {
   __shared__ WalkRec buf[2][64];
   const uint32_t lane = threadIdx.x;
-  const uint32_t k = wrec[p].key;
+  const uint32_t k = wrec.key(p);
   const uint64_t q0 = first ? p : *cursor_j;
   const uint64_t last = b.n - 1;
   Cache c{};
   uint64_t base = q0;
-  buf[0][lane] = load_rec(&wrec[base + lane < last ? base + lane : last]);
+  buf[0][lane] = wrec.at(base + lane < last ? base + lane : last);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   int cur = 0;
   for (;;) {
-    const WalkRec nx = load_rec(&wrec[base + 64 + lane < last ? base + 64 + lane : last]);
+    const WalkRec nx = wrec.at(base + 64 + lane < last ? base + 64 + lane : last);
     const WalkRec w = buf[cur][lane];
     const CtRec &r = w.r;
     const bool inrun = base + lane < b.n && w.key == k && w.idx < hi;
@@ -870,7 +883,7 @@ struct WalkPlan {
   uint32_t blk0[kRunClasses + 1];  // first block of each class
 };
 
-__global__ void ct_walk_kernel(CtBatch b, CtTable t, const WalkRec *wrec, int32_t *sres, const uint32_t *heads,
+__global__ void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t *sres, const uint32_t *heads,
                                WalkPlan plan, uint32_t *cursor, uint64_t hi, int first) {
   if (blockIdx.x < plan.blk0[1]) {             // 64-thread blocks: one wave per long run
     walk_long(b, t, wrec, sres, heads[blockIdx.x], &cursor[blockIdx.x], hi, first);
@@ -882,22 +895,22 @@ __global__ void ct_walk_kernel(CtBatch b, CtTable t, const WalkRec *wrec, int32_
   if (jj >= plan.cnt[cls]) return;
   const uint64_t j = class_off(b.n, cls) + jj;
   const uint32_t p = heads[j];
-  const uint32_t k = wrec[p].key;
+  const uint32_t k = wrec.key(p);
   uint64_t q = first ? p : cursor[j];
   const uint64_t last = b.n - 1;
   Cache c{};
   // two records in flight in named registers, A/B alternating (a register
   // move of an in-flight load would wait for it)
-  WalkRec A = load_rec(&wrec[q < last ? q : last]);
-  WalkRec B = load_rec(&wrec[q + 1 < last ? q + 1 : last]);
+  WalkRec A = wrec.at(q < last ? q : last);
+  WalkRec B = wrec.at(q + 1 < last ? q + 1 : last);
   for (;;) {
     if (q >= b.n || A.key != k || A.idx >= hi) break;
     sres[q] = step(b, t, c, A);
-    A = load_rec(&wrec[q + 2 < last ? q + 2 : last]);
+    A = wrec.at(q + 2 < last ? q + 2 : last);
     ++q;
     if (q >= b.n || B.key != k || B.idx >= hi) break;
     sres[q] = step(b, t, c, B);
-    B = load_rec(&wrec[q + 2 < last ? q + 2 : last]);
+    B = wrec.at(q + 2 < last ? q + 2 : last);
     ++q;
   }
   flush(c);
@@ -1104,7 +1117,8 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     if (s.brec) CT_CHECK(hipFree(s.brec));
     CT_CHECK(hipMalloc(&s.brec, n * sizeof(WalkRec)));
     if (s.wrec) CT_CHECK(hipFree(s.wrec));
-    CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
+    s.wrec = nullptr;
+    if (PCN_CT_GATHER) CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
     if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1..5] runs per class,
                                                               // [8] ct_prep's chunk counter
     s.cap = n;
@@ -1197,8 +1211,11 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
                                               st));
   CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 4 * kRunClasses, st));
-  hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec, sentinel);
-  CT_CHECK(hipGetLastError());
+  if (PCN_CT_GATHER) {
+    hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec, sentinel);
+    CT_CHECK(hipGetLastError());
+  }
+  const RecSrc src{PCN_CT_GATHER ? s.wrec : s.brec, s.idx2};
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + kHeadsPer * blk - 1) / (kHeadsPer * blk))),
                      dim3(blk), 0, st, b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel);
   CT_CHECK(hipGetLastError());
@@ -1223,7 +1240,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   for (size_t h = 0; h <= hard.size(); ++h) {
     const uint64_t hi = h < hard.size() ? hard[h] : b.n;
     if (wgrid) {
-      hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(wblk), 0, st, b, t, s.wrec, s.sres, s.heads, plan,
+      hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(wblk), 0, st, b, t, src, s.sres, s.heads, plan,
                          s.cursor, hi, first);
       CT_CHECK(hipGetLastError());
     }

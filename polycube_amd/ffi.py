@@ -6,7 +6,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpcn_ipt.so")
+# PCN_IPT_LIBRARY: an alternative build of the same library (A/B measurements, tools/)
+LIB_PATH = os.environ.get("PCN_IPT_LIBRARY") or os.path.join(_HERE, "libpcn_ipt.so")
 
 
 class LibraryMissing(RuntimeError):
