@@ -788,12 +788,18 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
   const uint64_t last = b.n - 1;
   Cache c{};
   uint64_t base = q0;
-  buf[0][lane] = wrec.at(base + lane < last ? base + lane : last);
+  auto ix = [&](uint64_t r) -> uint64_t {       // sorted position -> the record's index
+    r = r < last ? r : last;
+    return PCN_CT_GATHER ? r : wrec.sidx[r];
+  };
+  buf[0][lane] = load_rec(&wrec.rec[ix(base + lane)]);
+  uint64_t nidx = ix(base + 64 + lane);          // the next chunk's indices, a chunk ahead
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   int cur = 0;
   for (;;) {
-    const WalkRec nx = wrec.at(base + 64 + lane < last ? base + 64 + lane : last);
+    const WalkRec nx = load_rec(&wrec.rec[nidx]);
+    nidx = ix(base + 128 + lane);
     const WalkRec w = buf[cur][lane];
     const CtRec &r = w.r;
     const bool inrun = base + lane < b.n && w.key == k && w.idx < hi;
@@ -900,17 +906,25 @@ __global__ void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t 
   const uint64_t last = b.n - 1;
   Cache c{};
   // two records in flight in named registers, A/B alternating (a register
-  // move of an in-flight load would wait for it)
-  WalkRec A = wrec.at(q < last ? q : last);
-  WalkRec B = wrec.at(q + 1 < last ? q + 1 : last);
+  // move of an in-flight load would wait for it), and the batch indices of
+  // the two after them (the record loads never wait on an index load)
+  auto ix = [&](uint64_t r) -> uint64_t {
+    r = r < last ? r : last;
+    return PCN_CT_GATHER ? r : wrec.sidx[r];
+  };
+  WalkRec A = load_rec(&wrec.rec[ix(q)]);
+  WalkRec B = load_rec(&wrec.rec[ix(q + 1)]);
+  uint64_t IA = ix(q + 2), IB = ix(q + 3);
   for (;;) {
     if (q >= b.n || A.key != k || A.idx >= hi) break;
     sres[q] = step(b, t, c, A);
-    A = wrec.at(q + 2 < last ? q + 2 : last);
+    A = load_rec(&wrec.rec[IA]);
+    IA = ix(q + 4);
     ++q;
     if (q >= b.n || B.key != k || B.idx >= hi) break;
     sres[q] = step(b, t, c, B);
-    B = wrec.at(q + 2 < last ? q + 2 : last);
+    B = load_rec(&wrec.rec[IB]);
+    IB = ix(q + 4);
     ++q;
   }
   flush(c);
