@@ -221,7 +221,8 @@ __device__ uint32_t ports_lookback(const unsigned long long *desc, uint64_t g, c
 
 // Chain selection (ChainSelector_dp.c:131-298), the conntrack key and kind;
 // packets that need no table access get their final outcome here.
-__global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, uint32_t *keys, uint32_t *idx,
+__global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, uint32_t *lcs, uint32_t *keys,
+                               uint32_t *idx,
                                uint32_t kbits, uint32_t *hard_cnt, uint32_t *hard_list, unsigned long long *desc,
                                uint32_t *chunk_ctr) {
   const uint32_t sentinel = (1u << kbits) - 1;
@@ -337,6 +338,7 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, 
     const uint32_t key = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
                                 : sentinel;
     keys[i] = key;
+    lcs[i] = uint32_t(r.len) | uint32_t(r.cinfo) << 16;   // what ct_count reads (not the 64-byte record)
     WalkRec wr;
     wr.r = r;
     wr.key = key;
@@ -660,7 +662,7 @@ __device__ __forceinline__ int32_t step(const CtBatch &b, const CtTable &t, Cach
 // After the sort: walk records in sorted order (each walking lane then reads
 // consecutive lines) and the list of run heads.
 #ifndef PCN_CT_LONG_RUN
-#define PCN_CT_LONG_RUN 512
+#define PCN_CT_LONG_RUN 128
 #endif
 constexpr uint64_t kLongRun = PCN_CT_LONG_RUN;   // a run at least this long gets a whole wave
 
@@ -689,7 +691,7 @@ __device__ __forceinline__ uint32_t run_class(const uint32_t *skeys, uint64_t n,
   const uint32_t k = at(q), km = q ? at(q - 1) : 0xffffffffu;
   const uint32_t k1 = at(q + 1), k7 = at(q + 7), k63 = at(q + 63), kl = at(q + kLongRun);
   if (q >= n || k == sentinel || km == k) return kRunClasses;
-  return kl == k ? 0 : k63 == k ? 1 : k7 == k ? 2 : k1 == k ? 3 : 4;   // more than 512 / 63 / 7 / 1 packets
+  return kl == k ? 0 : k63 == k ? 1 : k7 == k ? 2 : k1 == k ? 3 : 4;   // more than kLongRun / 63 / 7 / 1 packets
 }
 
 __global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t *skeys, const uint32_t *sidx,
@@ -968,7 +970,7 @@ constexpr uint32_t kCountBlock = 1024;
 constexpr uint32_t kLdsRules = 1024;          // LDS bins per chain; rules above use global atomics
 constexpr uint64_t kCountChunk = 65536;       // packets per workgroup: u32 byte bins cannot wrap
 
-__global__ void ct_count_kernel(CtBatch b, const WalkRec *brec) {
+__global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs) {
   constexpr uint32_t per = 2 + kLdsRules;
   // groups 0-2: the chains; group 3: Horus rule ids (bins 2..)
   __shared__ uint32_t pk[4 * per], by[4 * per];
@@ -978,27 +980,27 @@ __global__ void ct_count_kernel(CtBatch b, const WalkRec *brec) {
   const uint64_t hi = lo + kCountChunk < b.n ? lo + kCountChunk : b.n;
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const int32_t rid = b.rule_ids[i];
-    const CtRec &r = brec[i].r;
+    const uint32_t lc = lcs[i], len = lc & 0xffff, cinfo = lc >> 16;
     if (rid <= PCN_IPT_RID_HORUS0) {                  // Horus_dp.c:80-90, counted at the lookup
       if (!b.horus_ctr) continue;
       const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
       if (id >= kLdsRules) {
         atomicAdd(&b.horus_ctr[2 * id], 1ull);
-        atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(r.len));
+        atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(len));
       } else {
         atomicAdd(&pk[3 * per + 2 + id], 1u);
-        atomicAdd(&by[3 * per + 2 + id], uint32_t(r.len));
+        atomicAdd(&by[3 * per + 2 + id], uint32_t(len));
       }
       continue;
     }
-    const uint32_t c = r.cinfo & 3;
+    const uint32_t c = cinfo & 3;
     if (c == 3) continue;
     uint32_t bin;
     if (rid >= 0) {
       if (uint32_t(rid) >= b.ncounted[c]) continue;
       if (uint32_t(rid) >= kLdsRules) {
         atomicAdd(&b.ctr[c][2 + 2 * uint64_t(rid)], 1ull);
-        atomicAdd(&b.ctr[c][3 + 2 * uint64_t(rid)], static_cast<unsigned long long>(r.len));
+        atomicAdd(&b.ctr[c][3 + 2 * uint64_t(rid)], static_cast<unsigned long long>(len));
         continue;
       }
       bin = 2 + uint32_t(rid);
@@ -1010,7 +1012,7 @@ __global__ void ct_count_kernel(CtBatch b, const WalkRec *brec) {
       continue;
     }
     atomicAdd(&pk[c * per + bin], 1u);
-    atomicAdd(&by[c * per + bin], uint32_t(r.len));
+    atomicAdd(&by[c * per + bin], uint32_t(len));
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) {
@@ -1064,6 +1066,7 @@ struct CtScratch {
   uint64_t cap = 0;
   unsigned long long *pdesc = nullptr;   // ct_prep: the ports word of every 64-frame group
   uint32_t *keys = nullptr, *keys2 = nullptr;
+  uint32_t *lcs = nullptr;                // per packet: len | cinfo << 16 (ct_count)
   uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *hard_cnt = nullptr;
   uint32_t *heads = nullptr;
   int32_t *sres = nullptr;
@@ -1079,7 +1082,7 @@ CtScratch *ct_scratch_new() { return new CtScratch(); }
 
 void ct_scratch_free(CtScratch *s) {
   if (!s) return;
-  for (void *p : {static_cast<void *>(s->pdesc),
+  for (void *p : {static_cast<void *>(s->pdesc), static_cast<void *>(s->lcs),
                   static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
                   static_cast<void *>(s->hard_cnt), static_cast<void *>(s->brec), static_cast<void *>(s->wrec),
@@ -1117,7 +1120,7 @@ void ct_table_free(CtTable &t) {
 
 static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
   if (s.cap < n) {
-    for (uint32_t **p : {&s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list,
+    for (uint32_t **p : {&s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list, &s.lcs,
                          reinterpret_cast<uint32_t **>(&s.sres)}) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, n * 4));
@@ -1216,7 +1219,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipMemsetAsync(s.hard_cnt + 8, 0, 4, st));
   CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
   const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + kPrepChunk - 1) / kPrepChunk));
-  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(blk), 0, st, b, t.carry, s.brec, s.keys, s.idx, kbits,
+  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(blk), 0, st, b, t.carry, s.brec, s.lcs, s.keys, s.idx, kbits,
                      s.hard_cnt, s.hard_list, s.pdesc, s.hard_cnt + 8);
   CT_CHECK(hipGetLastError());
   CT_CHECK(ct_advance_carry(b, s, t.carry, num_cus, stream));
@@ -1267,7 +1270,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
   CT_CHECK(hipGetLastError());
   const unsigned cgrid = static_cast<unsigned>((b.n + kCountChunk - 1) / kCountChunk);
-  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.brec);
+  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs);
   CT_CHECK(hipGetLastError());
   return hipSuccess;
 }

@@ -202,7 +202,7 @@ def test_headline_size_flows_parity(dev):
 
 @pytest.mark.parametrize("p_icmp", [0.0, 0.1])
 def test_long_runs_walk_a_wave_each(dev, p_icmp):
-    """Keys with >= PCN_CT_LONG_RUN (512) packets in one batch get a whole wave
+    """Keys with more than PCN_CT_LONG_RUN (128) packets in one batch get a whole wave
     (conntrack.hip walk_long: records staged in LDS 64 at a time, eligible
     segments labelled in parallel); interleaved with many short flows, TCP
     noise (INVALID paths, FIN/RST) and, with ICMP, echo replies that split the
@@ -220,7 +220,7 @@ def test_long_runs_walk_a_wave_each(dev, p_icmp):
     nb = np.empty((n, 64), np.uint8)
     nb[~slot] = fl.reshape(n_long, 64)
     nb[slot] = fs.reshape(n_short, 64)
-    # the long flows do give runs past the 512 threshold inside one batch
+    # the long flows give runs far past the threshold inside one batch
     ip = nb[:30000, 26:34].view(">u4")
     pt = nb[:30000, 34:38].view(">u2")
     key = np.stack([ip.min(1), ip.max(1), pt.min(1), pt.max(1), nb[:30000, 23]], 1).astype(np.int64)
