@@ -277,8 +277,10 @@ int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain);
  * While enabled, pcn_ipt_classify labels every IPv4 packet from the table and
  * every accepted packet updates it, with the result of running the batch one
  * packet at a time in index order (and batches in submission order).
- * Differences from the kernel LRU: entries are never evicted; an insert into a
- * full table is dropped and counted (pcn_ipt_ct_info.inserts_lost).  Entries
+ * Differences from the kernel LRU: entries are never evicted; an insert that
+ * finds no free slot within 512 slots of the key's home slot (a full or
+ * nearly full table) is dropped and counted (pcn_ipt_ct_info.inserts_lost),
+ * which bounds every lookup at 512 probes.  Entries
  * never expire in the reference either (ttl is written, never compared).
  * batch.ct_status must be NULL while enabled. */
 typedef struct {
@@ -291,7 +293,7 @@ typedef struct {
 typedef struct {
   uint32_t enabled, capacity_log2;
   uint64_t now;              /* timestamp used for new ttl values */
-  uint64_t inserts_lost;     /* inserts refused because the table was full */
+  uint64_t inserts_lost;     /* inserts refused: no free slot near the key's home (table (nearly) full) */
 } pcn_ipt_ct_info;
 /* capacity = 2^capacity_log2 slots (0 => 2^18); the table persists across enable/disable. */
 int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2);

@@ -412,11 +412,19 @@ struct SlotRef {
   CtSlot *e;
   Ent v;
 };
+//
+// A key lives within kMaxProbe slots of its home slot: an insert that finds
+// no empty slot that close is refused (counted in stats[0], as for a full
+// table), so a lookup stops there too.  Without the bound a nearly full
+// table made every miss and insert scan up to the whole table, ~1 us per
+// dependent probe.
+constexpr uint64_t kMaxProbe = 512;
 __device__ SlotRef table_slot(const CtTable &t, const Key &k, bool claim) {
   const uint64_t mask = (uint64_t(1) << t.cap_log2) - 1;
+  const uint64_t probes = mask < kMaxProbe ? mask + 1 : kMaxProbe;
   const bool zero_key = (k.src | k.dst | k.sport | k.dport | k.proto) == 0;
   uint64_t s = key_hash(k.src, k.dst, k.proto, k.sport, k.dport) >> 7;
-  for (uint64_t probe = 0; probe <= mask; ++probe, ++s) {
+  for (uint64_t probe = 0; probe < probes; ++probe, ++s) {
     CtSlot *e = &t.slots[s & mask];
     uint32_t tag = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tag == 0) {
@@ -436,7 +444,7 @@ __device__ SlotRef table_slot(const CtTable &t, const Key &k, bool claim) {
         (hi.w & 0xff) == k.proto)
       return SlotRef{e, slot_value(hi)};
   }
-  if (claim) atomicAdd(&t.stats[0], 1ull);          // table full: the insert is lost
+  if (claim) atomicAdd(&t.stats[0], 1ull);          // no free slot near home: the insert is lost
   return SlotRef{nullptr, Ent{}};
 }
 

@@ -259,6 +259,27 @@ def test_errors_quoting_the_all_zero_key_among_inserts(dev):
     assert_counters(o, ipt, n=3)
 
 
+def test_full_table_inserts_and_misses_stay_bounded(dev):
+    """A full table: every further insert and miss stops after 512 probes
+    (conntrack.hip kMaxProbe) instead of scanning the whole table, and the
+    live entries stay findable."""
+    import time
+    o, ipt = ct_pair({1: []}, {1: "ACCEPT"}, cap_log2=14)
+    n = 40000
+    f, _ = synth.flow_traffic(n, n, 23, stride=64, p_icmp=0.0, p_noise=0.0, p_err=0.0)   # one packet per flow
+    ipt.classify(t(dev, f), n=n, stride=64, fixed_len=64)
+    torch.cuda.synchronize()
+    assert ipt.ct_info()["inserts_lost"] > 0
+    live = len(ipt.ct_dump())
+    assert 0 < live <= 1 << 14
+    g, _ = synth.flow_traffic(n, n, 24, stride=64, p_icmp=0.0, p_noise=0.0, p_err=0.0)
+    t0 = time.perf_counter()
+    ipt.classify(t(dev, g), n=n, stride=64, fixed_len=64)
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 10.0
+    assert len(ipt.ct_dump()) >= live
+
+
 def test_full_table_drops_inserts_without_faulting(dev):
     o, ipt = ct_pair({1: []}, {1: "ACCEPT"}, cap_log2=10)
     f, _ = synth.flow_traffic(20000, 5000, 8, stride=64, p_icmp=0.0, p_noise=0.0)
