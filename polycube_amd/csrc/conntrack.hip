@@ -782,6 +782,23 @@ __global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *hea
 // +0.3 ms); 1: ct_gather copies the records into sorted order first
 #define PCN_CT_GATHER 0
 #endif
+#ifndef PCN_CT_DIRECT
+// 1: the walk writes the final verdicts / rule ids by batch index, no scatter
+// pass (A/B: walk +0.3..0.4 ms, scatter -0.7 ms a batch); 0: sorted-order
+// outcomes, then ct_scatter
+#define PCN_CT_DIRECT 1
+#endif
+// A walked packet's outcome: into sres at its sorted position (ct_scatter
+// moves it to batch order), or (PCN_CT_DIRECT) straight to batch index i.
+__device__ __forceinline__ void put_outcome(const CtBatch &b, int32_t *sres, uint64_t q, uint32_t i, int32_t o) {
+  if (PCN_CT_DIRECT) {
+    b.verdicts[i] = static_cast<uint8_t>(o & 1);
+    b.rule_ids[i] = o >> 1;
+  } else {
+    sres[q] = o;
+  }
+}
+
 struct RecSrc {
   const WalkRec *rec;     // sorted order (gathered) or batch order
   const uint32_t *sidx;   // sorted position -> batch index (PCN_CT_GATHER 0)
@@ -853,14 +870,14 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
       const uint32_t cnt = em == ~0ull >> u0 ? 64u - u0 : static_cast<uint32_t>(__builtin_ctzll(~em));
       const uint32_t end = u0 + cnt < m ? u0 + cnt : m;
       const bool mine = lane >= u0 && lane < end;
-      if (mine) sres[base + lane] = o;
+      if (mine) put_outcome(b, sres, base + lane, w.idx, o);
       const bool anyd = __ballot(mine && cls == 0 && cc.dirty) != 0;
       if (lane == 0 && anyd) c.dirty = true;
       u0 = end;
       if (u0 < m) {
         const int ecls = __shfl(cls, u0);
         if (ecls == 1) {                              // the changing record: its result is the new state
-          if (lane == u0) sres[base + lane] = o;
+          if (lane == u0) put_outcome(b, sres, base + lane, w.idx, o);
           const uint32_t nl = __shfl(static_cast<uint32_t>(cc.v.ttl), u0);
           const uint32_t nh = __shfl(static_cast<uint32_t>(cc.v.ttl >> 32), u0);
           const uint32_t ns = __shfl(cc.v.seq, u0);
@@ -873,7 +890,7 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
           }
         } else {                                      // the record that needs the table: the full step
           const WalkRec x = buf[cur][u0];
-          if (lane == 0) sres[base + u0] = step(b, t, c, x);
+          if (lane == 0) put_outcome(b, sres, base + u0, x.idx, step(b, t, c, x));
         }
         ++u0;
       }
@@ -927,12 +944,12 @@ __global__ void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t 
   uint64_t IA = ix(q + 2), IB = ix(q + 3);
   for (;;) {
     if (q >= b.n || A.key != k || A.idx >= hi) break;
-    sres[q] = step(b, t, c, A);
+    put_outcome(b, sres, q, A.idx, step(b, t, c, A));
     A = load_rec(&wrec.rec[IA]);
     IA = ix(q + 4);
     ++q;
     if (q >= b.n || B.key != k || B.idx >= hi) break;
-    sres[q] = step(b, t, c, B);
+    put_outcome(b, sres, q, B.idx, step(b, t, c, B));
     B = load_rec(&wrec.rec[IB]);
     IB = ix(q + 4);
     ++q;
@@ -1275,8 +1292,10 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
       CT_CHECK(hipGetLastError());
     }
   }
-  hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
-  CT_CHECK(hipGetLastError());
+  if (!PCN_CT_DIRECT) {
+    hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
+    CT_CHECK(hipGetLastError());
+  }
   const unsigned cgrid = static_cast<unsigned>((b.n + kCountChunk - 1) / kCountChunk);
   hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs);
   CT_CHECK(hipGetLastError());
