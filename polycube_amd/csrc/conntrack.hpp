@@ -7,14 +7,15 @@
 //   A. the classify kernel once per possible label (1 run when no reachable
 //      chain has conntrack rules, else 4), counters off, giving each packet's
 //      outcome as a function of its label;
-//   B. ct_parse -> max-scan -> ct_prep: stale ports (quirk Q4), the chain,
-//      the packet's conntrack key and kind; packets that need no table access
-//      are finished here;
+//   B. ct_prep: stale ports (quirk Q4, by look-back), the chain, the packet's
+//      conntrack key and kind, its walk record in batch order; packets that
+//      need no table access are finished here;
 //   C. a stable radix sort of the table-touching packets by key bucket, so
 //      every key's packets form one run in batch order;
-//   D. ct_walk: one lane per run walks its packets in order against the
-//      HBM-resident table (label -> outcome -> update), so the result equals
-//      processing the batch one packet at a time;
+//   D. ct_heads (runs by length class) -> ct_walk: a wave per long run, a lane
+//      per short one, walks its packets in order against the HBM-resident
+//      table (label -> outcome -> update), so the result equals processing the
+//      batch one packet at a time; outcomes go straight to batch order;
 //   E. ct_count: per-rule / default / accept-established counters from the
 //      final rule ids.
 // Echo replies long enough to carry a quoted header (>= 70 B) may read a
