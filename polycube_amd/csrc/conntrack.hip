@@ -104,7 +104,14 @@ __device__ __forceinline__ Parsed parse(const uint32_t w[18], uint32_t L, uint32
     }
   }
   p.L = L;
-  auto W = [&](int k) { return s ? w[k + 1] : w[k]; };   // bytes >= 12 move by one dword
+  // bytes >= 12 move by one dword.  The asm keeps both words in registers:
+  // folded into w[k + s], the window became a dynamically indexed array the
+  // compiler placed in LDS (72 KB a workgroup: two workgroups per CU).
+  auto W = [&](int k) {
+    uint32_t a = w[k], b = w[k + 1];
+    asm volatile("" : "+v"(a), "+v"(b));
+    return s ? b : a;
+  };
   if (L < 14) { p.status = 0; return p; }
   const uint32_t et = ((W(3) & 0xff) << 8) | ((W(3) >> 8) & 0xff);
   if (et != 0x0800) { p.status = 1; return p; }
