@@ -11,7 +11,8 @@
 // (one dependent table access per packet of a run), the sort is hipCUB's
 // onesweep radix sort on a key-bucket id.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <vector>
@@ -1150,6 +1151,22 @@ void ct_table_free(CtTable &t) {
     if (e_ != hipSuccess) return int(e_);   \
   } while (0)
 
+// The (key bucket, batch index) sort: rocPRIM's onesweep radix sort with
+// PCN_CT_RADIX_BITS bits per pass (its gfx950 default is 8: a 25-bit key
+// took four passes, the last for one bit).
+#ifndef PCN_CT_RADIX_BITS
+#define PCN_CT_RADIX_BITS 9   // A/B 8 / 9 / 11: 0.54 / 0.41 / 0.52 ms a 2^24 batch
+#endif
+using CtSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
+                                        PCN_CT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+static hipError_t sort_pairs(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                             uint32_t *vout, uint64_t n, uint32_t kbits, hipStream_t st) {
+  return rocprim::radix_sort_pairs<CtSortConfig>(temp, bytes, kin, kout, vin, vout, static_cast<unsigned int>(n), 0u,
+                                                 kbits, st);
+}
+
 static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
   if (s.cap < n) {
     for (uint32_t **p : {&s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list, &s.lcs,
@@ -1173,8 +1190,7 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     s.cap = n;
   }
   size_t need = 0;
-  CT_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, s.keys, s.keys2, s.idx, s.idx2, int(n), 0,
-                                              int(kbits), st));
+  CT_CHECK(sort_pairs(nullptr, need, s.keys, s.keys2, s.idx, s.idx2, n, kbits, st));
   if (s.temp_bytes < need) {
     if (s.temp) CT_CHECK(hipFree(s.temp));
     CT_CHECK(hipMalloc(&s.temp, need));
@@ -1257,8 +1273,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(ct_advance_carry(b, s, t.carry, num_cus, stream));
   size_t tb;
   tb = s.temp_bytes;
-  CT_CHECK(hipcub::DeviceRadixSort::SortPairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, int(b.n), 0, int(kbits),
-                                              st));
+  CT_CHECK(sort_pairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, b.n, kbits, st));
   CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 4 * kRunClasses, st));
   if (PCN_CT_GATHER) {
     hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec, sentinel);
