@@ -80,6 +80,23 @@ __device__ __forceinline__ T hdr_load(const T *p) {
   if (PCN_HDR_NT) return __builtin_nontemporal_load(p);
   return *p;
 }
+// Fixed-stride header chunks as asm loads the compiler does not count
+// (cdna_hip_programming.md §5.7 item 1): the compiler's own bookkeeping waited
+// vmcnt(0) at the loop head, draining the other stage's chunks (issued half an
+// iteration earlier) with this one's.  process() waits for a stage itself with
+// a counted vmcnt: every later stage's three chunk loads are unconditional, so
+// at least 3 (PF - 1) memory operations follow a stage's chunks.
+// Chain programs only (checked spill-free when built, jit.cpp); the generic
+// kernels keep compiler-counted loads.  A/B at config 3, hit rate 0 / 0.25 /
+// 0.5 / 0.75 / 1: +2.6 / -2.0 / -1.9 / -0.7 / -1.0 % kernel time
+// (profiles/r02_ab_hdr_asm.log).
+#ifndef PCN_HDR_ASM
+#ifdef PCN_JIT
+#define PCN_HDR_ASM 1
+#else
+#define PCN_HDR_ASM 0
+#endif
+#endif
 #ifndef PCN_STAGE_FAST
 #define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
 #endif
@@ -94,6 +111,18 @@ constexpr uint32_t kHashMul = 0x9E3779B1u;
 constexpr uint32_t kNoRule = 0xFFFFFFFFu;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#ifndef PCN_HDR_ASM_MEM
+#define PCN_HDR_ASM_MEM 0   // 1: the asm chunk loads ordered against the compiler's memory operations (A/B: slower)
+#endif
+__device__ __forceinline__ void hdr_load_asm(u32x4 &dst, const u32x4 *p) {
+  if (PCN_HDR_ASM_MEM) {
+    if (PCN_HDR_NT) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(dst) : "v"(p) : "memory");
+    else asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+  } else {
+    if (PCN_HDR_NT) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(dst) : "v"(p));
+    else asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p));
+  }
+}
 
 __device__ __forceinline__ uint32_t bswap16u(uint32_t x) { return ((x & 0xff) << 8) | ((x >> 8) & 0xff); }
 
@@ -704,14 +733,19 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         // the whole group is in the batch: scalar base + loop-invariant lane offsets
         const uint8_t *gb = a.frames + group * a.stride;
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          x.c[q] = hdr_load(reinterpret_cast<const u32x4 *>(gb + loff[q]));
+        for (int q = 0; q < 3; ++q) {
+          const u32x4 *src = reinterpret_cast<const u32x4 *>(gb + loff[q]);
+          if (PCN_HDR_ASM) hdr_load_asm(x.c[q], src);
+          else x.c[q] = hdr_load(src);
+        }
       } else {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           uint64_t f = group + cf[q];
           f = f < a.n ? f : last;
-          x.c[q] = hdr_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]));
+          const u32x4 *src = reinterpret_cast<const u32x4 *>(a.frames + f * a.stride + co[q]);
+          if (PCN_HDR_ASM) hdr_load_asm(x.c[q], src);
+          else x.c[q] = hdr_load(src);
         }
       }
     } else if (FIXED) {
@@ -752,8 +786,15 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         h.w[4 * q] = cur.c[q].x; h.w[4 * q + 1] = cur.c[q].y; h.w[4 * q + 2] = cur.c[q].z; h.w[4 * q + 3] = cur.c[q].w;
       }
     } else if (FIXED) {
+      if (PCN_HDR_ASM) {
+        static_assert(PF == 1 || PF == 2 || PF == 3, "counted header waits for PF 1..3");
+        if constexpr (PF == 1) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cur.c[0]), "+v"(cur.c[1]), "+v"(cur.c[2]));
+        else if constexpr (PF == 2) asm volatile("s_waitcnt vmcnt(3)" : "+v"(cur.c[0]), "+v"(cur.c[1]), "+v"(cur.c[2]));
+        else asm volatile("s_waitcnt vmcnt(6)" : "+v"(cur.c[0]), "+v"(cur.c[1]), "+v"(cur.c[2]));
+      } else {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
+        for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
+      }
       asm volatile("" ::: "memory");   // the region held the last iteration's WaveScratch
 #pragma unroll
       for (int q = 0; q < 3; ++q) hbuf[64 * q + lane] = cur.c[q];
@@ -1046,6 +1087,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     for (int d = 0; d < PF; ++d)
       if (d == 0 || i + d * step < n_round) process(i + d * step, st[d]);
   }
+  // the last stages' (unused) asm chunk loads land before the wave moves on
+  if (PCN_HDR_ASM && FIXED && PCN_HDR_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (PCN_ABLATE == 5) return;
   // ---- flush the workgroup histogram ----
