@@ -234,6 +234,34 @@ def test_long_runs_walk_a_wave_each(dev, p_icmp):
     assert_ae(o, ipt)
 
 
+def test_long_runs_resume_across_echo_reply_segments(dev):
+    """Long echo replies (>= 70 B, ct_hard) split the batch into segments; the
+    long runs walked by whole waves (walk_long) stop at each split and resume
+    from their cursor in the next segment, bit-exact vs the oracle."""
+    rng = np.random.default_rng(41)
+    o, ipt = ct_pair({1: [{"conntrack": "RELATED", "action": "ACCEPT"},
+                          {"conntrack": "INVALID", "action": "DROP"}] + synth.config_rules(2).rules()},
+                     {1: "ACCEPT"}, jit=1)
+    n = 40000
+    f, _ = synth.flow_traffic(n, 10, 41, stride=128, p_icmp=0.2, p_err=0.02, p_noise=0.03)
+    nb = f.reshape(n, 128)
+    icmp = nb[:, 23] == 1
+    rep = icmp & (rng.random(n) < 0.02)               # ~80 long echo replies: ~80 segments
+    nb[rep, 34] = 0
+    q = rng.integers(0, n, size=n)
+    nb[rep, 42] = 0x45
+    nb[rep, 51] = nb[q[rep], 23]
+    nb[rep, 54:58] = nb[q[rep], 26:30]
+    nb[rep, 58:62] = nb[q[rep], 30:34]
+    nb[rep, 62:66] = nb[q[rep], 34:38]
+    lens = np.where(rep, 98, 128).astype(np.uint16)
+    for lo, hi in ((0, 25000), (25000, n)):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, nb[lo:hi].reshape(-1), hi - lo, lens=lens[lo:hi])
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(synth.config_rules(2).rules()) + 3)
+
+
 def test_errors_quoting_the_all_zero_key_among_inserts(dev):
     """ICMP errors quoting proto 0 between 0.0.0.0 and itself, ports 0: the one
     key a stale (zero) read of a slot claimed in the same launch could match,
