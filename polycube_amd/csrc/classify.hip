@@ -1090,6 +1090,30 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // the last stages' (unused) asm chunk loads land before the wave moves on
   if (PCN_HDR_ASM && FIXED && PCN_HDR_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (chunked) {
+    // The launch's last workgroup to finish zeroes the start counter for the
+    // next launch (no memset per launch) and, on the batch's last launch,
+    // writes the carry: every group is published by then, so the look-back
+    // from the end gives the ports of the batch's last frame that wrote them,
+    // or the previous carry (no tail pass over the batch).
+    uint32_t *slot = reinterpret_cast<uint32_t *>(pcn_smem + a.lds_scratch);   // wave 0's region, free now
+    if (threadIdx.x == 0)
+      *slot = __hip_atomic_fetch_add(&a.chunk_ctr[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+              gridDim.x - 1;
+    __syncthreads();
+    const bool last_wg = *slot != 0;
+    __syncthreads();
+    if (last_wg && threadIdx.x < 64) {
+      if (a.carry_out) {
+        const uint32_t cout = stale_lookback(a, (a.gbase + a.n + 63) >> 6);
+        if (threadIdx.x == 0) *a.carry_out = cout;
+      }
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(&a.chunk_ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.chunk_ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   if (PCN_ABLATE == 5) return;
   // ---- flush the workgroup histogram ----
   // Workgroups finish together and all add into the same counters; each
@@ -1185,8 +1209,8 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
     if (a.has_stale) {   // contiguous chunks per workgroup, claimed in start order
       c.gbase = base;
       c.chunk_frames = (c.n + uint64_t(grid) * kBlock - 1) / (uint64_t(grid) * kBlock) * kBlock;
-      const hipError_t e = hipMemsetAsync(a.chunk_ctr, 0, 4, stream);
-      if (e != hipSuccess) return static_cast<int>(e);
+      // (the counters are zero: each launch's last workgroup resets them)
+      if (base + c.n < a.n) c.carry_out = nullptr;   // only the batch's last launch writes the carry
     }
     if (base) {
       if (!a.offsets) { c.frames = a.frames + base * a.stride; c.frames_bytes = a.frames_bytes - base * a.stride; }

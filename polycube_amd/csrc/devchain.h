@@ -179,10 +179,13 @@ struct LaunchArgs {
   int32_t hz_bins;               // first LDS counter bin of the Horus rule ids; -1 => wave-aggregated global atomics
   uint64_t *stale_desc;          // per 64-frame group of the batch: the published word (stale_word)
   const uint32_t *stale_carry;   // ports dword (wire bytes 34-37) the previous batches left (Q4)
-  uint32_t *chunk_ctr;           // workgroup start counter (zeroed before each launch)
+  uint32_t *chunk_ctr;           // [0] workgroup start counter, [1] workgroups finished; zero before a
+                                 // launch, and the launch's last workgroup zeroes both again
   uint64_t chunk_frames;         // frames per workgroup (a multiple of the block size)
   uint64_t gbase;                // batch index of this launch's frame 0 (a multiple of 64)
   uint32_t stale_epoch;          // this batch's publication epoch (24 bits, never 0)
+  uint32_t *carry_out;           // non-null on a batch's last launch: its last workgroup writes the
+                                 // ports the batch leaves to the next one (the carry, Q4)
 };
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)

@@ -780,7 +780,11 @@ struct StageA {
   int32_t *rule_ids;
 };
 
-int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa, const uint32_t *carry) {
+// carry_out (stateless batches that track the stale ports): when the kernel
+// computes them itself (has_stale), its last workgroup writes the carry there
+// and *carried becomes true; otherwise the caller advances the carry.
+int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa, const uint32_t *carry,
+                 uint32_t *carry_out = nullptr, bool *carried = nullptr) {
   {
     if (!b) return fail(-EINVAL, "null batch");
     if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
@@ -939,7 +943,10 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
           ctx->stale_groups = groups;
           ctx->stale_epoch = 0;
         }
-        if (!ctx->d_chunk_ctr) hip_check(hipMalloc(&ctx->d_chunk_ctr, 64), "hipMalloc(chunk counter)");
+        if (!ctx->d_chunk_ctr) {   // zero from here on: each launch's last workgroup resets it
+          hip_check(hipMalloc(&ctx->d_chunk_ctr, 64), "hipMalloc(chunk counter)");
+          hip_check(hipMemset(ctx->d_chunk_ctr, 0, 64), "hipMemset(chunk counter)");
+        }
         if (++ctx->stale_epoch >= (1u << 24)) {       // words of an old epoch must never match
           hip_check(hipMemsetAsync(ctx->d_stale_desc, 0, ctx->stale_groups * 8, static_cast<hipStream_t>(stream)),
                     "hipMemset(stale groups)");
@@ -950,6 +957,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
         a.stale_carry = carry;
         a.chunk_ctr = ctx->d_chunk_ctr;
         a.stale_epoch = ctx->stale_epoch;
+        a.carry_out = carry_out;
+        if (carried) *carried = carry_out != nullptr;
       }
     }
     // slot count of the chain program (the generic kernel always runs 6)
@@ -1076,8 +1085,9 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     // pcn-firewall with conntrack DISABLED: no labels and no table updates
     // (Firewall_ConntrackTableUpdate_dp.c:136-138), whatever the table holds
     if (!stateful) {
-      int rc = launch_batch(ctx, b, stream, nullptr, stale);
-      if (!rc) rc = advance_carry();
+      bool carried = false;
+      int rc = launch_batch(ctx, b, stream, nullptr, stale, track ? carry : nullptr, &carried);
+      if (!rc && !carried) rc = advance_carry();
       if (rc) return rc;
       if (!ae_mask) return mark();
       device_guard(ctx);
