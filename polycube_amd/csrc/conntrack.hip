@@ -208,7 +208,15 @@ __device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, ui
 // through the published words, {1:24 | status:2 | ports:32} (0: not yet).
 // A group only waits on lower groups, whose waves are running or done, so the
 // waits resolve.  (Was ct_parse + a max-scan + ct_carry: 0.32 ms a batch.)
-constexpr uint32_t kPrepChunk = 4096;                        // frames per claimed chunk
+// Frames per claimed chunk: 4096, or fewer (a multiple of 64, at least 512)
+// when the batch would otherwise not give every CU eight workgroups -- a
+// 2 M-frame batch (one rank's share of a flow split) ran 508 workgroups of
+// 256 threads, 8 waves per CU, on its dependent header reads.
+constexpr uint32_t kPrepChunk = 4096;
+__host__ __device__ inline uint32_t prep_chunk(uint64_t n, int num_cus) {
+  uint64_t c = (n / (uint64_t(num_cus) * 8) + 63) / 64 * 64;
+  return static_cast<uint32_t>(c < 512 ? 512 : c > kPrepChunk ? kPrepChunk : c);
+}
 constexpr unsigned long long kStLocal = 1, kStIncl = 2, kStNone = 3;
 __device__ __forceinline__ unsigned long long ports_word(unsigned long long st, uint32_t ports) {
   return (1ull << 40) | (st << 32) | ports;
@@ -232,17 +240,17 @@ __device__ uint32_t ports_lookback(const unsigned long long *desc, uint64_t g, c
 __global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, uint32_t *lcs, uint32_t *keys,
                                uint32_t *idx,
                                uint32_t kbits, uint32_t *hard_cnt, uint32_t *hard_list, unsigned long long *desc,
-                               uint32_t *chunk_ctr) {
+                               uint32_t *chunk_ctr, uint32_t chunk_frames) {
   const uint32_t sentinel = (1u << kbits) - 1;
   const uint32_t lane = __lane_id();
   __shared__ uint32_t chunk;
   for (;;) {
     if (threadIdx.x == 0) chunk = atomicAdd(chunk_ctr, 1u);
     __syncthreads();
-    const uint64_t lo = uint64_t(chunk) * kPrepChunk;
+    const uint64_t lo = uint64_t(chunk) * chunk_frames;
     __syncthreads();                                      // everyone has read `chunk`
     if (lo >= b.n) return;
-    const uint64_t hi = lo + kPrepChunk < b.n ? lo + kPrepChunk : b.n;
+    const uint64_t hi = lo + chunk_frames < b.n ? lo + chunk_frames : b.n;
   for (uint64_t i0 = lo + (threadIdx.x & ~63u); i0 < hi; i0 += blockDim.x) {   // one 64-frame group per wave
     const uint64_t i = i0 + lane;
     const bool valid = i < hi;
@@ -724,15 +732,21 @@ __global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t 
 // heads (LDS atomics per wave and class).  Per-wave
 // global atomics on the five counters serialised (2-6 ms a batch), and a
 // dependent key read per class probe left the kernel latency-bound.
+// Keys per thread: 64, or fewer (a multiple of 8) so that a smaller batch
+// still gives every CU a workgroup.
 constexpr uint32_t kHeadsPer = 64;
+inline uint32_t heads_per(uint64_t n, uint32_t blk, int num_cus) {
+  const uint64_t p = (n / (uint64_t(blk) * 2 * num_cus) + 7) / 8 * 8;   // two workgroups per CU
+  return static_cast<uint32_t>(p < 8 ? 8 : p > kHeadsPer ? kHeadsPer : p);
+}
 __global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads, uint32_t *nheads,
-                                uint32_t sentinel) {
+                                uint32_t sentinel, uint32_t per) {
   __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
-  const uint64_t lo = uint64_t(blockIdx.x) * kHeadsPer * blockDim.x;
+  const uint64_t lo = uint64_t(blockIdx.x) * per * blockDim.x;
   if (threadIdx.x < kRunClasses) cnt[threadIdx.x] = 0;
   __syncthreads();
   uint32_t mine[kRunClasses] = {};
-  for (uint32_t j = 0; j < kHeadsPer; j += 8) {
+  for (uint32_t j = 0; j < per; j += 8) {
 #pragma unroll
     for (uint32_t u = 0; u < 8; ++u) {
       const uint32_t c = run_class(skeys, n, lo + uint64_t(j + u) * blockDim.x + threadIdx.x, sentinel);
@@ -750,7 +764,7 @@ __global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *hea
   }
   __syncthreads();
   const uint32_t lane = __lane_id();
-  for (uint32_t it = 0; it < kHeadsPer; ++it) {                 // the keys are in L2 now
+  for (uint32_t it = 0; it < per; ++it) {                       // the keys are in L2 now
     const uint64_t q = lo + uint64_t(it) * blockDim.x + threadIdx.x;
     const uint32_t c = run_class(skeys, n, q, sentinel);
 #pragma unroll
@@ -1001,51 +1015,71 @@ __global__ void ct_hard_kernel(CtBatch b, CtTable t, const WalkRec *brec, uint32
 // Parser_dp.c:47-58) and accept-established (ConntrackLabel_dp.c:137-188).
 constexpr uint32_t kCountBlock = 1024;
 constexpr uint32_t kLdsRules = 1024;          // LDS bins per chain; rules above use global atomics
-constexpr uint64_t kCountChunk = 65536;       // packets per workgroup: u32 byte bins cannot wrap
+constexpr uint64_t kCountChunk = 65536;       // packets per workgroup at most: u32 byte bins cannot wrap
+// Packets per workgroup: kCountChunk, or fewer (a multiple of 4 x kCountBlock)
+// so that every CU gets a workgroup (a 2 M-frame batch ran 32 workgroups,
+// 93 us; 256 of them 29 us).
+inline uint64_t count_chunk(uint64_t n, int num_cus) {
+  constexpr uint64_t q = 4 * kCountBlock;
+  const uint64_t c = (n / uint64_t(num_cus) + q - 1) / q * q;   // (two per CU measured slower: 29 -> 36 us)
+  return c < q ? q : c > kCountChunk ? kCountChunk : c;
+}
 
-__global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs) {
+__global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) {
   constexpr uint32_t per = 2 + kLdsRules;
   // groups 0-2: the chains; group 3: Horus rule ids (bins 2..)
   __shared__ uint32_t pk[4 * per], by[4 * per];
   for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) { pk[k] = 0; by[k] = 0; }
   __syncthreads();
-  const uint64_t lo = uint64_t(blockIdx.x) * kCountChunk;
-  const uint64_t hi = lo + kCountChunk < b.n ? lo + kCountChunk : b.n;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const int32_t rid = b.rule_ids[i];
-    const uint32_t lc = lcs[i], len = lc & 0xffff, cinfo = lc >> 16;
-    if (rid <= PCN_IPT_RID_HORUS0) {                  // Horus_dp.c:80-90, counted at the lookup
-      if (!b.horus_ctr) continue;
-      const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
-      if (id >= kLdsRules) {
-        atomicAdd(&b.horus_ctr[2 * id], 1ull);
-        atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(len));
-      } else {
-        atomicAdd(&pk[3 * per + 2 + id], 1u);
-        atomicAdd(&by[3 * per + 2 + id], uint32_t(len));
-      }
-      continue;
+  const uint64_t lo = uint64_t(blockIdx.x) * chunk;
+  const uint64_t hi = lo + chunk < b.n ? lo + chunk : b.n;
+  constexpr uint32_t U = 4;     // packets per thread whose loads are in flight together
+  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
+    int32_t rids[U];
+    uint32_t lcv[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t i = i0 + u * blockDim.x;
+      rids[u] = i < hi ? b.rule_ids[i] : PCN_IPT_RID_NOCHAIN;
+      lcv[u] = i < hi ? lcs[i] : 3u << 16;
     }
-    const uint32_t c = cinfo & 3;
-    if (c == 3) continue;
-    uint32_t bin;
-    if (rid >= 0) {
-      if (uint32_t(rid) >= b.ncounted[c]) continue;
-      if (uint32_t(rid) >= kLdsRules) {
-        atomicAdd(&b.ctr[c][2 + 2 * uint64_t(rid)], 1ull);
-        atomicAdd(&b.ctr[c][3 + 2 * uint64_t(rid)], static_cast<unsigned long long>(len));
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const int32_t rid = rids[u];
+      const uint32_t lc = lcv[u], len = lc & 0xffff, cinfo = lc >> 16;
+      if (rid <= PCN_IPT_RID_HORUS0) {                  // Horus_dp.c:80-90, counted at the lookup
+        if (!b.horus_ctr) continue;
+        const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
+        if (id >= kLdsRules) {
+          atomicAdd(&b.horus_ctr[2 * id], 1ull);
+          atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(len));
+        } else {
+          atomicAdd(&pk[3 * per + 2 + id], 1u);
+          atomicAdd(&by[3 * per + 2 + id], uint32_t(len));
+        }
         continue;
       }
-      bin = 2 + uint32_t(rid);
-    } else if (rid == PCN_IPT_RID_DEFAULT) {
-      bin = 0;
-    } else if (rid == -3) {
-      bin = 1;
-    } else {
-      continue;
+      const uint32_t c = cinfo & 3;
+      if (c == 3) continue;
+      uint32_t bin;
+      if (rid >= 0) {
+        if (uint32_t(rid) >= b.ncounted[c]) continue;
+        if (uint32_t(rid) >= kLdsRules) {
+          atomicAdd(&b.ctr[c][2 + 2 * uint64_t(rid)], 1ull);
+          atomicAdd(&b.ctr[c][3 + 2 * uint64_t(rid)], static_cast<unsigned long long>(len));
+          continue;
+        }
+        bin = 2 + uint32_t(rid);
+      } else if (rid == PCN_IPT_RID_DEFAULT) {
+        bin = 0;
+      } else if (rid == -3) {
+        bin = 1;
+      } else {
+        continue;
+      }
+      atomicAdd(&pk[c * per + bin], 1u);
+      atomicAdd(&by[c * per + bin], uint32_t(len));
     }
-    atomicAdd(&pk[c * per + bin], 1u);
-    atomicAdd(&by[c * per + bin], uint32_t(len));
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) {
@@ -1266,10 +1300,13 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipMemsetAsync(s.hard_cnt, 0, 4, st));
   CT_CHECK(hipMemsetAsync(s.hard_cnt + 8, 0, 4, st));
   CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
-  const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + kPrepChunk - 1) / kPrepChunk));
+  const uint32_t pchunk = prep_chunk(b.n, num_cus);
+  const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
   hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(blk), 0, st, b, t.carry, s.brec, s.lcs, s.keys, s.idx, kbits,
-                     s.hard_cnt, s.hard_list, s.pdesc, s.hard_cnt + 8);
+                     s.hard_cnt, s.hard_list, s.pdesc, s.hard_cnt + 8, pchunk);
   CT_CHECK(hipGetLastError());
+  // (a carry written by ct_prep's last workgroup, as classify does, put
+  // ct_prep's 18-dword parse window in scratch: 0.68 -> 0.91 ms; not kept)
   CT_CHECK(ct_advance_carry(b, s, t.carry, num_cus, stream));
   size_t tb;
   tb = s.temp_bytes;
@@ -1280,8 +1317,9 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
     CT_CHECK(hipGetLastError());
   }
   const RecSrc src{PCN_CT_GATHER ? s.wrec : s.brec, s.idx2};
-  hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + kHeadsPer * blk - 1) / (kHeadsPer * blk))),
-                     dim3(blk), 0, st, b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel);
+  const uint32_t hper = heads_per(b.n, blk, num_cus);
+  hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + uint64_t(hper) * blk - 1) / (uint64_t(hper) * blk))),
+                     dim3(blk), 0, st, b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel, hper);
   CT_CHECK(hipGetLastError());
   uint32_t cnt[1 + kRunClasses] = {};
   CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
@@ -1318,8 +1356,9 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
     hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
     CT_CHECK(hipGetLastError());
   }
-  const unsigned cgrid = static_cast<unsigned>((b.n + kCountChunk - 1) / kCountChunk);
-  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs);
+  const uint64_t cchunk = count_chunk(b.n, num_cus);
+  const unsigned cgrid = static_cast<unsigned>((b.n + cchunk - 1) / cchunk);
+  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs, cchunk);
   CT_CHECK(hipGetLastError());
   return hipSuccess;
 }
