@@ -1191,9 +1191,16 @@ void ct_table_free(CtTable &t) {
 #ifndef PCN_CT_RADIX_BITS
 #define PCN_CT_RADIX_BITS 9   // A/B 8 / 9 / 11: 0.54 / 0.41 / 0.52 ms a 2^24 batch
 #endif
+#ifndef PCN_CT_SORT_BLOCK
+#define PCN_CT_SORT_BLOCK 1024
+#endif
+#ifndef PCN_CT_SORT_ITEMS
+#define PCN_CT_SORT_ITEMS 8    // A/B 16 / 12 / 8 items per thread: 3.13 / 3.13 / 2.98 ms a 2^24 batch (16 and 12 use scratch)
+#endif
 using CtSortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<PCN_CT_SORT_BLOCK, PCN_CT_SORT_ITEMS>,
+                                        rocprim::kernel_config<PCN_CT_SORT_BLOCK, PCN_CT_SORT_ITEMS>,
                                         PCN_CT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
 static hipError_t sort_pairs(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                              uint32_t *vout, uint64_t n, uint32_t kbits, hipStream_t st) {
