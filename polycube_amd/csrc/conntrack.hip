@@ -1015,7 +1015,8 @@ __global__ void ct_hard_kernel(CtBatch b, CtTable t, const WalkRec *brec, uint32
 // Parser_dp.c:47-58) and accept-established (ConntrackLabel_dp.c:137-188).
 constexpr uint32_t kCountBlock = 1024;
 constexpr uint32_t kLdsRules = 1024;          // LDS bins per chain; rules above use global atomics
-constexpr uint64_t kCountChunk = 65536;       // packets per workgroup at most: u32 byte bins cannot wrap
+constexpr uint64_t kCountChunk = 65536;       // packets per workgroup at most: packed bins cannot carry
+static_assert(kCountChunk * 65535 < (1ull << 40) && kCountChunk < (1ull << 24), "ct_count packed bins");
 // Packets per workgroup: kCountChunk, or fewer (a multiple of 4 x kCountBlock)
 // so that every CU gets a workgroup (a 2 M-frame batch ran 32 workgroups,
 // 93 us; 256 of them 29 us).
@@ -1027,9 +1028,11 @@ inline uint64_t count_chunk(uint64_t n, int num_cus) {
 
 __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) {
   constexpr uint32_t per = 2 + kLdsRules;
-  // groups 0-2: the chains; group 3: Horus rule ids (bins 2..)
-  __shared__ uint32_t pk[4 * per], by[4 * per];
-  for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) { pk[k] = 0; by[k] = 0; }
+  // groups 0-2: the chains; group 3: Horus rule ids (bins 2..).  One u64 LDS
+  // atomic per packet: pkts in bits 40-63, bytes in bits 0-39 (a workgroup's
+  // <= 2^16 packets of <= 65535 bytes cannot carry out of either field).
+  __shared__ unsigned long long bins[4 * per];
+  for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) bins[k] = 0;
   __syncthreads();
   const uint64_t lo = uint64_t(blockIdx.x) * chunk;
   const uint64_t hi = lo + chunk < b.n ? lo + chunk : b.n;
@@ -1054,8 +1057,7 @@ __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) 
           atomicAdd(&b.horus_ctr[2 * id], 1ull);
           atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(len));
         } else {
-          atomicAdd(&pk[3 * per + 2 + id], 1u);
-          atomicAdd(&by[3 * per + 2 + id], uint32_t(len));
+          atomicAdd(&bins[3 * per + 2 + id], (1ull << 40) | len);
         }
         continue;
       }
@@ -1077,21 +1079,21 @@ __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) 
       } else {
         continue;
       }
-      atomicAdd(&pk[c * per + bin], 1u);
-      atomicAdd(&by[c * per + bin], uint32_t(len));
+      atomicAdd(&bins[c * per + bin], (1ull << 40) | len);
     }
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) {
-    if (!pk[k]) continue;
+    const unsigned long long v = bins[k];
+    if (!v) continue;
     const uint32_t c = k / per, bin = k % per;
     unsigned long long *dp, *db;
     if (c == 3) { dp = &b.horus_ctr[2 * (bin - 2)]; db = &b.horus_ctr[2 * (bin - 2) + 1]; }
     else if (bin == 0) { dp = &b.ctr[c][0]; db = &b.ctr[c][1]; }
     else if (bin == 1) { dp = &b.ae_ctr[2 * c]; db = &b.ae_ctr[2 * c + 1]; }
     else { dp = &b.ctr[c][2 + 2 * (bin - 2)]; db = &b.ctr[c][3 + 2 * (bin - 2)]; }
-    atomicAdd(dp, static_cast<unsigned long long>(pk[k]));
-    atomicAdd(db, static_cast<unsigned long long>(by[k]));
+    atomicAdd(dp, v >> 40);
+    atomicAdd(db, v & ((1ull << 40) - 1));
   }
 }
 
