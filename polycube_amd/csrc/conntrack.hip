@@ -237,13 +237,28 @@ __device__ uint32_t ports_lookback(const unsigned long long *desc, uint64_t g, c
 
 // Chain selection (ChainSelector_dp.c:131-298), the conntrack key and kind;
 // packets that need no table access get their final outcome here.
-__global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, uint32_t *lcs, uint32_t *keys,
+// PCN_CT_PREP_LDS: a wave whose 64 frames sit at a 64-byte stride (the
+// fixed-stride batch) loads them as coalesced 16-byte chunks and transposes
+// them through LDS into per-lane windows, and writes its 64 walk records back
+// the same way, instead of one lane per 76-byte window / 64-byte record (every
+// wave instruction then touching 64 lines).
+#ifndef PCN_CT_PREP_LDS
+#define PCN_CT_PREP_LDS 1
+#endif
+constexpr uint32_t kPrepBlock = 256;
+constexpr uint32_t kPrepRow = 5;                 // 16-byte chunks per frame row in LDS (4 + 1 of padding)
+__global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, uint32_t *lcs, uint32_t *keys,
                                uint32_t *idx,
                                uint32_t kbits, uint32_t *hard_cnt, uint32_t *hard_list, unsigned long long *desc,
                                uint32_t *chunk_ctr, uint32_t chunk_frames) {
   const uint32_t sentinel = (1u << kbits) - 1;
   const uint32_t lane = __lane_id();
   __shared__ uint32_t chunk;
+#if PCN_CT_PREP_LDS
+  __shared__ ct_u32x4 prep_stage[(kPrepBlock / 64) * 65 * kPrepRow];
+  ct_u32x4 *const stage = prep_stage + (threadIdx.x >> 6) * 65 * kPrepRow;
+  const bool stride64 = !b.offsets && b.stride == 64 && (reinterpret_cast<uintptr_t>(b.frames) & 15) == 0;
+#endif
   for (;;) {
     if (threadIdx.x == 0) chunk = atomicAdd(chunk_ctr, 1u);
     __syncthreads();
@@ -255,7 +270,43 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, 
     const uint64_t i = i0 + lane;
     const bool valid = i < hi;
     uint32_t w[18], L;
+#if PCN_CT_PREP_LDS
+    // the group's 64 frames and the next frame's first chunk inside the buffer (wave-uniform)
+    const bool fast = stride64 && (i0 + 64) * 64 + 16 <= b.frames_bytes;
+    if (fast) {
+      const ct_u32x4 *src = reinterpret_cast<const ct_u32x4 *>(b.frames + i0 * 64);
+      ct_u32x4 c[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) c[q] = src[q * 64 + lane];   // chunk t = 64 q + lane: frame t / 4
+      const ct_u32x4 extra = src[256];                               // the next frame's bytes 0-15
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t t = q * 64 + lane;
+        stage[(t >> 2) * kPrepRow + (t & 3)] = c[q];
+      }
+      if (lane == 0) stage[64 * kPrepRow] = extra;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const ct_u32x4 *row = stage + lane * kPrepRow;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        const ct_u32x4 v = row[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+      }
+      const ct_u32x4 nx = row[kPrepRow];
+      w[16] = nx.x;
+      w[17] = nx.y;
+      L = b.lens ? b.lens[valid ? i : hi - 1] : b.fixed_len;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      load_window(b, valid ? i : hi - 1, w, L);
+    }
+#else
     load_window(b, valid ? i : hi - 1, w, L);
+#endif
     const Parsed p = parse(w, L, b.hook);
     // ---- the shared `packet` struct's ports as this frame sees them ----
     const uint32_t own = uint32_t(p.sport) | (uint32_t(p.dport) << 16);
@@ -274,104 +325,135 @@ __global__ void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, 
       if (!wm && lane == 0)
         __hip_atomic_store(&desc[g], ports_word(kStIncl, cin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!valid) continue;
-    CtRec r{};
-    r.len = static_cast<uint16_t>(p.L);
-    r.kind = K_NONE;
-    uint32_t chain = 3;
-    bool pass = false;
-    if (p.status == 2) {
-      bool labeled = true;
-      // a Horus hit (stage A found it: the same for every label) skips the
-      // ChainSelector / ChainForwarder: DROP is final, ACCEPT is PASS_LABELING
-      // (Horus_dp.c:150-160; Firewall_Horus_dp.c:151-161), or final for a
-      // pcn-firewall program built with conntrack off (:162-164)
-      const bool horus = b.a_rid[i] <= PCN_IPT_RID_HORUS0;
-      if (horus) {
-        if (b.a_verdict[i] == PCN_IPT_ACCEPT && !b.horus_final) pass = true;
-        else labeled = false;
-      } else if (b.fw) {
-        // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder
-        // (Firewall_ChainForwarder_dp.c:20-42).  An empty chain goes to
-        // DefaultAction after labelling, which stage A already resolved.
-        chain = b.direction == PCN_IPT_INGRESS ? PCN_IPT_FORWARD : PCN_IPT_OUTPUT;
-      } else if (b.direction == PCN_IPT_INGRESS) {
-        if (b.allow_logic) pass = true;
-        else chain = (b.nlocal && localip_has(b, p.dst)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
-      } else if (b.nlocal && localip_has(b, p.src)) {
-        chain = PCN_IPT_OUTPUT;
-      } else {
-        labeled = false;                                   // egress PASS, no labeling
-      }
-      if (!b.fw && labeled && chain < 3 && ((b.empty_mask >> chain) & 1)) {
-        if ((b.drop_mask >> chain) & 1) labeled = false;  // DROP_NO_LABELING (default counters)
-        else pass = true;                                  // PASS_LABELING
-      }
-      if (labeled) {
-        // the shared `packet` struct: ports stale for anything but TCP/UDP (Q4)
-        const uint32_t ports = p.ports_ok ? own : stale;
-        const uint16_t sp = static_cast<uint16_t>(ports & 0xffff), dp = static_cast<uint16_t>(ports >> 16);
-        // ConntrackLabel_dp.c:200-228
-        uint8_t ipRev, portRev;
-        if (p.src <= p.dst) { r.src = p.src; r.dst = p.dst; ipRev = 0; }
-        else { r.src = p.dst; r.dst = p.src; ipRev = 1; }
-        if (sp < dp) { r.sport = sp; r.dport = dp; portRev = 0; }
-        else if (sp > dp) { r.sport = dp; r.dport = sp; portRev = 1; }
-        else { r.sport = sp; r.dport = dp; portRev = ipRev; }
-        r.proto = p.proto;
-        r.rev = static_cast<uint8_t>(ipRev | (portRev << 1));
-        r.seq = p.seq;
-        r.ack = p.ack;
-        r.flags = p.flags;
-        r.icmp = p.icmp;
-        if (p.proto == 6) r.kind = K_TCP;
-        else if (p.proto == 17) r.kind = K_UDP;
-        else if (p.proto == 1) {
-          if (p.L < 42) r.kind = K_NONE;                   // RX_DROP (:441-443)
-          else if (p.icmp == 8) r.kind = K_ECHO;
-          else if (p.icmp == 0) r.kind = p.L >= 70 ? K_HARD : K_REPLY;
-          else if (p.icmp >= 13 && p.icmp <= 18) r.kind = K_INV;
-          else if (p.L < 70) r.kind = K_NONE;              // RX_DROP (:486-505)
-          else r.kind = K_ERR;
-          if (r.kind == K_ERR || r.kind == K_HARD) {      // the quoted header's key (:491-529)
-            const uint32_t qs = p.isrc <= p.idst ? p.isrc : p.idst, qd = p.isrc <= p.idst ? p.idst : p.isrc;
-            const uint16_t qa = p.isport <= p.idport ? p.isport : p.idport;
-            const uint16_t qb = p.isport <= p.idport ? p.idport : p.isport;
-            if (r.kind == K_ERR) {
-              r.src = qs; r.dst = qd; r.sport = qa; r.dport = qb; r.proto = p.iproto;
-            } else {
-              r.seq = qs; r.ack = qd; r.flags = p.iproto; r.iports = uint32_t(qa) | (uint32_t(qb) << 16);
-            }
-          }
+    WalkRec wr;
+    if (valid) {
+      CtRec r{};
+      r.len = static_cast<uint16_t>(p.L);
+      r.kind = K_NONE;
+      uint32_t chain = 3;
+      bool pass = false;
+      if (p.status == 2) {
+        bool labeled = true;
+        // a Horus hit (stage A found it: the same for every label) skips the
+        // ChainSelector / ChainForwarder: DROP is final, ACCEPT is PASS_LABELING
+        // (Horus_dp.c:150-160; Firewall_Horus_dp.c:151-161), or final for a
+        // pcn-firewall program built with conntrack off (:162-164)
+        const bool horus = b.a_rid[i] <= PCN_IPT_RID_HORUS0;
+        if (horus) {
+          if (b.a_verdict[i] == PCN_IPT_ACCEPT && !b.horus_final) pass = true;
+          else labeled = false;
+        } else if (b.fw) {
+          // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder
+          // (Firewall_ChainForwarder_dp.c:20-42).  An empty chain goes to
+          // DefaultAction after labelling, which stage A already resolved.
+          chain = b.direction == PCN_IPT_INGRESS ? PCN_IPT_FORWARD : PCN_IPT_OUTPUT;
+        } else if (b.direction == PCN_IPT_INGRESS) {
+          if (b.allow_logic) pass = true;
+          else chain = (b.nlocal && localip_has(b, p.dst)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
+        } else if (b.nlocal && localip_has(b, p.src)) {
+          chain = PCN_IPT_OUTPUT;
         } else {
-          r.kind = K_INV;                                  // :562-566
+          labeled = false;                                   // egress PASS, no labeling
+        }
+        if (!b.fw && labeled && chain < 3 && ((b.empty_mask >> chain) & 1)) {
+          if ((b.drop_mask >> chain) & 1) labeled = false;  // DROP_NO_LABELING (default counters)
+          else pass = true;                                  // PASS_LABELING
+        }
+        if (labeled) {
+          // the shared `packet` struct: ports stale for anything but TCP/UDP (Q4)
+          const uint32_t ports = p.ports_ok ? own : stale;
+          const uint16_t sp = static_cast<uint16_t>(ports & 0xffff), dp = static_cast<uint16_t>(ports >> 16);
+          // ConntrackLabel_dp.c:200-228
+          uint8_t ipRev, portRev;
+          if (p.src <= p.dst) { r.src = p.src; r.dst = p.dst; ipRev = 0; }
+          else { r.src = p.dst; r.dst = p.src; ipRev = 1; }
+          if (sp < dp) { r.sport = sp; r.dport = dp; portRev = 0; }
+          else if (sp > dp) { r.sport = dp; r.dport = sp; portRev = 1; }
+          else { r.sport = sp; r.dport = dp; portRev = ipRev; }
+          r.proto = p.proto;
+          r.rev = static_cast<uint8_t>(ipRev | (portRev << 1));
+          r.seq = p.seq;
+          r.ack = p.ack;
+          r.flags = p.flags;
+          r.icmp = p.icmp;
+          if (p.proto == 6) r.kind = K_TCP;
+          else if (p.proto == 17) r.kind = K_UDP;
+          else if (p.proto == 1) {
+            if (p.L < 42) r.kind = K_NONE;                   // RX_DROP (:441-443)
+            else if (p.icmp == 8) r.kind = K_ECHO;
+            else if (p.icmp == 0) r.kind = p.L >= 70 ? K_HARD : K_REPLY;
+            else if (p.icmp >= 13 && p.icmp <= 18) r.kind = K_INV;
+            else if (p.L < 70) r.kind = K_NONE;              // RX_DROP (:486-505)
+            else r.kind = K_ERR;
+            if (r.kind == K_ERR || r.kind == K_HARD) {      // the quoted header's key (:491-529)
+              const uint32_t qs = p.isrc <= p.idst ? p.isrc : p.idst, qd = p.isrc <= p.idst ? p.idst : p.isrc;
+              const uint16_t qa = p.isport <= p.idport ? p.isport : p.idport;
+              const uint16_t qb = p.isport <= p.idport ? p.idport : p.isport;
+              if (r.kind == K_ERR) {
+                r.src = qs; r.dst = qd; r.sport = qa; r.dport = qb; r.proto = p.iproto;
+              } else {
+                r.seq = qs; r.ack = qd; r.flags = p.iproto; r.iports = uint32_t(qa) | (uint32_t(qb) << 16);
+              }
+            }
+          } else {
+            r.kind = K_INV;                                  // :562-566
+          }
         }
       }
+      r.cinfo = static_cast<uint8_t>((chain & 3) | (pass ? 4 : 0));
+      idx[i] = static_cast<uint32_t>(i);
+      const bool member = r.kind >= K_TCP && r.kind <= K_ERR;
+      const uint32_t key = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
+                                  : sentinel;
+      keys[i] = key;
+      lcs[i] = uint32_t(r.len) | uint32_t(r.cinfo) << 16;   // what ct_count reads (not the 64-byte record)
+      wr.r = r;
+      wr.key = key;
+      wr.idx = static_cast<uint32_t>(i);
+      wr.o0 = pack_outcome(b, 0, i);
+      wr.o1 = pack_outcome(b, 1, i);
+      wr.o2 = pack_outcome(b, 2, i);
+      wr.o3 = pack_outcome(b, 3, i);
+      wr.pad[0] = wr.pad[1] = 0;
+#if PCN_CT_PREP_LDS
+      if (fast) {                                       // this lane's record into its LDS row
+        union {
+          ct_u32x4 v[4];
+          WalkRec rec;
+        } u;
+        u.rec = wr;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) stage[lane * kPrepRow + k] = u.v[k];
+      } else {
+        store_rec(&brec[i], wr);
+      }
+#else
+      store_rec(&brec[i], wr);
+#endif
+      if (r.kind == K_HARD) hard_list[atomicAdd(hard_cnt, 1u)] = static_cast<uint32_t>(i);
+      if (!member && r.kind != K_HARD) {
+        // no table access: the outcome of label INVALID (K_INV) or of any label
+        const uint32_t l = (r.kind == K_INV && !pass && b.nlab == 4) ? 3u : 0u;
+        b.verdicts[i] = b.a_verdict[l * b.n + i];
+        b.rule_ids[i] = b.a_rid[l * b.n + i];
+      }
     }
-    r.cinfo = static_cast<uint8_t>((chain & 3) | (pass ? 4 : 0));
-    idx[i] = static_cast<uint32_t>(i);
-    const bool member = r.kind >= K_TCP && r.kind <= K_ERR;
-    const uint32_t key = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
-                                : sentinel;
-    keys[i] = key;
-    lcs[i] = uint32_t(r.len) | uint32_t(r.cinfo) << 16;   // what ct_count reads (not the 64-byte record)
-    WalkRec wr;
-    wr.r = r;
-    wr.key = key;
-    wr.idx = static_cast<uint32_t>(i);
-    wr.o0 = pack_outcome(b, 0, i);
-    wr.o1 = pack_outcome(b, 1, i);
-    wr.o2 = pack_outcome(b, 2, i);
-    wr.o3 = pack_outcome(b, 3, i);
-    wr.pad[0] = wr.pad[1] = 0;
-    store_rec(&brec[i], wr);
-    if (r.kind == K_HARD) hard_list[atomicAdd(hard_cnt, 1u)] = static_cast<uint32_t>(i);
-    if (!member && r.kind != K_HARD) {
-      // no table access: the outcome of label INVALID (K_INV) or of any label
-      const uint32_t l = (r.kind == K_INV && !pass && b.nlab == 4) ? 3u : 0u;
-      b.verdicts[i] = b.a_verdict[l * b.n + i];
-      b.rule_ids[i] = b.a_rid[l * b.n + i];
+#if PCN_CT_PREP_LDS
+    if (fast) {                                         // the wave's records as coalesced chunks
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      ct_u32x4 *dst = reinterpret_cast<ct_u32x4 *>(brec + i0);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t t = q * 64 + lane;
+        if (i0 + (t >> 2) < hi) dst[t] = stage[(t >> 2) * kPrepRow + (t & 3)];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+#endif
   }
   }
 }
@@ -1311,7 +1393,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
   const uint32_t pchunk = prep_chunk(b.n, num_cus);
   const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
-  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(blk), 0, st, b, t.carry, s.brec, s.lcs, s.keys, s.idx, kbits,
+  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.lcs, s.keys, s.idx, kbits,
                      s.hard_cnt, s.hard_list, s.pdesc, s.hard_cnt + 8, pchunk);
   CT_CHECK(hipGetLastError());
   // (a carry written by ct_prep's last workgroup, as classify does, put
