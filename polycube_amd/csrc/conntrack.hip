@@ -1388,8 +1388,10 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint32_t sentinel = (1u << kbits) - 1;
   CT_CHECK(grow(s, b.n, kbits, st));
   const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
-  CT_CHECK(hipMemsetAsync(s.hard_cnt, 0, 4, st));
-  CT_CHECK(hipMemsetAsync(s.hard_cnt + 8, 0, 4, st));
+  // one memset for the long-echo-reply count [0], the run counts per class
+  // [1..5] (ct_heads) and ct_prep's chunk counter [8]: each memset is a
+  // launch of its own (~5 us between kernels)
+  CT_CHECK(hipMemsetAsync(s.hard_cnt, 0, 64, st));
   CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
   const uint32_t pchunk = prep_chunk(b.n, num_cus);
   const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
@@ -1402,7 +1404,6 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   size_t tb;
   tb = s.temp_bytes;
   CT_CHECK(sort_pairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, b.n, kbits, st));
-  CT_CHECK(hipMemsetAsync(s.hard_cnt + 1, 0, 4 * kRunClasses, st));
   if (PCN_CT_GATHER) {
     hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec, sentinel);
     CT_CHECK(hipGetLastError());
