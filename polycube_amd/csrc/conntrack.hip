@@ -790,16 +790,6 @@ __host__ __device__ constexpr uint64_t class_off(uint64_t n, uint32_t c) {
 }
 __host__ __device__ constexpr uint64_t heads_cap(uint64_t n) { return class_off(n, kRunClasses); }
 
-// The run class of sorted position q (kRunClasses: not a run head).  All six
-// key reads are issued unconditionally so they are in flight together.
-__device__ __forceinline__ uint32_t run_class(const uint32_t *skeys, uint64_t n, uint64_t q, uint32_t sentinel) {
-  auto at = [&](uint64_t j) { return j < n ? skeys[j] : 0xffffffffu; };   // never a key: kbits <= 30
-  const uint32_t k = at(q), km = q ? at(q - 1) : 0xffffffffu;
-  const uint32_t k1 = at(q + 1), k7 = at(q + 7), k63 = at(q + 63), kl = at(q + kLongRun);
-  if (q >= n || k == sentinel || km == k) return kRunClasses;
-  return kl == k ? 0 : k63 == k ? 1 : k7 == k ? 2 : k1 == k ? 3 : 4;   // more than kLongRun / 63 / 7 / 1 packets
-}
-
 __global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t *skeys, const uint32_t *sidx,
                                  WalkRec *wrec, uint32_t sentinel) {
   const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
@@ -807,34 +797,45 @@ __global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t 
     if (skeys[q] != sentinel) store_rec(&wrec[q], load_rec(&brec[sidx[q]]));
 }
 
-// The run heads of each class.  A workgroup takes a contiguous range of
-// kHeadsPer x blockDim sorted keys, counts its heads per class (eight
-// classifications' key reads in flight per lane), reserves its places with
-// one global atomic per class, then classifies again (from L2) and writes the
-// heads (LDS atomics per wave and class).  Per-wave
-// global atomics on the five counters serialised (2-6 ms a batch), and a
-// dependent key read per class probe left the kernel latency-bound.
-// Keys per thread: 64, or fewer (a multiple of 8) so that a smaller batch
-// still gives every CU a workgroup.
-constexpr uint32_t kHeadsPer = 64;
-inline uint32_t heads_per(uint64_t n, uint32_t blk, int num_cus) {
-  const uint64_t p = (n / (uint64_t(blk) * 2 * num_cus) + 7) / 8 * 8;   // two workgroups per CU
-  return static_cast<uint32_t>(p < 8 ? 8 : p > kHeadsPer ? kHeadsPer : p);
+// The run heads of each class.  A workgroup stages a contiguous tile of
+// `per` x kHeadsBlock sorted keys (plus the key before it and kLongRun
+// after it) in LDS with coalesced loads, counts its heads per class,
+// reserves its places with one global atomic per class, then classifies again
+// from LDS and writes the heads (LDS atomics per wave and class).  Per-wave
+// global atomics on the five counters serialised (2-6 ms a batch); reading
+// the six keys of a classification from L2, twice, cost 95 us a 2^24 batch.
+// Keys per thread: 16, or fewer (a multiple of 4) so that a smaller batch
+// still gives every CU two workgroups.
+constexpr uint32_t kHeadsBlock = 256;
+constexpr uint32_t kHeadsPer = 16;
+inline uint32_t heads_per(uint64_t n, int num_cus) {
+  const uint64_t p = (n / (uint64_t(kHeadsBlock) * 2 * num_cus) + 3) / 4 * 4;
+  return static_cast<uint32_t>(p < 4 ? 4 : p > kHeadsPer ? kHeadsPer : p);
 }
-__global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads, uint32_t *nheads,
-                                uint32_t sentinel, uint32_t per) {
+__global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads,
+                                                               uint32_t *nheads, uint32_t sentinel, uint32_t per) {
   __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
-  const uint64_t lo = uint64_t(blockIdx.x) * per * blockDim.x;
+  __shared__ uint32_t tile[kHeadsPer * kHeadsBlock + kLongRun + 1];   // keys [lo - 1, lo + T + kLongRun)
+  const uint32_t T = per * kHeadsBlock;
+  const uint64_t lo = uint64_t(blockIdx.x) * T;
   if (threadIdx.x < kRunClasses) cnt[threadIdx.x] = 0;
+  for (uint32_t j = threadIdx.x; j < T + kLongRun + 1; j += kHeadsBlock) {
+    const uint64_t q = lo + j;                     // tile[j] = key at q - 1 (never a key past the ends)
+    tile[j] = q >= 1 && q - 1 < n ? skeys[q - 1] : 0xffffffffu;
+  }
   __syncthreads();
+  // the class of tile position r (sorted position lo + r); kRunClasses: not a run head
+  auto run_class_lds = [&](uint32_t r) -> uint32_t {
+    const uint32_t k = tile[r + 1], km = tile[r];
+    const uint32_t k1 = tile[r + 2], k7 = tile[r + 8], k63 = tile[r + 64], kl = tile[r + 1 + kLongRun];
+    if (lo + r >= n || k == sentinel || km == k) return kRunClasses;
+    return kl == k ? 0 : k63 == k ? 1 : k7 == k ? 2 : k1 == k ? 3 : 4;   // more than kLongRun / 63 / 7 / 1 packets
+  };
   uint32_t mine[kRunClasses] = {};
-  for (uint32_t j = 0; j < per; j += 8) {
+  for (uint32_t j = 0; j < per; ++j) {
+    const uint32_t c = run_class_lds(j * kHeadsBlock + threadIdx.x);
 #pragma unroll
-    for (uint32_t u = 0; u < 8; ++u) {
-      const uint32_t c = run_class(skeys, n, lo + uint64_t(j + u) * blockDim.x + threadIdx.x, sentinel);
-#pragma unroll
-      for (uint32_t k = 0; k < kRunClasses; ++k) mine[k] += c == k;
-    }
+    for (uint32_t k = 0; k < kRunClasses; ++k) mine[k] += c == k;
   }
 #pragma unroll
   for (uint32_t k = 0; k < kRunClasses; ++k)
@@ -846,9 +847,10 @@ __global__ void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *hea
   }
   __syncthreads();
   const uint32_t lane = __lane_id();
-  for (uint32_t it = 0; it < per; ++it) {                       // the keys are in L2 now
-    const uint64_t q = lo + uint64_t(it) * blockDim.x + threadIdx.x;
-    const uint32_t c = run_class(skeys, n, q, sentinel);
+  for (uint32_t it = 0; it < per; ++it) {
+    const uint32_t r = it * kHeadsBlock + threadIdx.x;
+    const uint64_t q = lo + r;
+    const uint32_t c = run_class_lds(r);
 #pragma unroll
     for (uint32_t k = 0; k < kRunClasses; ++k) {
       const uint64_t m = __ballot(c == k);
@@ -1409,9 +1411,10 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
     CT_CHECK(hipGetLastError());
   }
   const RecSrc src{PCN_CT_GATHER ? s.wrec : s.brec, s.idx2};
-  const uint32_t hper = heads_per(b.n, blk, num_cus);
-  hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + uint64_t(hper) * blk - 1) / (uint64_t(hper) * blk))),
-                     dim3(blk), 0, st, b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel, hper);
+  const uint32_t hper = heads_per(b.n, num_cus);
+  const uint64_t htile = uint64_t(hper) * kHeadsBlock;
+  hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
+                     b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel, hper);
   CT_CHECK(hipGetLastError());
   uint32_t cnt[1 + kRunClasses] = {};
   CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
