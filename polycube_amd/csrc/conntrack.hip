@@ -812,9 +812,19 @@ inline uint32_t heads_per(uint64_t n, int num_cus) {
   const uint64_t p = (n / (uint64_t(kHeadsBlock) * 2 * num_cus) + 3) / 4 * 4;
   return static_cast<uint32_t>(p < 4 ? 4 : p > kHeadsPer ? kHeadsPer : p);
 }
+// Workgroup 0 also advances the carry (the ports the batch leaves to the
+// next one, Q4): ct_prep's groups are all published by now, so a look-back
+// from the batch end gives the ports of its last frame the Parser wrote them
+// for, or the old carry.  (Two tail kernels and a memset did this, ~27 us a
+// batch; ct_prep itself doing it put its parse window in scratch.)
 __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads,
-                                                               uint32_t *nheads, uint32_t sentinel, uint32_t per) {
+                                                               uint32_t *nheads, uint32_t sentinel, uint32_t per,
+                                                               const unsigned long long *desc, uint32_t *carry) {
   __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    const uint32_t c = ports_lookback(desc, (n + 63) / 64, carry);
+    if (threadIdx.x == 0) *carry = c;
+  }
   __shared__ uint32_t tile[kHeadsPer * kHeadsBlock + kLongRun + 1];   // keys [lo - 1, lo + T + kLongRun)
   const uint32_t T = per * kHeadsBlock;
   const uint64_t lo = uint64_t(blockIdx.x) * T;
@@ -1400,9 +1410,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.lcs, s.keys, s.idx, kbits,
                      s.hard_cnt, s.hard_list, s.pdesc, s.hard_cnt + 8, pchunk);
   CT_CHECK(hipGetLastError());
-  // (a carry written by ct_prep's last workgroup, as classify does, put
-  // ct_prep's 18-dword parse window in scratch: 0.68 -> 0.91 ms; not kept)
-  CT_CHECK(ct_advance_carry(b, s, t.carry, num_cus, stream));
+  // (ct_heads advances the carry from ct_prep's published groups)
   size_t tb;
   tb = s.temp_bytes;
   CT_CHECK(sort_pairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, b.n, kbits, st));
@@ -1414,7 +1422,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
-                     b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel, hper);
+                     b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel, hper, s.pdesc, t.carry);
   CT_CHECK(hipGetLastError());
   uint32_t cnt[1 + kRunClasses] = {};
   CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
