@@ -1239,6 +1239,7 @@ struct CtScratch {
   size_t temp_bytes = 0;
   // ct_advance_carry: 1 + the batch's last port-writing frame
   unsigned long long *zfound = nullptr;
+  uint32_t *h_cnt = nullptr;   // pinned host copy of hard_cnt[0..5] (a pageable target is staged: a slower read-back)
 };
 
 CtScratch *ct_scratch_new() { return new CtScratch(); }
@@ -1252,6 +1253,7 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
                   static_cast<void *>(s->zfound)})
     if (p) (void)hipFree(p);
+  if (s->h_cnt) (void)hipHostFree(s->h_cnt);
   delete s;
 }
 
@@ -1424,9 +1426,11 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
                      b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel, hper, s.pdesc, t.carry);
   CT_CHECK(hipGetLastError());
-  uint32_t cnt[1 + kRunClasses] = {};
-  CT_CHECK(hipMemcpyAsync(cnt, s.hard_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
+  if (!s.h_cnt) CT_CHECK(hipHostMalloc(reinterpret_cast<void **>(&s.h_cnt), 64, hipHostMallocDefault));
+  CT_CHECK(hipMemcpyAsync(s.h_cnt, s.hard_cnt, 4 * (1 + kRunClasses), hipMemcpyDeviceToHost, st));
   CT_CHECK(hipStreamSynchronize(st));
+  uint32_t cnt[1 + kRunClasses];
+  for (uint32_t c = 0; c <= kRunClasses; ++c) cnt[c] = s.h_cnt[c];
   const uint32_t nhard = cnt[0];
   std::vector<uint32_t> hard(nhard);
   if (nhard) {
