@@ -767,6 +767,9 @@ __device__ __forceinline__ int32_t step(const CtBatch &b, const CtTable &t, Cach
 
 // After the sort: walk records in sorted order (each walking lane then reads
 // consecutive lines) and the list of run heads.
+#ifndef PCN_CT_DBG
+#define PCN_CT_DBG 0   // measurement builds only: walk_long prints its round counts for long runs
+#endif
 #ifndef PCN_CT_LONG_RUN
 #define PCN_CT_LONG_RUN 128
 #endif
@@ -940,6 +943,9 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   int cur = 0;
+#if PCN_CT_DBG
+  uint32_t dbg_chunks = 0, dbg_rounds = 0, dbg_changes = 0, dbg_steps = 0, dbg_recs = 0;
+#endif
   for (;;) {
     const WalkRec nx = load_rec(&wrec.rec[nidx]);
     nidx = ix(base + 128 + lane);
@@ -949,7 +955,14 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
     const uint64_t rm = __ballot(inrun);           // the run's records: a prefix of the chunk
     const uint32_t m = rm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~rm));
     uint32_t u0 = 0;
+#if PCN_CT_DBG
+    ++dbg_chunks;
+    dbg_recs += m;
+#endif
     while (u0 < m) {
+#if PCN_CT_DBG
+      ++dbg_rounds;
+#endif
       // lane 0's cached connection, to every lane
       const uint32_t sv = __shfl(c.valid ? 1u | (c.v.live ? 2u : 0u) | (c.e ? 4u : 0u) : 0u, 0);
       const uint32_t ks = __shfl(c.k.src, 0), kd = __shfl(c.k.dst, 0);
@@ -992,6 +1005,9 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
       u0 = end;
       if (u0 < m) {
         const int ecls = __shfl(cls, u0);
+#if PCN_CT_DBG
+        if (ecls == 1) ++dbg_changes; else ++dbg_steps;
+#endif
         if (ecls == 1) {                              // the changing record: its result is the new state
           if (lane == u0) put_outcome(b, sres, base + lane, w.idx, o);
           const uint32_t nl = __shfl(static_cast<uint32_t>(cc.v.ttl), u0);
@@ -1012,6 +1028,11 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
       }
     }
     if (m < 64) {                                     // the run (or this round of it) ends here
+#if PCN_CT_DBG
+      if (lane == 0 && dbg_chunks >= 40)
+        printf("walk_long run: %u records, %u chunks, %u rounds, %u changes, %u table steps\n", dbg_recs, dbg_chunks,
+               dbg_rounds, dbg_changes, dbg_steps);
+#endif
       if (lane == 0) {
         flush(c);
         *cursor_j = static_cast<uint32_t>(base + m);
