@@ -110,6 +110,27 @@ def test_flow_traffic_parity_across_batches(dev, jit, mode):
     assert ipt.ct_info()["inserts_lost"] == 0
 
 
+@pytest.mark.parametrize("mode", ["plain", "ct_rules"])
+def test_fixed_stride_64_with_lengths(dev, mode):
+    """ct_prep's coalesced path (frames at a 64-byte stride, windows and walk records
+    transposed through LDS) with per-frame lengths, ragged batches whose last group falls
+    back to per-lane windows, and, with conntrack rules, four stage-A outcomes per record."""
+    rs = synth.config_rules(2)
+    rules = rs.rules()
+    if mode == "ct_rules":
+        rules = CT_RULES[1:] + rules
+    o, ipt = ct_pair({1: rules}, {1: "DROP"}, jit=1)
+    n = 20000
+    f, lens = synth.flow_traffic(n, 800, 9, stride=64, rs=rs, lens_mode="mixed", p_noise=0.1)
+    lens = np.minimum(lens, 64).astype(np.uint16)
+    for lo, hi in ((0, 6001), (6001, 6064), (6064, n)):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, f[lo * 64:hi * 64], hi - lo, stride=64, lens=lens[lo:hi])
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_ae(o, ipt)
+
+
 @pytest.mark.parametrize("seed", [1, 2])
 def test_fuzz_quirky_rules_both_directions_and_hooks(dev, seed):
     """Quirky rules with conntrack fields in all chains, localip, INPUT/FORWARD/OUTPUT,
