@@ -9,7 +9,9 @@ default counters); with N > 1 GPUs each rank owns its own 2^24-frame shard
 counters over xGMI (pcn_ipt_sync_counters).  Frames are in HBM before the timed
 region starts; the PCIe-inclusive rate is reported separately under "e2e".
 
-Run: python bench.py [--gpus N --steps K --warmup W]  (N > 1 under torch.distributed.run)
+Run: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no
+WORLD_SIZE in the environment it launches its N ranks itself (torch.distributed.run,
+before any GPU call); under an external launcher it is one of the ranks.
 """
 import argparse
 import json
@@ -193,6 +195,20 @@ def fw_rate(rules, frames, n, dev, s_ptr, jit, steps=20, horus=False, settle=0.5
     return n / (ms * 1e-3) / 1e6, ms, info
 
 
+def spawn_ranks(n):
+    """Run this script as N ranks (torch.distributed.run, one process per GPU,
+    rendezvous on 127.0.0.1); rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -217,16 +233,24 @@ def main():
                          "timed loop) instead of one pair around the whole timed region")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start N ranks under torch.distributed.run as
+        # children, before this process touches the GPU, and exit with their code
+        sys.exit(spawn_ranks(args.gpus))
+
     import torch
     import torch.distributed as dist
 
     from polycube_amd import Iptables, synth
+    from polycube_amd import dist as pdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if "PCN_BENCH_DEVICE" in os.environ:   # test hook: several ranks on one GPU (RCCL refuses that)
         local = int(os.environ["PCN_BENCH_DEVICE"])
+    if args.gpus != world:
+        log(f"[rank {rank}] --gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} rank(s)")
     if world > 1:
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
@@ -261,8 +285,8 @@ def main():
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         use_rccl = bool(ok.item())
         if not use_rccl:
-            collective = (f"gloo all-reduce of the counter block on the host, timing stand-in: the sums are not "
-                          f"written back to the device counters (RCCL init failed: {err[:160]})")
+            collective = (f"gloo all-gather of the counter blocks through the host (pcn_ipt_snapshot_counters -> "
+                          f"gloo -> pcn_ipt_sum_counter_blocks; RCCL init failed: {err[:160]})")
             log(f"[rank {rank}] {collective}")
 
     t = time.perf_counter()
@@ -289,10 +313,11 @@ def main():
             return
         if use_rccl:
             ipt.sync_counters(s_ptr)
-        else:   # fallback, timing only: the same per-step exchange through the host, sums discarded
-            pk, by, dp, db = fw.read_counters(len(rules))
-            blk = torch.tensor([dp, db] + pk + by, dtype=torch.int64)
-            dist.all_reduce(blk)
+        else:   # fallback: the same per-step exchange, the blocks moved through the host by gloo
+            blk = ipt.snapshot_counters("FORWARD", stream=s_ptr).cpu()
+            parts = [torch.empty_like(blk) for _ in range(world)]
+            dist.all_gather(parts, blk)
+            ipt.sum_counter_blocks("FORWARD", torch.stack(parts).to(dev), stream=s_ptr)
 
     def step():
         classify()
@@ -341,6 +366,18 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    sum_ok = None
+    if world > 1:
+        # the summed (scope 1) view must equal the sum of every rank's own counters
+        k = min(len(rules), 8000)
+        mine = torch.tensor(pdist.counter_block(*fw.read_counters(k, scope=0)), dtype=torch.int64)
+        total = mine.clone()
+        dist.all_reduce(total)
+        got = torch.tensor(pdist.counter_block(*fw.read_counters(k, scope=1)), dtype=torch.int64)
+        ok = torch.tensor([int(torch.equal(got, total))])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        sum_ok = bool(ok.item())
+
     value = n * world * args.steps / elapsed / 1e6
     bytes_per_pkt = BYTES_PER_PKT + (6 if cfg == 5 else 0)   # + offset and length per frame (§8d)
     achieved = bytes_per_pkt * n / (kern_ms * 1e-3) / 1e9
@@ -364,7 +401,7 @@ def main():
         ok = parity_sample(rules, frames_host, verdicts[: 1 << 16].cpu().numpy(), rid[: 1 << 16].cpu().numpy(),
                            offsets_host, lens_host, hook, big)
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
+            "metric": METRIC if world == 1 else METRIC.replace("1 GPU", f"{world} GPUs"), "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded synth.config_rules(3) + make_headers; no captured traffic)",
@@ -382,6 +419,7 @@ def main():
                                             "(includes the launch boundaries)"),
                          "bytes_per_unit": bytes_per_pkt, "units_per_launch": n},
             "parity_sample_vs_oracle": ok,
+            "counters_summed_over_ranks_ok": sum_ok,
             "settle": {"seconds": round(settle_s, 2), "steps": settle_steps,
                        "what": "untimed steps before the warmup steps, until the GPU clocks reach steady state"},
         }

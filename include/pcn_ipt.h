@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 5
+#define PCN_IPT_ABI_VERSION 6
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -423,6 +423,23 @@ int pcn_ipt_comm_init(pcn_ipt *ctx, int nranks, int rank, const uint8_t uid[128]
 /* All-gather every rank's per-rule/default counters over RCCL and sum them
  * into the scope=1 view.  Stream-ordered. */
 int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream);
+/* The two halves of pcn_ipt_sync_counters, for a caller that moves the counter
+ * blocks over its own transport (gloo, MPI, a test), or reads them raw.  The
+ * reference's only reduction is the control plane's sum over per-CPU counters
+ * (modules/ActionLookup.cpp:78-96); here each GPU is one "CPU".
+ * pcn_ipt_counter_block_words: u64 words in chain `chain`'s block,
+ *   [def_pkts, def_bytes, pkts_0, bytes_0, ...] = 2 + 2 * counted rules
+ *   (no device needed).
+ * pcn_ipt_snapshot_counters: copy this GPU's block into `block` (device,
+ *   >= block words), stream-ordered.
+ * pcn_ipt_sum_counter_blocks: sum `nranks` blocks (device, rank-major, `words`
+ *   u64 each, as ncclAllGather lays them out) into the scope=1 view of
+ *   `chain` with the device kernel the all-gather path runs; stream-ordered.
+ *   `words` must equal the chain's block words; 1 <= nranks <= 4096. */
+int pcn_ipt_counter_block_words(pcn_ipt *ctx, int chain);
+int pcn_ipt_snapshot_counters(pcn_ipt *ctx, int chain, uint64_t *block, void *stream);
+int pcn_ipt_sum_counter_blocks(pcn_ipt *ctx, int chain, const uint64_t *blocks, uint32_t nranks, uint64_t words,
+                               void *stream);
 
 /* Flow-affinity split for stateful conntrack on N GPUs.  Replaces the NIC's
  * RSS queue choice that spreads traffic over the reference's per-CPU datapath

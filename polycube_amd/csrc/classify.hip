@@ -895,7 +895,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       const uint64_t wm = __ballot(wrote);
       const uint64_t g = (a.gbase + i) >> 6;              // the wave's group (64-aligned frames)
       const uint32_t last_pd = __shfl(own_pd, wm ? 63 - __builtin_clzll(wm) : 0);
-      if (lane == 0)
+      // a wave wholly past the batch end publishes nothing: the host sizes
+      // stale_desc for the batch's groups (n / 64 + 1 words), not for the grid
+      if (lane == 0 && valid)
         __hip_atomic_store(&a.stale_desc[g], stale_word(a.stale_epoch, wm ? kStaleLocal : kStaleNone, last_pd),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t before = wm & ((1ull << lane) - 1);

@@ -934,6 +934,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       a.fast_chain = -1;                               // the lookup lives in the general path
       if (carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) {
         // the key reads ports: stale ones (Q4) computed in the kernel
+        // one word per 64-frame group of the batch (+1 for the look-back from
+        // the end); the kernel publishes only groups that hold frames
         const size_t groups = b->n / 64 + 1;
         if (ctx->stale_groups < groups) {
           if (ctx->d_stale_desc) hip_check(hipFree(ctx->d_stale_desc), "hipFree");
@@ -1066,7 +1068,10 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     if (serial && ctx->ct_pending) hip_check(hipStreamWaitEvent(st, ctx->ev_ct, 0), "hipStreamWaitEvent(serial)");
     // with the connection table on, its own copy (advanced by ct_run when stateful)
     uint32_t *carry = ctx->ct_on ? ctx->ct.carry : ctx->d_hz_carry;
-    const uint32_t *stale = track && want_stale ? carry : nullptr;
+    // A Horus program still in place after horus was turned off keys on the
+    // stale ports too: the table's copy while conntrack is on (the oracle's
+    // st->sport/dport), as the reference's one per-CPU struct would give.
+    const uint32_t *stale = want_stale && (track || ctx->ct_on) ? carry : nullptr;
     // the carry after this batch: the ports its last TCP/UDP frame left
     auto advance_carry = [&]() -> int {
       if (!track || stateful) return 0;
@@ -1090,6 +1095,9 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       if (!rc && !carried) rc = advance_carry();
       if (rc) return rc;
       if (!ae_mask) return mark();
+      // Not serialised with other streams' batches (ae_mask is not in
+      // `serial`): the accept-established counter move is an atomic exchange
+      // and add on d_ae, so interleaved batches neither lose nor double counts.
       device_guard(ctx);
       const int e = ct_ae_fixup(ct_batch(ctx, b, ae_mask), st);
       if (e != hipSuccess) return fail(-EIO, std::string("accept-established fixup: ") + hipGetErrorString(hipError_t(e)));
@@ -1347,6 +1355,45 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
     }
     hip_check(hipEventRecord(ctx->ev_gathered, cs_), "hipEventRecord");
     ctx->gather_pending = true;
+    return 0;
+  });
+}
+
+int pcn_ipt_counter_block_words(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    return static_cast<int>(2 + 2 * size_t(counted(ctx, ctx->chains[chain].info.nrules)));   // the applied chain
+  });
+}
+
+int pcn_ipt_snapshot_counters(pcn_ipt *ctx, int chain, uint64_t *block, void *stream) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (!block) return fail(-EINVAL, "null block");
+    device_guard(ctx);
+    ChainState &cs = ctx->chains[chain];
+    const size_t words = 2 + 2 * size_t(cs.desc.ncounted);
+    hip_check(hipMemcpyAsync(block, cs.ctr, words * 8, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)),
+              "hipMemcpyAsync(snapshot)");
+    return 0;
+  });
+}
+
+int pcn_ipt_sum_counter_blocks(pcn_ipt *ctx, int chain, const uint64_t *blocks, uint32_t nranks, uint64_t words,
+                               void *stream) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (!blocks) return fail(-EINVAL, "null blocks");
+    if (nranks < 1 || nranks > 4096) return fail(-EINVAL, "nranks must be 1..4096");
+    ChainState &cs = ctx->chains[chain];
+    if (words != 2 + 2 * uint64_t(cs.desc.ncounted) || words > ctx->ctr_words)
+      return fail(-EINVAL, "words != the chain's counter block words");
+    device_guard(ctx);
+    int rc = launch_sum_ranks(reinterpret_cast<const unsigned long long *>(blocks), cs.ctr_global, words,
+                              static_cast<int>(nranks), static_cast<hipStream_t>(stream));
+    if (rc != hipSuccess) return fail(-EIO, "sum_ranks launch failed");
     return 0;
   });
 }

@@ -88,7 +88,7 @@ class HorusInfo(C.Structure):
 
 
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
-ABI_VERSION = 5            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
+ABI_VERSION = 6            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
 
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
@@ -139,6 +139,10 @@ SIGNATURES = {
     "pcn_ipt_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "pcn_ipt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     "pcn_ipt_sync_counters": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pcn_ipt_counter_block_words": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_snapshot_counters": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "pcn_ipt_sum_counter_blocks": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_uint64,
+                                             C.c_void_p]),
     "pcn_ipt_flow_owner": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_uint32, C.c_void_p, C.c_void_p]),
     "pcn_ipt_flow_split": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]),

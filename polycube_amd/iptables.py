@@ -322,6 +322,35 @@ class Iptables:
     def sync_counters(self, stream=None):
         _check(ffi.lib().pcn_ipt_sync_counters(self._h, stream))
 
+    def counter_block_words(self, chain):
+        """u64 words of `chain`'s counter block [dp, db, p0, b0, ...] (pcn_ipt_counter_block_words)."""
+        return _check(ffi.lib().pcn_ipt_counter_block_words(self._h, self._chain_id(chain)))
+
+    def snapshot_counters(self, chain, block=None, stream=None):
+        """This GPU's counter block of `chain` as an int64 tensor on the device (the send half of
+        sync_counters; pcn_ipt_snapshot_counters)."""
+        import torch
+        cid = self._chain_id(chain)
+        if block is None:
+            block = torch.empty(self.counter_block_words(cid), dtype=torch.int64, device=f"cuda:{self.device}")
+        s = stream if stream is not None else torch.cuda.current_stream(block.device).cuda_stream
+        _check(ffi.lib().pcn_ipt_snapshot_counters(self._h, cid, block.data_ptr(), s))
+        return block
+
+    def sum_counter_blocks(self, chain, blocks, stream=None):
+        """Sum gathered blocks (a [nranks, words] int64 device tensor, rank-major) into the
+        scope=1 counters of `chain` (the receive half of sync_counters; pcn_ipt_sum_counter_blocks)."""
+        import torch
+        cid = self._chain_id(chain)
+        blocks = blocks.contiguous()
+        s = stream if stream is not None else torch.cuda.current_stream(blocks.device).cuda_stream
+        _check(ffi.lib().pcn_ipt_sum_counter_blocks(self._h, cid, blocks.data_ptr(), blocks.shape[0],
+                                                     blocks.shape[1], s))
+
+    @staticmethod
+    def _chain_id(chain):
+        return _CHAIN_NAMES[chain.upper()] if isinstance(chain, str) else int(chain)
+
     # ---- flow-affinity split (stateful conntrack on N GPUs) ----
     @staticmethod
     def _frames_batch(frames, n, offsets, lens, stride, fixed_len, in_port, const_in_port, hook):

@@ -484,3 +484,38 @@ def test_stale_ports_across_a_split_launch(dev):
     assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
     assert (r_o[lo:split + 3000] == RID_HORUS0).all()
     assert o.read_horus_counters(2) == ipt.read_horus_counters(2)
+
+
+def test_horus_off_program_in_place_keys_on_table_ports(dev):
+    """horus turned OFF, the program still in place (no update since), conntrack
+    on: an ICMP packet's Horus key reads the ports the connection table's
+    copy of the Parser struct holds (Q4), as in the oracle."""
+    rules = rule_sets()["proto_ports"]
+    o, ipt = setup(rules, ct=True)
+    ipt.horus = "OFF"
+    o.set_horus(False)
+    assert ipt.horus_info()["runtime"] == 1
+    rng = np.random.default_rng(5)
+    pk = []
+    for _ in range(40):
+        pk += rule_packets(rng, rules[2]) + rule_packets(rng, rules[0])    # UDP lead, ICMP; TCP
+    v_o, r_o, v_g, r_g = run(o, ipt, dev, pk)
+    assert_same(v_o, r_o, v_g, r_g)
+    assert (r_o == RID_HORUS0 - 2).sum() > 0               # the ICMP rule hit on the stale ports
+    assert_horus_counters(o, ipt)
+
+
+@pytest.mark.parametrize("fixed", [False, True], ids=["lens", "fixed"])
+def test_stale_ports_ragged_batches(dev, fixed):
+    """Batch sizes that leave the last workgroup's waves past the batch end
+    (1, 63, 100, 193, 1000, 2^16 + 1): those waves publish no stale-port group
+    word (the host holds n / 64 + 1 words), and every frame stays bit-exact."""
+    rules = rule_sets()["proto_ports"]
+    o, ipt = setup(rules)
+    rng = np.random.default_rng(9)
+    go = run_fixed if fixed else run
+    for n in (1, 63, 100, 193, 1000, (1 << 16) + 1):
+        pk = traffic(rng, n, ADDRS, key_ports(rules), rules)[:n]
+        v_o, r_o, v_g, r_g = go(o, ipt, dev, pk)
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_horus_counters(o, ipt)

@@ -1,8 +1,10 @@
 """World-size-2 gloo run of the multi-GPU partitioning on CPU.
 
-Each rank classifies its contiguous shard (the oracle stands in for its GPU),
-the ranks all-gather their counter blocks (the RCCL all-gather of
-pcn_ipt_sync_counters, here over gloo) and sum them.  The result must equal a
+Each rank classifies its contiguous shard (the oracle stands in for its GPU:
+there is none here), lays its counters out as the library's block
+(pcn_ipt_counter_block_words), the ranks all-gather the blocks (the RCCL
+all-gather of pcn_ipt_sync_counters, here over gloo) and sum them.  The same
+exchange through the library on a GPU: tests/test_gpu_multirank.py.  The result must equal a
 single unsharded pass: verdicts are a pure function of each packet (no conntrack
 state), so sharding by index changes nothing."""
 import os
@@ -35,6 +37,16 @@ def _worker(rank, world, port, n, q):
     o.set_chain(1, rules, "DROP")
     v, r = o.classify(frames[lo:hi].reshape(-1), n=hi - lo)
     blk = torch.tensor(pdist.counter_block(*o.read_counters(1, len(rules))), dtype=torch.int64)
+    # the block has the library's layout and size (what pcn_ipt_snapshot_counters sends)
+    from polycube_amd import Iptables
+    ipt = Iptables(device=-1)
+    ipt.interactive = False
+    ch = ipt.chain("FORWARD")
+    for r in rules:
+        ch.append(**r)
+    ch.apply_rules()
+    assert blk.numel() == ipt.counter_block_words("FORWARD")
+    ipt.close()
     gathered = [torch.zeros_like(blk) for _ in range(world)]
     dist.all_gather(gathered, blk)
     vs = [torch.zeros(pdist.shard_range(n, world, k)[1] - pdist.shard_range(n, world, k)[0],
