@@ -48,19 +48,100 @@ def gen_frames(n, rs, seed, chunk=1 << 22, protos=(6, 17)):
     return out.reshape(-1)
 
 
-def cpu_baseline(rules, frames, n, threads, min_seconds=8.0):
-    """The oracle (scalar C restatement of the reference eBPF algorithm) on the host cores."""
+def cpu_baseline(rules, frames, n, threads, min_seconds=8.0, offsets=None, lens=None, hook=0, big=None):
+    """The oracle (scalar C restatement of the reference eBPF algorithm) on the host cores:
+    passes over the same batch until min_seconds have gone by.  Returns (Mpkt/s, frames, seconds)."""
     from oracle.ffi import Oracle
-    o = Oracle()
+    big = big or {}
+    o = Oracle(big.get("max_counted_rules", 0), big.get("max_action_rules", 0))
     o.set_chain(1, rules, "DROP")
     done, t0 = 0, time.perf_counter()
     while True:
-        o.classify(frames, n=n, nthreads=threads)
+        if offsets is None:
+            o.classify(frames, n=n, nthreads=threads, hook=hook)
+        else:
+            o.classify(frames, n=n, offsets=offsets[:n], lens=lens[:n], nthreads=threads, hook=hook)
         done += n
         el = time.perf_counter() - t0
         if el >= min_seconds:
             break
     return done / el / 1e6, done, el
+
+
+def cgroup_cpus():
+    """CPUs the cgroup's CFS quota grants (cgroup v2 cpu.max / v1 cfs_quota_us), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_cores():
+    """(threads the baseline runs on, nproc): the CPUs this process may run on --
+    its affinity set, capped by the cgroup's CPU quota (a GPU box shows the whole
+    machine in nproc but grants a share of it) -- and the machine's count."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    quota = cgroup_cpus()
+    return (min(usable, quota) if quota else usable), os.cpu_count() or usable
+
+
+def cpu_rates(rules, frames, n, label, offsets=None, lens=None, hook=0, big=None, s1=3.0, sall=6.0,
+              with_nproc=False):
+    """cpu_baseline object: every core this process is granted, and one core, on the same
+    batch; with_nproc also times nproc threads (more than the grant: oversubscribed)."""
+    cores, nproc = host_cores()
+    kw = dict(offsets=offsets, lens=lens, hook=hook, big=big)
+    one = min(n, 1 << 20)
+    v1, done1, el1 = cpu_baseline(rules, frames, one, 1, min_seconds=s1, **kw)
+    vT, doneT, elT = cpu_baseline(rules, frames, n, cores, min_seconds=sall, **kw)
+    out = {"value": round(vT, 2), "unit": "Mpkt/s", "cores": cores, "nproc": nproc, "kind": "port",
+           "sample": f"{label}: {doneT} frames ({doneT // n} passes over the same {n}-frame batch) in {elT:.1f}s "
+                     f"on {cores} threads (the CPUs granted to this process: affinity set capped by the cgroup "
+                     f"quota {cgroup_cpus()}; nproc {nproc})",
+           "single_core": {"value": round(v1, 2), "cores": 1,
+                           "sample": f"{done1} frames (passes over the batch's first {one}) in {el1:.1f}s"}}
+    if with_nproc and nproc != cores:
+        vN, doneN, elN = cpu_baseline(rules, frames, n, nproc, min_seconds=s1, **kw)
+        out["nproc_threads"] = {"value": round(vN, 2), "cores": nproc,
+                                "sample": f"{doneN} frames in {elN:.1f}s on {nproc} threads (beyond the grant)"}
+    return out
+
+
+def secondary_cpu_baselines(log):
+    """configs 1, 2 and 5: the oracle at one core and all cores, each on its
+    own config's rules and frames (config 5: 2^20 of its IMIX frames, XDP hook)."""
+    from polycube_amd import synth
+    out = {}
+    for cfg, n in ((1, 1 << 22), (2, 1 << 20), (5, 1 << 20)):
+        t = time.perf_counter()
+        rs = synth.config_rules(cfg)
+        rules = rs.rules()
+        if cfg == 5:
+            frames, offs, lens = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5])
+            big = dict(max_counted_rules=10000, max_action_rules=10000)
+        else:
+            frames, offs, lens, big = synth.config_frames(cfg, n, rs).reshape(-1), None, None, None
+        out[f"config{cfg}"] = dict(cpu_rates(rules, frames, n, f"config {cfg}, {len(rules)} rules", offs, lens,
+                                             big=big, s1=2.0, sall=3.0), rules=len(rules), frames=n)
+        log(f"[bench] cpu baseline config {cfg}: {out[f'config{cfg}']['value']} Mpkt/s "
+            f"({time.perf_counter() - t:.1f}s)")
+    return out
 
 
 def parity_sample(o_rules, frames, v_dev, r_dev, offsets=None, lens=None, hook=0, big=None, k=1 << 16):
@@ -259,6 +340,8 @@ def main():
     cfg = args.config
     if cfg == 5 and args.log2n == 24:
         args.log2n = 22                      # config 5 is 2^22 IMIX frames
+    if cfg == 2 and args.log2n == 24:
+        args.log2n = 20                      # BASELINE.json configs[1]: 1M frames
     n = 1 << args.log2n
     hook = 1 if args.hook == "tc" else 0
     rs = synth.config_rules(cfg)
@@ -324,8 +407,17 @@ def main():
         exchange()
 
     # clock settle: untimed steps until the GPU has run the workload for `settle` seconds
+    # (every rank runs the same number of steps: each step may hold a collective,
+    # so the ranks agree after each chunk whether to go on)
     settle_steps, t_settle = 0, time.perf_counter()
-    while time.perf_counter() - t_settle < args.settle:
+    while True:
+        go = time.perf_counter() - t_settle < args.settle
+        if world > 1:
+            flag = torch.tensor([int(go)])
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            go = bool(flag.item())
+        if not go:
+            break
         for _ in range(64):
             step()
         settle_steps += 64
@@ -406,7 +498,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded synth.config_rules(3) + make_headers; no captured traffic)",
             "config": {"workload": WORKLOADS[cfg] + (", TC hook" if hook else ""),
-                       "rules": len(rules), "frames_per_gpu": n, "frame_bytes": 64,
+                       "rules": len(rules), "frames_per_gpu": n,
+                       "frame_bytes": "IMIX 64/576/1500 (7:4:1)" if cfg == 5 else 64,
                        "parallelism": (f"dp{world} (packet-index shards, "
                                        + ("RCCL counter all-gather)" if use_rccl else "host gloo counter all-reduce)")
                                        if world > 1 else "dp1 (one packet shard, no exchange)"),
@@ -423,15 +516,11 @@ def main():
             "settle": {"seconds": round(settle_s, 2), "steps": settle_steps,
                        "what": "untimed steps before the warmup steps, until the GPU clocks reach steady state"},
         }
-        if world == 1 and not args.no_cpu and cfg != 5:
-            threads = min(16, os.cpu_count() or 1)
-            sample = 1 << 22
-            v1, done1, el1 = cpu_baseline(rules, frames_host, sample, 1, min_seconds=3.0)
-            vT, doneT, elT = cpu_baseline(rules, frames_host, n, threads, min_seconds=6.0)
-            line["cpu_baseline"] = {
-                "value": round(vT, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
-                "sample": f"{doneT} frames ({doneT // n} passes over the same 2^{args.log2n} batch) in {elT:.1f}s",
-                "single_core": {"value": round(v1, 2), "sample": f"{done1} frames of the batch in {el1:.1f}s"}}
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_rates(rules, frames_host, n, WORKLOADS[cfg], offsets_host, lens_host, hook,
+                                             big or None, with_nproc=True)
+            if cfg == 3:
+                line["cpu_baselines"] = secondary_cpu_baselines(log)
         if world == 1 and not args.no_e2e and cfg != 5:
             line["e2e"] = {"value": round(e2e_rate(ipt, frames_host, n), 2), "unit": "Mpkt/s",
                            "what": "host ingest ring (pcn_ipt_ring): pinned slots -> H2D -> classify -> D2H verdicts, "

@@ -71,6 +71,35 @@ def A(**r):
     return ["append", "FORWARD", r]
 
 
+def I(**r):  # noqa: E743 (pcn-iptables -I FORWARD: insert at 0)
+    return ["insert", "FORWARD", 0, r]
+
+
+def D(**r):
+    return ["deletes", "FORWARD", r]
+
+
+def P(chain, action):
+    return ["default", chain, action]
+
+
+def tagged(*exchanges):
+    """Exchange-tagged probe (tests/helpers.py exchange_replay): a dropped
+    packet ends its exchange, so what it would have caused is never sent."""
+    return [dict(p, ex=k) for k, ex in enumerate(exchanges) for p in ex]
+
+
+def icmp(src, dst, icmp_type, port):
+    return {"dir": "ingress", "port": PORTS[port], "src": src, "dst": dst, "proto": 1, "sport": 0, "dport": 0,
+            "flags": 0, "icmp_type": icmp_type, "len": 98}
+
+
+def ping_ns1(count=2):
+    """`ip netns exec ns1 ping 10.0.2.1 -c 2`: each request forwarded from
+    veth1, its reply from veth2 (the cube's FORWARD chain sees both at ingress)."""
+    return tagged(*[[icmp(NS1, NS2, 8, "veth1"), icmp(NS2, NS1, 0, "veth2")] for _ in range(count)])
+
+
 def step(ops=(), probe=None, expect=None, line=None, session=None):
     s = {"ops": list(ops)}
     if probe is not None:
@@ -118,6 +147,41 @@ def scenarios():
     out.append({"name": "conntrack_udp_2", "source": t, "steps": [
         step([["default", "FORWARD", "DROP"]] + rules, nping(NS2, NS1, 50000, 50000), "pass", f"{t}:(1)"),
         step([], nping(NS1, NS2, 50000, 50000), "pass", f"{t}:(2)"),
+    ]})
+    # ---------------- local_test6_iptables.sh: ctstate NEW/ESTABLISHED in FORWARD ----------------
+    # test_tcp (:17-22) = netcat -nvz 10.0.2.1 60123 from ns1 (a new client port
+    # each time); test_tcp_fail (:24-29) expects it to fail.  drop_at: the
+    # packet whose drop ends the exchange (derived from the rules, not asserted
+    # by the script, which only sees the connect fail).
+    t = "src/services/pcn-iptables/test/local_test6_iptables.sh"
+    ns = [P("INPUT", "DROP"), P("OUTPUT", "DROP")]
+
+    def nc(k):
+        return tagged(netcat(41000 + k, 60123, isn_c=0x11110000 * (k + 1), isn_s=0x22220000 * (k + 1)))
+    steps = [step([], ping_ns1(), "pass", f"{t}:54"),
+             step(ns, ping_ns1(), "pass", f"{t}:59"),
+             step([], nc(0), "pass", f"{t}:61"),
+             step([P("INPUT", "ACCEPT"), P("OUTPUT", "ACCEPT"), P("FORWARD", "DROP")], nc(1), "fail", f"{t}:67"),
+             step(ns + [A(conntrack="ESTABLISHED", action="ACCEPT")], nc(2), "fail", f"{t}:74"),
+             step([I(conntrack="NEW", action="ACCEPT")], nc(3), "pass", f"{t}:78"),
+             step([D(conntrack="NEW", action="ACCEPT")], nc(4), "fail", f"{t}:82"),
+             step([A(conntrack="NEW", action="ACCEPT")], nc(5), "pass", f"{t}:86"),
+             step([D(conntrack="NEW", action="ACCEPT"), D(conntrack="ESTABLISHED", action="ACCEPT")], nc(6), "fail",
+                  f"{t}:91"),
+             step([A(src=NS1, dst=NS2, action="ACCEPT")], nc(7), "fail", f"{t}:95"),
+             step([I(conntrack="ESTABLISHED", action="ACCEPT")], nc(8), "pass", f"{t}:99")]
+    for st, at in zip(steps, [None, None, None, 0, 0, None, 0, None, 0, 1, None]):
+        if at is not None:
+            st["drop_at"] = at
+    out.append({"name": "local_test6_iptables", "source": t, "steps": steps})
+    # ---------------- local_test7_iptables.sh: the same topology, address rules (table on) ----------------
+    t = "src/services/pcn-iptables/test/local_test7_iptables.sh"
+    out.append({"name": "local_test7_iptables_ct", "source": t, "steps": [
+        step([], ping_ns1(), "pass", f"{t}:57"),
+        step(ns, ping_ns1(), "pass", f"{t}:62"),
+        dict(step([P("INPUT", "ACCEPT"), P("OUTPUT", "ACCEPT"), P("FORWARD", "DROP")], ping_ns1(), "fail",
+                  f"{t}:68"), drop_at=0),
+        step(ns + [A(src=NS1, action="ACCEPT"), A(src=NS2, action="ACCEPT")], ping_ns1(), "pass", f"{t}:76"),
     ]})
     return out
 

@@ -67,6 +67,58 @@ def netcat_from_ns1(port):
             pkt("ingress", NS1, HOST, 6, 40000, port, 0x10, length=66, seq=1001, ack=5001)]
 
 
+def tagged(*exchanges):
+    """Exchange-tagged probe (tests/helpers.py exchange_replay): packets go one
+    at a time and a dropped packet ends its exchange -- a dropped echo request
+    has no reply, a dropped SYN no SYN-ACK -- so connection state only ever
+    sees what the real exchange would have put through the cube."""
+    return [dict(p, ex=k) for k, ex in enumerate(exchanges) for p in ex]
+
+
+def pings_from_ns1(n=2):
+    return tagged(*[[pkt("ingress", NS1, HOST, 1, icmp_type=8), pkt("egress", HOST, NS1, 1, icmp_type=0)]
+                    for _ in range(n)])
+
+
+def pings_from_host(n=2):
+    return tagged(*[[pkt("egress", HOST, NS1, 1, icmp_type=8), pkt("ingress", NS1, HOST, 1, icmp_type=0)]
+                    for _ in range(n)])
+
+
+def nping_udp(src_side, sport=50000, dport=50000):
+    """`nping --udp -c 1 -p <dport> -g <sport>` from ns1 ("ns1") or the host:
+    the 42-byte datagram; nothing listens, so the peer answers with an ICMP
+    port-unreachable (type 3) quoting the datagram's IP header + 8 bytes
+    (70-byte frame).  "Rcvd: 1" means that answer came back."""
+    if src_side == "ns1":
+        d = pkt("ingress", NS1, HOST, 17, sport, dport, length=42)
+        e = pkt("egress", HOST, NS1, 1, icmp_type=3, length=70)
+    else:
+        d = pkt("egress", HOST, NS1, 17, sport, dport, length=42)
+        e = pkt("ingress", NS1, HOST, 1, icmp_type=3, length=70)
+    e["inner"] = {"src": d["src"], "dst": d["dst"], "proto": 17, "sport": sport, "dport": dport}
+    return tagged([d, e])
+
+
+def netcat_session(client, port, cport=40100, close=True, isn_c=0x3C4D0000, isn_s=0x7A8B0000):
+    """`nc -nvz <server> <port>` from `client` ("ns1" or "host"): SYN, SYN-ACK,
+    ACK and, with close, the -z close (FIN-ACK, FIN-ACK, ACK), sequence
+    numbers consistent; one exchange."""
+    out_dir, in_dir = ("ingress", "egress") if client == "ns1" else ("egress", "ingress")
+    c_ip, s_ip = (NS1, HOST) if client == "ns1" else (HOST, NS1)
+    X, Y = isn_c, isn_s
+
+    def c(fl, sq, ak, ln=74):
+        return pkt(out_dir, c_ip, s_ip, 6, cport, port, fl, length=ln, seq=sq, ack=ak)
+
+    def sv(fl, sq, ak, ln=74):
+        return pkt(in_dir, s_ip, c_ip, 6, port, cport, fl, length=ln, seq=sq, ack=ak)
+    ex = [c(0x02, X, 0), sv(0x12, Y, X + 1), c(0x10, X + 1, Y + 1, 66)]
+    if close:
+        ex += [c(0x11, X + 1, Y + 1, 66), sv(0x11, Y + 1, X + 2, 66), c(0x10, X + 2, Y + 2, 66)]
+    return tagged(ex)
+
+
 def step(ops, probe=None, expect=None, line=None, counters=None):
     s = {"ops": ops}
     if probe is not None:
@@ -247,6 +299,152 @@ def scenarios():
               ["add", "EGRESS", 1, {"conntrack": "ESTABLISHED", "action": "ACCEPT"}]],
              ping_from_ns1(), "fail", "conntrack/test_disable_enable.sh:74"),
         step([], ping_from_host(), "pass", "conntrack/test_disable_enable.sh:81")]})
+    # ---- conntrack/: the stateful tests not transcribed before (round 3) ----
+    # ICMP errors: the RELATED label (Firewall_ConntrackLabel_dp.c, the
+    # pcn-iptables code at Iptables_ConntrackLabel_dp.c:482-531)
+    err_rules = [["append", "INGRESS", {"l4proto": "UDP", "action": "ACCEPT"}],
+                 ["append", "INGRESS", {"l4proto": "ICMP", "conntrack": "RELATED", "action": "ACCEPT"}],
+                 ["append", "INGRESS", {"l4proto": "ICMP", "action": "DROP"}],
+                 ["append", "EGRESS", {"l4proto": "UDP", "action": "ACCEPT"}],
+                 ["append", "EGRESS", {"l4proto": "ICMP", "conntrack": "RELATED", "action": "ACCEPT"}],
+                 ["append", "EGRESS", {"l4proto": "ICMP", "action": "DROP"}]]
+    for name in ("conntrack/test_icmp_error", "conntrack/test_icmp_error_2"):
+        S.append({"name": name, "steps": [
+            step(FWSETUP + err_rules, nping_udp("ns1"), "pass", name + ".sh:37-41"),
+            step([], nping_udp("ns1"), "pass", name + ".sh:46-50"),
+            step([], pings_from_ns1(), "fail", name + ".sh:54-58"),
+            step([], pings_from_host(), "fail", name + ".sh:61-65")]})
+    # TCP handshakes started by the host towards ns1 (nc exit status only: no close asserted)
+    S.append({"name": "conntrack/test_tcp_handshake_1", "steps": [
+        step(FWSETUP + [["append", "INGRESS", {"l4proto": "TCP", "conntrack": "ESTABLISHED", "action": "ACCEPT"}],
+                        ["append", "INGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}],
+                        ["append", "EGRESS", {"l4proto": "TCP", "conntrack": "NEW", "action": "ACCEPT"}],
+                        ["append", "EGRESS", {"l4proto": "TCP", "conntrack": "ESTABLISHED", "action": "ACCEPT"}],
+                        ["append", "EGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}]],
+             netcat_session("host", 60123, close=False), "pass", "conntrack/test_tcp_handshake_1.sh:39-44")]})
+    S.append({"name": "conntrack/test_tcp_handshake_2", "steps": [
+        step(FWSETUP + [["accept_established", "ON"],
+                        ["append", "INGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}],
+                        ["append", "EGRESS", {"l4proto": "TCP", "conntrack": "NEW", "action": "ACCEPT"}],
+                        ["append", "EGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}]],
+             netcat_session("host", 60123, close=False), "pass", "conntrack/test_tcp_handshake_2.sh:39-44")]})
+
+    # TCP connections with the graceful close the scripts check ((2): the server exited)
+    def complete(server_side, est_chain, new_chain, auto):
+        ops = FWSETUP + ([["accept_established", "ON"]] if auto else [])
+        ops += [["append", est_chain, {"l4proto": "TCP", "conntrack": "ESTABLISHED", "action": "ACCEPT"}],
+                ["append", est_chain, {"conntrack": "INVALID", "action": "DROP"}],
+                ["append", new_chain, {"l4proto": "TCP", "conntrack": "NEW", "action": "ACCEPT"}],
+                ["append", new_chain, {"l4proto": "TCP", "conntrack": "ESTABLISHED", "action": "ACCEPT"}],
+                ["append", new_chain, {"conntrack": "INVALID", "action": "DROP"}]]
+        return ops
+    S.append({"name": "conntrack/test_tcp_complete_2", "steps": [
+        step(complete("host", "EGRESS", "INGRESS", False), netcat_session("ns1", 60123), "pass",
+             "conntrack/test_tcp_complete_2.sh:42-55")]})
+    S.append({"name": "conntrack/test_tcp_complete_3", "steps": [
+        step(complete("ns1", "INGRESS", "EGRESS", True), netcat_session("host", 60123), "pass",
+             "conntrack/test_tcp_complete_3.sh:44-57")]})
+    S.append({"name": "conntrack/test_tcp_complete_4", "steps": [
+        step(complete("host", "EGRESS", "INGRESS", True), netcat_session("ns1", 60123), "pass",
+             "conntrack/test_tcp_complete_4.sh:44-57")]})
+    # UDP: (1) a NEW datagram from ns1 is refused; (2) the host's datagram opens the
+    # connection; (3)-(4) ns1's datagrams are then ESTABLISHED
+    udp_manual = [["accept_established", "OFF"],
+                  ["append", "INGRESS", {"l4proto": "UDP", "conntrack": "ESTABLISHED", "action": "ACCEPT"}],
+                  ["append", "INGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}],
+                  ["default", "INGRESS", "DROP"],
+                  ["append", "EGRESS", {"l4proto": "UDP", "conntrack": "NEW", "action": "ACCEPT"}],
+                  ["append", "EGRESS", {"l4proto": "UDP", "conntrack": "ESTABLISHED", "action": "ACCEPT"}],
+                  ["append", "EGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}],
+                  ["default", "EGRESS", "DROP"]]
+    udp_auto = [["accept_established", "ON"],
+                ["append", "INGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}],
+                ["default", "INGRESS", "DROP"],
+                ["append", "EGRESS", {"l4proto": "UDP", "conntrack": "NEW", "action": "ACCEPT"}],
+                ["append", "EGRESS", {"l4proto": "ICMP", "action": "ACCEPT"}],
+                ["default", "EGRESS", "DROP"]]
+    for name, rules, l1 in (("conntrack/test_udp", udp_manual, 39), ("conntrack/test_udp_2", udp_manual, 39),
+                            ("conntrack/test_udp_3", udp_auto, 38), ("conntrack/test_udp_4", udp_auto, 37)):
+        S.append({"name": name, "steps": [
+            step(FWSETUP + rules, nping_udp("ns1"), "fail", f"{name}.sh:{l1}"),
+            step([], nping_udp("host"), "pass", f"{name}.sh:{l1 + 8}"),
+            step([], nping_udp("ns1"), "pass", f"{name}.sh:{l1 + 15}"),
+            step([], nping_udp("ns1"), "pass", f"{name}.sh:{l1 + 25}")]})
+    # ICMP echo: the NEW request from ns1 is refused, the host's ping passes
+    echo_manual = [["accept_established", "OFF"],
+                   ["append", "INGRESS", {"conntrack": "NEW", "action": "DROP"}],
+                   ["append", "INGRESS", {"conntrack": "ESTABLISHED", "action": "ACCEPT"}],
+                   ["append", "EGRESS", {"conntrack": "NEW", "action": "ACCEPT"}],
+                   ["append", "EGRESS", {"conntrack": "ESTABLISHED", "action": "ACCEPT"}]]
+    echo_auto = [["accept_established", "ON"],
+                 ["append", "INGRESS", {"l4proto": "ICMP", "conntrack": "NEW", "action": "DROP"}],
+                 ["append", "EGRESS", {"l4proto": "ICMP", "conntrack": "NEW", "action": "ACCEPT"}]]
+    for name, rules, l1 in (("conntrack/test_icmp_echo_2", echo_manual, 37),
+                            ("conntrack/test_icmp_echo_3", echo_auto, 35),
+                            ("conntrack/test_icmp_echo_4", echo_auto, 36)):
+        S.append({"name": name, "steps": [
+            step(FWSETUP + rules, pings_from_ns1(), "fail", f"{name}.sh:{l1}"),
+            step([], pings_from_host(), "pass", f"{name}.sh:{l1 + 7}")]})
+    # ---- ping/ ----
+    # test_ping_11.sh sends its second batch (the EGRESS-style rules) to INGRESS too
+    # (:56): EGRESS stays empty with default DROP, and the replies pass as
+    # ESTABLISHED under the default AUTOMATIC mode
+    ing = batch_rules(2, lambda i: r_10(i, 31, "SYN"), 2, [ICMP_ACCEPT_IN], 3, 2, None)
+    ing2 = batch_rules(2, lambda i: r_10(i, 32, "!SYN"), 2, [ICMP_ACCEPT_OUT], 3, 2, None)
+    S.append({"name": "ping/test_ping_11", "steps": [
+        step(FWSETUP + [["batch", "INGRESS", ing], ["batch", "INGRESS", ing2]], pings_from_ns1(), "pass",
+             "ping/test_ping_11.sh:59")]})
+    S.append({"name": "ping/test_ping_21.1", "steps": [
+        step(FWSETUP + [["add", "INGRESS", i, r_10(i, 31, "SYN")] for i in range(2)] +
+             [["add", "INGRESS", 2, ICMP_ACCEPT_IN]] +
+             [["add", "EGRESS", i, r_10(i, 32, "!SYN")] for i in range(2)] +
+             [["add", "EGRESS", 2, ICMP_ACCEPT_OUT]], pings_from_ns1(), "pass", "ping/test_ping_21.1.sh:48")]})
+    # test_ping_5.1.sh: 4000 / 4000 rules per chain, an accept-all rule at 3500 / 3501
+    ing = [dict(r_10(i, 31, "SYN"), operation="append") for i in range(3500)]
+    ing += [{"operation": "append", "action": "ACCEPT"}]
+    ing += [dict(r_11(i, None, None), operation="append") for i in range(3501, 4001)]
+    egr = [dict(r_10(i, 32, "!SYN"), operation="append") for i in range(3501)]
+    egr += [{"operation": "append", "action": "ACCEPT"}]
+    egr += [dict(r_11(i, 16, "!ACK"), operation="append") for i in range(3502, 4001)]
+    S.append({"name": "ping/test_ping_5.1", "steps": [
+        step(FWSETUP + [["accept_established", "OFF"], ["batch", "INGRESS", ing], ["batch", "EGRESS", egr]],
+             pings_from_ns1(), "pass", "ping/test_ping_5.1.sh:77"),
+        step([], pings_from_host(), "pass", "ping/test_ping_5.1.sh:78")]})
+    S.append({"name": "ping/test_ping_7", "steps": [
+        step(FWSETUP + [["add", "INGRESS", 0, ICMP_ACCEPT_IN], ["add", "EGRESS", 0, ICMP_ACCEPT_OUT]],
+             pings_from_ns1(), "pass", "ping/test_ping_7.sh:36"),
+        step([], pings_from_host(), "pass", "ping/test_ping_7.sh:37")]})
+    # test_ping_1_xdp.sh runs test_ping_1.sh with an argument test_ping_1.sh never reads:
+    # the same rules and probe (replayed at the XDP hook, as every probe here)
+    S.append(dict(next(x for x in S if x["name"] == "ping/test_ping_1"), name="ping/test_ping_1_xdp"))
+    # ---- tcp/ ----
+    tcp_in = [{"src": NS1, "dst": HOST, "l4proto": "TCP", "dport": 60123, "tcpflags": f, "action": "ACCEPT"}
+              for f in ("SYN, !ACK, !RST, !FIN", "!SYN, ACK, !RST, !FIN", "!SYN, !RST, FIN")]
+    tcp_out = [{"src": HOST, "dst": NS1, "l4proto": "TCP", "sport": 60123, "tcpflags": f, "action": "ACCEPT"}
+               for f in ("SYN, ACK, !RST", "ACK, !SYN", "FIN, !SYN")]
+    # test_tcp_2.sh: its netcat client runs in the background and is not asserted
+    ing = batch_rules(126, lambda i: r_10(i, 31, "SYN"), 126, tcp_in, 129, 512, lambda i: r_11(i, None, None))
+    egr = batch_rules(127, lambda i: r_10(i, 32, "!SYN"), 127, tcp_out, 130, 260, lambda i: r_11(i, 16, "!ACK"))
+    S.append({"name": "tcp/test_tcp_2", "asserted": False, "steps": [
+        step(FWSETUP + [["batch", "INGRESS", ing], ["batch", "EGRESS", egr]], netcat_session("ns1", 60123),
+             "pass", "tcp/test_tcp_2.sh:91 (background, unasserted)")]})
+    ing = batch_rules(6001, lambda i: r_10(i, 31, "SYN"), 6001, tcp_in, 6004, 6999, lambda i: r_11(i, None, None))
+    egr = batch_rules(6997, lambda i: r_10(i, 32, "!SYN"), 127, tcp_out, 1, 0, None)
+    S.append({"name": "tcp/test_tcp_4", "steps": [
+        step(FWSETUP + [["accept_established", "OFF"], ["batch", "INGRESS", ing], ["batch", "EGRESS", egr]],
+             netcat_session("ns1", 60123), "pass", "tcp/test_tcp_4.sh:86")]})
+    ing = batch_rules(101, lambda i: r_10(i, 31, "SYN"), 101, [{"action": "ACCEPT"}], 102, 200,
+                      lambda i: r_11(i, None, None))
+    egr = [dict(r_10(i, 32, "!SYN"), operation="append") for i in range(63)]
+    egr += [{"operation": "append", "id": 63, "action": "ACCEPT"}]
+    egr += [dict({"src": f"10.1.0.{i % 255}", "dst": f"10.1.0.{i % 255}/16", "l4proto": "TCP", "sport": i,
+                  "dport": i, "tcpflags": "!ACK", "action": "DROP"}, operation="append") for i in range(64, 129)]
+    S.append({"name": "tcp/test_tcp_5", "steps": [
+        step(FWSETUP + [["accept_established", "OFF"], ["batch", "INGRESS", ing], ["batch", "EGRESS", egr]],
+             netcat_session("ns1", 60123), "pass", "tcp/test_tcp_5.sh:84")]})
+    S.append({"name": "test1", "steps": [
+        step(FWSETUP + [["add", "INGRESS", 0, ICMP_ACCEPT_IN], ["add", "EGRESS", 0, ICMP_ACCEPT_OUT]],
+             pings_from_ns1(), "pass", "test1.sh:34")]})
     return S
 
 
@@ -255,7 +453,7 @@ def main():
            "scenarios": scenarios()}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fw_scenarios.json")
     with open(path, "w") as fh:
-        json.dump(out, fh, indent=1)
+        json.dump(out, fh, separators=(",", ":"))        # compact: the rule batches hold ~30 K rules
     print(f"wrote {path}: {len(out['scenarios'])} scenarios")
 
 

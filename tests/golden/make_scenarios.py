@@ -52,6 +52,14 @@ def ping_fwd():
             pkt("egress", "veth1", "10.0.2.1", "10.0.1.1", 1, icmp_type=0)]
 
 
+def ping_fwd_rev():
+    """`ip netns exec ns2 ping 10.0.1.1`: the same exchange started from ns2."""
+    return [pkt("ingress", "veth2", "10.0.2.1", "10.0.1.1", 1, icmp_type=8),
+            pkt("egress", "veth1", "10.0.2.1", "10.0.1.1", 1, icmp_type=8),
+            pkt("ingress", "veth1", "10.0.1.1", "10.0.2.1", 1, icmp_type=0),
+            pkt("egress", "veth2", "10.0.1.1", "10.0.2.1", 1, icmp_type=0)]
+
+
 def tcp_fwd(port):
     """`netcat -nvz 10.0.2.1 <port>` from ns1: SYN forward, SYN-ACK back."""
     return [pkt("ingress", "veth1", "10.0.1.1", "10.0.2.1", 6, 40000, port, 0x02),
@@ -209,6 +217,76 @@ def scenarios():
              counters={"chain": "FORWARD", "rule": 1, "pkts": 5}),
         step([["flush", "FORWARD"], ["interactive", False]] + big + [["apply", "FORWARD"]], nping_udp(), "pass",
              counters={"chain": "FORWARD", "rule": 1, "pkts": 5}),
+    ]})
+    # ---------------- local_test1_iptables.sh ----------------
+    # local_test1.sh through the pcn-iptables CLI; `--tcp-flags SYN SYN` (mask
+    # SYN, set SYN) is the tcpflags='SYN' of local_test1.sh:30-34
+    t = "src/services/pcn-iptables/test/local_test1_iptables.sh"
+    out.append({"name": "local_test1_iptables", "source": t, "steps": [
+        step([], ping_host(), "pass", f"{t}:19"),
+        step([P("INPUT", "ACCEPT"), P("OUTPUT", "ACCEPT")], ping_host(), "pass", f"{t}:24"),
+        step([P("INPUT", "DROP")], ping_host(), "fail", f"{t}:29"),
+        step([A("INPUT", src=IP, dst="10.0.22.0/24", l4proto="TCP", sport=80, dport=90, tcpflags="SYN",
+                action="ACCEPT")], ping_host(), "fail", f"{t}:33"),
+        step([A("INPUT", src=IP, dst=IP, l4proto="TCP", sport=80, dport=90, tcpflags="SYN", action="ACCEPT")],
+             ping_host(), "fail", f"{t}:37"),
+        step([A("INPUT", src=IP, l4proto="ICMP", action="ACCEPT")], ping_host(), "pass", f"{t}:41"),
+        step([P("OUTPUT", "DROP")], ping_host(), "fail", f"{t}:46"),
+        step([A("OUTPUT", dst=IP, src="10.0.22.0/24", l4proto="TCP", sport=80, dport=90, tcpflags="SYN",
+                action="ACCEPT")], ping_host(), "fail", f"{t}:50"),
+        step([A("OUTPUT", src=IP, dst=IP, l4proto="TCP", sport=80, dport=90, tcpflags="SYN", action="ACCEPT")],
+             ping_host(), "fail", f"{t}:54"),
+        step([A("OUTPUT", dst=IP, l4proto="ICMP", action="ACCEPT")], ping_host(), "pass", f"{t}:59"),
+    ]})
+    # ---------------- local_test2_iptables.sh ----------------
+    t = "src/services/pcn-iptables/test/local_test2_iptables.sh"
+    out.append({"name": "local_test2_iptables", "source": t, "steps": [
+        step([], ping_host(), "pass", f"{t}:18"),
+        step([P("INPUT", "ACCEPT"), P("OUTPUT", "ACCEPT")], ping_host(), "pass", f"{t}:23"),
+        step([P("INPUT", "DROP")], ping_host(), "fail", f"{t}:27"),
+        step([A("INPUT", src=IP, action="ACCEPT")], ping_host(), "pass", f"{t}:31"),
+        step([I("INPUT", 0, src=IP, action="DROP")], ping_host(), "fail", f"{t}:35"),
+        step([D("INPUT", src=IP, action="DROP")], ping_host(), "pass", f"{t}:39"),
+    ]})
+    # ---------------- local_test4_iptables.sh ----------------
+    t = "src/services/pcn-iptables/test/local_test4_iptables.sh"
+    out.append({"name": "local_test4_iptables", "source": t, "steps": [
+        step([], ping_fwd(), "pass", f"{t}:41"),
+        step([P("INPUT", "DROP"), P("OUTPUT", "DROP")], ping_fwd(), "pass", f"{t}:46"),
+        step([P("FORWARD", "DROP")], ping_fwd(), "fail", f"{t}:50"),
+    ]})
+    # ---------------- local_test5_iptables.sh ----------------
+    # bidirectional FORWARD drops with insert/delete; both ping directions asserted
+    t = "src/services/pcn-iptables/test/local_test5_iptables.sh"
+    both = ping_fwd() + ping_fwd_rev()
+    out.append({"name": "local_test5_iptables", "source": t, "steps": [
+        step([], ping_fwd(), "pass", f"{t}:41"),
+        step([P("INPUT", "DROP"), P("OUTPUT", "DROP")], ping_fwd(), "pass", f"{t}:46"),
+        step([P("FORWARD", "DROP")], ping_fwd(), "fail", f"{t}:50"),
+        step([A("FORWARD", dst="10.0.2.1", src="10.0.1.1", action="DROP")], ping_fwd(), "fail", f"{t}:54"),
+        step([], ping_fwd_rev(), "fail", f"{t}:55"),
+        step([I("FORWARD", 0, src="10.0.2.1", dst="10.0.1.1", action="DROP")], ping_fwd(), "fail", f"{t}:59"),
+        step([], ping_fwd_rev(), "fail", f"{t}:60"),
+        step([P("INPUT", "ACCEPT"), P("OUTPUT", "ACCEPT")], ping_fwd(), "fail", f"{t}:65"),
+        step([], ping_fwd_rev(), "fail", f"{t}:66"),
+        step([P("INPUT", "DROP"), P("OUTPUT", "DROP"), I("FORWARD", 0, src="10.0.2.1", action="ACCEPT"),
+              I("FORWARD", 0, src="10.0.1.1", action="ACCEPT")], both, "pass", f"{t}:74-75"),
+        step([D("FORWARD", src="10.0.2.1", action="ACCEPT"), D("FORWARD", src="10.0.1.1", action="ACCEPT")],
+             ping_fwd(), "fail", f"{t}:80"),
+        step([], ping_fwd_rev(), "fail", f"{t}:81"),
+        step([D("FORWARD", dst="10.0.2.1", src="10.0.1.1", action="DROP"),
+              D("FORWARD", src="10.0.2.1", dst="10.0.1.1", action="DROP")], ping_fwd(), "fail", f"{t}:86"),
+        step([], ping_fwd_rev(), "fail", f"{t}:87"),
+        step([P("FORWARD", "DROP"), A("FORWARD", l4proto="ICMP", action="ACCEPT")], both, "pass", f"{t}:93-94"),
+    ]})
+    # ---------------- local_test7_iptables.sh ----------------
+    t = "src/services/pcn-iptables/test/local_test7_iptables.sh"
+    out.append({"name": "local_test7_iptables", "source": t, "steps": [
+        step([], ping_fwd(), "pass", f"{t}:57"),
+        step([P("INPUT", "DROP"), P("OUTPUT", "DROP")], ping_fwd(), "pass", f"{t}:62"),
+        step([P("INPUT", "ACCEPT"), P("OUTPUT", "ACCEPT"), P("FORWARD", "DROP")], ping_fwd(), "fail", f"{t}:68"),
+        step([P("INPUT", "DROP"), P("OUTPUT", "DROP"), A("FORWARD", src="10.0.1.1", action="ACCEPT"),
+              A("FORWARD", src="10.0.2.1", action="ACCEPT")], ping_fwd(), "pass", f"{t}:76"),
     ]})
     # ---------------- local_test_horus1.sh ----------------
     # `polycubectl pcn-iptables set horus=ON|OFF` only sets the flag

@@ -63,6 +63,23 @@ def ct_probe_frames(packets, stride=128):
     return f.reshape(-1), lens, ports
 
 
+def exchange_replay(packets, send_one):
+    """Replay `packets` one at a time when they carry exchange tags ("ex"): a
+    dropped packet ends its exchange, so the packets it would have caused (a
+    reply, the rest of a handshake) are never sent -- verdict -1.  Returns
+    None for an untagged probe (the caller batches it as before)."""
+    if not any("ex" in p for p in packets):
+        return None
+    out, broken = [-1] * len(packets), set()
+    for i, p in enumerate(packets):
+        if p.get("ex") in broken:
+            continue
+        out[i] = int(send_one(i))
+        if out[i] != 1:
+            broken.add(p.get("ex"))
+    return out
+
+
 def session_states(entries, ip):
     """States of the session-table rows naming `ip` (Iptables::getSessionTableList:
     src/dst restored from ipRev), as `polycubectl ... session-table show | grep ip`."""
@@ -148,6 +165,13 @@ class OracleCube:
 
     def ct_probe(self, packets):
         """Stateful: the packets in order (direction runs split into batches)."""
+        def one(k):
+            f, lens, ports = ct_probe_frames(packets[k:k + 1])
+            return self.o.classify(f, n=1, lens=lens, stride=128, in_port=ports,
+                                   direction=DIRS[packets[k]["dir"]])[0][0]
+        ex = exchange_replay(packets, one)
+        if ex is not None:
+            return ex
         out = []
         i = 0
         while i < len(packets):
@@ -163,6 +187,13 @@ class OracleCube:
         return out
 
     def probe(self, packets):
+        def one(k):
+            f, lens, ports, ct = probe_frames(packets[k:k + 1])
+            return self.o.classify(f, n=1, lens=lens, stride=128, in_port=ports,
+                                   direction=DIRS[packets[k]["dir"]], ct_status=ct)[0][0]
+        ex = exchange_replay(packets, one)
+        if ex is not None:
+            return ex
         out = []
         for d, dcode in DIRS.items():
             sel = [p for p in packets if p["dir"] == d]
@@ -216,6 +247,9 @@ class GpuCube:
         """Stateful: the packets in order (direction runs split into batches)."""
         torch = self.torch
         dev = torch.device("cuda", self.ipt.device)
+        ex = exchange_replay(packets, lambda k: self.ct_probe([_untag(packets[k])])[0])
+        if ex is not None:
+            return ex
         out = []
         i = 0
         while i < len(packets):
@@ -235,6 +269,9 @@ class GpuCube:
 
     def probe(self, packets):
         torch = self.torch
+        ex = exchange_replay(packets, lambda k: self.probe([_untag(packets[k])])[0])
+        if ex is not None:
+            return ex
         out = []
         for d, dcode in DIRS.items():
             sel = [p for p in packets if p["dir"] == d]
@@ -251,6 +288,10 @@ class GpuCube:
             torch.cuda.synchronize()
             out.extend(int(x) for x in v.cpu().numpy())
         return out
+
+
+def _untag(p):
+    return {k: v for k, v in p.items() if k != "ex"}
 
 
 # ---- pcn-firewall (tests/golden/fw_scenarios.json) ----
@@ -407,7 +448,17 @@ class OracleFwCube:
         return [tuple(x) for x in self.stats[c]], (dp - b[0], db - b[1])
 
     def probe(self, packets):
-        """In order, direction runs split into batches; returns (verdicts, labels)."""
+        """In order, direction runs split into batches; returns (verdicts, labels).
+        Exchange-tagged probes go one packet at a time (exchange_replay); an
+        unsent packet has verdict -1 and label None."""
+        if any("ex" in p for p in packets):
+            labels = [None] * len(packets)
+
+            def one(k):
+                v, lab = self.probe([_untag(packets[k])])
+                labels[k] = lab[0]
+                return v[0]
+            return exchange_replay(packets, one), labels
         out, labels = [], []
         i = 0
         while i < len(packets):
@@ -477,6 +528,15 @@ class GpuFwCube:
     def probe(self, packets, labels):
         torch = self.torch
         dev = torch.device("cuda", self.fw.device)
+        if any("ex" in p for p in packets):
+            rids = [None] * len(packets)
+
+            def one(k):
+                lab = None if labels is None else [labels[k] if labels[k] is not None else 0]
+                v, r = self.probe([_untag(packets[k])], lab)
+                rids[k] = r[0]
+                return v[0]
+            return exchange_replay(packets, one), rids
         out, rids = [], []
         i = 0
         while i < len(packets):

@@ -79,6 +79,9 @@ def test_reference_conntrack_scenarios_on_gpu(dev, sc):
             v = cube.ct_probe(st["probe"])
             got = "pass" if all(x == 1 for x in v) else "fail"
             assert got == st["expect"], f"{sc['name']} step {k} ({st.get('ref_line')}): {v}"
+            if "drop_at" in st:
+                d = st["drop_at"]
+                assert v[d] == 0 and all(x == 1 for x in v[:d]), f"{sc['name']} step {k}: {v}"
         if "session" in st:
             assert st["session"]["state"] in session_states(ipt.ct_dump(), st["session"]["match"])
 

@@ -31,7 +31,10 @@ def test_reference_conntrack_scenarios_on_oracle(sc):
         if "probe" in st:
             v = c.ct_probe(st["probe"])
             got = "pass" if all(x == 1 for x in v) else "fail"
-            if st["expect"] == "fail":
+            if "drop_at" in st:                  # exchange-tagged: every packet before it passed
+                d = st["drop_at"]
+                assert v[d] == 0 and all(x == 1 for x in v[:d]), f"{sc['name']} step {k}: {v}"
+            elif st["expect"] == "fail":
                 assert v[0] == 0, f"{sc['name']} step {k}: {v}"
             assert got == st["expect"], f"{sc['name']} step {k} ({st.get('ref_line')}): {v}"
         if "session" in st:

@@ -23,6 +23,16 @@ echo "== bench"; timeout -k 10 600 python bench.py --steps $STEPS --warmup 10 > 
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; tail -3 gpurun_out/bench_$TAG.err
 if fatal $rc; then exit $rc; fi
 
+if [ "${SKIP_MULTI:-0}" != 1 ]; then
+  # bench.py launches its own ranks (--gpus 2, no WORLD_SIZE); on a one-GPU box both share
+  # device 0 (PCN_BENCH_DEVICE), RCCL refuses that, and the counter blocks go through gloo
+  echo "== bench --gpus 2"
+  PCN_BENCH_DEVICE=0 timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-e2e --no-ct --no-fw \
+    > gpurun_out/bench_${TAG}_2rank.json 2> gpurun_out/bench_${TAG}_2rank.err
+  rc=$?; echo "bench 2-rank rc=$rc"; cat gpurun_out/bench_${TAG}_2rank.json; tail -3 gpurun_out/bench_${TAG}_2rank.err
+  if fatal $rc; then exit $rc; fi
+fi
+
 if [ "${SKIP_PROF:-0}" != 1 ]; then
   echo "== rocprofv3 kernel trace"
   cd /tmp && export TMPDIR=/tmp
