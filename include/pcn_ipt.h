@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 6
+#define PCN_IPT_ABI_VERSION 7
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -277,12 +277,18 @@ int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain);
  * While enabled, pcn_ipt_classify labels every IPv4 packet from the table and
  * every accepted packet updates it, with the result of running the batch one
  * packet at a time in index order (and batches in submission order).
- * Differences from the kernel LRU: entries are never evicted; an insert that
- * finds no free slot within 512 slots of the key's home slot (a full or
- * nearly full table) is dropped and counted (pcn_ipt_ct_info.inserts_lost),
- * which bounds every lookup at 512 probes.  Entries
- * never expire in the reference either (ttl is written, never compared).
- * batch.ct_status must be NULL while enabled. */
+ * Capacity: the reference's lru_hash holds 65536 entries.  Here the LRU works
+ * at batch granularity: a packet touches its table key (its own, an ICMP
+ * error's quoted one) when the entry is live after it; after each batch the
+ * least recently touched live entries are deleted down to max_entries
+ * (pcn_ipt_ct_set_max_entries: 65536 by default, 0 = unbounded), counted in
+ * pcn_ipt_ct_info.evicted.  Within a batch nothing is evicted (the kernel's
+ * own LRU is approximate: per-CPU lists, reference bits).  Independently of
+ * that, an insert that finds no free slot within 512 slots of the key's home
+ * slot (a full or nearly full table: 2^capacity_log2 slots, deleted keys keep
+ * theirs) is dropped and counted (inserts_lost), which bounds every lookup at
+ * 512 probes.  Entries never expire in the reference either (ttl is written,
+ * never compared).  batch.ct_status must be NULL while enabled. */
 typedef struct {
   uint32_t src_ip, dst_ip;   /* ct_k as stored: ordered NBO u32 */
   uint16_t sport, dport;     /* ct_k ports as stored: ordered NBO u16 */
@@ -294,11 +300,16 @@ typedef struct {
   uint32_t enabled, capacity_log2;
   uint64_t now;              /* timestamp used for new ttl values */
   uint64_t inserts_lost;     /* inserts refused: no free slot near the key's home (table (nearly) full) */
+  uint64_t max_entries;      /* live entries kept after each batch (LRU; 0 = unbounded) */
+  uint64_t evicted;          /* entries deleted by the LRU so far */
 } pcn_ipt_ct_info;
 /* capacity = 2^capacity_log2 slots (0 => 2^18); the table persists across enable/disable. */
 int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2);
 int pcn_ipt_ct_disable(pcn_ipt *ctx);
 int pcn_ipt_ct_clear(pcn_ipt *ctx);
+/* Live entries kept after each batch (default 65536, the lru_hash size of
+ * Iptables_ConntrackLabel_dp.c:112; 0 = unbounded); takes effect at the next batch. */
+int pcn_ipt_ct_set_max_entries(pcn_ipt *ctx, uint64_t max_entries);
 /* The `timestamp` percpu value ConntrackTableUpdate::updateTimestamp writes
  * every second (modules/ConntrackTableUpdate.cpp:108-137). */
 int pcn_ipt_ct_set_time(pcn_ipt *ctx, uint64_t ns);

@@ -56,6 +56,8 @@ def lib():
         h.orc_ct_enable.argtypes = [vp, C.c_int]
         h.orc_ct_set_time.argtypes = [vp, C.c_uint64]
         h.orc_ct_dump.argtypes = [vp, vp, C.c_uint32]
+        h.orc_ct_set_max_entries.argtypes = [vp, C.c_uint64]
+        h.orc_ct_info.argtypes = [vp, u64p]
         h.orc_apply_accept_established.argtypes = [vp, C.c_int]
         h.orc_set_accept_established.argtypes = [vp, C.c_int, C.c_int]
         h.orc_get_accept_established.argtypes = [vp, C.c_int]
@@ -158,6 +160,15 @@ class Oracle:
 
     def ct_set_time(self, ns):
         assert lib().orc_ct_set_time(self._h, int(ns)) == 0
+
+    def ct_set_max_entries(self, m):
+        """Live entries kept after each batch (LRU over the touches; 0: unbounded)."""
+        assert lib().orc_ct_set_max_entries(self._h, int(m)) == 0
+
+    def ct_info(self):
+        out = (C.c_uint64 * 4)()
+        assert lib().orc_ct_info(self._h, out) == 0
+        return {"live": out[0], "evicted": out[1], "max_entries": out[2], "seq": out[3]}
 
     def ct_dump(self, cap=1 << 20):
         out = np.zeros(cap, CT_ENTRY)

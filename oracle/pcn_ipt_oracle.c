@@ -805,8 +805,16 @@ static int ct_label_empty(int proto, uint8_t flags, int icmp_type) {
  *    (the control plane only lists it, Iptables.cpp:527-566).  `now` is the
  *    `timestamp` percpu value the control plane refreshes every second
  *    (modules/ConntrackTableUpdate.cpp:108-137); tests set it explicitly.
- *  - The table here is unbounded: parity with the kernel LRU holds while the
- *    live flows fit its 65536 entries (LRU eviction is not restated).
+ *  - Capacity (the lru_hash's 65536 entries, :112): restated at batch
+ *    granularity.  A packet touches its table key (its own, or for an ICMP
+ *    error the quoted one) when the entry is live after the packet; the touch
+ *    stamp is (batch sequence << 32 | index in the batch).  After a batch, if
+ *    more than max_entries are live, the live entries with the oldest stamps
+ *    are deleted down to max_entries (exact LRU over the touches; within a
+ *    batch nothing is evicted, so a connection the kernel would evict mid-batch
+ *    stays visible to the batch's later packets).  The kernel's own LRU is
+ *    approximate (per-CPU free lists, reference bits), so no order is more
+ *    faithful than this one; the GPU applies the same rule (conntrack.hip).
  *  - `packet` is one per-CPU struct shared by ingress and egress
  *    (Iptables_Parser_dp.c:44-56): the Parser writes srcPort/dstPort only for
  *    TCP/UDP (:122-143), so an ICMP packet's conntrack key carries the ports
@@ -830,11 +838,13 @@ enum { ST_NEW = 0, ST_ESTABLISHED, ST_RELATED, ST_INVALID, ST_SYN_SENT, ST_SYN_R
 
 typedef struct { uint32_t src, dst; uint8_t proto; uint16_t sport, dport; } ctk_t;  /* struct ct_k */
 typedef struct { uint64_t ttl; uint8_t state, ipRev, portRev; uint32_t seq; } ctv_t; /* struct ct_v */
-typedef struct { ctk_t k; ctv_t v; int used; } cte_t;    /* used: 0 empty, 1 live, 2 deleted */
+typedef struct { ctk_t k; ctv_t v; int used; uint64_t touch; } cte_t;    /* used: 0 empty, 1 live, 2 deleted */
 
 struct ctstate {
   cte_t *tab; size_t cap, live, used;
   uint64_t now;
+  uint64_t bseq, max_entries, evicted;  /* LRU at batch granularity (see above) */
+  ctk_t tkey; int has_tkey;             /* the current packet's table key */
   /* the shared per-CPU `packet` struct: fields the Parser leaves stale */
   uint16_t sport, dport; uint32_t seq, ack; uint8_t flags;
 };
@@ -915,6 +925,51 @@ static inline int synack_only(uint8_t f) {
   return (f & TCPHDR_ACK) && (f & TCPHDR_SYN) && (f | (TCPHDR_SYN | TCPHDR_ACK)) == (TCPHDR_SYN | TCPHDR_ACK);
 }
 static inline uint16_t ld16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+
+/* The key a labelled packet is tracked under for the LRU touch: its own, or
+ * an ICMP error's quoted header's; none for packets that never reach the table
+ * (short ICMP dropped, timestamp/info types, other protocols). */
+static void ct_note_key(struct ctstate *t, const ctpkt_t *p, const uint8_t *f, uint32_t L) {
+  uint8_t a, b;
+  t->has_tkey = 0;
+  if (p->proto == 6 || p->proto == 17) {
+    t->tkey = ct_key(p, &a, &b);
+    t->has_tkey = 1;
+  } else if (p->proto == 1 && L >= 42) {
+    const uint8_t type = f[34];
+    if (type == 8 || type == 0) {
+      t->tkey = ct_key(p, &a, &b);
+      t->has_tkey = 1;
+    } else if (!(type >= 13 && type <= 18) && L >= 70) {
+      uint32_t is = ld32(f + 54), id = ld32(f + 58);
+      uint16_t x = ld16(f + 62), y = ld16(f + 64);
+      t->tkey = (ctk_t){is <= id ? is : id, is <= id ? id : is, f[51], x <= y ? x : y, x <= y ? y : x};
+      t->has_tkey = 1;
+    }
+  }
+}
+
+/* After a batch: delete the least recently touched live entries down to
+ * max_entries (0: unbounded); then the next batch's sequence number. */
+static int cmp_touch(const void *a, const void *b) {
+  const uint64_t x = (*(cte_t *const *)a)->touch, y = (*(cte_t *const *)b)->touch;
+  return x < y ? -1 : x > y;
+}
+static void ct_end_batch(struct ctstate *t) {
+  if (t->max_entries && t->live > t->max_entries) {
+    cte_t **ls = malloc(t->live * sizeof *ls);
+    size_t m = 0;
+    for (size_t i = 0; i < t->cap; i++)
+      if (t->tab[i].used == 1) ls[m++] = &t->tab[i];
+    qsort(ls, m, sizeof *ls, cmp_touch);
+    const size_t k = m - t->max_entries;
+    for (size_t i = 0; i < k; i++) ls[i]->used = 2;
+    t->live -= k;
+    t->evicted += k;
+    free(ls);
+  }
+  t->bseq++;
+}
 
 /* ConntrackLabel_dp.c:190-531: the packet's connStatus, or -1 for RX_DROP
  * (the ICMP length checks, :441-443, :486-505). */
@@ -1170,6 +1225,7 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
     ct = ct_in >= 0 ? ct_in : CT_NEW; /* DISABLED: connStatus is never written (per-CPU zero) */
     if (c->fw_ct_mode != FW_CT_DISABLED) {
       if (st) {
+        ct_note_key(st, &cp, f, L);
         ct = ct_label(st, &cp, f, L);                  /* Firewall_ConntrackLabel_dp.c:116-460 */
         if (ct < 0) return RX_DROP;
       } else {
@@ -1227,6 +1283,7 @@ static int classify_one(const orc_ctx *c, int dir, int hook, const uint8_t *f, u
   }
 labeling:
   if (st) {
+    ct_note_key(st, &cp, f, L);
     ct = ct_label(st, &cp, f, L);                    /* ConntrackLabel_dp.c:190-531 */
     if (ct < 0) return RX_DROP;
     *label = ct;
@@ -1345,7 +1402,12 @@ static void *run_job(void *arg) {
     int ct = j->ct ? j->ct[i] : -1;
     int32_t rid;
     int lab;
+    if (j->st) j->st->has_tkey = 0;
     int v = classify_one(j->c, j->dir, j->hook, f, L, port, ct, &j->pc, &rid, j->st, &lab, j->hzp, j->hz);
+    if (j->st && j->st->has_tkey) {         /* the LRU touch: the entry is live after this packet */
+      cte_t *e = ct_find(j->st, &j->st->tkey);
+      if (e) e->touch = j->st->bseq << 32 | i;
+    }
     if (j->labels) j->labels[i] = (uint8_t)lab;
     j->verdicts[i] = v == RX_DROP ? 0 : 1;
     if (j->rule_ids) j->rule_ids[i] = rid;
@@ -1412,6 +1474,8 @@ int orc_classify_labels(orc_ctx *c, int dir, int hook, const uint8_t *frames, co
     free(jobs[t].pc.hz_pkts); free(jobs[t].pc.hz_bytes);
   }
   free(jobs); free(th);
+  /* a batch that ran the table (pcn-firewall DISABLED does not) */
+  if (c->ct && n && !(c->service == ORC_SVC_FIREWALL && c->fw_ct_mode == FW_CT_DISABLED)) ct_end_batch(c->ct);
   return 0;
 }
 
@@ -1421,6 +1485,8 @@ int orc_ct_enable(orc_ctx *c, int on) {
   if (on && !c->ct) {
     c->ct = calloc(1, sizeof(struct ctstate));
     if (!c->ct) return -ENOMEM;
+    c->ct->bseq = 1;
+    c->ct->max_entries = 65536;               /* connections: lru_hash of 65536 (ConntrackLabel_dp.c:112) */
   } else if (!on && c->ct) {
     ct_free(c->ct);
     c->ct = NULL;
@@ -1431,6 +1497,18 @@ int orc_ct_enable(orc_ctx *c, int on) {
 int orc_ct_set_time(orc_ctx *c, uint64_t ns) {
   if (!c->ct) return -EINVAL;
   c->ct->now = ns;
+  return 0;
+}
+
+int orc_ct_set_max_entries(orc_ctx *c, uint64_t max) {
+  if (!c->ct) return -EINVAL;
+  c->ct->max_entries = max;
+  return 0;
+}
+
+int orc_ct_info(orc_ctx *c, uint64_t out[4]) {
+  if (!c->ct) return -EINVAL;
+  out[0] = c->ct->live; out[1] = c->ct->evicted; out[2] = c->ct->max_entries; out[3] = c->ct->bseq;
   return 0;
 }
 

@@ -132,6 +132,11 @@ typedef struct {
 int orc_ct_enable(orc_ctx *c, int on);
 int orc_ct_set_time(orc_ctx *c, uint64_t ns);
 int orc_ct_dump(orc_ctx *c, orc_ct_entry *out, uint32_t cap);
+/* Capacity: after a batch the least recently touched live entries are deleted
+ * down to max (0: unbounded; 65536 at enable, the lru_hash size).  info:
+ * {live entries, evicted so far, max_entries, next batch sequence}. */
+int orc_ct_set_max_entries(orc_ctx *c, uint64_t max);
+int orc_ct_info(orc_ctx *c, uint64_t out[4]);
 /* accept-established optimization (rule 0 == {conntrack ESTABLISHED, ACCEPT}) */
 int orc_apply_accept_established(orc_ctx *c, int chain);
 int orc_set_accept_established(orc_ctx *c, int chain, int on);

@@ -551,9 +551,10 @@ struct Cache {              // the key a walking lane last touched, its slot and
   CtSlot *e;                // slot holding k (live or deleted), or null
   Ent v;
   bool valid, dirty;
+  uint32_t touch;           // 1 + the batch index of the last packet after which k was live (0: none)
 };
 
-__device__ __forceinline__ void flush(Cache &c) {
+__device__ __forceinline__ void flush(const CtTable &t, Cache &c) {
   if (c.dirty && c.e) {     // the value half in one store (proto is the key's)
     ct_u32x4 hi;
     hi.x = static_cast<uint32_t>(c.v.ttl);
@@ -562,13 +563,15 @@ __device__ __forceinline__ void flush(Cache &c) {
     hi.w = uint32_t(c.k.proto) | uint32_t(c.v.live) << 8 | uint32_t(c.v.state) << 16 | uint32_t(c.v.rev) << 24;
     reinterpret_cast<ct_u32x4 *>(c.e)[1] = hi;
   }
+  if (c.touch && c.e) t.touch[c.e - t.slots] = static_cast<unsigned long long>(t.seq) << 32 | (c.touch - 1);
   c.dirty = false;
+  c.touch = 0;
 }
 
 // connections.lookup: makes k the cached key; returns whether it is live (value in c.v).
 __device__ __forceinline__ bool lookup(const CtTable &t, Cache &c, const Key &k) {
   if (!c.valid || !same(c.k, k)) {
-    flush(c);
+    flush(t, c);
     c.k = k;
     const SlotRef r = table_slot(t, k, false);
     c.e = r.e;
@@ -600,9 +603,19 @@ __device__ __forceinline__ bool synack_only(uint8_t f) {
   return (f & ACK) && (f & SYN) && (f | (SYN | ACK)) == (SYN | ACK);
 }
 
-// ConntrackLabel_dp.c:230-433 for TCP/UDP/echo/echo-reply(short)/errors
-// against the entry e (live or not); -1 = RX_DROP.
-__device__ int label_of(const CtRec &r, bool live, const Ent &e) {
+// A long echo reply's quoted header (ConntrackLabel_dp.c:491-529), read
+// without touching the walking lane's cache.  Only K_HARD records whose
+// quoted key bucket holds no packet of the batch are walked (ct_hard_split),
+// so nothing in this launch writes that key: the read is exact wherever in
+// the walk it happens.
+__device__ __forceinline__ bool quoted_live(const CtTable &t, const CtRec &r) {
+  const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
+  return table_slot(t, q, false).v.live;
+}
+
+// ConntrackLabel_dp.c:230-433 for TCP/UDP/echo/echo-replies/errors against the
+// entry e (live or not); -1 = RX_DROP.
+__device__ int label_of(const CtTable &t, const CtRec &r, bool live, const Ent &e) {
   const bool fwd = live && e.rev == r.rev;
   const bool rev = live && ((e.rev ^ r.rev) == 3);
   switch (r.kind) {
@@ -629,6 +642,9 @@ __device__ int label_of(const CtRec &r, bool live, const Ent &e) {
   case K_REPLY:                                   // < 70 bytes: the miss path drops
     if (!live) return ST_INV;
     return rev ? ST_EST : -1;
+  case K_HARD:                                    // >= 70 bytes: ICMP_MISS reads the quoted header
+    if (!live) return ST_INV;
+    return rev ? ST_EST : quoted_live(t, r) ? ST_REL : ST_INV;
   case K_ERR:
     return live ? ST_REL : ST_INV;
   default:
@@ -721,7 +737,7 @@ __device__ __forceinline__ int32_t outcome(const CtBatch &b, int32_t o0, int32_t
 __device__ __forceinline__ int32_t process(const CtBatch &b, const CtTable &t, Cache &c, const WalkRec &w) {
   const CtRec &r = w.r;
   const bool live = lookup(t, c, Key{r.src, r.dst, r.sport, r.dport, r.proto});
-  const int l = label_of(r, live, c.v);
+  const int l = label_of(t, r, live, c.v);
   const int32_t o = outcome(b, w.o0, w.o1, w.o2, w.o3, r, l);
   if ((o & 1) == PCN_IPT_ACCEPT && l >= 0 && r.kind != K_ERR) update(t, c, r, l);
   return o;
@@ -761,8 +777,9 @@ __device__ __forceinline__ bool fast_step(const CtBatch &b, const CtTable &t, Ca
 
 __device__ __forceinline__ int32_t step(const CtBatch &b, const CtTable &t, Cache &c, const WalkRec &w) {
   int32_t o;
-  if (PCN_CT_FAST && fast_step(b, t, c, w, o)) return o;
-  return process(b, t, c, w);
+  if (!(PCN_CT_FAST && fast_step(b, t, c, w, o))) o = process(b, t, c, w);
+  if (c.v.live && c.e) c.touch = w.idx + 1;        // the LRU touch (the cached key is the record's)
+  return o;
 }
 
 // After the sort: walk records in sorted order (each walking lane then reads
@@ -987,7 +1004,7 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
                    static_cast<uint8_t>((sv >> 1) & 1)};
         cc.valid = true;
         cc.dirty = false;
-        const int l = label_of(r, cc.v.live, cc.v);
+        const int l = label_of(t, r, cc.v.live, cc.v);
         o = outcome(b, w.o0, w.o1, w.o2, w.o3, r, l);
         if ((o & 1) == PCN_IPT_ACCEPT && l >= 0 && r.kind != K_ERR) update<true>(t, cc, r, l);
         cls = !cc.valid ? 2
@@ -1002,6 +1019,9 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
       if (mine) put_outcome(b, sres, base + lane, w.idx, o);
       const bool anyd = __ballot(mine && cls == 0 && cc.dirty) != 0;
       if (lane == 0 && anyd) c.dirty = true;
+      // the LRU touch: records that leave the connection as it is touch it if it is live
+      const uint32_t lidx = __shfl(w.idx, end > u0 ? end - 1 : u0);
+      if (lane == 0 && end > u0 && (sv & 2)) c.touch = lidx + 1;
       u0 = end;
       if (u0 < m) {
         const int ecls = __shfl(cls, u0);
@@ -1015,10 +1035,12 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
           const uint32_t ns = __shfl(cc.v.seq, u0);
           const uint32_t nf = __shfl(uint32_t(cc.v.state) | uint32_t(cc.v.rev) << 8 | uint32_t(cc.v.live) << 16 |
                                          uint32_t(cc.dirty) << 24, u0);
+          const uint32_t cidx = __shfl(w.idx, u0);
           if (lane == 0) {
             c.v = Ent{uint64_t(nh) << 32 | nl, ns, static_cast<uint8_t>(nf), static_cast<uint8_t>(nf >> 8),
                       static_cast<uint8_t>(nf >> 16)};
             if (nf >> 24) c.dirty = true;
+            if (c.v.live && c.e) c.touch = cidx + 1;
           }
         } else {                                      // the record that needs the table: the full step
           const WalkRec x = buf[cur][u0];
@@ -1034,7 +1056,7 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
                dbg_rounds, dbg_changes, dbg_steps);
 #endif
       if (lane == 0) {
-        flush(c);
+        flush(t, c);
         *cursor_j = static_cast<uint32_t>(base + m);
       }
       return;
@@ -1050,49 +1072,319 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
 
 struct WalkPlan {
   uint32_t cnt[kRunClasses];       // runs per class
-  uint32_t blk0[kRunClasses + 1];  // first block of each class
+  uint32_t blk0[kRunClasses + 1];  // first virtual block of each class
 };
 
-__global__ void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t *sres, const uint32_t *heads,
-                               WalkPlan plan, uint32_t *cursor, uint64_t hi, int first) {
-  if (blockIdx.x < plan.blk0[1]) {             // 64-thread blocks: one wave per long run
-    walk_long(b, t, wrec, sres, heads[blockIdx.x], &cursor[blockIdx.x], hi, first);
+// The batch's control words (CtScratch::ctl, u32), all on the device: the walk
+// is planned and sized there, so ct_run never reads anything back (the stream
+// stays asynchronous).
+constexpr uint32_t kCtlHard = 0;      // long echo replies (K_HARD) in hard_list
+constexpr uint32_t kCtlClass = 1;     // [1..5] runs per length class (ct_heads)
+constexpr uint32_t kCtlChunk = 8;     // ct_prep's chunk counter
+constexpr uint32_t kCtlTh = 9;        // K_HARD records the walk cannot take (th_list)
+constexpr uint32_t kCtlThFirst = 10;  // 0xFFFFFFFF - the first of them (0: none)
+constexpr uint32_t kCtlLive = 12;     // LRU: live entries after the batch (ct_ev_pass 0)
+constexpr uint32_t kCtlEvict = 13;    //      1 when more than max_entries are live
+constexpr uint32_t kCtlEvK = 14;      //      rank (1-based) of the newest stamp to evict, within the prefix
+constexpr uint32_t kCtlEvDone = 15;   //      workgroups done with the current pass
+constexpr uint32_t kCtlPlan = 16;     // WalkPlan (ct_plan)
+constexpr uint32_t kCtlEvPrefix = 28; // u64: the stamp digits chosen so far
+constexpr uint32_t kCtlZero = 32;     // words zeroed per batch
+constexpr uint32_t kCtlWords = 64;
+
+__global__ void ct_plan_kernel(uint32_t *ctl) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  WalkPlan *plan = reinterpret_cast<WalkPlan *>(ctl + kCtlPlan);
+  uint32_t b0 = 0;
+  for (uint32_t c = 0; c < kRunClasses; ++c) {
+    const uint32_t cnt = ctl[kCtlClass + c];
+    plan->cnt[c] = cnt;
+    plan->blk0[c] = b0;
+    b0 += c == 0 ? cnt : (cnt + 63) / 64;      // one wave per long run, one lane per shorter run
+  }
+  plan->blk0[kRunClasses] = b0;
+}
+
+__device__ __forceinline__ uint64_t walk_hi(const CtBatch &b, const uint32_t *ctl) {
+  const uint32_t th = ctl[kCtlThFirst];
+  return th ? uint64_t(0xFFFFFFFFu - th) : b.n;
+}
+
+// Virtual block vb of the plan (one 64-lane wave): a long run, or up to 64
+// shorter runs of one class, one per lane, each from its head (first) or its
+// cursor up to batch index hi.  Every lane returns here (no early exit), so a
+// persistent wave can take the next block.
+__device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, const uint32_t *heads,
+                        const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first, uint32_t vb) {
+  if (vb < plan->blk0[1]) {                       // one wave per long run
+    walk_long(b, t, wrec, sres, heads[vb], &cursor[vb], hi, first);
     return;
   }
   uint32_t cls = 1;
-  while (cls + 1 < kRunClasses && blockIdx.x >= plan.blk0[cls + 1]) ++cls;
-  const uint32_t jj = (blockIdx.x - plan.blk0[cls]) * blockDim.x + threadIdx.x;
-  if (jj >= plan.cnt[cls]) return;
-  const uint64_t j = class_off(b.n, cls) + jj;
-  const uint32_t p = heads[j];
-  const uint32_t k = wrec.key(p);
-  uint64_t q = first ? p : cursor[j];
-  const uint64_t last = b.n - 1;
-  Cache c{};
-  // two records in flight in named registers, A/B alternating (a register
-  // move of an in-flight load would wait for it), and the batch indices of
-  // the two after them (the record loads never wait on an index load)
-  auto ix = [&](uint64_t r) -> uint64_t {
-    r = r < last ? r : last;
-    return PCN_CT_GATHER ? r : wrec.sidx[r];
-  };
-  WalkRec A = load_rec(&wrec.rec[ix(q)]);
-  WalkRec B = load_rec(&wrec.rec[ix(q + 1)]);
-  uint64_t IA = ix(q + 2), IB = ix(q + 3);
-  for (;;) {
-    if (q >= b.n || A.key != k || A.idx >= hi) break;
-    put_outcome(b, sres, q, A.idx, step(b, t, c, A));
-    A = load_rec(&wrec.rec[IA]);
-    IA = ix(q + 4);
-    ++q;
-    if (q >= b.n || B.key != k || B.idx >= hi) break;
-    put_outcome(b, sres, q, B.idx, step(b, t, c, B));
-    B = load_rec(&wrec.rec[IB]);
-    IB = ix(q + 4);
-    ++q;
+  while (cls + 1 < kRunClasses && vb >= plan->blk0[cls + 1]) ++cls;
+  const uint32_t jj = (vb - plan->blk0[cls]) * 64 + threadIdx.x;
+  if (jj < plan->cnt[cls]) {
+    const uint64_t j = class_off(b.n, cls) + jj;
+    const uint32_t p = heads[j];
+    const uint32_t k = wrec.key(p);
+    uint64_t q = first ? p : cursor[j];
+    const uint64_t last = b.n - 1;
+    Cache c{};
+    // two records in flight in named registers, A/B alternating (a register
+    // move of an in-flight load would wait for it), and the batch indices of
+    // the two after them (the record loads never wait on an index load)
+    auto ix = [&](uint64_t r) -> uint64_t {
+      r = r < last ? r : last;
+      return PCN_CT_GATHER ? r : wrec.sidx[r];
+    };
+    WalkRec A = load_rec(&wrec.rec[ix(q)]);
+    WalkRec B = load_rec(&wrec.rec[ix(q + 1)]);
+    uint64_t IA = ix(q + 2), IB = ix(q + 3);
+    for (;;) {
+      if (q >= b.n || A.key != k || A.idx >= hi) break;
+      put_outcome(b, sres, q, A.idx, step(b, t, c, A));
+      A = load_rec(&wrec.rec[IA]);
+      IA = ix(q + 4);
+      ++q;
+      if (q >= b.n || B.key != k || B.idx >= hi) break;
+      put_outcome(b, sres, q, B.idx, step(b, t, c, B));
+      B = load_rec(&wrec.rec[IB]);
+      IB = ix(q + 4);
+      ++q;
+    }
+    flush(t, c);
+    cursor[j] = static_cast<uint32_t>(q);
   }
-  flush(c);
-  cursor[j] = static_cast<uint32_t>(q);
+}
+
+// The walk: one 64-lane workgroup per virtual block of the device-side plan
+// (long runs first), up to the first long echo reply it cannot take (or the
+// batch end).  The host launches the plan's upper bound, n / 64 + 6 blocks
+// (a run of class 0 has >= 64 packets, a lane of the others >= 1), and the
+// blocks past the plan return at once: a workgroup that returns costs the
+// dispatcher next to nothing, where a persistent grid taking blocks from one
+// counter serialised ~10^5 atomics on one address (7.1 vs 2.9 ms a batch).
+__global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t *sres,
+                                                     const uint32_t *heads, const uint32_t *ctl, uint32_t *cursor) {
+  // (the plan is read in place: a local copy indexed by class went to scratch)
+  const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
+  const uint32_t vb = blockIdx.x;
+  if (vb >= plan->blk0[kRunClasses]) return;
+  walk_vb(b, t, wrec, sres, heads, plan, cursor, walk_hi(b, ctl), 1, vb);
+}
+
+// An echo reply long enough to quote a header (ConntrackLabel_dp.c:450-531)
+// whose quoted key bucket also has packets in the batch, so that key's state
+// at its position is only known once everything before it has been walked:
+// its own key decides ESTABLISHED; otherwise ICMP_MISS reads the quoted key.
+__device__ void hard_step(const CtBatch &b, const CtTable &t, const WalkRec *brec, uint32_t i) {
+  const CtRec r = brec[i].r;
+  Cache c2{};
+  const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
+  const bool quoted = lookup(t, c2, q);            // read-only
+  Cache c{};
+  const bool live = lookup(t, c, Key{r.src, r.dst, r.sport, r.dport, r.proto});
+  const int l = !live ? ST_INV : ((c.v.rev ^ r.rev) == 3) ? ST_EST : quoted ? ST_REL : ST_INV;
+  const int32_t o = outcome(b, pack_outcome(b, 0, i), pack_outcome(b, 1, i), pack_outcome(b, 2, i),
+                            pack_outcome(b, 3, i), r, l);
+  if ((o & 1) == PCN_IPT_ACCEPT && l >= 0) update(t, c, r, l);
+  if (c.v.live && c.e) c.touch = i + 1;
+  flush(t, c);
+  b.verdicts[i] = static_cast<uint8_t>(o & 1);
+  b.rule_ids[i] = o >> 1;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t u = __shfl_xor(v, o);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+
+// The rest of the batch from the first long echo reply the walk could not
+// take, in one wave: that reply (its own and its quoted key read from the
+// table, everything before it being done), then every run walked on from its
+// cursor up to the next such reply, and so on to the batch end.  A batch
+// without them returns at once.  (These need an echo-reply payload that reads
+// as a header of a connection with packets in the same batch: rare, and slow
+// here, but exact.)
+__global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const RecSrc wrec, const WalkRec *brec,
+                                                     int32_t *sres, const uint32_t *heads, const uint32_t *ctl,
+                                                     const uint32_t *th_list, uint32_t *cursor) {
+  const uint32_t th = ctl[kCtlThFirst];
+  if (!th) return;
+  const uint32_t nth = ctl[kCtlTh];
+  const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
+  const uint32_t total = plan->blk0[kRunClasses];
+  uint32_t cur = 0xFFFFFFFFu - th;
+  for (;;) {
+    if (threadIdx.x == 0) hard_step(b, t, brec, cur);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // its table writes before any lane reads on
+    __syncthreads();
+    uint32_t nxt = 0xFFFFFFFFu;
+    for (uint32_t k = threadIdx.x; k < nth; k += 64) {
+      const uint32_t v = th_list[k];
+      if (v > cur && v < nxt) nxt = v;
+    }
+    nxt = wave_min(nxt);
+    const uint64_t hi = nxt == 0xFFFFFFFFu ? b.n : nxt;
+    for (uint32_t vb = 0; vb < total; ++vb) {
+      walk_vb(b, t, wrec, sres, heads, plan, cursor, hi, 0, vb);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __syncthreads();
+    }
+    if (nxt == 0xFFFFFFFFu) return;
+    cur = nxt;
+  }
+}
+
+// ---- LRU at batch granularity (Iptables_ConntrackLabel_dp.c:112: lru_hash of
+// 65536) ----
+// After the walk, if more than max_entries entries are live, the live entries
+// with the oldest touch stamps (batch seq << 32 | batch index of the last
+// packet after which each was live; distinct, since a packet touches one key)
+// are deleted down to max_entries.  The cut is a radix select on the 64-bit
+// stamps: six passes of 11 / 11 / 11 / 11 / 11 / 9 bits, each a histogram of
+// the live stamps that match the digits chosen so far; the last workgroup of a
+// pass picks the next digit (no grid-wide wait).  Pass 0 also counts the live
+// entries; every later pass and the eviction return at once when nothing is
+// to be evicted.
+constexpr uint32_t kEvBins = 2048;
+constexpr int kEvPasses = 6;
+__device__ __forceinline__ uint32_t ev_shift(int p) { return p < 5 ? 53 - 11 * p : 0; }
+__device__ __forceinline__ uint32_t ev_width(int p) { return p < 5 ? 11 : 9; }
+
+__device__ __forceinline__ bool slot_live(const CtSlot *e) {
+  return ((slot_half(e, 1).w >> 8) & 0xff) != 0;    // valid (a claimed or empty slot reads 0)
+}
+
+__global__ __launch_bounds__(256) void ct_ev_pass_kernel(CtTable t, uint32_t *ctl, uint32_t *hist, int p) {
+  __shared__ uint32_t h[kEvBins];
+  __shared__ uint32_t live_s;
+  __shared__ bool last;
+  if (p > 0 && !ctl[kCtlEvict]) return;
+  for (uint32_t k = threadIdx.x; k < kEvBins; k += blockDim.x) h[k] = 0;
+  if (threadIdx.x == 0) live_s = 0;
+  __syncthreads();
+  const uint64_t prefix = *reinterpret_cast<const unsigned long long *>(ctl + kCtlEvPrefix);
+  const uint32_t shift = ev_shift(p), width = ev_width(p);
+  const uint64_t above = p == 0 ? 0ull : ~((uint64_t(1) << (shift + width)) - 1);
+  const uint64_t cap = uint64_t(1) << t.cap_log2;
+  uint32_t live = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < cap; i += uint64_t(gridDim.x) * blockDim.x) {
+    if (!slot_live(&t.slots[i])) continue;
+    ++live;
+    const uint64_t key = t.touch[i];
+    if ((key & above) != prefix) continue;
+    atomicAdd(&h[(key >> shift) & ((1u << width) - 1)], 1u);
+  }
+  if (p == 0 && live) atomicAdd(&live_s, live);
+  __syncthreads();
+  uint32_t *hp = hist + p * kEvBins;
+  for (uint32_t k = threadIdx.x; k < kEvBins; k += blockDim.x)
+    if (h[k]) atomicAdd(&hp[k], h[k]);
+  if (p == 0 && threadIdx.x == 0 && live_s) atomicAdd(&ctl[kCtlLive], live_s);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&ctl[kCtlEvDone], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  // the last workgroup: every histogram of this pass is in
+  ctl[kCtlEvDone] = 0;
+  uint32_t k;
+  if (p == 0) {
+    const uint32_t lv = __hip_atomic_load(&ctl[kCtlLive], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!t.max_entries || lv <= t.max_entries) return;     // kCtlEvict stays 0
+    k = lv - static_cast<uint32_t>(t.max_entries);
+    ctl[kCtlEvict] = 1;
+  } else {
+    k = ctl[kCtlEvK];
+  }
+  uint32_t d = 0, below = 0;
+  for (; d < (1u << width); ++d) {
+    const uint32_t c = __hip_atomic_load(&hp[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (below + c >= k) break;
+    below += c;
+  }
+  ctl[kCtlEvK] = k - below;
+  *reinterpret_cast<unsigned long long *>(ctl + kCtlEvPrefix) = prefix | (uint64_t(d) << shift);
+}
+
+// Delete the live entries whose stamp is at most the chosen one (exactly the
+// oldest live - max_entries), count them, and clear the histograms.
+__global__ __launch_bounds__(256) void ct_ev_evict_kernel(CtTable t, const uint32_t *ctl, uint32_t *hist) {
+  const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
+  const uint64_t g = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (uint64_t k = g; k < uint64_t(kEvPasses) * kEvBins; k += stp) hist[k] = 0;
+  if (!ctl[kCtlEvict]) return;
+  const uint64_t cut = *reinterpret_cast<const unsigned long long *>(ctl + kCtlEvPrefix);
+  const uint64_t cap = uint64_t(1) << t.cap_log2;
+  uint32_t n = 0;
+  for (uint64_t i = g; i < cap; i += stp) {
+    CtSlot *e = &t.slots[i];
+    if (!slot_live(e) || t.touch[i] > cut) continue;
+    ct_u32x4 hi = slot_half(e, 1);
+    hi.w &= ~0xff00u;                                  // valid = 0: connections.delete
+    reinterpret_cast<ct_u32x4 *>(e)[1] = hi;
+    ++n;
+  }
+  if (n) atomicAdd(&t.stats[1], static_cast<unsigned long long>(n));
+}
+
+// Long echo replies (K_HARD) into the walk: a reply joins its own key's run
+// unless its quoted key's bucket holds a packet of the batch (or another
+// reply's own key), which only the tail can order.  Three passes over a
+// bitmap of the batch's key buckets; each returns at once without replies.
+__global__ void ct_hbits_clear_kernel(const uint32_t *ctl, uint32_t *bm, uint64_t words) {
+  if (!ctl[kCtlHard]) return;
+  const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < words; w += stp) bm[w] = 0;
+}
+
+__device__ __forceinline__ void set_bit(uint32_t *bm, uint32_t k) {
+  const uint32_t m = 1u << (k & 31);
+  if (!(bm[k >> 5] & m)) atomicOr(&bm[k >> 5], m);   // hot keys: most of their packets find it set
+}
+
+__device__ __forceinline__ uint32_t own_bucket(const CtRec &r, uint32_t sentinel) {
+  return static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel);
+}
+
+__global__ void ct_hbits_set_kernel(uint64_t n, const uint32_t *ctl, const uint32_t *keys, const uint32_t *hard_list,
+                                    const WalkRec *brec, uint32_t *bm, uint32_t sentinel) {
+  const uint32_t nh = ctl[kCtlHard];
+  if (!nh) return;
+  const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stp) {
+    const uint32_t k = keys[i];
+    if (k != sentinel) set_bit(bm, k);
+  }
+  for (uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; h < nh; h += stp)
+    set_bit(bm, own_bucket(brec[hard_list[h]].r, sentinel));
+}
+
+__global__ void ct_hard_split_kernel(uint32_t *ctl, const uint32_t *hard_list, WalkRec *brec, uint32_t *keys,
+                                     const uint32_t *bm, uint32_t sentinel, uint32_t *th_list) {
+  const uint32_t nh = ctl[kCtlHard];
+  const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; h < nh; h += stp) {
+    const uint32_t i = hard_list[h];
+    const CtRec r = brec[i].r;
+    const uint32_t qb = static_cast<uint32_t>(
+        key_hash(r.seq, r.ack, r.flags, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16)) %
+        sentinel);
+    if ((bm[qb >> 5] >> (qb & 31)) & 1) {
+      th_list[atomicAdd(&ctl[kCtlTh], 1u)] = i;
+      atomicMax(&ctl[kCtlThFirst], 0xFFFFFFFFu - i);
+    } else {
+      const uint32_t k = own_bucket(r, sentinel);
+      keys[i] = k;
+      brec[i].key = k;
+    }
+  }
 }
 
 __global__ void ct_scatter_kernel(CtBatch b, const uint32_t *skeys, const uint32_t *sidx, const int32_t *sres,
@@ -1105,25 +1397,6 @@ __global__ void ct_scatter_kernel(CtBatch b, const uint32_t *skeys, const uint32
     b.verdicts[i] = static_cast<uint8_t>(o & 1);
     b.rule_ids[i] = o >> 1;
   }
-}
-
-// An echo reply long enough to quote a header (ConntrackLabel_dp.c:450-531):
-// its own key decides ESTABLISHED; otherwise ICMP_MISS reads the quoted key.
-__global__ void ct_hard_kernel(CtBatch b, CtTable t, const WalkRec *brec, uint32_t i) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const CtRec r = brec[i].r;
-  Cache c2{};
-  const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
-  const bool quoted = lookup(t, c2, q);            // read-only
-  Cache c{};
-  const bool live = lookup(t, c, Key{r.src, r.dst, r.sport, r.dport, r.proto});
-  const int l = !live ? ST_INV : ((c.v.rev ^ r.rev) == 3) ? ST_EST : quoted ? ST_REL : ST_INV;
-  const int32_t o = outcome(b, pack_outcome(b, 0, i), pack_outcome(b, 1, i), pack_outcome(b, 2, i),
-                            pack_outcome(b, 3, i), r, l);
-  if ((o & 1) == PCN_IPT_ACCEPT && l >= 0) update(t, c, r, l);
-  flush(c);
-  b.verdicts[i] = static_cast<uint8_t>(o & 1);
-  b.rule_ids[i] = o >> 1;
 }
 
 // Counters from the final rule ids: per-rule and default (ActionLookup_dp.c:96-111,
@@ -1251,7 +1524,11 @@ struct CtScratch {
   unsigned long long *pdesc = nullptr;   // ct_prep: the ports word of every 64-frame group
   uint32_t *keys = nullptr, *keys2 = nullptr;
   uint32_t *lcs = nullptr;                // per packet: len | cinfo << 16 (ct_count)
-  uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *hard_cnt = nullptr;
+  uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *ctl = nullptr;
+  uint32_t *th_list = nullptr;            // long echo replies left to ct_tail
+  uint32_t *bm = nullptr;                 // key-bucket bitmap (ct_hbits_*)
+  uint32_t *evh = nullptr;                // LRU radix-select histograms (kEvPasses x kEvBins, kept zeroed)
+  uint64_t bm_bytes = 0;
   uint32_t *heads = nullptr;
   int32_t *sres = nullptr;
   WalkRec *brec = nullptr;   // batch order
@@ -1260,7 +1537,6 @@ struct CtScratch {
   size_t temp_bytes = 0;
   // ct_advance_carry: 1 + the batch's last port-writing frame
   unsigned long long *zfound = nullptr;
-  uint32_t *h_cnt = nullptr;   // pinned host copy of hard_cnt[0..5] (a pageable target is staged: a slower read-back)
 };
 
 CtScratch *ct_scratch_new() { return new CtScratch(); }
@@ -1270,11 +1546,11 @@ void ct_scratch_free(CtScratch *s) {
   for (void *p : {static_cast<void *>(s->pdesc), static_cast<void *>(s->lcs),
                   static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
-                  static_cast<void *>(s->hard_cnt), static_cast<void *>(s->brec), static_cast<void *>(s->wrec),
+                  static_cast<void *>(s->ctl), static_cast<void *>(s->brec), static_cast<void *>(s->wrec),
                   static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
-                  static_cast<void *>(s->zfound)})
+                  static_cast<void *>(s->zfound), static_cast<void *>(s->th_list), static_cast<void *>(s->bm),
+                  static_cast<void *>(s->evh)})
     if (p) (void)hipFree(p);
-  if (s->h_cnt) (void)hipHostFree(s->h_cnt);
   delete s;
 }
 
@@ -1286,16 +1562,21 @@ int ct_table_init(CtTable &t, uint32_t cap_log2) {
   if (e == hipSuccess) e = hipMalloc(&t.carry, 64);
   if (e == hipSuccess) e = hipMemset(t.carry, 0, 64);
   if (e == hipSuccess) t.stats = reinterpret_cast<unsigned long long *>(t.carry + 2);
+  if (e == hipSuccess) e = hipMalloc(&t.touch, n * 8);
+  if (e == hipSuccess) e = hipMemset(t.touch, 0, n * 8);
   t.cap_log2 = cap_log2;
+  t.seq = 1;
   return e;
 }
 
 void ct_table_free(CtTable &t) {
   if (t.slots) (void)hipFree(t.slots);
   if (t.carry) (void)hipFree(t.carry);
+  if (t.touch) (void)hipFree(t.touch);
   t.slots = nullptr;
   t.carry = nullptr;
   t.stats = nullptr;
+  t.touch = nullptr;
 }
 
 #define CT_CHECK(x)                         \
@@ -1329,7 +1610,7 @@ static hipError_t sort_pairs(void *temp, size_t &bytes, const uint32_t *kin, uin
 
 static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
   if (s.cap < n) {
-    for (uint32_t **p : {&s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list, &s.lcs,
+    for (uint32_t **p : {&s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list, &s.th_list, &s.lcs,
                          reinterpret_cast<uint32_t **>(&s.sres)}) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, n * 4));
@@ -1345,9 +1626,18 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     if (s.wrec) CT_CHECK(hipFree(s.wrec));
     s.wrec = nullptr;
     if (PCN_CT_GATHER) CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
-    if (!s.hard_cnt) CT_CHECK(hipMalloc(&s.hard_cnt, 64));   // [0] long echo replies, [1..5] runs per class,
-                                                              // [8] ct_prep's chunk counter
+    if (!s.ctl) CT_CHECK(hipMalloc(&s.ctl, kCtlWords * 4));   // the kCtl* words + the walk plan
+    if (!s.evh) {
+      CT_CHECK(hipMalloc(&s.evh, kEvPasses * kEvBins * 4));
+      CT_CHECK(hipMemset(s.evh, 0, kEvPasses * kEvBins * 4));
+    }
     s.cap = n;
+  }
+  const uint64_t bmb = (uint64_t(1) << kbits) / 8;
+  if (s.bm_bytes < bmb) {
+    if (s.bm) CT_CHECK(hipFree(s.bm));
+    CT_CHECK(hipMalloc(&s.bm, bmb));
+    s.bm_bytes = bmb;
   }
   size_t need = 0;
   CT_CHECK(sort_pairs(nullptr, need, s.keys, s.keys2, s.idx, s.idx2, n, kbits, st));
@@ -1423,15 +1713,26 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint32_t sentinel = (1u << kbits) - 1;
   CT_CHECK(grow(s, b.n, kbits, st));
   const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
-  // one memset for the long-echo-reply count [0], the run counts per class
-  // [1..5] (ct_heads) and ct_prep's chunk counter [8]: each memset is a
-  // launch of its own (~5 us between kernels)
-  CT_CHECK(hipMemsetAsync(s.hard_cnt, 0, 64, st));
+  // one memset for the control words (long echo replies, run counts per
+  // class, ct_prep's chunk counter, ...; kCtl*): each memset is a launch of
+  // its own (~5 us between kernels)
+  CT_CHECK(hipMemsetAsync(s.ctl, 0, kCtlZero * 4, st));
   CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
   const uint32_t pchunk = prep_chunk(b.n, num_cus);
   const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
   hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.lcs, s.keys, s.idx, kbits,
-                     s.hard_cnt, s.hard_list, s.pdesc, s.hard_cnt + 8, pchunk);
+                     s.ctl + kCtlHard, s.hard_list, s.pdesc, s.ctl + kCtlChunk, pchunk);
+  CT_CHECK(hipGetLastError());
+  // long echo replies join their own key's run unless their quoted key's
+  // bucket is in the batch (each kernel returns at once without replies)
+  const uint64_t bm_words = (uint64_t(1) << kbits) / 32;
+  hipLaunchKernelGGL(ct_hbits_clear_kernel, dim3(grid), dim3(blk), 0, st, s.ctl, s.bm, bm_words);
+  CT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(ct_hbits_set_kernel, dim3(grid), dim3(blk), 0, st, b.n, s.ctl, s.keys, s.hard_list, s.brec, s.bm,
+                     sentinel);
+  CT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(ct_hard_split_kernel, dim3(grid), dim3(blk), 0, st, s.ctl, s.hard_list, s.brec, s.keys, s.bm,
+                     sentinel, s.th_list);
   CT_CHECK(hipGetLastError());
   // (ct_heads advances the carry from ct_prep's published groups)
   size_t tb;
@@ -1445,41 +1746,28 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
-                     b.n, s.keys2, s.heads, s.hard_cnt + 1, sentinel, hper, s.pdesc, t.carry);
+                     b.n, s.keys2, s.heads, s.ctl + kCtlClass, sentinel, hper, s.pdesc, t.carry);
   CT_CHECK(hipGetLastError());
-  if (!s.h_cnt) CT_CHECK(hipHostMalloc(reinterpret_cast<void **>(&s.h_cnt), 64, hipHostMallocDefault));
-  CT_CHECK(hipMemcpyAsync(s.h_cnt, s.hard_cnt, 4 * (1 + kRunClasses), hipMemcpyDeviceToHost, st));
-  CT_CHECK(hipStreamSynchronize(st));
-  uint32_t cnt[1 + kRunClasses];
-  for (uint32_t c = 0; c <= kRunClasses; ++c) cnt[c] = s.h_cnt[c];
-  const uint32_t nhard = cnt[0];
-  std::vector<uint32_t> hard(nhard);
-  if (nhard) {
-    CT_CHECK(hipMemcpy(hard.data(), s.hard_list, nhard * 4ull, hipMemcpyDeviceToHost));
-    std::sort(hard.begin(), hard.end());
-  }
-  const unsigned wblk = 64;
-  WalkPlan plan{};
-  plan.blk0[0] = 0;
-  for (uint32_t c = 0; c < kRunClasses; ++c) {
-    plan.cnt[c] = cnt[1 + c];
-    plan.blk0[c + 1] = plan.blk0[c] + (c == 0 ? plan.cnt[c] : (plan.cnt[c] + wblk - 1) / wblk);
-  }
-  const unsigned wgrid = plan.blk0[kRunClasses];
-  int first = 1;
-  for (size_t h = 0; h <= hard.size(); ++h) {
-    const uint64_t hi = h < hard.size() ? hard[h] : b.n;
-    if (wgrid) {
-      hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(wblk), 0, st, b, t, src, s.sres, s.heads, plan,
-                         s.cursor, hi, first);
+  // the walk plan, sized on the device: no read-back, the stream stays asynchronous
+  hipLaunchKernelGGL(ct_plan_kernel, dim3(1), dim3(64), 0, st, s.ctl);
+  CT_CHECK(hipGetLastError());
+  const unsigned wgrid = static_cast<unsigned>(b.n / 64 + kRunClasses + 1);   // the plan's upper bound
+  hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.sres, s.heads, s.ctl, s.cursor);
+  CT_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.sres, s.heads, s.ctl, s.th_list,
+                     s.cursor);
+  CT_CHECK(hipGetLastError());
+  if (t.max_entries) {                         // LRU down to max_entries (no read-back either)
+    const uint64_t cap = uint64_t(1) << t.cap_log2;
+    const unsigned egrid = static_cast<unsigned>(std::min<uint64_t>(cap / 256 + 1, uint64_t(num_cus) * 4));
+    for (int p = 0; p < kEvPasses; ++p) {
+      hipLaunchKernelGGL(ct_ev_pass_kernel, dim3(egrid), dim3(256), 0, st, t, s.ctl, s.evh, p);
       CT_CHECK(hipGetLastError());
     }
-    first = 0;
-    if (h < hard.size()) {
-      hipLaunchKernelGGL(ct_hard_kernel, dim3(1), dim3(64), 0, st, b, t, s.brec, hard[h]);
-      CT_CHECK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(ct_ev_evict_kernel, dim3(egrid), dim3(256), 0, st, t, s.ctl, s.evh);
+    CT_CHECK(hipGetLastError());
   }
+  ++t.seq;                                     // the next batch's touch stamps are newer
   if (!PCN_CT_DIRECT) {
     hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
     CT_CHECK(hipGetLastError());

@@ -70,8 +70,15 @@ struct CtTable {
   CtSlot *slots = nullptr;
   uint32_t cap_log2 = 0;
   uint32_t *carry = nullptr;             // stale ports of the shared `packet` struct
-  unsigned long long *stats = nullptr;   // [0] inserts refused because the table was full
+  unsigned long long *stats = nullptr;   // [0] inserts refused because the table was full, [1] entries evicted
   unsigned long long now = 0;            // the `timestamp` the control plane sets
+  // LRU at batch granularity (the lru_hash of 65536 entries,
+  // Iptables_ConntrackLabel_dp.c:112): per slot, the stamp (batch seq << 32 |
+  // batch index) of the last packet after which its entry was live; after a
+  // batch the oldest live entries are deleted down to max_entries (0: unbounded).
+  unsigned long long *touch = nullptr;
+  uint32_t seq = 1;
+  uint64_t max_entries = 65536;
 };
 
 struct CtScratch;   // device buffers, grown as batches need (conntrack.hip)

@@ -1432,6 +1432,16 @@ int pcn_ipt_ct_clear(pcn_ipt *ctx) {
     hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_check(hipMemset(ctx->ct.slots, 0, (size_t(1) << ctx->ct.cap_log2) * sizeof(CtSlot)), "hipMemset(conntrack)");
     hip_check(hipMemset(ctx->ct.carry, 0, 64), "hipMemset(conntrack)");
+    hip_check(hipMemset(ctx->ct.touch, 0, (size_t(1) << ctx->ct.cap_log2) * 8), "hipMemset(conntrack)");
+    ctx->ct.seq = 1;
+    return 0;
+  });
+}
+
+int pcn_ipt_ct_set_max_entries(pcn_ipt *ctx, uint64_t max_entries) {
+  return guarded(ctx, [&] {
+    if (max_entries > (uint64_t(1) << 32) - 1) return fail(-EINVAL, "max_entries must be below 2^32");
+    ctx->ct.max_entries = max_entries;
     return 0;
   });
 }
@@ -1481,10 +1491,12 @@ int pcn_ipt_ct_get_info(pcn_ipt *ctx, pcn_ipt_ct_info *out) {
     if (ctx->ct.carry) {
       device_guard(ctx);
       hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-      unsigned long long lost = 0;
-      hip_check(hipMemcpy(&lost, ctx->ct.stats, 8, hipMemcpyDeviceToHost), "hipMemcpy(conntrack stats)");
-      out->inserts_lost = lost;
+      unsigned long long st[2] = {0, 0};
+      hip_check(hipMemcpy(st, ctx->ct.stats, 16, hipMemcpyDeviceToHost), "hipMemcpy(conntrack stats)");
+      out->inserts_lost = st[0];
+      out->evicted = st[1];
     }
+    out->max_entries = ctx->ct.max_entries;
     return 0;
   });
 }

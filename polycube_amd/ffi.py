@@ -79,7 +79,7 @@ class ChainInfo(C.Structure):
 
 class CtInfo(C.Structure):
     _fields_ = [("enabled", C.c_uint32), ("capacity_log2", C.c_uint32), ("now", C.c_uint64),
-                ("inserts_lost", C.c_uint64)]
+                ("inserts_lost", C.c_uint64), ("max_entries", C.c_uint64), ("evicted", C.c_uint64)]
 
 
 class HorusInfo(C.Structure):
@@ -88,7 +88,7 @@ class HorusInfo(C.Structure):
 
 
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
-ABI_VERSION = 6            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
+ABI_VERSION = 7            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
 
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
@@ -149,6 +149,7 @@ SIGNATURES = {
     "pcn_ipt_ct_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pcn_ipt_ct_disable": (C.c_int, [C.c_void_p]),
     "pcn_ipt_ct_clear": (C.c_int, [C.c_void_p]),
+    "pcn_ipt_ct_set_max_entries": (C.c_int, [C.c_void_p, C.c_uint64]),
     "pcn_ipt_ct_set_time": (C.c_int, [C.c_void_p, C.c_uint64]),
     "pcn_ipt_ct_dump": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "pcn_ipt_ct_get_info": (C.c_int, [C.c_void_p, C.POINTER(CtInfo)]),

@@ -295,6 +295,10 @@ class Iptables:
     def ct_set_time(self, ns):
         _check(ffi.lib().pcn_ipt_ct_set_time(self._h, int(ns)))
 
+    def ct_set_max_entries(self, m):
+        """Live entries kept after each batch (LRU over the touches; 0: unbounded)."""
+        _check(ffi.lib().pcn_ipt_ct_set_max_entries(self._h, int(m)))
+
     def ct_dump(self):
         """Live connections (session table), as a numpy array of CT_ENTRY, sorted by key."""
         import numpy as np

@@ -163,8 +163,9 @@ def test_fuzz_quirky_rules_both_directions_and_hooks(dev, seed):
 
 def test_long_echo_replies_read_the_quoted_flow(dev):
     """Echo replies >= 70 B whose own entry is not reversed take ICMP_MISS and
-    look up the quoted header's key (ConntrackLabel_dp.c:450-531): they split
-    the batch into segments (ct_hard)."""
+    look up the quoted header's key (ConntrackLabel_dp.c:450-531).  Quoting
+    flows with packets in the same batch, most of them go to ct_tail (the
+    walk stops at the first, one wave takes the rest in order)."""
     rng = np.random.default_rng(9)
     o, ipt = ct_pair({1: [{"conntrack": "RELATED", "action": "ACCEPT"},
                           {"conntrack": "INVALID", "action": "DROP"}]}, {1: "ACCEPT"})
@@ -259,9 +260,10 @@ def test_long_runs_walk_a_wave_each(dev, p_icmp):
 
 
 def test_long_runs_resume_across_echo_reply_segments(dev):
-    """Long echo replies (>= 70 B, ct_hard) split the batch into segments; the
-    long runs walked by whole waves (walk_long) stop at each split and resume
-    from their cursor in the next segment, bit-exact vs the oracle."""
+    """Long echo replies (>= 70 B) quoting flows of the same batch: the walk
+    stops every run at the first of them, and ct_tail resumes the long runs
+    (walk_long) and the short ones from their cursors between them, bit-exact
+    vs the oracle."""
     rng = np.random.default_rng(41)
     o, ipt = ct_pair({1: [{"conntrack": "RELATED", "action": "ACCEPT"},
                           {"conntrack": "INVALID", "action": "DROP"}] + synth.config_rules(2).rules()},
@@ -372,3 +374,116 @@ def test_ring_over_many_streams_keeps_batch_order(dev):
     assert_tables(o, ipt)
     assert_counters(o, ipt, n=len(rules) + 1)
     assert_ae(o, ipt)
+
+
+def test_ping_replies_of_98_bytes_walk_in_their_runs(dev):
+    """Ordinary pings: 98-byte echo replies (>= 70 B, so ICMP_MISS may read
+    their payload as a quoted header) whose payload quotes nothing of the
+    batch -- walked inside their own key's run with a direct read of the
+    quoted key (ct_hard_split), no tail.  A few replies quote live flows of the
+    batch (the tail).  Verdicts, rule ids, counters and the table vs the oracle."""
+    rng = np.random.default_rng(77)
+    rules = [{"conntrack": "RELATED", "action": "ACCEPT"}, {"conntrack": "INVALID", "action": "DROP"},
+             {"l4proto": "ICMP", "conntrack": "NEW", "action": "ACCEPT"}] + synth.config_rules(2).rules()
+    o, ipt = ct_pair({1: rules}, {1: "ACCEPT"}, cap_log2=18, jit=1)
+    n = 1 << 18
+    f, _ = synth.flow_traffic(n, 4000, 77, stride=128, p_icmp=0.5, p_err=0.01, p_noise=0.02)
+    nb = f.reshape(n, 128)
+    icmp = nb[:, 23] == 1
+    reply = icmp & (nb[:, 34] == 0)
+    lens = np.where(icmp, 98, 128).astype(np.uint16)
+    nb[reply, 42:98] = rng.integers(0, 256, size=(int(reply.sum()), 56), dtype=np.uint8)   # ping payload
+    quote = reply & (rng.random(n) < 0.001)                 # a few quote a flow of the batch
+    q = rng.integers(0, n, size=n)
+    nb[quote, 42] = 0x45
+    nb[quote, 51] = nb[q[quote], 23]
+    nb[quote, 54:62] = nb[q[quote], 26:34]
+    nb[quote, 62:66] = nb[q[quote], 34:38]
+    assert reply.sum() > 20000
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, nb[lo:hi].reshape(-1), hi - lo, lens=lens[lo:hi])
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+
+
+def test_stateful_classify_is_stream_asynchronous(dev):
+    """pcn_ipt_classify with the connection table on queues the whole pipeline
+    (plan and walk sized on the device, no read-back): right after the call on
+    a 2^24-frame batch the stream still has work, and the call returns in a
+    fraction of the batch's time."""
+    import time
+    rs = synth.config_rules(3)
+    from polycube_amd import Iptables
+    ipt = Iptables(device=0, jit=1)
+    ipt.interactive = False
+    ch = ipt.chain("FORWARD")
+    for r in rs.rules():
+        ch.append(**r)
+    ch.default = "DROP"
+    ch.apply_rules()
+    ipt.ct_enable(20)
+    ipt.ct_set_time(NOW)
+    base, _ = synth.flow_traffic(1 << 20, 1 << 14, 5, stride=64, rs=rs)
+    frames = torch.from_numpy(base).to(dev).repeat(16)
+    n = 1 << 24
+    v = torch.empty(n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        ipt.classify(frames, n=n, verdicts=v, stream=s.cuda_stream)     # warm: scratch allocations
+        s.synchronize()
+        t0 = time.perf_counter()
+        ipt.classify(frames, n=n, verdicts=v, stream=s.cuda_stream)
+        t_call = time.perf_counter() - t0
+        busy = not s.query()
+        s.synchronize()
+        t_all = time.perf_counter() - t0
+    assert busy, "the stream was idle right after the call: the call waited for the batch"
+    assert t_call < 0.5 * t_all, (t_call, t_all)
+    ipt.close()
+
+
+@pytest.mark.parametrize("max_entries", [700, 2000])
+def test_lru_capacity_evicts_like_the_oracle(dev, max_entries):
+    """More live connections than max_entries: after every batch both drop the
+    least recently touched entries down to max_entries (conntrack.hip ct_ev_*:
+    a radix select over the touch stamps).  Verdicts, rule ids, counters, the
+    whole table and the eviction count equal the oracle's, batch after batch,
+    with ICMP errors (touching the quoted key), long runs and echo replies."""
+    rules = CT_RULES + synth.config_rules(2).rules()
+    o, ipt = ct_pair({1: rules}, {1: "DROP"}, cap_log2=15, jit=1)
+    o.ct_set_max_entries(max_entries)
+    ipt.ct_set_max_entries(max_entries)
+    f, lens = synth.flow_traffic(60000, 9000, 13, stride=128, lens_mode="mixed", p_err=0.05, p_icmp=0.2)
+    nb = f.reshape(60000, 128)
+    for lo, hi in ((0, 15000), (15000, 15001), (15001, 40000), (40000, 60000)):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, nb[lo:hi].reshape(-1), hi - lo, lens=lens[lo:hi])
+        assert_same(v_o, r_o, v_g, r_g)
+        assert_tables(o, ipt)
+        assert len(ipt.ct_dump()) <= max_entries
+    assert ipt.ct_info()["evicted"] == o.ct_info()["evicted"]
+    assert o.ct_info()["evicted"] > 0
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_ae(o, ipt)
+
+
+def test_lru_crosses_the_reference_capacity(dev):
+    """The default max_entries is the reference's 65536 (lru_hash,
+    Iptables_ConntrackLabel_dp.c:112): 2^17 UDP connections over three
+    batches leave exactly 65536 live entries, the most recently touched ones."""
+    rs = synth.config_rules(2)
+    o, ipt = ct_pair({1: rs.rules()}, {1: "ACCEPT"}, cap_log2=19)
+    assert ipt.ct_info()["max_entries"] == o.ct_info()["max_entries"] == 65536
+    n = 3 * (1 << 17)
+    rng = np.random.default_rng(3)
+    src = rng.integers(0, 2**32, size=1 << 17, dtype=np.uint64).astype(np.uint32)
+    sp = rng.integers(1024, 65535, size=1 << 17)
+    pick = np.concatenate([np.arange(1 << 17), rng.integers(0, 1 << 17, size=n - (1 << 17))])
+    f = synth.build_frames(src[pick], np.full(n, 0x0A000001, np.uint32), np.full(n, 17), sp[pick],
+                           np.full(n, 53), np.zeros(n, np.int32), frame_len=64).reshape(-1)
+    for lo, hi in ((0, 1 << 17), (1 << 17, 2 << 17), (2 << 17, n)):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, f[lo * 64:hi * 64], hi - lo, stride=64)
+        assert_same(v_o, r_o, v_g, r_g)
+        assert_tables(o, ipt)
+    assert len(ipt.ct_dump()) == 65536
+    assert ipt.ct_info()["evicted"] == o.ct_info()["evicted"]

@@ -186,3 +186,46 @@ def test_flow_traffic_matches_between_one_and_two_batches():
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert np.array_equal(outs[0][2], outs[1][2])
     assert ip_nbo("1.2.3.4") != 0
+
+
+def test_lru_keeps_the_most_recently_touched_entries():
+    """Capacity at batch granularity (Iptables_ConntrackLabel_dp.c:112, an
+    lru_hash of 65536): after a batch the live entries touched longest ago are
+    deleted down to max_entries; a touch is a packet after which its entry is
+    live; within a batch nothing is evicted."""
+    o = fresh()
+    o.ct_set_max_entries(2)
+    A, B, C, D = ("10.0.0.%d" % k for k in (1, 2, 3, 4))
+    H = "10.9.9.9"
+
+    def udp(src, sport):
+        return P(src, H, 17, sport, 53)
+    run(o, [udp(A, 1000), udp(B, 1001), udp(C, 1002)])       # three inserts in one batch
+    info = o.ct_info()
+    assert (info["live"], info["evicted"]) == (2, 1)
+    live = {int(e["src_ip"]) for e in o.ct_dump()}
+    assert live == {ip_nbo(B), ip_nbo(C)}                     # A: touched first
+    run(o, [udp(B, 1001), udp(D, 1003)])                      # B touched again, D inserted
+    assert {int(e["src_ip"]) for e in o.ct_dump()} == {ip_nbo(B), ip_nbo(D)}   # C: oldest touch
+    # an evicted connection starts over: its next datagram is NEW again
+    v, r = run(o, [udp(A, 1000)])
+    assert o.ct_info()["evicted"] == 3
+    o.ct_set_max_entries(0)                                   # unbounded from the next batch on
+    run(o, [udp(C, 1002), udp(A, 1005)])
+    assert o.ct_info()["live"] == 4
+
+
+def test_lru_within_a_batch_nothing_is_evicted():
+    """The reply of an evicted-at-batch-end flow in the same batch still finds
+    its entry (ESTABLISHED): eviction happens between batches."""
+    rules = [{"conntrack": "ESTABLISHED", "action": "ACCEPT"}, {"conntrack": "NEW", "l4proto": "UDP",
+                                                                "action": "ACCEPT"}]
+    o = fresh(rules, "DROP")
+    o.ct_set_max_entries(1)
+    H = "10.9.9.9"
+    pk = [P("10.0.0.1", H, 17, 1000, 53), P("10.0.0.2", H, 17, 1001, 53), P(H, "10.0.0.1", 17, 53, 1000)]
+    v, r = run(o, pk)
+    assert list(r) == [1, 1, -3]                              # the reply: ESTABLISHED (accept-established)
+    assert o.ct_info()["live"] == 1
+    v, r = run(o, [P(H, "10.0.0.2", 17, 53, 1001)])          # 10.0.0.2's entry was evicted
+    assert list(r) == [1]                                     # NEW again: rule 1
