@@ -300,6 +300,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe end-to-end leg")
     ap.add_argument("--config", type=int, default=3, choices=(2, 3, 5),
                     help="BASELINE.json config: 3 = the headline (default); 2 and 5 are secondary measurements")
+    ap.add_argument("--imix-align", type=int, default=1, choices=(1, 64),
+                    help="config 5 layout: 1 = frames packed back to back (default), 64 = each at a 64-byte "
+                         "boundary, as NIC RX buffers place them")
     ap.add_argument("--hook", default="xdp", choices=("xdp", "tc"),
                     help="attach-point semantics (tc: outer VLAN tags stripped before classification)")
     ap.add_argument("--no-ct", action="store_true", help="skip the stateful-conntrack leg")
@@ -375,7 +378,8 @@ def main():
     t = time.perf_counter()
     offsets_host = lens_host = None
     if cfg == 5:
-        frames_host, offsets_host, lens_host = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5] + 7919 * rank)
+        frames_host, offsets_host, lens_host = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5] + 7919 * rank,
+                                                                 align=args.imix_align)
     else:
         frames_host = gen_frames(n, rs, synth.CONFIG_SEEDS[cfg] + 7919 * rank,
                                  protos=(synth.UDP,) if cfg == 2 else (synth.TCP, synth.UDP))
@@ -500,6 +504,8 @@ def main():
             "config": {"workload": WORKLOADS[cfg] + (", TC hook" if hook else ""),
                        "rules": len(rules), "frames_per_gpu": n,
                        "frame_bytes": "IMIX 64/576/1500 (7:4:1)" if cfg == 5 else 64,
+                       "layout": ("packed back to back" if args.imix_align == 1 else "64-byte aligned")
+                       if cfg == 5 else "64-byte stride",
                        "parallelism": (f"dp{world} (packet-index shards, "
                                        + ("RCCL counter all-gather)" if use_rccl else "host gloo counter all-reduce)")
                                        if world > 1 else "dp1 (one packet shard, no exchange)"),

@@ -100,6 +100,16 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 #ifndef PCN_STAGE_FAST
 #define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
 #endif
+// Offsets / lengths batches (IMIX): a wave's 64 scattered headers are fetched
+// four lanes to a frame, one 16-byte chunk each from the frame's 16-byte
+// aligned start, so one load instruction reads 16 frames' contiguous bytes
+// (tools/gather_probe.hip on config 5's layout: 0.080 ms for 2^22 frames,
+// against 0.132 ms one lane per frame), and the chunks are transposed through
+// the wave's LDS region (16 frames a round, 80-byte rows: the 1.25 KB the
+// candidate stage uses later).  0: one lane per header (load_generic).
+#ifndef PCN_GEN_QUAD
+#define PCN_GEN_QUAD 1
+#endif
 // Tuning switches (tools/ablate.py builds experiment variants with -D...).
 
 namespace pcn {
@@ -703,8 +713,11 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // 3 KB per-wave LDS buffer into one header per lane.  Each instruction then
   // touches ~11 cache lines instead of 32.
   struct Stage {
-    Hdr h;          // generic path
+    Hdr h;          // generic path (PCN_GEN_QUAD 0)
     u32x4 c[3];     // fixed path: this lane's three chunks
+    u32x4 g[5];     // generic path, quad gather: the chunks this lane fetched (see prefetch)
+    uint32_t sh;    // generic path: the frame start's offset in its 16-byte chunk
+    bool quad;      // generic path: g[0..3] hold other frames' chunks (transpose in process)
     uint32_t L, port, ct;
   };
   const uint32_t lane = threadIdx.x & 63;
@@ -753,6 +766,41 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
 #pragma unroll
       for (int q = 0; q < 3; ++q)
         x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride) + q);
+    } else if (PCN_GEN_QUAD) {
+      const uint64_t jf = j < a.n ? j : last;
+      const uint64_t at = reinterpret_cast<uintptr_t>(a.frames) + (a.offsets ? uint64_t(a.offsets[jf]) : jf * a.stride);
+      const uint64_t end = reinterpret_cast<uintptr_t>(a.frames) + a.frames_bytes;
+      const uint64_t abase = at & ~uint64_t(15);
+      x.L = a.lens ? a.lens[jf] : a.fixed_len;
+      x.sh = static_cast<uint32_t>(at & 15);
+      uint64_t group = j - lane;                 // wave-uniform
+      group = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(group >> 32))) << 32) |
+              __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(group));
+      // the whole group in the batch, and every frame's 80 aligned bytes inside the buffer
+      x.quad = group + 64 <= a.n && __ballot(abase + 80 > end) == 0;
+      if (x.quad) {
+        // instruction q: lane l fetches chunk (l & 3) of frame 16 q + (l >> 2)
+        const uint32_t lo = static_cast<uint32_t>(abase), hi = static_cast<uint32_t>(abase >> 32);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int src = 16 * q + static_cast<int>(lane >> 2);
+          const uint64_t fb = (static_cast<uint64_t>(__shfl(hi, src)) << 32) | __shfl(lo, src);
+          x.g[q] = hdr_load(reinterpret_cast<const u32x4 *>(fb) + (lane & 3));
+        }
+        // chunk 4 (bytes 64..79) only matters when the 52-byte window crosses
+        // into it; otherwise the load re-reads chunk 3's line (no new traffic)
+        x.g[4] = hdr_load(reinterpret_cast<const u32x4 *>(abase) + (x.sh > 12 ? 4 : 3));
+      } else {
+        // one lane per frame: its own 80 bytes, each dword only if inside the buffer
+        uint32_t d[20];
+#pragma unroll
+        for (int k = 0; k < 20; ++k) {
+          const uint64_t p = abase + 4u * k;
+          d[k] = p + 4 <= end ? *reinterpret_cast<const uint32_t *>(p) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 5; ++q) x.g[q] = u32x4{d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]};
+      }
     } else {
       x.L = a.fixed_len;
       load_header<FIXED>(a, j < a.n ? j : last, x.h, x.L);
@@ -808,6 +856,55 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else if (PCN_GEN_QUAD) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) asm volatile("" : "+v"(cur.g[q]));
+      uint32_t d[17];
+      if (cur.quad) {                              // wave-uniform
+        // four rounds of 16 frames: every lane writes the chunk it fetched into
+        // its frame's row, then the 16 lanes whose frames these are read their rows
+        u32x4 *rows = hbuf;                        // 16 rows x 5 chunks (80 B: 4 used + padding)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          asm volatile("" ::: "memory");           // the region held the last iteration's WaveScratch
+          rows[(lane >> 2) * 5 + (lane & 3)] = cur.g[q];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if ((lane >> 4) == static_cast<uint32_t>(q)) {
+            const u32x4 *row = rows + (lane & 15) * 5;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const u32x4 v = row[c];
+              d[4 * c] = v.x; d[4 * c + 1] = v.y; d[4 * c + 2] = v.z; d[4 * c + 3] = v.w;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          d[4 * c] = cur.g[c].x; d[4 * c + 1] = cur.g[c].y; d[4 * c + 2] = cur.g[c].z; d[4 * c + 3] = cur.g[c].w;
+        }
+      }
+      d[16] = cur.g[4].x;
+      // the window starts cur.sh bytes into the chunk: dword shift, then byte shift
+      const uint32_t dsh = cur.sh >> 2, bsh = cur.sh & 3;
+      // (the asm keeps both operands in registers: folded into d[k + dsh],
+      // the window became a dynamically indexed array in scratch)
+      auto sel = [](bool c, uint32_t x, uint32_t y) {
+        asm volatile("" : "+v"(x), "+v"(y));
+        return c ? y : x;
+      };
+      uint32_t f1[16], f2[14];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) f1[k] = sel(dsh & 1, d[k], d[k + 1]);
+#pragma unroll
+      for (int k = 0; k < 14; ++k) f2[k] = sel(dsh & 2, f1[k], f1[k + 2]);
+#pragma unroll
+      for (int k = 0; k < 13; ++k) h.w[k] = __builtin_amdgcn_alignbyte(f2[k + 1], f2[k], bsh);
     } else {
 #pragma unroll
       for (int k = 0; k < 13; ++k) asm volatile("" : "+v"(cur.h.w[k]));

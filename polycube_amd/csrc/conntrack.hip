@@ -563,7 +563,12 @@ __device__ __forceinline__ void flush(const CtTable &t, Cache &c) {
     hi.w = uint32_t(c.k.proto) | uint32_t(c.v.live) << 8 | uint32_t(c.v.state) << 16 | uint32_t(c.v.rev) << 24;
     reinterpret_cast<ct_u32x4 *>(c.e)[1] = hi;
   }
-  if (c.touch && c.e) t.touch[c.e - t.slots] = static_cast<unsigned long long>(t.seq) << 32 | (c.touch - 1);
+  // the LRU stamp: this batch's last touch, or ~0 once the entry is gone
+  // (touch[] holds a stamp exactly for the live entries: the eviction reads nothing else)
+  if (c.e) {
+    if (c.v.live && c.touch) t.touch[c.e - t.slots] = static_cast<unsigned long long>(t.seq) << 32 | (c.touch - 1);
+    else if (!c.v.live && c.dirty) t.touch[c.e - t.slots] = ~0ull;
+  }
   c.dirty = false;
   c.touch = 0;
 }
@@ -942,19 +947,26 @@ struct RecSrc {
   __device__ __forceinline__ uint32_t key(uint64_t q) const { return rec[PCN_CT_GATHER ? q : sidx[q]].key; }
 };
 
-__device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec, int32_t *sres, uint32_t p,
-                          uint32_t *cursor_j, uint64_t hi, int first) {
-  __shared__ WalkRec buf[2][64];
+// The walk of one long run's records in chunks of 64, from sorted position q0
+// up to `bound` (or the run's end, or the first record at batch index >= hi),
+// with lane 0's cache `c` as the connection's state on entry and on return.
+// Returns the sorted position where it stopped.  kSpec: a speculative segment
+// (walk_seg): it may not touch the table, so where a record needs it (cls 2)
+// the walk stops there and sets `aborted`.
+template <bool kSpec>
+__device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres,
+                                                WalkRec (*buf)[64], uint32_t k, uint64_t q0, uint64_t hi,
+                                                uint64_t bound, Cache &c, bool &aborted) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t k = wrec.key(p);
-  const uint64_t q0 = first ? p : *cursor_j;
   const uint64_t last = b.n - 1;
-  Cache c{};
+  const uint64_t lim = bound < b.n ? bound : b.n;
   uint64_t base = q0;
+  aborted = false;
   auto ix = [&](uint64_t r) -> uint64_t {       // sorted position -> the record's index
     r = r < last ? r : last;
     return PCN_CT_GATHER ? r : wrec.sidx[r];
   };
+  __syncthreads();                               // a previous walk of this workgroup is done with buf
   buf[0][lane] = load_rec(&wrec.rec[ix(base + lane)]);
   uint64_t nidx = ix(base + 64 + lane);          // the next chunk's indices, a chunk ahead
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -968,7 +980,7 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
     nidx = ix(base + 128 + lane);
     const WalkRec w = buf[cur][lane];
     const CtRec &r = w.r;
-    const bool inrun = base + lane < b.n && w.key == k && w.idx < hi;
+    const bool inrun = base + lane < lim && w.key == k && w.idx < hi;
     const uint64_t rm = __ballot(inrun);           // the run's records: a prefix of the chunk
     const uint32_t m = rm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~rm));
     uint32_t u0 = 0;
@@ -1042,6 +1054,9 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
             if (nf >> 24) c.dirty = true;
             if (c.v.live && c.e) c.touch = cidx + 1;
           }
+        } else if (kSpec) {                           // the table is not ours to touch: give up here
+          aborted = true;
+          return base + u0;
         } else {                                      // the record that needs the table: the full step
           const WalkRec x = buf[cur][u0];
           if (lane == 0) put_outcome(b, sres, base + u0, x.idx, step(b, t, c, x));
@@ -1049,17 +1064,13 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
         ++u0;
       }
     }
-    if (m < 64) {                                     // the run (or this round of it) ends here
+    if (m < 64) {                                     // the run (or this part of it) ends here
 #if PCN_CT_DBG
       if (lane == 0 && dbg_chunks >= 40)
         printf("walk_long run: %u records, %u chunks, %u rounds, %u changes, %u table steps\n", dbg_recs, dbg_chunks,
                dbg_rounds, dbg_changes, dbg_steps);
 #endif
-      if (lane == 0) {
-        flush(t, c);
-        *cursor_j = static_cast<uint32_t>(base + m);
-      }
-      return;
+      return base + m;
     }
     base += 64;
     __syncthreads();
@@ -1068,6 +1079,142 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc wrec,
     __syncthreads();
     cur ^= 1;
   }
+}
+
+// ---- speculative segments of long runs --------------------------------------
+// The walk of a long run is sequential in its records, ~14 us per chunk of
+// 64: the heaviest run of a batch (thousands of packets of one key) bounded
+// the whole walk.  So a long run is cut at the sorted positions that are
+// multiples of kSeg.  Its head wave walks up to the first cut; every later
+// segment is walked at the same time by a wave of its own (walk_seg) that
+// takes as its entry state the key's entry as the table holds it at the start
+// of the batch (nothing else writes that key in this launch), with the ttl
+// unknown (kTtlUnset: a ttl, once set, is now + a constant, never read).  It
+// writes its outcomes and its exit state but nothing to the table, and stops
+// (aborted) at the first record that would need the table.  ct_seg_fix then
+// chains the segments in order: a segment whose entry guess equals the state
+// its predecessor actually left is right as walked (the walk reads nothing
+// else: the ttl is never compared, a long echo reply's quoted key is not
+// written in the batch), and its exit becomes the state; any other segment is
+// walked again from the true state, its outcomes overwritten.  The flows of
+// the bench traffic keep their state across the batch, so their segments all
+// hold; a connection opened or closed mid-run costs one re-walked segment.
+#ifndef PCN_CT_SEG
+#define PCN_CT_SEG 512   // records per segment (a power of two >= kLongRun); 0: no segments
+#endif
+constexpr uint64_t kSeg = PCN_CT_SEG;
+static_assert(kSeg == 0 || (kSeg >= kLongRun && (kSeg & (kSeg - 1)) == 0), "PCN_CT_SEG");
+constexpr unsigned long long kTtlUnset = ~0ull;
+__host__ __device__ constexpr uint64_t seg_count(uint64_t n) { return kSeg ? n / (kSeg ? kSeg : 1) + 1 : 0; }
+
+struct alignas(16) SegRec {       // 64 bytes, one per cut j (sorted position j * kSeg)
+  uint32_t src, dst, ports, gx;   // the guess: key, proto | state << 8 | rev << 16 | live << 24
+  uint32_t gseq, gslot;           //            seq, slot index (~0: none)
+  uint32_t ttl_lo, ttl_hi;        // the exit: ttl (kTtlUnset: none set), seq,
+  uint32_t xseq, xx;              //           state | rev << 8 | live << 16 | dirty << 24
+  uint32_t touch, stop, status;   // LRU touch, where the walk stopped, 0 none / 1 walked / 2 aborted
+  uint32_t pad[3];
+};
+struct alignas(16) HeadExit {     // the head wave's state at its run's first cut
+  uint32_t src, dst, ports, px;   // px: proto | state << 8 | rev << 16 | live << 24
+  uint32_t ttl_lo, ttl_hi, seq, slot;
+  uint32_t flags, touch, vb;      // flags: valid | dirty << 1
+  uint32_t pad[5];
+};
+
+__device__ __forceinline__ uint32_t cache_px(const Cache &c) {
+  return uint32_t(c.k.proto) | uint32_t(c.v.state) << 8 | uint32_t(c.v.rev) << 16 | uint32_t(c.v.live) << 24;
+}
+
+// A long run's head wave: from its head (first) or its cursor up to hi.  With
+// segments, the first pass stops at the run's first cut; if the run goes on
+// there, the state is left to ct_seg_fix (no flush, no cursor).
+__device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, WalkRec (*buf)[64],
+                          uint32_t p, uint32_t *cursor, uint32_t vb, uint64_t hi, int first, HeadExit *hx) {
+  const uint32_t k = wrec.key(p);
+  const uint64_t q0 = first ? p : cursor[vb];
+  const uint64_t bound = (first != 0 && kSeg != 0) ? (p / (kSeg ? kSeg : 1) + 1) * kSeg : ~0ull;
+  Cache c{};
+  bool ab;
+  const uint64_t stop = walk_chunks<false>(b, t, wrec, sres, buf, k, q0, hi, bound, c, ab);
+  bool cont = false;
+  if (stop == bound && bound < b.n) {
+    const uint64_t x = PCN_CT_GATHER ? bound : wrec.sidx[bound];
+    cont = wrec.rec[x].key == k && wrec.rec[x].idx < hi;
+  }
+  if (threadIdx.x != 0) return;
+  if (cont) {
+    HeadExit h{};
+    h.src = c.k.src;
+    h.dst = c.k.dst;
+    h.ports = uint32_t(c.k.sport) | uint32_t(c.k.dport) << 16;
+    h.px = cache_px(c);
+    h.ttl_lo = static_cast<uint32_t>(c.v.ttl);
+    h.ttl_hi = static_cast<uint32_t>(c.v.ttl >> 32);
+    h.seq = c.v.seq;
+    h.slot = c.e ? static_cast<uint32_t>(c.e - t.slots) : ~0u;
+    h.flags = uint32_t(c.valid) | uint32_t(c.dirty) << 1;
+    h.touch = c.touch;
+    h.vb = vb;
+    hx[bound / kSeg] = h;
+  } else {
+    flush(t, c);
+    cursor[vb] = static_cast<uint32_t>(stop);
+  }
+}
+
+// Cut j: if a long run goes on across sorted position B = j * kSeg (the keys
+// at B - 1 and B are the same, and more than kLongRun of them: that run is
+// class 0, exactly as ct_heads decides it), walk its records in [B, B + kSeg)
+// speculatively.  Every cut writes its status.
+__device__ __forceinline__ void walk_seg(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, WalkRec (*buf)[64],
+                         const uint32_t *skeys, uint32_t sentinel, SegRec *seg, uint32_t j, uint64_t hi) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t B = uint64_t(j) * kSeg;
+  bool ok = B > 0 && B < b.n;
+  const uint32_t k = ok ? skeys[B] : 0u;
+  ok = ok && k != sentinel && skeys[B - 1] == k;
+  if (ok) {                                        // the run's length inside [B - kLongRun, B + kLongRun)
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 2 * kLongRun / 64; ++i) {
+      const uint64_t q = B - kLongRun + i * 64 + lane;
+      cnt += static_cast<uint32_t>(__popcll(__ballot(q < b.n && skeys[q] == k)));
+    }
+    ok = cnt > kLongRun;
+  }
+  const WalkRec x = wrec.at(ok ? B : 0);
+  ok = ok && x.idx < hi;
+  if (!ok) {
+    if (lane == 0) seg[j].status = 0;
+    return;
+  }
+  const Key gk{x.r.src, x.r.dst, x.r.sport, x.r.dport, x.r.proto};
+  const SlotRef g = table_slot(t, gk, false);     // the key's entry as the batch found it
+  Cache c{};
+  c.k = gk;
+  c.e = g.e;
+  c.v = g.v;
+  c.v.ttl = kTtlUnset;
+  c.valid = true;
+  bool ab;
+  const uint64_t stop = walk_chunks<true>(b, t, wrec, sres, buf, k, B, hi, B + kSeg, c, ab);
+  if (lane != 0) return;
+  SegRec s{};
+  s.src = gk.src;
+  s.dst = gk.dst;
+  s.ports = uint32_t(gk.sport) | uint32_t(gk.dport) << 16;
+  s.gx = uint32_t(gk.proto) | uint32_t(g.v.state) << 8 | uint32_t(g.v.rev) << 16 | uint32_t(g.v.live) << 24;
+  s.gseq = g.v.seq;
+  s.gslot = g.e ? static_cast<uint32_t>(g.e - t.slots) : ~0u;
+  s.ttl_lo = static_cast<uint32_t>(c.v.ttl);
+  s.ttl_hi = static_cast<uint32_t>(c.v.ttl >> 32);
+  s.xseq = c.v.seq;
+  s.xx = uint32_t(c.v.state) | uint32_t(c.v.rev) << 8 | uint32_t(c.v.live) << 16 | uint32_t(c.dirty) << 24;
+  s.touch = c.touch;
+  s.stop = static_cast<uint32_t>(stop);
+  s.status = ab ? 2u : 1u;
+  seg[j] = s;
 }
 
 struct WalkPlan {
@@ -1114,10 +1261,11 @@ __device__ __forceinline__ uint64_t walk_hi(const CtBatch &b, const uint32_t *ct
 // shorter runs of one class, one per lane, each from its head (first) or its
 // cursor up to batch index hi.  Every lane returns here (no early exit), so a
 // persistent wave can take the next block.
-__device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, const uint32_t *heads,
-                        const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first, uint32_t vb) {
+__device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, WalkRec (*buf)[64],
+                        const uint32_t *heads, const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first,
+                        uint32_t vb, HeadExit *hx) {
   if (vb < plan->blk0[1]) {                       // one wave per long run
-    walk_long(b, t, wrec, sres, heads[vb], &cursor[vb], hi, first);
+    walk_long(b, t, wrec, sres, buf, heads[vb], cursor, vb, hi, first, hx);
     return;
   }
   uint32_t cls = 1;
@@ -1164,13 +1312,82 @@ __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec, 
 // blocks past the plan return at once: a workgroup that returns costs the
 // dispatcher next to nothing, where a persistent grid taking blocks from one
 // counter serialised ~10^5 atomics on one address (7.1 vs 2.9 ms a batch).
+// With segments, the first seg_count(n) workgroups are the cuts (walk_seg).
 __global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t *sres,
-                                                     const uint32_t *heads, const uint32_t *ctl, uint32_t *cursor) {
+                                                     const uint32_t *heads, const uint32_t *ctl, uint32_t *cursor,
+                                                     const uint32_t *skeys, uint32_t sentinel, SegRec *seg,
+                                                     HeadExit *hx) {
+  __shared__ WalkRec buf[2][64];
+  const uint32_t nseg = static_cast<uint32_t>(seg_count(b.n));
+  if (blockIdx.x < nseg) {
+    walk_seg(b, t, wrec, sres, buf, skeys, sentinel, seg, blockIdx.x, walk_hi(b, ctl));
+    return;
+  }
   // (the plan is read in place: a local copy indexed by class went to scratch)
   const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
-  const uint32_t vb = blockIdx.x;
+  const uint32_t vb = blockIdx.x - nseg;
   if (vb >= plan->blk0[kRunClasses]) return;
-  walk_vb(b, t, wrec, sres, heads, plan, cursor, walk_hi(b, ctl), 1, vb);
+  walk_vb(b, t, wrec, sres, buf, heads, plan, cursor, walk_hi(b, ctl), 1, vb, hx);
+}
+
+// One wave per cut j that is its run's first (the head stopped there): chain
+// the run's segments in order from the head's state, re-walking those whose
+// guess does not hold, then flush the connection and set the run's cursor.
+__global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t *sres,
+                                                        const uint32_t *skeys, const SegRec *seg, const HeadExit *hx,
+                                                        uint32_t *cursor, const uint32_t *ctl) {
+  __shared__ WalkRec buf[2][64];
+  const uint32_t j = blockIdx.x;
+  const uint64_t B = uint64_t(j) * kSeg;
+  if (j == 0 || B >= b.n || seg[j].status == 0) return;
+  const uint32_t k = skeys[B];
+  if (j > 1 && skeys[B - kSeg - 1] == k) return;   // the run started before cut j - 1: not its first cut
+  const uint64_t hi = walk_hi(b, ctl);
+  const HeadExit h = hx[j];
+  Cache c{};
+  c.k = Key{h.src, h.dst, static_cast<uint16_t>(h.ports), static_cast<uint16_t>(h.ports >> 16),
+            static_cast<uint8_t>(h.px)};
+  c.e = h.slot != ~0u ? &t.slots[h.slot] : nullptr;
+  c.v = Ent{uint64_t(h.ttl_hi) << 32 | h.ttl_lo, h.seq, static_cast<uint8_t>(h.px >> 8),
+            static_cast<uint8_t>(h.px >> 16), static_cast<uint8_t>(h.px >> 24)};
+  c.valid = h.flags & 1;
+  c.dirty = (h.flags >> 1) & 1;
+  c.touch = h.touch;
+  uint64_t stop = B;
+  for (uint64_t jj = j;; ++jj) {
+    const uint64_t cut = jj * kSeg;
+    if (cut >= b.n) { stop = b.n; break; }
+    const SegRec s = seg[jj];
+    if (s.status == 0) { stop = cut; break; }      // the run ends at this cut (or hi cuts it there)
+    bool held = false;
+    if (threadIdx.x == 0)
+      held = s.status == 1 && c.valid && c.k.src == s.src && c.k.dst == s.dst &&
+             (uint32_t(c.k.sport) | uint32_t(c.k.dport) << 16) == s.ports &&
+             (c.e ? static_cast<uint32_t>(c.e - t.slots) : ~0u) == s.gslot &&
+             cache_px(c) == s.gx && c.v.seq == s.gseq;
+    held = __shfl(held ? 1 : 0, 0) != 0;
+    if (held) {                                    // the segment as walked: its exit is the state
+      if (threadIdx.x == 0) {
+        const unsigned long long ttl = uint64_t(s.ttl_hi) << 32 | s.ttl_lo;
+        if (ttl != kTtlUnset) c.v.ttl = ttl;
+        c.v.seq = s.xseq;
+        c.v.state = static_cast<uint8_t>(s.xx);
+        c.v.rev = static_cast<uint8_t>(s.xx >> 8);
+        c.v.live = static_cast<uint8_t>(s.xx >> 16);
+        if (s.xx >> 24) c.dirty = true;
+        if (s.touch) c.touch = s.touch;
+      }
+      stop = s.stop;
+    } else {
+      bool ab;
+      stop = walk_chunks<false>(b, t, wrec, sres, buf, k, cut, hi, cut + kSeg, c, ab);
+    }
+    if (stop < cut + kSeg) break;                  // the run ended inside this segment
+  }
+  if (threadIdx.x == 0) {
+    flush(t, c);
+    cursor[h.vb] = static_cast<uint32_t>(stop);
+  }
 }
 
 // An echo reply long enough to quote a header (ConntrackLabel_dp.c:450-531)
@@ -1219,6 +1436,7 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
   const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
   const uint32_t total = plan->blk0[kRunClasses];
   uint32_t cur = 0xFFFFFFFFu - th;
+  __shared__ WalkRec buf[2][64];
   for (;;) {
     if (threadIdx.x == 0) hard_step(b, t, brec, cur);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // its table writes before any lane reads on
@@ -1231,7 +1449,7 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
     nxt = wave_min(nxt);
     const uint64_t hi = nxt == 0xFFFFFFFFu ? b.n : nxt;
     for (uint32_t vb = 0; vb < total; ++vb) {
-      walk_vb(b, t, wrec, sres, heads, plan, cursor, hi, 0, vb);
+      walk_vb(b, t, wrec, sres, buf, heads, plan, cursor, hi, 0, vb, nullptr);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __syncthreads();
     }
@@ -1245,23 +1463,25 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
 // After the walk, if more than max_entries entries are live, the live entries
 // with the oldest touch stamps (batch seq << 32 | batch index of the last
 // packet after which each was live; distinct, since a packet touches one key)
-// are deleted down to max_entries.  The cut is a radix select on the 64-bit
-// stamps: six passes of 11 / 11 / 11 / 11 / 11 / 9 bits, each a histogram of
-// the live stamps that match the digits chosen so far; the last workgroup of a
-// pass picks the next digit (no grid-wide wait).  Pass 0 also counts the live
-// entries; every later pass and the eviction return at once when nothing is
-// to be evicted.
+// are deleted down to max_entries.  touch[] holds the stamp of every live
+// entry and ~0 for every other slot, so the cut reads 8 bytes a slot and
+// nothing else: a radix select in six passes of 11 / 11 / 11 / 11 / 11 / 9
+// bits, each a histogram of the stamps that match the digits chosen so far.
+// A pass runs few, large workgroups (each merges its LDS histogram into the
+// global one with one atomic per non-empty bin: with a workgroup per 256
+// slots those merges serialised on the hot bins, 70-320 us a pass), and its
+// last workgroup picks the next digit with a block-wide scan.  Pass 0 also
+// counts the live entries; the later passes and the eviction return at once
+// when nothing is to be evicted.
 constexpr uint32_t kEvBins = 2048;
 constexpr int kEvPasses = 6;
+constexpr uint32_t kEvBlock = 1024;
 __device__ __forceinline__ uint32_t ev_shift(int p) { return p < 5 ? 53 - 11 * p : 0; }
 __device__ __forceinline__ uint32_t ev_width(int p) { return p < 5 ? 11 : 9; }
 
-__device__ __forceinline__ bool slot_live(const CtSlot *e) {
-  return ((slot_half(e, 1).w >> 8) & 0xff) != 0;    // valid (a claimed or empty slot reads 0)
-}
-
-__global__ __launch_bounds__(256) void ct_ev_pass_kernel(CtTable t, uint32_t *ctl, uint32_t *hist, int p) {
+__global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_t *ctl, uint32_t *hist, int p) {
   __shared__ uint32_t h[kEvBins];
+  __shared__ uint32_t scan[kEvBlock];
   __shared__ uint32_t live_s;
   __shared__ bool last;
   if (p > 0 && !ctl[kCtlEvict]) return;
@@ -1272,13 +1492,18 @@ __global__ __launch_bounds__(256) void ct_ev_pass_kernel(CtTable t, uint32_t *ct
   const uint32_t shift = ev_shift(p), width = ev_width(p);
   const uint64_t above = p == 0 ? 0ull : ~((uint64_t(1) << (shift + width)) - 1);
   const uint64_t cap = uint64_t(1) << t.cap_log2;
+  const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
   uint32_t live = 0;
-  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < cap; i += uint64_t(gridDim.x) * blockDim.x) {
-    if (!slot_live(&t.slots[i])) continue;
-    ++live;
-    const uint64_t key = t.touch[i];
-    if ((key & above) != prefix) continue;
-    atomicAdd(&h[(key >> shift) & ((1u << width) - 1)], 1u);
+  for (uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i0 < cap; i0 += 4 * stp) {
+    unsigned long long key[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) key[u] = i0 + u * stp < cap ? t.touch[i0 + u * stp] : ~0ull;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (key[u] == ~0ull) continue;
+      ++live;
+      if ((key[u] & above) == prefix) atomicAdd(&h[(key[u] >> shift) & ((1u << width) - 1)], 1u);
+    }
   }
   if (p == 0 && live) atomicAdd(&live_s, live);
   __syncthreads();
@@ -1290,27 +1515,41 @@ __global__ __launch_bounds__(256) void ct_ev_pass_kernel(CtTable t, uint32_t *ct
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(&ctl[kCtlEvDone], 1u) == gridDim.x - 1;
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
+  if (!last) return;
   __threadfence();
-  // the last workgroup: every histogram of this pass is in
-  ctl[kCtlEvDone] = 0;
+  // the last workgroup: every histogram of this pass is in; the digit whose
+  // bin holds the k-th smallest matching stamp, by a block-wide scan
   uint32_t k;
   if (p == 0) {
     const uint32_t lv = __hip_atomic_load(&ctl[kCtlLive], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!t.max_entries || lv <= t.max_entries) return;     // kCtlEvict stays 0
+    if (!t.max_entries || lv <= t.max_entries) {
+      if (threadIdx.x == 0) ctl[kCtlEvDone] = 0;
+      return;                                          // kCtlEvict stays 0
+    }
     k = lv - static_cast<uint32_t>(t.max_entries);
-    ctl[kCtlEvict] = 1;
   } else {
     k = ctl[kCtlEvK];
   }
-  uint32_t d = 0, below = 0;
-  for (; d < (1u << width); ++d) {
-    const uint32_t c = __hip_atomic_load(&hp[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (below + c >= k) break;
-    below += c;
+  const uint32_t b0 = 2 * threadIdx.x;                 // this thread's two bins
+  const uint32_t c0 = __hip_atomic_load(&hp[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t c1 = __hip_atomic_load(&hp[b0 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  scan[threadIdx.x] = c0 + c1;
+  __syncthreads();
+  for (uint32_t o = 1; o < kEvBlock; o <<= 1) {        // inclusive scan
+    const uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0u;
+    __syncthreads();
+    scan[threadIdx.x] += v;
+    __syncthreads();
   }
-  ctl[kCtlEvK] = k - below;
-  *reinterpret_cast<unsigned long long *>(ctl + kCtlEvPrefix) = prefix | (uint64_t(d) << shift);
+  const uint32_t incl = scan[threadIdx.x], excl = incl - c0 - c1;
+  if (excl < k && k <= incl) {                         // exactly one thread
+    const uint32_t d = excl + c0 >= k ? b0 : b0 + 1;
+    const uint32_t below = d == b0 ? excl : excl + c0;
+    ctl[kCtlEvK] = k - below;
+    *reinterpret_cast<unsigned long long *>(ctl + kCtlEvPrefix) = prefix | (uint64_t(d) << shift);
+    if (p == 0) ctl[kCtlEvict] = 1;
+  }
+  if (threadIdx.x == 0) ctl[kCtlEvDone] = 0;          // for the next pass
 }
 
 // Delete the live entries whose stamp is at most the chosen one (exactly the
@@ -1324,11 +1563,13 @@ __global__ __launch_bounds__(256) void ct_ev_evict_kernel(CtTable t, const uint3
   const uint64_t cap = uint64_t(1) << t.cap_log2;
   uint32_t n = 0;
   for (uint64_t i = g; i < cap; i += stp) {
+    const unsigned long long key = t.touch[i];
+    if (key > cut) continue;                           // newer, or not live (~0)
     CtSlot *e = &t.slots[i];
-    if (!slot_live(e) || t.touch[i] > cut) continue;
     ct_u32x4 hi = slot_half(e, 1);
     hi.w &= ~0xff00u;                                  // valid = 0: connections.delete
     reinterpret_cast<ct_u32x4 *>(e)[1] = hi;
+    t.touch[i] = ~0ull;
     ++n;
   }
   if (n) atomicAdd(&t.stats[1], static_cast<unsigned long long>(n));
@@ -1530,6 +1771,8 @@ struct CtScratch {
   uint32_t *evh = nullptr;                // LRU radix-select histograms (kEvPasses x kEvBins, kept zeroed)
   uint64_t bm_bytes = 0;
   uint32_t *heads = nullptr;
+  SegRec *seg = nullptr;                  // speculative segments of long runs (walk_seg, ct_seg_fix)
+  HeadExit *hx = nullptr;
   int32_t *sres = nullptr;
   WalkRec *brec = nullptr;   // batch order
   WalkRec *wrec = nullptr;
@@ -1549,7 +1792,7 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->ctl), static_cast<void *>(s->brec), static_cast<void *>(s->wrec),
                   static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
                   static_cast<void *>(s->zfound), static_cast<void *>(s->th_list), static_cast<void *>(s->bm),
-                  static_cast<void *>(s->evh)})
+                  static_cast<void *>(s->evh), static_cast<void *>(s->seg), static_cast<void *>(s->hx)})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -1563,7 +1806,7 @@ int ct_table_init(CtTable &t, uint32_t cap_log2) {
   if (e == hipSuccess) e = hipMemset(t.carry, 0, 64);
   if (e == hipSuccess) t.stats = reinterpret_cast<unsigned long long *>(t.carry + 2);
   if (e == hipSuccess) e = hipMalloc(&t.touch, n * 8);
-  if (e == hipSuccess) e = hipMemset(t.touch, 0, n * 8);
+  if (e == hipSuccess) e = hipMemset(t.touch, 0xff, n * 8);     // ~0: no live entry
   t.cap_log2 = cap_log2;
   t.seq = 1;
   return e;
@@ -1626,6 +1869,12 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     if (s.wrec) CT_CHECK(hipFree(s.wrec));
     s.wrec = nullptr;
     if (PCN_CT_GATHER) CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
+    if (kSeg) {
+      if (s.seg) CT_CHECK(hipFree(s.seg));
+      if (s.hx) CT_CHECK(hipFree(s.hx));
+      CT_CHECK(hipMalloc(&s.seg, (seg_count(n) + 1) * sizeof(SegRec)));
+      CT_CHECK(hipMalloc(&s.hx, (seg_count(n) + 1) * sizeof(HeadExit)));
+    }
     if (!s.ctl) CT_CHECK(hipMalloc(&s.ctl, kCtlWords * 4));   // the kCtl* words + the walk plan
     if (!s.evh) {
       CT_CHECK(hipMalloc(&s.evh, kEvPasses * kEvBins * 4));
@@ -1751,19 +2000,27 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   // the walk plan, sized on the device: no read-back, the stream stays asynchronous
   hipLaunchKernelGGL(ct_plan_kernel, dim3(1), dim3(64), 0, st, s.ctl);
   CT_CHECK(hipGetLastError());
-  const unsigned wgrid = static_cast<unsigned>(b.n / 64 + kRunClasses + 1);   // the plan's upper bound
-  hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.sres, s.heads, s.ctl, s.cursor);
+  // the cuts of long runs, then the plan's upper bound
+  const unsigned wgrid = static_cast<unsigned>(seg_count(b.n) + b.n / 64 + kRunClasses + 1);
+  hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.sres, s.heads, s.ctl, s.cursor,
+                     s.keys2, sentinel, s.seg, s.hx);
   CT_CHECK(hipGetLastError());
+  if (kSeg) {
+    hipLaunchKernelGGL(ct_seg_fix_kernel, dim3(static_cast<unsigned>(seg_count(b.n))), dim3(64), 0, st, b, t, src,
+                       s.sres, s.keys2, s.seg, s.hx, s.cursor, s.ctl);
+    CT_CHECK(hipGetLastError());
+  }
   hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.sres, s.heads, s.ctl, s.th_list,
                      s.cursor);
   CT_CHECK(hipGetLastError());
   if (t.max_entries) {                         // LRU down to max_entries (no read-back either)
     const uint64_t cap = uint64_t(1) << t.cap_log2;
-    const unsigned egrid = static_cast<unsigned>(std::min<uint64_t>(cap / 256 + 1, uint64_t(num_cus) * 4));
+    const unsigned pgrid2 = static_cast<unsigned>(std::min<uint64_t>(cap / (4 * kEvBlock) + 1, 64));
     for (int p = 0; p < kEvPasses; ++p) {
-      hipLaunchKernelGGL(ct_ev_pass_kernel, dim3(egrid), dim3(256), 0, st, t, s.ctl, s.evh, p);
+      hipLaunchKernelGGL(ct_ev_pass_kernel, dim3(pgrid2), dim3(kEvBlock), 0, st, t, s.ctl, s.evh, p);
       CT_CHECK(hipGetLastError());
     }
+    const unsigned egrid = static_cast<unsigned>(std::min<uint64_t>(cap / 256 + 1, uint64_t(num_cus) * 4));
     hipLaunchKernelGGL(ct_ev_evict_kernel, dim3(egrid), dim3(256), 0, st, t, s.ctl, s.evh);
     CT_CHECK(hipGetLastError());
   }

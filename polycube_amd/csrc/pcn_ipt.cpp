@@ -1432,7 +1432,7 @@ int pcn_ipt_ct_clear(pcn_ipt *ctx) {
     hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_check(hipMemset(ctx->ct.slots, 0, (size_t(1) << ctx->ct.cap_log2) * sizeof(CtSlot)), "hipMemset(conntrack)");
     hip_check(hipMemset(ctx->ct.carry, 0, 64), "hipMemset(conntrack)");
-    hip_check(hipMemset(ctx->ct.touch, 0, (size_t(1) << ctx->ct.cap_log2) * 8), "hipMemset(conntrack)");
+    hip_check(hipMemset(ctx->ct.touch, 0xff, (size_t(1) << ctx->ct.cap_log2) * 8), "hipMemset(conntrack)");
     ctx->ct.seq = 1;
     return 0;
   });

@@ -217,14 +217,17 @@ def config_frames(cfg, n, rs=None, seed=None):
     return build_frames(*cols, frame_len=64)
 
 
-def imix_frames(rs, n, seed, *, vlan_frac=0.3, ipv6_frac=0.3):
+def imix_frames(rs, n, seed, *, vlan_frac=0.3, ipv6_frac=0.3, align=1):
     """Config 5: IMIX 7:4:1 of 64/576/1500-byte frames packed back to back, with
-    802.1Q-tagged and IPv6 frames mixed in.  Returns (buffer, offsets, lens)."""
+    802.1Q-tagged and IPv6 frames mixed in.  align=64 starts every frame at a
+    64-byte boundary instead (how NIC RX buffers place them); the frames and
+    their lengths are the same.  Returns (buffer, offsets, lens)."""
     rng = np.random.default_rng(seed ^ 0x1111)
     sizes = rng.choice(np.array([64, 576, 1500]), p=[7 / 12, 4 / 12, 1 / 12], size=n).astype(np.int64)
+    slots = (sizes + align - 1) // align * align
     offsets = np.zeros(n, np.int64)
-    offsets[1:] = np.cumsum(sizes)[:-1]
-    total = int(sizes.sum())
+    offsets[1:] = np.cumsum(slots)[:-1]
+    total = int(slots.sum())
     buf = np.zeros(total + 64, np.uint8)
     cols = make_headers(rs, n, seed)
     hdr = build_frames(*cols, frame_len=64)

@@ -487,3 +487,110 @@ def test_lru_crosses_the_reference_capacity(dev):
         assert_tables(o, ipt)
     assert len(ipt.ct_dump()) == 65536
     assert ipt.ct_info()["evicted"] == o.ct_info()["evicted"]
+
+
+def _elephants(rng, flows, phase, per, *, close_at=None, reopen_at=None):
+    """`per` packets of each long flow (proto, src, dst, sport, dport, X, Y) in
+    arrival order, randomly interleaved: phase "open" starts TCP with its
+    handshake, "data" continues it; a flow in `close_at` (flow -> fraction)
+    sends FIN-ACK, FIN-ACK, ACK there and data after it, one in `reopen_at`
+    a new SYN.  UDP flows alternate directions."""
+    cols = {k: [] for k in ("t", "src", "dst", "proto", "sport", "dport", "flags", "seq", "ack")}
+    for f, (proto, a, b, pa, pb, X, Y) in enumerate(flows):
+        t = np.sort(rng.random(per))
+        rev = (np.arange(per) % 2).astype(bool)
+        flags = np.where(rng.random(per) < 0.3, 0x18, 0x10)
+        seq = np.where(rev, Y + 1, X + 1)
+        ack = np.where(rev, X + 1, Y + 1)
+        if proto == synth.TCP and phase == "open":
+            rev[:3] = (False, True, False)
+            flags[:3] = (0x02, 0x12, 0x10)
+            seq[:3] = (X, Y, X + 1)
+            ack[:3] = (0, X + 1, Y + 1)
+        if proto == synth.TCP and close_at and f in close_at:
+            c = int(per * close_at[f])
+            rev[c:c + 3] = (False, True, False)
+            flags[c:c + 3] = (0x11, 0x11, 0x10)
+            seq[c:c + 3] = (X + 1, Y + 1, X + 2)
+            ack[c:c + 3] = (Y + 1, X + 2, Y + 2)
+        if proto == synth.TCP and reopen_at and f in reopen_at:
+            c = int(per * reopen_at[f])
+            rev[c], flags[c], seq[c], ack[c] = False, 0x02, X + 7, 0
+        cols["t"].append(t)
+        cols["src"].append(np.where(rev, b, a))
+        cols["dst"].append(np.where(rev, a, b))
+        cols["sport"].append(np.where(rev, pb, pa))
+        cols["dport"].append(np.where(rev, pa, pb))
+        cols["proto"].append(np.full(per, proto))
+        cols["flags"].append(np.where(proto == synth.TCP, flags, 0))
+        cols["seq"].append(seq & 0xFFFFFFFF)
+        cols["ack"].append(ack & 0xFFFFFFFF)
+    c = {k: np.concatenate(v) for k, v in cols.items()}
+    o = np.argsort(c["t"], kind="stable")
+    c = {k: v[o] for k, v in c.items()}
+    f = synth.build_frames(c["src"].astype(np.uint32), c["dst"].astype(np.uint32), c["proto"].astype(np.int32),
+                           c["sport"], c["dport"], c["flags"].astype(np.int32), frame_len=128)
+    synth.set_tcp_seq(f, c["proto"] == synth.TCP, c["seq"].astype(np.uint64), c["ack"].astype(np.uint64))
+    return f
+
+
+def test_long_runs_in_speculative_segments(dev):
+    """Runs of thousands of packets cut every PCN_CT_SEG (512) sorted positions:
+    the head wave walks to the first cut, every later segment is walked at once
+    from the key's entry as the batch found it, and ct_seg_fix chains them,
+    re-walking those whose guess did not hold.  Batch 1 opens the flows (no
+    guess holds), batch 2 continues them under a new clock (every guess holds,
+    the ttl set anew), batch 3 closes some mid-run (FIN) and reopens one (SYN),
+    batch 4 adds ICMP errors quoting them and long echo replies quoting them
+    (the walk stops at the first; ct_tail resumes).  Interleaved with short
+    flows.  Bit-exact vs the oracle: verdicts, rule ids, counters, the table."""
+    rng = np.random.default_rng(57)
+    rules = CT_RULES + synth.config_rules(2).rules()
+    o, ipt = ct_pair({1: rules}, {1: "ACCEPT"}, cap_log2=16, jit=1)
+    ips = rng.integers(1, 2**32, size=(9, 2), dtype=np.uint64)
+    flows = [(synth.TCP if k < 6 else synth.UDP, int(ips[k, 0]), int(ips[k, 1]), 1000 + k, 80 + k,
+              int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32))) for k in range(9)]
+    short, _ = synth.flow_traffic(8000 * 4, 2000, 58, stride=128, p_icmp=0.1, p_err=0.02)
+    short = short.reshape(-1, 128)
+    phases = [("open", {}, {}), ("data", {}, {}), ("data", {0: 0.4, 2: 0.05, 4: 0.93}, {2: 0.7}), ("data", {}, {})]
+    for k, (phase, close, reopen) in enumerate(phases):
+        ipt.ct_set_time(NOW + k * 10**9)
+        o.ct_set_time(NOW + k * 10**9)
+        el = _elephants(rng, flows, phase, 3000, close_at=close, reopen_at=reopen)
+        n = len(el) + 8000
+        nb = np.empty((n, 128), np.uint8)
+        slot = np.zeros(n, bool)
+        slot[rng.choice(n, size=8000, replace=False)] = True
+        nb[~slot] = el
+        nb[slot] = short[k * 8000:(k + 1) * 8000]
+        lens = np.full(n, 128, np.uint16)
+        if k == 3:
+            # ICMP errors quoting the long flows (their runs), and long echo
+            # replies quoting them (their quoted bucket is in the batch: ct_tail)
+            m = rng.choice(n, size=300, replace=False)
+            err, rep = m[:250], m[250:]
+            q = rng.integers(0, 9, size=300)
+            qa = np.array([flows[j][1] for j in q], np.uint64)
+            qb = np.array([flows[j][2] for j in q], np.uint64)
+            mask = np.zeros(n, bool)
+            mask[m] = True
+            nb[m, 23] = 1
+            nb[err, 34] = 3
+            nb[rep, 34] = 0
+            nb[m, 35] = 0
+            isrc = np.zeros(n, np.uint64)
+            idst = np.zeros(n, np.uint64)
+            ipr = np.zeros(n, np.int64)
+            isp = np.zeros(n, np.int64)
+            idp = np.zeros(n, np.int64)
+            isrc[m], idst[m] = qa, qb
+            ipr[m] = [flows[j][0] for j in q]
+            isp[m] = [flows[j][3] for j in q]
+            idp[m] = [flows[j][4] for j in q]
+            synth.set_icmp_inner(nb, mask, isrc, idst, ipr, isp, idp)
+            lens[rep] = 98
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, nb.reshape(-1), n, lens=lens)
+        assert_same(v_o, r_o, v_g, r_g)
+        assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_ae(o, ipt)

@@ -168,15 +168,17 @@ def test_fuzz_parity(dev, seed, jit):
 
 @JIT
 @pytest.mark.parametrize("hook", [0, 1], ids=["xdp", "tc"])
-def test_imix_config5_parity(dev, jit, hook):
+@pytest.mark.parametrize("align", [1, 64], ids=["packed", "aligned"])
+def test_imix_config5_parity(dev, jit, hook, align):
     """10k rules (extended limits), IMIX 64/576/1500 with VLAN/IPv6 mixed in
-    (variable offsets).  XDP: tagged and IPv6 frames pass unclassified; TC:
-    the outer VLAN tag is stripped first and the inner IPv4 is classified."""
+    (variable offsets), packed back to back or 64-byte aligned.  XDP: tagged
+    and IPv6 frames pass unclassified; TC: the outer VLAN tag is stripped first
+    and the inner IPv4 is classified."""
     rs = synth.config_rules(5)
     o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, max_rules=16384, max_counted_rules=10000,
                        max_action_rules=10000, jit=jit)
     n = 1 << 17
-    buf, offsets, lens = synth.imix_frames(rs, n, 5)
+    buf, offsets, lens = synth.imix_frames(rs, n, 5, align=align)
     v_o, r_o, v_g, r_g = run_both(o, ipt, dev, buf, n, offsets=offsets, lens=lens, hook=hook)
     assert_same(v_o, r_o, v_g, r_g)
     assert_counters(o, ipt, n=10000)

@@ -33,8 +33,8 @@ def child(lib, hit, log2n, iters, cfg, jit):
     fw.apply_rules()
     n = 1 << log2n
     kw = {}
-    if cfg == 5:      # IMIX offsets/lens, TC hook when CFG5_HOOK=tc
-        buf, off, ln = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5])
+    if cfg == 5:      # IMIX offsets/lens, TC hook when CFG5_HOOK=tc, 64-byte aligned when CFG5_ALIGN=64
+        buf, off, ln = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5], align=int(os.environ.get("CFG5_ALIGN", "1")))
         frames = torch.from_numpy(buf).cuda()
         kw = dict(offsets=torch.from_numpy(off.view(np.int32)).cuda(), lens=torch.from_numpy(ln.view(np.int16)).cuda(),
                   hook=1 if os.environ.get("CFG5_HOOK") == "tc" else 0)
