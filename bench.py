@@ -192,6 +192,30 @@ def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3):
     return best
 
 
+def gather_ceiling(frames, offsets, lens, n, s_ptr, kern_ms):
+    """Config 5: the read ceiling of its own access pattern on the same device
+    buffers -- per frame the offset, the length and the 52-byte header window,
+    one verdict byte out, no classification (tools/gather_ceiling.hip, four
+    lanes per frame, 16-byte loads).  None when the probe library is absent."""
+    import ctypes
+    import torch
+    path = os.path.join(ROOT, "tools", "libgather_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.gather_ceiling_ms.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+    out = torch.empty(n, dtype=torch.uint8, device=frames.device)
+    ms = ctypes.c_float(0)
+    rc = lib.gather_ceiling_ms(frames.data_ptr(), offsets.data_ptr(), lens.data_ptr(), out.data_ptr(), n, 200, 50,
+                               ctypes.c_void_p(s_ptr), ctypes.byref(ms))
+    if rc != 0:
+        return {"error": rc}
+    return {"ms": round(ms.value, 4), "frac_of_ceiling": round(ms.value / kern_ms, 4),
+            "what": "tools/gather_ceiling.hip on the same buffers: offset + length + 52-byte header window per "
+                    "frame (4 lanes x 16-byte loads), one byte out, no classification"}
+
+
 def ct_rate(ipt, rs, n, dev, steps=5, warmup=2, flows=1 << 16, seed=0xC7):
     """Stateful conntrack (pcn_ipt_ct_*) on the same chain: n 64-byte frames of
     `flows` interleaved connections (TCP handshakes/closes, UDP, ICMP), the
@@ -522,6 +546,8 @@ def main():
             "settle": {"seconds": round(settle_s, 2), "steps": settle_steps,
                        "what": "untimed steps before the warmup steps, until the GPU clocks reach steady state"},
         }
+        if cfg == 5:
+            line["roofline"]["gather_ceiling"] = gather_ceiling(frames, offsets, lens, n, s_ptr, kern_ms)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_rates(rules, frames_host, n, WORKLOADS[cfg], offsets_host, lens_host, hook,
                                              big or None, with_nproc=True)

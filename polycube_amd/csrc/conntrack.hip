@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <vector>
@@ -161,40 +162,81 @@ __device__ __forceinline__ uint64_t key_hash(uint32_t src, uint32_t dst, uint8_t
   return h ^ (h >> 32);
 }
 
-// A packet's walk input (64 B: one line): its record, key bucket, batch index
-// and stage-A outcomes (rule id << 1 | verdict per label).  ct_prep writes
-// them in batch order (coalesced reads of the stage-A outcomes), ct_gather
-// moves them into sorted order with one 64-byte read each.
-struct alignas(16) WalkRec {
+// A packet's walk record in HBM (32 B), written by ct_prep in batch order and
+// read by the walk through the sorted index: the fields the label / update
+// code reads and the stage-A outcome of label 0 (rule id << 1 | verdict).
+// The key bucket and batch index come from the sorted arrays, the outcomes of
+// labels 1-3 (only when a chain has conntrack rules) from a side array.  (A
+// 64-byte record held all of them: twice the bytes for ct_prep to write and
+// for the walk's random gathers to read.)
+struct alignas(16) PackedRec {
+  uint32_t src, dst;
+  uint32_t ports;          // sport | dport << 16
+  uint32_t seq, ack, iports;
+  uint32_t pfk;            // proto | flags << 8 | kind << 16 | (rev | cinfo << 2) << 24
+  int32_t o0;
+};
+static_assert(sizeof(PackedRec) == 32, "PackedRec is 32 bytes");
+
+// The walk's working copy of a record, in registers.
+struct WalkRec {
   CtRec r;
   uint32_t key, idx;
   int32_t o0, o1, o2, o3;
-  uint32_t pad[2];
 };
-static_assert(sizeof(WalkRec) == 64, "WalkRec is 64 bytes");
 
-// One record as four 16-byte loads (a field-by-field copy of the packed
-// struct issues ~20 narrow loads per record on the walk's critical path).
-__device__ __forceinline__ WalkRec load_rec(const WalkRec *p) {
-  const ct_u32x4 *s = reinterpret_cast<const ct_u32x4 *>(p);
-  union {
-    ct_u32x4 v[4];
-    WalkRec w;
-  } u;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) u.v[k] = s[k];
-  return u.w;
+__device__ __forceinline__ PackedRec pack_rec(const CtRec &r, int32_t o0) {
+  PackedRec p;
+  p.src = r.src;
+  p.dst = r.dst;
+  p.ports = uint32_t(r.sport) | uint32_t(r.dport) << 16;
+  p.seq = r.seq;
+  p.ack = r.ack;
+  p.iports = r.iports;
+  p.pfk = uint32_t(r.proto) | uint32_t(r.flags) << 8 | uint32_t(r.kind) << 16 | uint32_t(r.rev | r.cinfo << 2) << 24;
+  p.o0 = o0;
+  return p;
 }
 
-__device__ __forceinline__ void store_rec(WalkRec *p, const WalkRec &w) {
+__device__ __forceinline__ CtRec ct_rec(const PackedRec &p) {
+  CtRec r{};
+  r.src = p.src;
+  r.dst = p.dst;
+  r.sport = static_cast<uint16_t>(p.ports);
+  r.dport = static_cast<uint16_t>(p.ports >> 16);
+  r.seq = p.seq;
+  r.ack = p.ack;
+  r.iports = p.iports;
+  r.proto = static_cast<uint8_t>(p.pfk);
+  r.flags = static_cast<uint8_t>(p.pfk >> 8);
+  r.kind = static_cast<uint8_t>(p.pfk >> 16);
+  r.rev = static_cast<uint8_t>((p.pfk >> 24) & 3);
+  r.cinfo = static_cast<uint8_t>(p.pfk >> 26);
+  return r;
+}
+
+// One record as two 16-byte loads (a field-by-field copy of the packed
+// struct issues narrow loads on the walk's critical path).
+__device__ __forceinline__ PackedRec load_prec(const PackedRec *p) {
+  const ct_u32x4 *s = reinterpret_cast<const ct_u32x4 *>(p);
   union {
-    ct_u32x4 v[4];
-    WalkRec w;
+    ct_u32x4 v[2];
+    PackedRec r;
   } u;
-  u.w = w;
+  u.v[0] = s[0];
+  u.v[1] = s[1];
+  return u.r;
+}
+
+__device__ __forceinline__ void store_prec(PackedRec *p, const PackedRec &r) {
+  union {
+    ct_u32x4 v[2];
+    PackedRec r;
+  } u;
+  u.r = r;
   ct_u32x4 *d = reinterpret_cast<ct_u32x4 *>(p);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) d[k] = u.v[k];
+  d[0] = u.v[0];
+  d[1] = u.v[1];
 }
 
 __device__ __forceinline__ int32_t pack_outcome(const CtBatch &b, uint32_t l, uint64_t i) {
@@ -247,9 +289,8 @@ __device__ uint32_t ports_lookback(const unsigned long long *desc, uint64_t g, c
 #endif
 constexpr uint32_t kPrepBlock = 256;
 constexpr uint32_t kPrepRow = 5;                 // 16-byte chunks per frame row in LDS (4 + 1 of padding)
-__global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const uint32_t *carry, WalkRec *brec, uint32_t *lcs, uint32_t *keys,
-                               uint32_t *idx,
-                               uint32_t kbits, uint32_t *hard_cnt, uint32_t *hard_list, unsigned long long *desc,
+__global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const uint32_t *carry, PackedRec *brec,
+                               ct_u32x4 *ox, uint32_t *lcs, uint32_t *keys, uint32_t kbits, uint32_t *hard_cnt, uint32_t *hard_list, unsigned long long *desc,
                                uint32_t *chunk_ctr, uint32_t chunk_frames) {
   const uint32_t sentinel = (1u << kbits) - 1;
   const uint32_t lane = __lane_id();
@@ -325,7 +366,7 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
       if (!wm && lane == 0)
         __hip_atomic_store(&desc[g], ports_word(kStIncl, cin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    WalkRec wr;
+    PackedRec pr;
     if (valid) {
       CtRec r{};
       r.len = static_cast<uint16_t>(p.L);
@@ -401,42 +442,39 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
         }
       }
       r.cinfo = static_cast<uint8_t>((chain & 3) | (pass ? 4 : 0));
-      idx[i] = static_cast<uint32_t>(i);
       const bool member = r.kind >= K_TCP && r.kind <= K_ERR;
       const uint32_t key = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
                                   : sentinel;
       keys[i] = key;
       lcs[i] = uint32_t(r.len) | uint32_t(r.cinfo) << 16;   // what ct_count reads (not the 64-byte record)
-      wr.r = r;
-      wr.key = key;
-      wr.idx = static_cast<uint32_t>(i);
-      wr.o0 = pack_outcome(b, 0, i);
-      wr.o1 = pack_outcome(b, 1, i);
-      wr.o2 = pack_outcome(b, 2, i);
-      wr.o3 = pack_outcome(b, 3, i);
-      wr.pad[0] = wr.pad[1] = 0;
+      const int32_t o0 = pack_outcome(b, 0, i);
+      pr = pack_rec(r, o0);
+      if (b.nlab == 4)
+        ox[i] = ct_u32x4{static_cast<uint32_t>(o0), static_cast<uint32_t>(pack_outcome(b, 1, i)),
+                         static_cast<uint32_t>(pack_outcome(b, 2, i)), static_cast<uint32_t>(pack_outcome(b, 3, i))};
 #if PCN_CT_PREP_LDS
       if (fast) {                                       // this lane's record into its LDS row
         union {
-          ct_u32x4 v[4];
-          WalkRec rec;
+          ct_u32x4 v[2];
+          PackedRec rec;
         } u;
-        u.rec = wr;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) stage[lane * kPrepRow + k] = u.v[k];
+        u.rec = pr;
+        stage[lane * kPrepRow] = u.v[0];
+        stage[lane * kPrepRow + 1] = u.v[1];
       } else {
-        store_rec(&brec[i], wr);
+        store_prec(&brec[i], pr);
       }
 #else
-      store_rec(&brec[i], wr);
+      store_prec(&brec[i], pr);
 #endif
       if (r.kind == K_HARD) hard_list[atomicAdd(hard_cnt, 1u)] = static_cast<uint32_t>(i);
-      if (!member && r.kind != K_HARD) {
-        // no table access: the outcome of label INVALID (K_INV) or of any label
-        const uint32_t l = (r.kind == K_INV && !pass && b.nlab == 4) ? 3u : 0u;
-        b.verdicts[i] = b.a_verdict[l * b.n + i];
-        b.rule_ids[i] = b.a_rid[l * b.n + i];
-      }
+      // every packet's outcome as far as it is known here, coalesced: final for
+      // those with no table access (label INVALID for K_INV, else any label);
+      // the label-0 one for the rest, which the walk overwrites only where it
+      // differs (put_outcome)
+      const uint32_t l = (!member && r.kind == K_INV && !pass && b.nlab == 4) ? 3u : 0u;
+      b.verdicts[i] = b.a_verdict[l * b.n + i];
+      b.rule_ids[i] = b.a_rid[l * b.n + i];
     }
 #if PCN_CT_PREP_LDS
     if (fast) {                                         // the wave's records as coalesced chunks
@@ -445,9 +483,9 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       ct_u32x4 *dst = reinterpret_cast<ct_u32x4 *>(brec + i0);
 #pragma unroll
-      for (uint32_t q = 0; q < 4; ++q) {
+      for (uint32_t q = 0; q < 2; ++q) {
         const uint32_t t = q * 64 + lane;
-        if (i0 + (t >> 2) < hi) dst[t] = stage[(t >> 2) * kPrepRow + (t & 3)];
+        if (i0 + (t >> 1) < hi) dst[t] = stage[(t >> 1) * kPrepRow + (t & 1)];
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -815,12 +853,6 @@ __host__ __device__ constexpr uint64_t class_off(uint64_t n, uint32_t c) {
 }
 __host__ __device__ constexpr uint64_t heads_cap(uint64_t n) { return class_off(n, kRunClasses); }
 
-__global__ void ct_gather_kernel(CtBatch b, const WalkRec *brec, const uint32_t *skeys, const uint32_t *sidx,
-                                 WalkRec *wrec, uint32_t sentinel) {
-  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < b.n; q += step)
-    if (skeys[q] != sentinel) store_rec(&wrec[q], load_rec(&brec[sidx[q]]));
-}
 
 // The run heads of each class.  A workgroup stages a contiguous tile of
 // `per` x kHeadsBlock sorted keys (plus the key before it and kLongRun
@@ -917,34 +949,49 @@ __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const
 // its result becomes the cache; only a record that needs the table itself (a
 // slot to claim, another key of the bucket) takes step() on lane 0.  The next
 // round starts after that record, so a chunk costs one round per change.
-#ifndef PCN_CT_GATHER
-// 0: the walk reads each record from batch order through the sorted index
-// (a dependent load, but no gather pass: -0.4..-0.6 ms a batch, the walk
-// +0.3 ms); 1: ct_gather copies the records into sorted order first
-#define PCN_CT_GATHER 0
-#endif
-#ifndef PCN_CT_DIRECT
-// 1: the walk writes the final verdicts / rule ids by batch index, no scatter
-// pass (A/B: walk +0.3..0.4 ms, scatter -0.7 ms a batch); 0: sorted-order
-// outcomes, then ct_scatter
-#define PCN_CT_DIRECT 1
-#endif
-// A walked packet's outcome: into sres at its sorted position (ct_scatter
-// moves it to batch order), or (PCN_CT_DIRECT) straight to batch index i.
-__device__ __forceinline__ void put_outcome(const CtBatch &b, int32_t *sres, uint64_t q, uint32_t i, int32_t o) {
-  if (PCN_CT_DIRECT) {
-    b.verdicts[i] = static_cast<uint8_t>(o & 1);
-    b.rule_ids[i] = o >> 1;
-  } else {
-    sres[q] = o;
+// (The walk reads each record from batch order through the sorted index: a
+// dependent load, but no gather pass into sorted order, which cost 0.4-0.6 ms
+// a batch more than the walk saved.)
+// A walked packet's outcome, by batch index.  ct_prep has already written
+// every packet's label-0 outcome (coalesced), so a walk stores only the
+// outcomes that differ from it (sparse): the scattered one-byte and four-byte
+// stores by batch index cost the walk as much as its record gathers, and with
+// rules that do not match on conntrack state nearly every outcome is the
+// label-0 one.  A re-walk over a speculative segment stores them all (dense),
+// since the speculation may have stored others.  (Writing sorted-order
+// outcomes and scattering them in a pass of their own cost 0.3-0.4 ms more.)
+__device__ __forceinline__ void put_outcome(const CtBatch &b, const WalkRec &w, int32_t o, bool dense) {
+  if (dense || o != w.o0) {
+    b.verdicts[w.idx] = static_cast<uint8_t>(o & 1);
+    b.rule_ids[w.idx] = o >> 1;
   }
 }
 
 struct RecSrc {
-  const WalkRec *rec;     // sorted order (gathered) or batch order
-  const uint32_t *sidx;   // sorted position -> batch index (PCN_CT_GATHER 0)
-  __device__ __forceinline__ WalkRec at(uint64_t q) const { return load_rec(&rec[PCN_CT_GATHER ? q : sidx[q]]); }
-  __device__ __forceinline__ uint32_t key(uint64_t q) const { return rec[PCN_CT_GATHER ? q : sidx[q]].key; }
+  const PackedRec *rec;   // batch order
+  const uint32_t *sidx;   // sorted position -> batch index
+  const uint32_t *skeys;  // sorted position -> key bucket
+  const ct_u32x4 *ox;     // the four stage-A outcomes per packet (lab4 only)
+  uint32_t lab4;          // the batch has four labels (a chain with conntrack rules)
+  // the record of batch index i at sorted position q
+  __device__ __forceinline__ WalkRec load(uint32_t i, uint64_t q) const {
+    WalkRec w;
+    const PackedRec p = load_prec(&rec[i]);
+    w.r = ct_rec(p);
+    w.key = skeys[q];
+    w.idx = i;
+    w.o0 = p.o0;
+    w.o1 = w.o2 = w.o3 = 0;
+    if (lab4) {
+      const ct_u32x4 v = ox[i];
+      w.o1 = static_cast<int32_t>(v.y);
+      w.o2 = static_cast<int32_t>(v.z);
+      w.o3 = static_cast<int32_t>(v.w);
+    }
+    return w;
+  }
+  __device__ __forceinline__ WalkRec at(uint64_t q) const { return load(sidx[q], q); }
+  __device__ __forceinline__ uint32_t key(uint64_t q) const { return skeys[q]; }
 };
 
 // The walk of one long run's records in chunks of 64, from sorted position q0
@@ -953,32 +1000,55 @@ struct RecSrc {
 // Returns the sorted position where it stopped.  kSpec: a speculative segment
 // (walk_seg): it may not touch the table, so where a record needs it (cls 2)
 // the walk stops there and sets `aborted`.
+// A lane's record, to every lane (one record of a chunk: the rare table step).
+__device__ __forceinline__ WalkRec shfl_rec(const WalkRec &w, uint32_t from) {
+  const int f = static_cast<int>(from);
+  union {
+    ct_u32x4 v[2];
+    PackedRec p;
+  } u;
+  u.p = pack_rec(w.r, w.o0);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    u.v[q].x = __shfl(u.v[q].x, f);
+    u.v[q].y = __shfl(u.v[q].y, f);
+    u.v[q].z = __shfl(u.v[q].z, f);
+    u.v[q].w = __shfl(u.v[q].w, f);
+  }
+  WalkRec x;
+  x.r = ct_rec(u.p);
+  x.key = __shfl(w.key, f);
+  x.idx = __shfl(w.idx, f);
+  x.o0 = u.p.o0;
+  x.o1 = __shfl(w.o1, f);
+  x.o2 = __shfl(w.o2, f);
+  x.o3 = __shfl(w.o3, f);
+  return x;
+}
+
+// The chunk a lane walks is its own record in registers, and the next chunk's
+// record is in flight meanwhile (one load per lane).  (The first version staged
+// chunks in LDS behind two workgroup barriers each, whose release waited for
+// the chunk's scattered outcome stores.)
 template <bool kSpec>
-__device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres,
-                                                WalkRec (*buf)[64], uint32_t k, uint64_t q0, uint64_t hi,
-                                                uint64_t bound, Cache &c, bool &aborted) {
+__device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
+                                                uint32_t k, uint64_t q0, uint64_t hi, uint64_t bound, Cache &c,
+                                                bool &aborted, bool dense = false) {
   const uint32_t lane = threadIdx.x;
   const uint64_t last = b.n - 1;
   const uint64_t lim = bound < b.n ? bound : b.n;
   uint64_t base = q0;
   aborted = false;
-  auto ix = [&](uint64_t r) -> uint64_t {       // sorted position -> the record's index
-    r = r < last ? r : last;
-    return PCN_CT_GATHER ? r : wrec.sidx[r];
-  };
-  __syncthreads();                               // a previous walk of this workgroup is done with buf
-  buf[0][lane] = load_rec(&wrec.rec[ix(base + lane)]);
-  uint64_t nidx = ix(base + 64 + lane);          // the next chunk's indices, a chunk ahead
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __syncthreads();
-  int cur = 0;
+  auto cl = [&](uint64_t r) -> uint64_t { return r < last ? r : last; };
+  WalkRec w = wrec.load(wrec.sidx[cl(base + lane)], cl(base + lane));
+  uint32_t nidx = wrec.sidx[cl(base + 64 + lane)];   // the next chunk's indices, a chunk ahead
 #if PCN_CT_DBG
   uint32_t dbg_chunks = 0, dbg_rounds = 0, dbg_changes = 0, dbg_steps = 0, dbg_recs = 0;
+  const uint64_t dbg_t0 = wall_clock64();
 #endif
   for (;;) {
-    const WalkRec nx = load_rec(&wrec.rec[nidx]);
-    nidx = ix(base + 128 + lane);
-    const WalkRec w = buf[cur][lane];
+    const WalkRec nx = wrec.load(nidx, cl(base + 64 + lane));
+    nidx = wrec.sidx[cl(base + 128 + lane)];
     const CtRec &r = w.r;
     const bool inrun = base + lane < lim && w.key == k && w.idx < hi;
     const uint64_t rm = __ballot(inrun);           // the run's records: a prefix of the chunk
@@ -1028,7 +1098,7 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
       const uint32_t cnt = em == ~0ull >> u0 ? 64u - u0 : static_cast<uint32_t>(__builtin_ctzll(~em));
       const uint32_t end = u0 + cnt < m ? u0 + cnt : m;
       const bool mine = lane >= u0 && lane < end;
-      if (mine) put_outcome(b, sres, base + lane, w.idx, o);
+      if (mine) put_outcome(b, w, o, dense);
       const bool anyd = __ballot(mine && cls == 0 && cc.dirty) != 0;
       if (lane == 0 && anyd) c.dirty = true;
       // the LRU touch: records that leave the connection as it is touch it if it is live
@@ -1041,7 +1111,7 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
         if (ecls == 1) ++dbg_changes; else ++dbg_steps;
 #endif
         if (ecls == 1) {                              // the changing record: its result is the new state
-          if (lane == u0) put_outcome(b, sres, base + lane, w.idx, o);
+          if (lane == u0) put_outcome(b, w, o, dense);
           const uint32_t nl = __shfl(static_cast<uint32_t>(cc.v.ttl), u0);
           const uint32_t nh = __shfl(static_cast<uint32_t>(cc.v.ttl >> 32), u0);
           const uint32_t ns = __shfl(cc.v.seq, u0);
@@ -1058,47 +1128,46 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
           aborted = true;
           return base + u0;
         } else {                                      // the record that needs the table: the full step
-          const WalkRec x = buf[cur][u0];
-          if (lane == 0) put_outcome(b, sres, base + u0, x.idx, step(b, t, c, x));
+          const WalkRec x = shfl_rec(w, u0);
+          if (lane == 0) put_outcome(b, x, step(b, t, c, x), dense);
         }
         ++u0;
       }
     }
     if (m < 64) {                                     // the run (or this part of it) ends here
 #if PCN_CT_DBG
-      if (lane == 0 && dbg_chunks >= 40)
-        printf("walk_long run: %u records, %u chunks, %u rounds, %u changes, %u table steps\n", dbg_recs, dbg_chunks,
-               dbg_rounds, dbg_changes, dbg_steps);
+      if (lane == 0 && (dbg_chunks >= 40 || (q0 & 4095) < 64))   // the long ones, and a sample
+        printf("walk_long run: %u records, %u chunks, %u rounds, %u changes, %u table steps, %llu us\n", dbg_recs,
+               dbg_chunks, dbg_rounds, dbg_changes, dbg_steps, (unsigned long long)((wall_clock64() - dbg_t0) / 100));
 #endif
       return base + m;
     }
     base += 64;
-    __syncthreads();
-    buf[cur ^ 1][lane] = nx;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    cur ^= 1;
+    w = nx;
   }
 }
 
 // ---- speculative segments of long runs --------------------------------------
 // The walk of a long run is sequential in its records, ~14 us per chunk of
 // 64: the heaviest run of a batch (thousands of packets of one key) bounded
-// the whole walk.  So a long run is cut at the sorted positions that are
-// multiples of kSeg.  Its head wave walks up to the first cut; every later
-// segment is walked at the same time by a wave of its own (walk_seg) that
-// takes as its entry state the key's entry as the table holds it at the start
-// of the batch (nothing else writes that key in this launch), with the ttl
-// unknown (kTtlUnset: a ttl, once set, is now + a constant, never read).  It
-// writes its outcomes and its exit state but nothing to the table, and stops
-// (aborted) at the first record that would need the table.  ct_seg_fix then
-// chains the segments in order: a segment whose entry guess equals the state
-// its predecessor actually left is right as walked (the walk reads nothing
-// else: the ttl is never compared, a long echo reply's quoted key is not
-// written in the batch), and its exit becomes the state; any other segment is
-// walked again from the true state, its outcomes overwritten.  The flows of
-// the bench traffic keep their state across the batch, so their segments all
-// hold; a connection opened or closed mid-run costs one re-walked segment.
+// the whole walk.  So a run is cut at the sorted positions B that are
+// multiples of kSeg and have at least kSeg of its records from B on ("active"
+// cuts: a run's active cuts are consecutive from its first cut, and its last
+// segment holds kSeg to 2 kSeg - 1 records).  Runs of ordinary flows (a few
+// hundred packets) are never cut.  The head wave walks up to the first active
+// cut; every later segment is walked at the same time by a wave of its own
+// (walk_seg) that takes as its entry state the key's entry as the table holds
+// it at the start of the batch (nothing else writes that key in this launch),
+// with the ttl unknown (kTtlUnset: a ttl, once set, is now + a constant,
+// never read).  It writes its outcomes and its exit state but nothing to the
+// table, and stops (aborted) at the first record that would need the table.
+// ct_seg_fix then chains the segments in order: a segment whose entry guess
+// equals the state its predecessor actually left is right as walked (the walk
+// reads nothing else: the ttl is never compared, a long echo reply's quoted
+// key is not written in the batch), and its exit becomes the state; any other
+// segment is walked again from the true state, its outcomes overwritten.  A
+// key that keeps its state through the batch has every guess hold; a
+// connection opened or closed mid-run costs re-walked segments from there on.
 #ifndef PCN_CT_SEG
 #define PCN_CT_SEG 512   // records per segment (a power of two >= kLongRun); 0: no segments
 #endif
@@ -1122,25 +1191,35 @@ struct alignas(16) HeadExit {     // the head wave's state at its run's first cu
   uint32_t pad[5];
 };
 
+// Cut B is active for the run of key bucket k: the run holds B - 1 and at
+// least kSeg records from B on (sorted keys are contiguous, so two probes).
+__device__ __forceinline__ bool cut_active(const uint32_t *skeys, uint64_t n, uint64_t B, uint32_t k) {
+  return B >= 1 && B + kSeg <= n && skeys[B - 1] == k && skeys[B + kSeg - 1] == k;
+}
+
 __device__ __forceinline__ uint32_t cache_px(const Cache &c) {
   return uint32_t(c.k.proto) | uint32_t(c.v.state) << 8 | uint32_t(c.v.rev) << 16 | uint32_t(c.v.live) << 24;
 }
 
 // A long run's head wave: from its head (first) or its cursor up to hi.  With
-// segments, the first pass stops at the run's first cut; if the run goes on
-// there, the state is left to ct_seg_fix (no flush, no cursor).
-__device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, WalkRec (*buf)[64],
-                          uint32_t p, uint32_t *cursor, uint32_t vb, uint64_t hi, int first, HeadExit *hx) {
+// segments, the first pass stops at the run's first cut if that is active; if
+// the walk gets there, the state is left to ct_seg_fix (no flush, no cursor).
+__device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
+                          const uint32_t *skeys, uint32_t p, uint32_t *cursor, uint32_t vb, uint64_t hi, int first,
+                          HeadExit *hx) {
   const uint32_t k = wrec.key(p);
   const uint64_t q0 = first ? p : cursor[vb];
-  const uint64_t bound = (first != 0 && kSeg != 0) ? (p / (kSeg ? kSeg : 1) + 1) * kSeg : ~0ull;
+  uint64_t bound = ~0ull;
+  if (first != 0 && kSeg != 0) {
+    const uint64_t B1 = (p / (kSeg ? kSeg : 1) + 1) * kSeg;
+    if (cut_active(skeys, b.n, B1, k)) bound = B1;
+  }
   Cache c{};
   bool ab;
-  const uint64_t stop = walk_chunks<false>(b, t, wrec, sres, buf, k, q0, hi, bound, c, ab);
+  const uint64_t stop = walk_chunks<false>(b, t, wrec, k, q0, hi, bound, c, ab);
   bool cont = false;
-  if (stop == bound && bound < b.n) {
-    const uint64_t x = PCN_CT_GATHER ? bound : wrec.sidx[bound];
-    cont = wrec.rec[x].key == k && wrec.rec[x].idx < hi;
+  if (stop == bound) {                           // (an active cut: the key goes on there)
+    cont = wrec.sidx[bound] < hi;
   }
   if (threadIdx.x != 0) return;
   if (cont) {
@@ -1163,26 +1242,16 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
   }
 }
 
-// Cut j: if a long run goes on across sorted position B = j * kSeg (the keys
-// at B - 1 and B are the same, and more than kLongRun of them: that run is
-// class 0, exactly as ct_heads decides it), walk its records in [B, B + kSeg)
-// speculatively.  Every cut writes its status.
-__device__ __forceinline__ void walk_seg(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, WalkRec (*buf)[64],
-                         const uint32_t *skeys, uint32_t sentinel, SegRec *seg, uint32_t j, uint64_t hi) {
+// Cut j: if it is active for the run across sorted position B = j * kSeg,
+// walk that run's records from B speculatively, up to the next cut if that is
+// active too, else to the run's end.  Every cut writes its status.
+__device__ __forceinline__ void walk_seg(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
+                                         const uint32_t *skeys, uint32_t sentinel, SegRec *seg,
+                                         uint32_t j, uint64_t hi) {
   const uint32_t lane = threadIdx.x;
   const uint64_t B = uint64_t(j) * kSeg;
-  bool ok = B > 0 && B < b.n;
-  const uint32_t k = ok ? skeys[B] : 0u;
-  ok = ok && k != sentinel && skeys[B - 1] == k;
-  if (ok) {                                        // the run's length inside [B - kLongRun, B + kLongRun)
-    uint32_t cnt = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 2 * kLongRun / 64; ++i) {
-      const uint64_t q = B - kLongRun + i * 64 + lane;
-      cnt += static_cast<uint32_t>(__popcll(__ballot(q < b.n && skeys[q] == k)));
-    }
-    ok = cnt > kLongRun;
-  }
+  const uint32_t k = B < b.n ? skeys[B] : sentinel;
+  bool ok = k != sentinel && cut_active(skeys, b.n, B, k);
   const WalkRec x = wrec.at(ok ? B : 0);
   ok = ok && x.idx < hi;
   if (!ok) {
@@ -1198,7 +1267,8 @@ __device__ __forceinline__ void walk_seg(const CtBatch &b, const CtTable &t, con
   c.v.ttl = kTtlUnset;
   c.valid = true;
   bool ab;
-  const uint64_t stop = walk_chunks<true>(b, t, wrec, sres, buf, k, B, hi, B + kSeg, c, ab);
+  const uint64_t bound = cut_active(skeys, b.n, B + kSeg, k) ? B + kSeg : ~0ull;
+  const uint64_t stop = walk_chunks<true>(b, t, wrec, k, B, hi, bound, c, ab);
   if (lane != 0) return;
   SegRec s{};
   s.src = gk.src;
@@ -1261,11 +1331,11 @@ __device__ __forceinline__ uint64_t walk_hi(const CtBatch &b, const uint32_t *ct
 // shorter runs of one class, one per lane, each from its head (first) or its
 // cursor up to batch index hi.  Every lane returns here (no early exit), so a
 // persistent wave can take the next block.
-__device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec, int32_t *sres, WalkRec (*buf)[64],
-                        const uint32_t *heads, const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first,
+__device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
+                        const uint32_t *skeys, const uint32_t *heads, const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first,
                         uint32_t vb, HeadExit *hx) {
   if (vb < plan->blk0[1]) {                       // one wave per long run
-    walk_long(b, t, wrec, sres, buf, heads[vb], cursor, vb, hi, first, hx);
+    walk_long(b, t, wrec, skeys, heads[vb], cursor, vb, hi, first, hx);
     return;
   }
   uint32_t cls = 1;
@@ -1281,23 +1351,20 @@ __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec, 
     // two records in flight in named registers, A/B alternating (a register
     // move of an in-flight load would wait for it), and the batch indices of
     // the two after them (the record loads never wait on an index load)
-    auto ix = [&](uint64_t r) -> uint64_t {
-      r = r < last ? r : last;
-      return PCN_CT_GATHER ? r : wrec.sidx[r];
-    };
-    WalkRec A = load_rec(&wrec.rec[ix(q)]);
-    WalkRec B = load_rec(&wrec.rec[ix(q + 1)]);
-    uint64_t IA = ix(q + 2), IB = ix(q + 3);
+    auto cl = [&](uint64_t r) -> uint64_t { return r < last ? r : last; };
+    WalkRec A = wrec.load(wrec.sidx[cl(q)], cl(q));
+    WalkRec B = wrec.load(wrec.sidx[cl(q + 1)], cl(q + 1));
+    uint32_t IA = wrec.sidx[cl(q + 2)], IB = wrec.sidx[cl(q + 3)];
     for (;;) {
       if (q >= b.n || A.key != k || A.idx >= hi) break;
-      put_outcome(b, sres, q, A.idx, step(b, t, c, A));
-      A = load_rec(&wrec.rec[IA]);
-      IA = ix(q + 4);
+      put_outcome(b, A, step(b, t, c, A), false);
+      A = wrec.load(IA, cl(q + 2));
+      IA = wrec.sidx[cl(q + 4)];
       ++q;
       if (q >= b.n || B.key != k || B.idx >= hi) break;
-      put_outcome(b, sres, q, B.idx, step(b, t, c, B));
-      B = load_rec(&wrec.rec[IB]);
-      IB = ix(q + 4);
+      put_outcome(b, B, step(b, t, c, B), false);
+      B = wrec.load(IB, cl(q + 2));
+      IB = wrec.sidx[cl(q + 4)];
       ++q;
     }
     flush(t, c);
@@ -1313,35 +1380,42 @@ __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec, 
 // dispatcher next to nothing, where a persistent grid taking blocks from one
 // counter serialised ~10^5 atomics on one address (7.1 vs 2.9 ms a batch).
 // With segments, the first seg_count(n) workgroups are the cuts (walk_seg).
-__global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t *sres,
+__global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec,
                                                      const uint32_t *heads, const uint32_t *ctl, uint32_t *cursor,
                                                      const uint32_t *skeys, uint32_t sentinel, SegRec *seg,
                                                      HeadExit *hx) {
-  __shared__ WalkRec buf[2][64];
   const uint32_t nseg = static_cast<uint32_t>(seg_count(b.n));
+#if PCN_CT_DBG
+  const uint64_t dbg_t0 = wall_clock64();
+#endif
   if (blockIdx.x < nseg) {
-    walk_seg(b, t, wrec, sres, buf, skeys, sentinel, seg, blockIdx.x, walk_hi(b, ctl));
+    walk_seg(b, t, wrec, skeys, sentinel, seg, blockIdx.x, walk_hi(b, ctl));
+#if PCN_CT_DBG
+    const uint64_t dt = wall_clock64() - dbg_t0;
+    if (threadIdx.x == 0 && seg[blockIdx.x].status)
+      printf("seg %u: status %u, walked %u, %llu us\n", blockIdx.x, seg[blockIdx.x].status,
+             seg[blockIdx.x].stop - blockIdx.x * uint32_t(kSeg), (unsigned long long)(dt / 100));
+#endif
     return;
   }
   // (the plan is read in place: a local copy indexed by class went to scratch)
   const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
   const uint32_t vb = blockIdx.x - nseg;
   if (vb >= plan->blk0[kRunClasses]) return;
-  walk_vb(b, t, wrec, sres, buf, heads, plan, cursor, walk_hi(b, ctl), 1, vb, hx);
+  walk_vb(b, t, wrec, skeys, heads, plan, cursor, walk_hi(b, ctl), 1, vb, hx);
 }
 
 // One wave per cut j that is its run's first (the head stopped there): chain
 // the run's segments in order from the head's state, re-walking those whose
 // guess does not hold, then flush the connection and set the run's cursor.
-__global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, const RecSrc wrec, int32_t *sres,
+__global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, const RecSrc wrec,
                                                         const uint32_t *skeys, const SegRec *seg, const HeadExit *hx,
                                                         uint32_t *cursor, const uint32_t *ctl) {
-  __shared__ WalkRec buf[2][64];
   const uint32_t j = blockIdx.x;
   const uint64_t B = uint64_t(j) * kSeg;
   if (j == 0 || B >= b.n || seg[j].status == 0) return;
   const uint32_t k = skeys[B];
-  if (j > 1 && skeys[B - kSeg - 1] == k) return;   // the run started before cut j - 1: not its first cut
+  if (j > 1 && skeys[B - kSeg - 1] == k) return;   // the run holds cut j - 1 too: not its first cut
   const uint64_t hi = walk_hi(b, ctl);
   const HeadExit h = hx[j];
   Cache c{};
@@ -1356,9 +1430,9 @@ __global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, co
   uint64_t stop = B;
   for (uint64_t jj = j;; ++jj) {
     const uint64_t cut = jj * kSeg;
-    if (cut >= b.n) { stop = b.n; break; }
     const SegRec s = seg[jj];
-    if (s.status == 0) { stop = cut; break; }      // the run ends at this cut (or hi cuts it there)
+    if (s.status == 0) { stop = cut; break; }      // hi cuts the run at this (active) cut
+    const bool more = cut_active(skeys, b.n, cut + kSeg, k);   // this segment ends at the next cut
     bool held = false;
     if (threadIdx.x == 0)
       held = s.status == 1 && c.valid && c.k.src == s.src && c.k.dst == s.dst &&
@@ -1380,9 +1454,13 @@ __global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, co
       stop = s.stop;
     } else {
       bool ab;
-      stop = walk_chunks<false>(b, t, wrec, sres, buf, k, cut, hi, cut + kSeg, c, ab);
+      stop = walk_chunks<false>(b, t, wrec, k, cut, hi, more ? cut + kSeg : ~0ull, c, ab, true);
     }
-    if (stop < cut + kSeg) break;                  // the run ended inside this segment
+#if PCN_CT_DBG
+    if (threadIdx.x == 0)
+      printf("fix %u: cut %u status %u %s\n", j, static_cast<uint32_t>(jj), s.status, held ? "held" : "re-walked");
+#endif
+    if (!more || stop < cut + kSeg) break;         // the run ended in this segment (or hi cut it)
   }
   if (threadIdx.x == 0) {
     flush(t, c);
@@ -1394,8 +1472,8 @@ __global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, co
 // whose quoted key bucket also has packets in the batch, so that key's state
 // at its position is only known once everything before it has been walked:
 // its own key decides ESTABLISHED; otherwise ICMP_MISS reads the quoted key.
-__device__ void hard_step(const CtBatch &b, const CtTable &t, const WalkRec *brec, uint32_t i) {
-  const CtRec r = brec[i].r;
+__device__ void hard_step(const CtBatch &b, const CtTable &t, const PackedRec *brec, uint32_t i) {
+  const CtRec r = ct_rec(load_prec(&brec[i]));
   Cache c2{};
   const Key q{r.seq, r.ack, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16), r.flags};
   const bool quoted = lookup(t, c2, q);            // read-only
@@ -1427,8 +1505,8 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 // without them returns at once.  (These need an echo-reply payload that reads
 // as a header of a connection with packets in the same batch: rare, and slow
 // here, but exact.)
-__global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const RecSrc wrec, const WalkRec *brec,
-                                                     int32_t *sres, const uint32_t *heads, const uint32_t *ctl,
+__global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const RecSrc wrec, const PackedRec *brec,
+                                                     const uint32_t *heads, const uint32_t *ctl,
                                                      const uint32_t *th_list, uint32_t *cursor) {
   const uint32_t th = ctl[kCtlThFirst];
   if (!th) return;
@@ -1436,7 +1514,6 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
   const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
   const uint32_t total = plan->blk0[kRunClasses];
   uint32_t cur = 0xFFFFFFFFu - th;
-  __shared__ WalkRec buf[2][64];
   for (;;) {
     if (threadIdx.x == 0) hard_step(b, t, brec, cur);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // its table writes before any lane reads on
@@ -1449,7 +1526,7 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
     nxt = wave_min(nxt);
     const uint64_t hi = nxt == 0xFFFFFFFFu ? b.n : nxt;
     for (uint32_t vb = 0; vb < total; ++vb) {
-      walk_vb(b, t, wrec, sres, buf, heads, plan, cursor, hi, 0, vb, nullptr);
+      walk_vb(b, t, wrec, nullptr, heads, plan, cursor, hi, 0, vb, nullptr);   // (no cuts)
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __syncthreads();
     }
@@ -1595,7 +1672,7 @@ __device__ __forceinline__ uint32_t own_bucket(const CtRec &r, uint32_t sentinel
 }
 
 __global__ void ct_hbits_set_kernel(uint64_t n, const uint32_t *ctl, const uint32_t *keys, const uint32_t *hard_list,
-                                    const WalkRec *brec, uint32_t *bm, uint32_t sentinel) {
+                                    const PackedRec *brec, uint32_t *bm, uint32_t sentinel) {
   const uint32_t nh = ctl[kCtlHard];
   if (!nh) return;
   const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
@@ -1604,16 +1681,16 @@ __global__ void ct_hbits_set_kernel(uint64_t n, const uint32_t *ctl, const uint3
     if (k != sentinel) set_bit(bm, k);
   }
   for (uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; h < nh; h += stp)
-    set_bit(bm, own_bucket(brec[hard_list[h]].r, sentinel));
+    set_bit(bm, own_bucket(ct_rec(load_prec(&brec[hard_list[h]])), sentinel));
 }
 
-__global__ void ct_hard_split_kernel(uint32_t *ctl, const uint32_t *hard_list, WalkRec *brec, uint32_t *keys,
+__global__ void ct_hard_split_kernel(uint32_t *ctl, const uint32_t *hard_list, const PackedRec *brec, uint32_t *keys,
                                      const uint32_t *bm, uint32_t sentinel, uint32_t *th_list) {
   const uint32_t nh = ctl[kCtlHard];
   const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
   for (uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; h < nh; h += stp) {
     const uint32_t i = hard_list[h];
-    const CtRec r = brec[i].r;
+    const CtRec r = ct_rec(load_prec(&brec[i]));
     const uint32_t qb = static_cast<uint32_t>(
         key_hash(r.seq, r.ack, r.flags, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16)) %
         sentinel);
@@ -1623,20 +1700,7 @@ __global__ void ct_hard_split_kernel(uint32_t *ctl, const uint32_t *hard_list, W
     } else {
       const uint32_t k = own_bucket(r, sentinel);
       keys[i] = k;
-      brec[i].key = k;
     }
-  }
-}
-
-__global__ void ct_scatter_kernel(CtBatch b, const uint32_t *skeys, const uint32_t *sidx, const int32_t *sres,
-                                  uint32_t sentinel) {
-  const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < b.n; q += step) {
-    if (skeys[q] == sentinel) continue;
-    const uint32_t i = sidx[q];
-    const int32_t o = sres[q];
-    b.verdicts[i] = static_cast<uint8_t>(o & 1);
-    b.rule_ids[i] = o >> 1;
   }
 }
 
@@ -1765,7 +1829,7 @@ struct CtScratch {
   unsigned long long *pdesc = nullptr;   // ct_prep: the ports word of every 64-frame group
   uint32_t *keys = nullptr, *keys2 = nullptr;
   uint32_t *lcs = nullptr;                // per packet: len | cinfo << 16 (ct_count)
-  uint32_t *idx = nullptr, *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *ctl = nullptr;
+  uint32_t *idx2 = nullptr, *cursor = nullptr, *hard_list = nullptr, *ctl = nullptr;
   uint32_t *th_list = nullptr;            // long echo replies left to ct_tail
   uint32_t *bm = nullptr;                 // key-bucket bitmap (ct_hbits_*)
   uint32_t *evh = nullptr;                // LRU radix-select histograms (kEvPasses x kEvBins, kept zeroed)
@@ -1773,9 +1837,9 @@ struct CtScratch {
   uint32_t *heads = nullptr;
   SegRec *seg = nullptr;                  // speculative segments of long runs (walk_seg, ct_seg_fix)
   HeadExit *hx = nullptr;
-  int32_t *sres = nullptr;
-  WalkRec *brec = nullptr;   // batch order
-  WalkRec *wrec = nullptr;
+  PackedRec *brec = nullptr;  // walk records, batch order
+  ct_u32x4 *ox = nullptr;     // the four stage-A outcomes per packet (batches with four labels)
+  uint64_t ox_cap = 0;
   void *temp = nullptr;
   size_t temp_bytes = 0;
   // ct_advance_carry: 1 + the batch's last port-writing frame
@@ -1787,10 +1851,10 @@ CtScratch *ct_scratch_new() { return new CtScratch(); }
 void ct_scratch_free(CtScratch *s) {
   if (!s) return;
   for (void *p : {static_cast<void *>(s->pdesc), static_cast<void *>(s->lcs),
-                  static_cast<void *>(s->keys), static_cast<void *>(s->keys2), static_cast<void *>(s->idx),
+                  static_cast<void *>(s->keys), static_cast<void *>(s->keys2),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
-                  static_cast<void *>(s->ctl), static_cast<void *>(s->brec), static_cast<void *>(s->wrec),
-                  static_cast<void *>(s->heads), static_cast<void *>(s->sres), s->temp,
+                  static_cast<void *>(s->ctl), static_cast<void *>(s->brec), static_cast<void *>(s->ox),
+                  static_cast<void *>(s->heads), s->temp,
                   static_cast<void *>(s->zfound), static_cast<void *>(s->th_list), static_cast<void *>(s->bm),
                   static_cast<void *>(s->evh), static_cast<void *>(s->seg), static_cast<void *>(s->hx)})
     if (p) (void)hipFree(p);
@@ -1845,16 +1909,22 @@ using CtSortConfig = rocprim::radix_sort_config<
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<PCN_CT_SORT_BLOCK, PCN_CT_SORT_ITEMS>,
                                         rocprim::kernel_config<PCN_CT_SORT_BLOCK, PCN_CT_SORT_ITEMS>,
                                         PCN_CT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
-static hipError_t sort_pairs(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
-                             uint32_t *vout, uint64_t n, uint32_t kbits, hipStream_t st) {
-  return rocprim::radix_sort_pairs<CtSortConfig>(temp, bytes, kin, kout, vin, vout, static_cast<unsigned int>(n), 0u,
-                                                 kbits, st);
+// The values are the batch indices 0..n-1, generated by the sort's first pass
+// (a counting iterator): nothing writes or reads an index array for them.
+static hipError_t sort_pairs(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout, uint32_t *vout,
+                             uint64_t n, uint32_t kbits, hipStream_t st) {
+  return rocprim::radix_sort_pairs<CtSortConfig>(temp, bytes, kin, kout, rocprim::counting_iterator<uint32_t>(0u), vout,
+                                                 static_cast<unsigned int>(n), 0u, kbits, st);
 }
 
-static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
+static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4, hipStream_t st) {
+  if (lab4 && s.ox_cap < n) {                  // only batches with four labels read it
+    if (s.ox) CT_CHECK(hipFree(s.ox));
+    CT_CHECK(hipMalloc(&s.ox, n * sizeof(ct_u32x4)));
+    s.ox_cap = n;
+  }
   if (s.cap < n) {
-    for (uint32_t **p : {&s.keys, &s.keys2, &s.idx, &s.idx2, &s.hard_list, &s.th_list, &s.lcs,
-                         reinterpret_cast<uint32_t **>(&s.sres)}) {
+    for (uint32_t **p : {&s.keys, &s.keys2, &s.idx2, &s.hard_list, &s.th_list, &s.lcs}) {
       if (*p) CT_CHECK(hipFree(*p));
       CT_CHECK(hipMalloc(p, n * 4));
     }
@@ -1865,10 +1935,7 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     if (s.pdesc) CT_CHECK(hipFree(s.pdesc));
     CT_CHECK(hipMalloc(&s.pdesc, (n / 64 + 2) * 8));
     if (s.brec) CT_CHECK(hipFree(s.brec));
-    CT_CHECK(hipMalloc(&s.brec, n * sizeof(WalkRec)));
-    if (s.wrec) CT_CHECK(hipFree(s.wrec));
-    s.wrec = nullptr;
-    if (PCN_CT_GATHER) CT_CHECK(hipMalloc(&s.wrec, n * sizeof(WalkRec)));
+    CT_CHECK(hipMalloc(&s.brec, n * sizeof(PackedRec)));
     if (kSeg) {
       if (s.seg) CT_CHECK(hipFree(s.seg));
       if (s.hx) CT_CHECK(hipFree(s.hx));
@@ -1889,7 +1956,7 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, hipStream_t st) {
     s.bm_bytes = bmb;
   }
   size_t need = 0;
-  CT_CHECK(sort_pairs(nullptr, need, s.keys, s.keys2, s.idx, s.idx2, n, kbits, st));
+  CT_CHECK(sort_pairs(nullptr, need, s.keys, s.keys2, s.idx2, n, kbits, st));
   if (s.temp_bytes < need) {
     if (s.temp) CT_CHECK(hipFree(s.temp));
     CT_CHECK(hipMalloc(&s.temp, need));
@@ -1960,7 +2027,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   uint32_t kbits = 8;
   while (kbits < 30 && (uint64_t(1) << kbits) < 2 * b.n) ++kbits;
   const uint32_t sentinel = (1u << kbits) - 1;
-  CT_CHECK(grow(s, b.n, kbits, st));
+  CT_CHECK(grow(s, b.n, kbits, b.nlab == 4, st));
   const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
   // one memset for the control words (long echo replies, run counts per
   // class, ct_prep's chunk counter, ...; kCtl*): each memset is a launch of
@@ -1969,7 +2036,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
   const uint32_t pchunk = prep_chunk(b.n, num_cus);
   const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
-  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.lcs, s.keys, s.idx, kbits,
+  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.ox, s.lcs, s.keys, kbits,
                      s.ctl + kCtlHard, s.hard_list, s.pdesc, s.ctl + kCtlChunk, pchunk);
   CT_CHECK(hipGetLastError());
   // long echo replies join their own key's run unless their quoted key's
@@ -1986,12 +2053,8 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   // (ct_heads advances the carry from ct_prep's published groups)
   size_t tb;
   tb = s.temp_bytes;
-  CT_CHECK(sort_pairs(s.temp, tb, s.keys, s.keys2, s.idx, s.idx2, b.n, kbits, st));
-  if (PCN_CT_GATHER) {
-    hipLaunchKernelGGL(ct_gather_kernel, dim3(grid), dim3(blk), 0, st, b, s.brec, s.keys2, s.idx2, s.wrec, sentinel);
-    CT_CHECK(hipGetLastError());
-  }
-  const RecSrc src{PCN_CT_GATHER ? s.wrec : s.brec, s.idx2};
+  CT_CHECK(sort_pairs(s.temp, tb, s.keys, s.keys2, s.idx2, b.n, kbits, st));
+  const RecSrc src{s.brec, s.idx2, s.keys2, s.ox, b.nlab == 4 ? 1u : 0u};
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
@@ -2002,15 +2065,15 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipGetLastError());
   // the cuts of long runs, then the plan's upper bound
   const unsigned wgrid = static_cast<unsigned>(seg_count(b.n) + b.n / 64 + kRunClasses + 1);
-  hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.sres, s.heads, s.ctl, s.cursor,
+  hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.heads, s.ctl, s.cursor,
                      s.keys2, sentinel, s.seg, s.hx);
   CT_CHECK(hipGetLastError());
   if (kSeg) {
     hipLaunchKernelGGL(ct_seg_fix_kernel, dim3(static_cast<unsigned>(seg_count(b.n))), dim3(64), 0, st, b, t, src,
-                       s.sres, s.keys2, s.seg, s.hx, s.cursor, s.ctl);
+                       s.keys2, s.seg, s.hx, s.cursor, s.ctl);
     CT_CHECK(hipGetLastError());
   }
-  hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.sres, s.heads, s.ctl, s.th_list,
+  hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.heads, s.ctl, s.th_list,
                      s.cursor);
   CT_CHECK(hipGetLastError());
   if (t.max_entries) {                         // LRU down to max_entries (no read-back either)
@@ -2025,10 +2088,6 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
     CT_CHECK(hipGetLastError());
   }
   ++t.seq;                                     // the next batch's touch stamps are newer
-  if (!PCN_CT_DIRECT) {
-    hipLaunchKernelGGL(ct_scatter_kernel, dim3(grid), dim3(blk), 0, st, b, s.keys2, s.idx2, s.sres, sentinel);
-    CT_CHECK(hipGetLastError());
-  }
   const uint64_t cchunk = count_chunk(b.n, num_cus);
   const unsigned cgrid = static_cast<unsigned>((b.n + cchunk - 1) / cchunk);
   hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs, cchunk);
