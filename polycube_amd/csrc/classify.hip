@@ -1169,7 +1169,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       const DevChain &ch = CH < 3 ? run_ch : a.ch[c];
       if (valid && cchain == c && rid >= 0 && static_cast<uint32_t>(rid) < ch.ncounted) {
         if (PCN_ABLATE == 6) {
-        } else if (ch.lds_bins >= 0) {
+        } else if (ch.lds_bins >= 0 && static_cast<uint32_t>(rid) < ch.lds_nrules) {
           uint32_t b = static_cast<uint32_t>(ch.lds_bins) + static_cast<uint32_t>(rid);
           if (PCN_ABLATE == 7) bins[b] = 1u;   // measurement: a plain store instead of the atomic
           else atomicAdd(&bins[b], 1u);
@@ -1232,7 +1232,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       for (int c = 0; c < 3; ++c) {
         const DevChain &ch = c == CH ? run_ch : a.ch[c];
         if (ch.lds_bins >= 0 && b >= static_cast<uint32_t>(ch.lds_bins) &&
-            b < static_cast<uint32_t>(ch.lds_bins) + ch.ncounted)
+            b < static_cast<uint32_t>(ch.lds_bins) + ch.lds_nrules)
           dst = ch.ctr + 2 + 2 * (b - static_cast<uint32_t>(ch.lds_bins));
       }
       if (a.hz_bins >= 0 && b >= static_cast<uint32_t>(a.hz_bins) && a.horus_ctr)

@@ -1306,7 +1306,10 @@ constexpr uint32_t kCtlEvK = 14;      //      rank (1-based) of the newest stamp
 constexpr uint32_t kCtlEvDone = 15;   //      workgroups done with the current pass
 constexpr uint32_t kCtlPlan = 16;     // WalkPlan (ct_plan)
 constexpr uint32_t kCtlEvPrefix = 28; // u64: the stamp digits chosen so far
-constexpr uint32_t kCtlZero = 32;     // words zeroed per batch
+constexpr uint32_t kCtlEvLow = 30;    //      the stamp bits below this one are still to choose
+constexpr uint32_t kCtlEvNotMin = 32; //      u64: ~(the oldest live stamp) (a max, so zero-initialised)
+constexpr uint32_t kCtlEvMax = 34;    //      u64: the newest live stamp
+constexpr uint32_t kCtlZero = 36;     // words zeroed per batch
 constexpr uint32_t kCtlWords = 64;
 
 __global__ void ct_plan_kernel(uint32_t *ctl) {
@@ -1542,71 +1545,129 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
 // packet after which each was live; distinct, since a packet touches one key)
 // are deleted down to max_entries.  touch[] holds the stamp of every live
 // entry and ~0 for every other slot, so the cut reads 8 bytes a slot and
-// nothing else: a radix select in six passes of 11 / 11 / 11 / 11 / 11 / 9
-// bits, each a histogram of the stamps that match the digits chosen so far.
-// A pass runs few, large workgroups (each merges its LDS histogram into the
-// global one with one atomic per non-empty bin: with a workgroup per 256
-// slots those merges serialised on the hot bins, 70-320 us a pass), and its
-// last workgroup picks the next digit with a block-wide scan.  Pass 0 also
-// counts the live entries; the later passes and the eviction return at once
-// when nothing is to be evicted.
+// nothing else: a radix select, each pass a histogram of the stamps that
+// match the digits chosen so far.
+// Pass 0 counts the live entries and finds the oldest and newest live
+// stamp: every stamp shares the bits above their highest difference, so the
+// digit passes start there (a batch's stamps differ in the batch index and a
+// few low bits of the batch sequence: four passes instead of six).  Pass p > 0
+// takes the next 11 bits (fewer at the bottom) below the chosen prefix and
+// returns at once when nothing is left to choose.  Every workgroup merges its
+// LDS histogram into the global one with one atomic per non-empty bin, and
+// the pass's last workgroup picks the digit with a block-wide scan.  (Six
+// fixed 11-bit passes of 64 workgroups took 26 us each, 0.19 ms a batch:
+// profiles/r03_s24_ev_ab.log.)
 constexpr uint32_t kEvBins = 2048;
-constexpr int kEvPasses = 6;
+constexpr uint32_t kEvDigit = 11;
+constexpr int kEvPasses = 7;          // pass 0 + up to six 11-bit digits (64 bits)
 constexpr uint32_t kEvBlock = 1024;
-__device__ __forceinline__ uint32_t ev_shift(int p) { return p < 5 ? 53 - 11 * p : 0; }
-__device__ __forceinline__ uint32_t ev_width(int p) { return p < 5 ? 11 : 9; }
 
 __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_t *ctl, uint32_t *hist, int p) {
   __shared__ uint32_t h[kEvBins];
   __shared__ uint32_t scan[kEvBlock];
   __shared__ uint32_t live_s;
+  __shared__ unsigned long long lo_s, hi_s;
   __shared__ bool last;
-  if (p > 0 && !ctl[kCtlEvict]) return;
+  uint32_t low = 0;
+  if (p > 0) {
+    if (!ctl[kCtlEvict]) return;
+    low = ctl[kCtlEvLow];
+    if (low == 0) return;                              // every bit chosen
+  }
+  const uint32_t width = low < kEvDigit ? low : kEvDigit, shift = low - width;
   for (uint32_t k = threadIdx.x; k < kEvBins; k += blockDim.x) h[k] = 0;
-  if (threadIdx.x == 0) live_s = 0;
+  if (threadIdx.x == 0) {
+    live_s = 0;
+    lo_s = 0;
+    hi_s = 0;
+  }
   __syncthreads();
   const uint64_t prefix = *reinterpret_cast<const unsigned long long *>(ctl + kCtlEvPrefix);
-  const uint32_t shift = ev_shift(p), width = ev_width(p);
-  const uint64_t above = p == 0 ? 0ull : ~((uint64_t(1) << (shift + width)) - 1);
+  const uint64_t above = low >= 64 ? 0ull : ~((uint64_t(1) << low) - 1);
   const uint64_t cap = uint64_t(1) << t.cap_log2;
   const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
   uint32_t live = 0;
+  unsigned long long nmin = 0, mx = 0;                 // ~oldest, newest
   for (uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i0 < cap; i0 += 4 * stp) {
     unsigned long long key[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) key[u] = i0 + u * stp < cap ? t.touch[i0 + u * stp] : ~0ull;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (key[u] == ~0ull) continue;
-      ++live;
-      if ((key[u] & above) == prefix) atomicAdd(&h[(key[u] >> shift) & ((1u << width) - 1)], 1u);
+      const bool in = key[u] != ~0ull && (p == 0 || (key[u] & above) == prefix);
+      if (p == 0) {
+        if (in) {
+          ++live;
+          nmin = ~key[u] > nmin ? ~key[u] : nmin;
+          mx = key[u] > mx ? key[u] : mx;
+        }
+        continue;
+      }
+      // LDS atomics on one address serialise (~20 ns each), and the high
+      // digits put every stamp in one bin: the lanes that share the first
+      // lane's digit add together, the others one by one
+      const uint64_t im = __ballot(in);
+      if (!im) continue;
+      const uint32_t d = static_cast<uint32_t>(key[u] >> shift) & ((1u << width) - 1);
+      const uint32_t d0 = __shfl(d, static_cast<int>(__builtin_ctzll(im)));
+      const uint64_t same = __ballot(in && d == d0);
+      if ((threadIdx.x & 63) == __builtin_ctzll(im)) atomicAdd(&h[d0], static_cast<uint32_t>(__builtin_popcountll(same)));
+      else if (in && d != d0) atomicAdd(&h[d], 1u);
     }
   }
-  if (p == 0 && live) atomicAdd(&live_s, live);
-  __syncthreads();
   uint32_t *hp = hist + p * kEvBins;
-  for (uint32_t k = threadIdx.x; k < kEvBins; k += blockDim.x)
-    if (h[k]) atomicAdd(&hp[k], h[k]);
-  if (p == 0 && threadIdx.x == 0 && live_s) atomicAdd(&ctl[kCtlLive], live_s);
+  if (p == 0) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {              // one LDS atomic per wave
+      live += __shfl_xor(live, o);
+      const unsigned long long a = __shfl_xor(nmin, o), b = __shfl_xor(mx, o);
+      nmin = a > nmin ? a : nmin;
+      mx = b > mx ? b : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && live) {
+      atomicAdd(&live_s, live);
+      atomicMax(&lo_s, nmin);
+      atomicMax(&hi_s, mx);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && live_s) {
+      atomicAdd(&ctl[kCtlLive], live_s);
+      atomicMax(reinterpret_cast<unsigned long long *>(ctl + kCtlEvNotMin), lo_s);
+      atomicMax(reinterpret_cast<unsigned long long *>(ctl + kCtlEvMax), hi_s);
+    }
+  } else {
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kEvBins; k += blockDim.x)
+      if (h[k]) atomicAdd(&hp[k], h[k]);
+  }
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(&ctl[kCtlEvDone], 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
   __threadfence();
-  // the last workgroup: every histogram of this pass is in; the digit whose
-  // bin holds the k-th smallest matching stamp, by a block-wide scan
-  uint32_t k;
-  if (p == 0) {
-    const uint32_t lv = __hip_atomic_load(&ctl[kCtlLive], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!t.max_entries || lv <= t.max_entries) {
-      if (threadIdx.x == 0) ctl[kCtlEvDone] = 0;
-      return;                                          // kCtlEvict stays 0
+  if (p == 0) {                                        // the last workgroup: evict at all, and from which bit
+    if (threadIdx.x == 0) {
+      ctl[kCtlEvDone] = 0;
+      const uint32_t lv = __hip_atomic_load(&ctl[kCtlLive], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t.max_entries && lv > t.max_entries) {
+        const uint64_t oldest = ~__hip_atomic_load(reinterpret_cast<unsigned long long *>(ctl + kCtlEvNotMin),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t newest = __hip_atomic_load(reinterpret_cast<unsigned long long *>(ctl + kCtlEvMax),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // bits above the highest one where the oldest and newest differ are common to all
+        const uint32_t top = oldest == newest ? 0u : 64u - static_cast<uint32_t>(__builtin_clzll(oldest ^ newest));
+        ctl[kCtlEvK] = lv - static_cast<uint32_t>(t.max_entries);
+        *reinterpret_cast<unsigned long long *>(ctl + kCtlEvPrefix) =
+            top >= 64 ? 0ull : oldest & ~((uint64_t(1) << top) - 1);
+        ctl[kCtlEvLow] = top;
+        ctl[kCtlEvict] = 1;
+      }                                                // (else kCtlEvict stays 0)
     }
-    k = lv - static_cast<uint32_t>(t.max_entries);
-  } else {
-    k = ctl[kCtlEvK];
+    return;
   }
+  // the digit whose bin holds the k-th smallest matching stamp, by a block-wide scan
+  const uint32_t k = ctl[kCtlEvK];
   const uint32_t b0 = 2 * threadIdx.x;                 // this thread's two bins
   const uint32_t c0 = __hip_atomic_load(&hp[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t c1 = __hip_atomic_load(&hp[b0 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1624,7 +1685,7 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
     const uint32_t below = d == b0 ? excl : excl + c0;
     ctl[kCtlEvK] = k - below;
     *reinterpret_cast<unsigned long long *>(ctl + kCtlEvPrefix) = prefix | (uint64_t(d) << shift);
-    if (p == 0) ctl[kCtlEvict] = 1;
+    ctl[kCtlEvLow] = shift;
   }
   if (threadIdx.x == 0) ctl[kCtlEvDone] = 0;          // for the next pass
 }
@@ -2078,7 +2139,9 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipGetLastError());
   if (t.max_entries) {                         // LRU down to max_entries (no read-back either)
     const uint64_t cap = uint64_t(1) << t.cap_log2;
-    const unsigned pgrid2 = static_cast<unsigned>(std::min<uint64_t>(cap / (4 * kEvBlock) + 1, 64));
+    // few workgroups: each one's merge and finish atomics land on the same few
+    // addresses, which serialise at ~0.1 us apiece (256 workgroups: 69 us a pass)
+    const unsigned pgrid2 = static_cast<unsigned>(std::min<uint64_t>(cap / (4 * kEvBlock) + 1, 32));
     for (int p = 0; p < kEvPasses; ++p) {
       hipLaunchKernelGGL(ct_ev_pass_kernel, dim3(pgrid2), dim3(kEvBlock), 0, st, t, s.ctl, s.evh, p);
       CT_CHECK(hipGetLastError());

@@ -129,6 +129,8 @@ struct DevChain {
   uint32_t lds_limit;            // image bytes staged in LDS: all, the per-packet prefix
                                  // [0, lay.pbase) when the whole does not fit, or 0
   int32_t lds_bins;              // first LDS counter bin of this chain's rules; -1 => global atomics
+  uint32_t lds_nrules;           // rule ids [0, lds_nrules) count in the LDS bins from lds_bins, the
+                                 // rest with global atomics (a chain too large for a bin per rule)
 };
 
 // LDS layout of a classify workgroup: [chain images][counter bins (u32 x2)][localip][per-wave regions]

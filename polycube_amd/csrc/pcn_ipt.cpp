@@ -65,6 +65,18 @@ constexpr uint32_t kLdsBudget = PCN_DEBUG_LDS_BUDGET;  // gfx950 LDS per CU (one
 // Measurement knob (tools/ablate.py experiments): bytes per wave region
 // (default PCN_WAVE_LDS_BYTES; a kernel built without the header transpose
 // needs only its candidate scratch).
+// LDS counter bins for the lowest rule ids of a chain too large for a bin
+// per rule, in what is left of the LDS budget after `used` bytes (the bins
+// round up to 16 bytes): first-match traffic falls on low rule ids more
+// often than on high ones (an earlier rule shadows later ones).  0: too few
+// to bother.
+uint32_t partial_rule_bins(uint32_t used, uint32_t per_bin, uint32_t ncounted) {
+  constexpr uint32_t kMinBins = 256;
+  if (used + 16 + kMinBins * per_bin > kLdsBudget) return 0;
+  const uint32_t nb = (kLdsBudget - used - 16) / per_bin;
+  return nb < ncounted ? nb : ncounted;
+}
+
 uint32_t wave_region_bytes(bool fixed) {
   static const uint32_t v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_WAVE_BYTES");
@@ -229,6 +241,7 @@ void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
     d.default_action = img.default_action;
     d.lds_image = 0;
     d.lds_bins = -1;
+    d.lds_nrules = 0;
     cs.desc = d;
     cs.active = next;
   }
@@ -836,8 +849,14 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     uint32_t base = 3;
     for (int c : order) {
       uint32_t nc = a.ch[c].ncounted;
-      if (nc && base - 3 + nc <= kMaxLdsRuleBins) { a.ch[c].lds_bins = static_cast<int32_t>(base); base += nc; }
-      else a.ch[c].lds_bins = -1;
+      if (nc && base - 3 + nc <= kMaxLdsRuleBins) {
+        a.ch[c].lds_bins = static_cast<int32_t>(base);
+        a.ch[c].lds_nrules = nc;
+        base += nc;
+      } else {
+        a.ch[c].lds_bins = -1;
+        a.ch[c].lds_nrules = 0;
+      }
     }
     // Horus hits count into the same workgroup histogram (a hot key would
     // otherwise serialize on one global address)
@@ -873,9 +892,26 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       }
       if (mode == 2 || kLdsDescBytes + img_bytes + tail <= kLdsBudget) break;
     }
+    // A chain that runs rules here but got no bin per rule (more rules than
+    // the histogram budget): bins for its lowest rule ids in the LDS the
+    // images leave over, the rest counted with global atomics.  Placed after
+    // the choice above, so no image loses its place in LDS to them.
+    for (int c : order) {
+      if (!runs(c) || a.ch[c].lds_bins >= 0 || !a.ch[c].ncounted) continue;
+      const uint32_t nb = partial_rule_bins(kLdsDescBytes + img_bytes + tail, fixed ? 4 : 8, a.ch[c].ncounted);
+      if (nb) {                    // before the Horus bins, which the flush takes to run to the end
+        a.ch[c].lds_bins = a.hz_bins >= 0 ? a.hz_bins : static_cast<int32_t>(base);
+        a.ch[c].lds_nrules = nb;
+        if (a.hz_bins >= 0) a.hz_bins += static_cast<int32_t>(nb);
+        base += nb;
+        a.nbins = base;
+      }
+      break;
+    }
+    const uint32_t all_bin_bytes = (fixed ? 4 : 8) * a.nbins;
     a.lds_images_bytes = img_bytes;
     a.bins_offset = kLdsDescBytes + img_bytes;
-    a.lds_localip = a.bins_offset + (bin_bytes + 15) / 16 * 16;
+    a.lds_localip = a.bins_offset + (all_bin_bytes + 15) / 16 * 16;
     a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
     a.wave_bytes = wave_region_bytes(fixed);
     a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
@@ -1168,12 +1204,17 @@ int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
     d.default_action = cs.default_action;
     d.lds_image = kLdsDescBytes;
     d.lds_bins = d.ncounted <= kMaxLdsRuleBins ? 3 : -1;
-    const uint32_t nbins = 3 + (d.lds_bins >= 0 ? d.ncounted : 0);
+    d.lds_nrules = d.lds_bins >= 0 ? d.ncounted : 0;
+    const uint32_t nbins = 3 + d.lds_nrules;
     const uint32_t tail = (nbins * 4 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
                           (PCN_BLOCK / 64) * wave_region_bytes(true);
     d.lds_limit = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget   ? d.lay.bytes
                   : kLdsDescBytes + d.lay.pbase + tail <= kLdsBudget ? d.lay.pbase
                                                                      : 0;
+    if (d.lds_bins < 0) {          // as launch_batch: bins for the lowest rule ids in the LDS left over
+      d.lds_nrules = partial_rule_bins(kLdsDescBytes + d.lds_limit + tail, 4, d.ncounted);
+      if (d.lds_nrules) d.lds_bins = 3;
+    }
     JitShape shape;
     shape.fixed = true;
     shape.lds = d.lds_limit > 0;
