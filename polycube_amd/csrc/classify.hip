@@ -439,7 +439,7 @@ __device__ __forceinline__ void pin_regs(u32x4 (&r)[N]) {
 }
 
 struct WaveScratch {
-  u32x4 item[64];        // (owner lane << 8 | candidate bit, the owner's classes as u16 pairs)
+  u32x4 item[64];        // (owner lane << 16 | candidate word, the owner's classes as u16 pairs)
   uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
 #if !PCN_ITEM_CLS
   u32x4 cls[64];         // each owner's classes
@@ -449,12 +449,15 @@ static_assert(sizeof(WaveScratch) <= PCN_WAVE_SCRATCH_BYTES && PCN_WAVE_SCRATCH_
               "scratch fits the per-wave region");
 
 // ---- rule-chain stage, part 2 (whole wave, converged) ----
-// Lanes with `active` AND their class summaries into a candidate-word mask.
-// The (lane, word) candidate pairs of the whole wave are then dealt out one
-// per lane, 64 at a time, so a lane with many candidates does not hold the
-// wave hostage: each worker re-reads its owner's class records, ANDs the
-// partial words of its one word and folds the matched entry into the
-// owner's slot with an LDS atomic min.  Returns the owner's best entry.
+// Lanes with `active` AND their class summaries into a candidate-word mask,
+// one 64-word block at a time.  The (lane, word) candidate pairs of the whole
+// wave, over all blocks, are queued in the wave's LDS scratch and dealt out
+// one per lane, 64 at a time, so a lane with many candidates does not hold
+// the wave hostage and a chain of several blocks (config 5: 10k rules) pays
+// one deal per 64 candidates, not one per block: each worker re-reads its
+// owner's class records, ANDs the partial words of its one word and folds the
+// matched entry into the owner's slot with an LDS atomic min.  Returns the
+// owner's best entry.
 template <bool LDS, int NS>
 __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[NS],
                                                      WaveScratch *ws) {
@@ -463,8 +466,86 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
   const Tab<LDS> t{ch.image, ch.lds_image, ch.lds_limit};
   const TableLayout &lay = ch.lay;
   const uint32_t nrw = ch.nrw, nsw = ch.nsw;
-  bool staged = false;  // class rows / best slots written (only once some lane has a candidate)
+  bool staged = false;  // best slots written (only once some lane has a candidate)
   uint64_t mseen = 0;   // PCN_ABLATE == 3 only
+  // worker side: the first `cnt` queued items
+  auto drain = [&](uint32_t cnt) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < cnt) {
+      u32x4 it;
+      if (PCN_ITEM_CLS) {
+        it = ws->item[lane];
+      } else {
+        const uint32_t x = reinterpret_cast<const uint32_t *>(ws->item)[lane];
+#if !PCN_ITEM_CLS
+        it = ws->cls[x >> 16];
+#endif
+        it.x = x;
+      }
+      const uint32_t owner = it.x >> 16, w = it.x & 0xffff, k = w >> 6, bit = w & 63;
+      const uint64_t below = (1ull << bit) - 1;
+      const uint32_t packed[3] = {it.y, it.z, it.w};
+      uint32_t oc[NS];
+#pragma unroll
+      for (int f = 0; f < NS; ++f) oc[f] = (packed[f / 2] >> (16 * (f & 1))) & 0xffff;
+      // At a candidate word every field's summary bit is set, so a field is
+      // PARTIAL there iff its PM bit is set; one 16-byte read gives PM and
+      // PBASE.  Straight-line on purpose: every record read, then every word
+      // read, issue back to back.  A FULL field reads POOL[0], the all-ones
+      // word (indexed PART: through the zero cell, index 0).
+      uint32_t at[NS];   // LDS/image offset of each field's u64 word
+      u32x4 recs[NS];
+      if (!lay.part_dense) {
+        // all NS records in flight together: one LDS round trip (left to
+        // itself the compiler recycles two record registers and waits
+        // between pairs)
+#pragma unroll
+        for (int f = 0; f < NS; ++f) recs[f] = t.u128(lay.pbase, 16 * (oc[f] * nsw + k));
+        if (PCN_REC_PIN) pin_regs<NS>(recs);
+      }
+#pragma unroll
+      for (int f = 0; f < NS; ++f) {
+        if (lay.part_dense) {
+          const uint32_t cell = oc[f] * nrw + w;
+          at[f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
+          continue;
+        }
+        const u32x4 r = recs[f];
+        const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;
+        const uint32_t j = r.z + static_cast<uint32_t>(__builtin_popcountll(pm & below));
+        const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
+        if (lay.part_direct) {
+          at[f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));
+        } else {
+          const bool wide = lay.part_wide;
+          const uint32_t ia = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
+          at[f] = lay.pool + 8 * (wide ? t.u32(lay.part, ia - lay.part) : t.u16(lay.part, ia - lay.part));
+        }
+      }
+      uint64_t acc = ~0ull;
+#pragma unroll
+      for (int f = 0; f < NS; ++f) acc &= t.u64(lay.pool, at[f] - lay.pool);   // (PART and POOL are on the same side of the limit)
+      if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
+        const uint32_t e = t.u16(lay.perm, 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
+        atomicMin(&ws->best[owner], e);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  u32x4 mine;   // this lane's classes ride along with each of its candidates
+  {
+    uint32_t pk[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int f = 0; f < NS; ++f) pk[f / 2] |= cls[f] << (16 * (f & 1));
+    mine.y = pk[0];
+    mine.z = pk[1];
+    mine.w = pk[2];
+  }
+  uint32_t qn = 0;      // items queued, not yet dealt (wave-uniform, < 64)
   for (uint32_t k = 0; k < nsw; ++k) {
     const uint32_t live = nrw - k * 64;
     uint64_t m = 0;
@@ -487,16 +568,8 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       total += static_cast<uint32_t>(__builtin_popcountll(bm)) << b;
       if (__ballot(c >> (b + 1)) == 0) break;
     }
-    if (total == 0) continue;
-    u32x4 mine;   // this lane's classes ride along with each of its candidates
-    {
-      uint32_t pk[3] = {0u, 0u, 0u};
-#pragma unroll
-      for (int f = 0; f < NS; ++f) pk[f / 2] |= cls[f] << (16 * (f & 1));
-      mine.y = pk[0];
-      mine.z = pk[1];
-      mine.w = pk[2];
-    }
+    const bool last_block = k + 1 == nsw;
+    if (total == 0 && (!last_block || qn == 0)) continue;
     if (!staged) {
       staged = true;
       ws->best[lane] = kNoRule;
@@ -504,81 +577,24 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       ws->cls[lane] = mine;
 #endif
     }
-    for (uint32_t done = 0; done < total; done += 64) {
-      // deal: each owner writes its candidates that fall in [done, done + 64)
-      while (m && pos < done + 64) {
-        mine.x = (lane << 8) | static_cast<uint32_t>(__builtin_ctzll(m));
-        if (PCN_ITEM_CLS) ws->item[pos - done] = mine;
-        else reinterpret_cast<uint32_t *>(ws->item)[pos - done] = mine.x;
+    // this block's items go to queue positions [qn, qn + total): each owner
+    // writes those that fall in the current window of 64, which is dealt
+    // when it is full or after the last block (one call site: a chain of one
+    // block runs the code of a plain per-block deal)
+    uint32_t p = qn + pos, end = qn + total;
+    for (;;) {
+      while (m && p < 64) {
+        mine.x = (lane << 16) | (k * 64 + static_cast<uint32_t>(__builtin_ctzll(m)));
+        if (PCN_ITEM_CLS) ws->item[p] = mine;
+        else reinterpret_cast<uint32_t *>(ws->item)[p] = mine.x;
         m &= m - 1;
-        ++pos;
+        ++p;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (lane < total - done) {
-        u32x4 it;
-        if (PCN_ITEM_CLS) {
-          it = ws->item[lane];
-        } else {
-          const uint32_t x = reinterpret_cast<const uint32_t *>(ws->item)[lane];
-#if !PCN_ITEM_CLS
-          it = ws->cls[x >> 8];
-#endif
-          it.x = x;
-        }
-        const uint32_t owner = it.x >> 8, bit = it.x & 63;
-        const uint64_t below = (1ull << bit) - 1;
-        const uint32_t packed[3] = {it.y, it.z, it.w};
-        uint32_t oc[NS];
-#pragma unroll
-        for (int f = 0; f < NS; ++f) oc[f] = (packed[f / 2] >> (16 * (f & 1))) & 0xffff;
-        // At a candidate word every field's summary bit is set, so a field is
-        // PARTIAL there iff its PM bit is set; one 16-byte read gives PM and
-        // PBASE.  Straight-line on purpose: every record read, then every word
-        // read, issue back to back.  A FULL field reads POOL[0], the all-ones
-        // word (indexed PART: through the zero cell, index 0).
-        uint32_t at[NS];   // LDS/image offset of each field's u64 word
-        u32x4 recs[NS];
-        if (!lay.part_dense) {
-          // all NS records in flight together: one LDS round trip (left to
-          // itself the compiler recycles two record registers and waits
-          // between pairs)
-#pragma unroll
-          for (int f = 0; f < NS; ++f) recs[f] = t.u128(lay.pbase, 16 * (oc[f] * nsw + k));
-          if (PCN_REC_PIN) pin_regs<NS>(recs);
-        }
-#pragma unroll
-        for (int f = 0; f < NS; ++f) {
-          if (lay.part_dense) {
-            const uint32_t cell = oc[f] * nrw + k * 64 + bit;
-            at[f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
-            continue;
-          }
-          const u32x4 r = recs[f];
-          const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;
-          const uint32_t j = r.z + static_cast<uint32_t>(__builtin_popcountll(pm & below));
-          const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
-          if (lay.part_direct) {
-            at[f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));
-          } else {
-            const bool wide = lay.part_wide;
-            const uint32_t ia = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
-            at[f] = lay.pool + 8 * (wide ? t.u32(lay.part, ia - lay.part) : t.u16(lay.part, ia - lay.part));
-          }
-        }
-        uint64_t acc = ~0ull;
-#pragma unroll
-        for (int f = 0; f < NS; ++f) acc &= t.u64(lay.pool, at[f] - lay.pool);   // (PART and POOL are on the same side of the limit)
-        if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
-          const uint32_t w = k * 64 + bit;
-          const uint32_t e = t.u16(lay.perm, 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
-          atomicMin(&ws->best[owner], e);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (end < 64 && !last_block) { qn = end; break; }
+      drain(end < 64 ? end : 64u);
+      if (end <= 64) { qn = 0; break; }
+      p -= 64;
+      end -= 64;
     }
   }
   if (PCN_ABLATE == 3) return mseen ? 0u : kNoRule;
