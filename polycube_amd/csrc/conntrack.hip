@@ -287,9 +287,17 @@ __device__ uint32_t ports_lookback(const unsigned long long *desc, uint64_t g, c
 #ifndef PCN_CT_PREP_LDS
 #define PCN_CT_PREP_LDS 1
 #endif
+#ifndef PCN_CT_PREP_PF
+#define PCN_CT_PREP_PF 1     // the next group's loads in flight (fixed-stride path)
+#endif
 constexpr uint32_t kPrepBlock = 256;
 constexpr uint32_t kPrepRow = 5;                 // 16-byte chunks per frame row in LDS (4 + 1 of padding)
-__global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const uint32_t *carry, PackedRec *brec,
+#ifdef PCN_CT_PREP_WAVES
+#define PCN_CT_PREP_ATTR __attribute__((amdgpu_waves_per_eu(PCN_CT_PREP_WAVES)))
+#else
+#define PCN_CT_PREP_ATTR
+#endif
+__global__ __launch_bounds__(kPrepBlock) PCN_CT_PREP_ATTR void ct_prep_kernel(CtBatch b, const uint32_t *carry, PackedRec *brec,
                                ct_u32x4 *ox, uint32_t *lcs, uint32_t *keys, uint32_t kbits, uint32_t *hard_cnt, uint32_t *hard_list, unsigned long long *desc,
                                uint32_t *chunk_ctr, uint32_t chunk_frames) {
   const uint32_t sentinel = (1u << kbits) - 1;
@@ -307,19 +315,52 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
     __syncthreads();                                      // everyone has read `chunk`
     if (lo >= b.n) return;
     const uint64_t hi = lo + chunk_frames < b.n ? lo + chunk_frames : b.n;
+#if PCN_CT_PREP_LDS && PCN_CT_PREP_PF
+    // The next group's frames and label-0 outcome are in flight while a wave
+    // works on its group (one group's loads at a time left the waves waiting
+    // on memory three quarters of their life).
+    ct_u32x4 pc[4] = {}, pex = {};
+    int32_t prid = 0;
+    uint8_t pver = 0;
+    auto fetch = [&](uint64_t g0) {
+      if (stride64 && (g0 + 64) * 64 + 16 <= b.frames_bytes) {
+        const ct_u32x4 *src = reinterpret_cast<const ct_u32x4 *>(b.frames + g0 * 64);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) pc[q] = src[q * 64 + lane];
+        pex = src[256];
+      }
+      const uint64_t j = g0 + lane < hi ? g0 + lane : hi - 1;
+      prid = b.a_rid[j];
+      pver = b.a_verdict[j];
+    };
+    if (lo + (threadIdx.x & ~63u) < hi) fetch(lo + (threadIdx.x & ~63u));
+#endif
   for (uint64_t i0 = lo + (threadIdx.x & ~63u); i0 < hi; i0 += blockDim.x) {   // one 64-frame group per wave
     const uint64_t i = i0 + lane;
     const bool valid = i < hi;
     uint32_t w[18], L;
+#if PCN_CT_PREP_LDS && PCN_CT_PREP_PF
+    const int32_t rid0 = prid;
+    const uint8_t ver0 = pver;
+#else
+    const int32_t rid0 = b.a_rid[valid ? i : hi - 1];
+    const uint8_t ver0 = b.a_verdict[valid ? i : hi - 1];
+#endif
 #if PCN_CT_PREP_LDS
     // the group's 64 frames and the next frame's first chunk inside the buffer (wave-uniform)
     const bool fast = stride64 && (i0 + 64) * 64 + 16 <= b.frames_bytes;
+#if PCN_CT_PREP_PF
+    const ct_u32x4 c[4] = {pc[0], pc[1], pc[2], pc[3]};
+    const ct_u32x4 extra = pex;
+#endif
     if (fast) {
+#if !PCN_CT_PREP_PF
       const ct_u32x4 *src = reinterpret_cast<const ct_u32x4 *>(b.frames + i0 * 64);
       ct_u32x4 c[4];
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q) c[q] = src[q * 64 + lane];   // chunk t = 64 q + lane: frame t / 4
       const ct_u32x4 extra = src[256];                               // the next frame's bytes 0-15
+#endif
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q) {
         const uint32_t t = q * 64 + lane;
@@ -345,6 +386,9 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
     } else {
       load_window(b, valid ? i : hi - 1, w, L);
     }
+#if PCN_CT_PREP_PF
+    if (i0 + blockDim.x < hi) fetch(i0 + blockDim.x);   // after the group's chunks went to LDS
+#endif
 #else
     load_window(b, valid ? i : hi - 1, w, L);
 #endif
@@ -379,9 +423,9 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
         // ChainSelector / ChainForwarder: DROP is final, ACCEPT is PASS_LABELING
         // (Horus_dp.c:150-160; Firewall_Horus_dp.c:151-161), or final for a
         // pcn-firewall program built with conntrack off (:162-164)
-        const bool horus = b.a_rid[i] <= PCN_IPT_RID_HORUS0;
+        const bool horus = rid0 <= PCN_IPT_RID_HORUS0;
         if (horus) {
-          if (b.a_verdict[i] == PCN_IPT_ACCEPT && !b.horus_final) pass = true;
+          if (ver0 == PCN_IPT_ACCEPT && !b.horus_final) pass = true;
           else labeled = false;
         } else if (b.fw) {
           // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder
@@ -447,7 +491,7 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
                                   : sentinel;
       keys[i] = key;
       lcs[i] = uint32_t(r.len) | uint32_t(r.cinfo) << 16;   // what ct_count reads (not the 64-byte record)
-      const int32_t o0 = pack_outcome(b, 0, i);
+      const int32_t o0 = b.nlab ? (rid0 * 2) | ver0 : 0;   // pack_outcome(b, 0, i)
       pr = pack_rec(r, o0);
       if (b.nlab == 4)
         ox[i] = ct_u32x4{static_cast<uint32_t>(o0), static_cast<uint32_t>(pack_outcome(b, 1, i)),
@@ -472,9 +516,9 @@ __global__ __launch_bounds__(kPrepBlock) void ct_prep_kernel(CtBatch b, const ui
       // those with no table access (label INVALID for K_INV, else any label);
       // the label-0 one for the rest, which the walk overwrites only where it
       // differs (put_outcome)
-      const uint32_t l = (!member && r.kind == K_INV && !pass && b.nlab == 4) ? 3u : 0u;
-      b.verdicts[i] = b.a_verdict[l * b.n + i];
-      b.rule_ids[i] = b.a_rid[l * b.n + i];
+      const bool l3 = !member && r.kind == K_INV && !pass && b.nlab == 4;
+      b.verdicts[i] = l3 ? b.a_verdict[3 * b.n + i] : ver0;
+      b.rule_ids[i] = l3 ? b.a_rid[3 * b.n + i] : rid0;
     }
 #if PCN_CT_PREP_LDS
     if (fast) {                                         // the wave's records as coalesced chunks
