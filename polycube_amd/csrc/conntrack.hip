@@ -598,6 +598,9 @@ struct SlotRef {
 // table), so a lookup stops there too.  Without the bound a nearly full
 // table made every miss and insert scan up to the whole table, ~1 us per
 // dependent probe.
+#ifndef PCN_CT_SLOT1
+#define PCN_CT_SLOT1 1
+#endif
 constexpr uint64_t kMaxProbe = 512;
 __device__ SlotRef table_slot(const CtTable &t, const Key &k, bool claim) {
   const uint64_t mask = (uint64_t(1) << t.cap_log2) - 1;
@@ -606,7 +609,15 @@ __device__ SlotRef table_slot(const CtTable &t, const Key &k, bool claim) {
   uint64_t s = key_hash(k.src, k.dst, k.proto, k.sport, k.dport) >> 7;
   for (uint64_t probe = 0; probe < probes; ++probe, ++s) {
     CtSlot *e = &t.slots[s & mask];
+#if PCN_CT_SLOT1
+    // the whole slot in one round trip: the tag is the key half's first word
+    // (a tag load, then the halves, was two dependent loads per probe -- the
+    // head of every walking wave's and lane's first lookup)
+    ct_u32x4 lo = slot_half(e, 0), hi = slot_half(e, 1);
+    uint32_t tag = lo.x;
+#else
     uint32_t tag = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     if (tag == 0) {
       if (!claim) return SlotRef{nullptr, Ent{}};
       if (atomicCAS(&e->tag, 0u, 2u) == 0u) {
@@ -616,10 +627,21 @@ __device__ SlotRef table_slot(const CtTable &t, const Key &k, bool claim) {
         return SlotRef{e, Ent{}};
       }
       tag = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if PCN_CT_SLOT1
+      if (tag == 1) { lo = slot_half(e, 0); hi = slot_half(e, 1); }   // published under us: read it again
+#endif
     }
     if (tag != 1) continue;
+#if PCN_CT_SLOT1
+    if (zero_key) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      lo = slot_half(e, 0);
+      hi = slot_half(e, 1);
+    }
+#else
     if (zero_key) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const ct_u32x4 lo = slot_half(e, 0), hi = slot_half(e, 1);
+#endif
     if (lo.y == k.src && lo.z == k.dst && lo.w == (uint32_t(k.sport) | uint32_t(k.dport) << 16) &&
         (hi.w & 0xff) == k.proto)
       return SlotRef{e, slot_value(hi)};
