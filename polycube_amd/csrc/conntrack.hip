@@ -893,6 +893,13 @@ __device__ __forceinline__ int32_t step(const CtBatch &b, const CtTable &t, Cach
 
 // After the sort: walk records in sorted order (each walking lane then reads
 // consecutive lines) and the list of run heads.
+#ifndef PCN_CT_DBG_T
+#define PCN_CT_DBG_T 0 // measurement builds only: per walk block, its entry / run start / first chunk / end clocks
+#endif
+#if PCN_CT_DBG_T
+constexpr uint32_t kDbgWaves = 1u << 17;
+__device__ unsigned long long g_walk_t[4 * kDbgWaves];
+#endif
 #ifndef PCN_CT_DBG
 #define PCN_CT_DBG 0   // measurement builds only: walk_long prints its round counts for long runs
 #endif
@@ -1099,7 +1106,7 @@ __device__ __forceinline__ WalkRec shfl_rec(const WalkRec &w, uint32_t from) {
 template <bool kSpec>
 __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
                                                 uint32_t k, uint64_t q0, uint64_t hi, uint64_t bound, Cache &c,
-                                                bool &aborted, bool dense = false) {
+                                                bool &aborted, bool dense = false, uint64_t *tfirst = nullptr) {
   const uint32_t lane = threadIdx.x;
   const uint64_t last = b.n - 1;
   const uint64_t lim = bound < b.n ? bound : b.n;
@@ -1200,6 +1207,9 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
         ++u0;
       }
     }
+#if PCN_CT_DBG_T
+    if (tfirst && !*tfirst) *tfirst = wall_clock64();
+#endif
     if (m < 64) {                                     // the run (or this part of it) ends here
 #if PCN_CT_DBG
       if (lane == 0 && (dbg_chunks >= 40 || (q0 & 4095) < 64))   // the long ones, and a sample
@@ -1282,7 +1292,18 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
   }
   Cache c{};
   bool ab;
+#if PCN_CT_DBG_T
+  const uint64_t dt0 = wall_clock64();
+  uint64_t dt1 = 0;
+  const uint64_t stop = walk_chunks<false>(b, t, wrec, k, q0, hi, bound, c, ab, false, &dt1);
+  if (threadIdx.x == 0 && vb < kDbgWaves) {
+    g_walk_t[4 * vb + 1] = dt0;
+    g_walk_t[4 * vb + 2] = dt1;
+    g_walk_t[4 * vb + 3] = wall_clock64() | (stop - q0) << 48;
+  }
+#else
   const uint64_t stop = walk_chunks<false>(b, t, wrec, k, q0, hi, bound, c, ab);
+#endif
   bool cont = false;
   if (stop == bound) {                           // (an active cut: the key goes on there)
     cont = wrec.sidx[bound] < hi;
@@ -1468,6 +1489,9 @@ __global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const
     return;
   }
   // (the plan is read in place: a local copy indexed by class went to scratch)
+#if PCN_CT_DBG_T
+  if (threadIdx.x == 0 && blockIdx.x >= nseg && blockIdx.x - nseg < kDbgWaves) g_walk_t[4 * (blockIdx.x - nseg)] = wall_clock64();
+#endif
   const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
   const uint32_t vb = blockIdx.x - nseg;
   if (vb >= plan->blk0[kRunClasses]) return;
@@ -2450,3 +2474,15 @@ int ct_flow_split(const CtBatch &b, const uint16_t *in_port, uint16_t const_in_p
 }
 
 }  // namespace pcn
+
+#if PCN_CT_DBG_T
+// measurement builds only (tools/walk_times.py): the walk's per-block clocks
+extern "C" int pcn_ipt_dbg_walk_times(unsigned long long *out, size_t words) {
+  if (words > 4 * size_t(pcn::kDbgWaves)) words = 4 * size_t(pcn::kDbgWaves);
+  return int(hipMemcpyFromSymbol(out, HIP_SYMBOL(pcn::g_walk_t), words * 8));
+}
+extern "C" int pcn_ipt_dbg_walk_clear() {
+  static unsigned long long zero[4 * pcn::kDbgWaves];
+  return int(hipMemcpyToSymbol(HIP_SYMBOL(pcn::g_walk_t), zero, sizeof(zero)));
+}
+#endif
