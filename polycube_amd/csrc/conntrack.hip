@@ -1103,10 +1103,35 @@ __device__ __forceinline__ WalkRec shfl_rec(const WalkRec &w, uint32_t from) {
 // record is in flight meanwhile (one load per lane).  (The first version staged
 // chunks in LDS behind two workgroup barriers each, whose release waited for
 // the chunk's scattered outcome stores.)
+// A run is one key *bucket*, and a bucket can hold several connections (25-bit
+// buckets: ~64 colliding pairs among 2^16 flows).  Walked as one sequence, two
+// interleaved connections made every other record a table step on lane 0
+// (flush, probe, ~1.5 us each): a 500-record run of two flows took up to 0.8
+// ms, the whole walk's tail.  The connections of a bucket are independent, so
+// the head wave walks them one after the other instead: pass j takes the
+// records of the j-th connection to appear in the run (its key in `PassKeys`,
+// LDS) and skips the others, noting the first record of a connection it has
+// not seen; past kPassKeys connections the last pass takes all the rest as one
+// sequence (the old way).  kAllKeys: every record (segments, and the runs
+// whose walk a segment continues).
+constexpr int kPassKeys = 4;
+constexpr int kAllKeys = -2, kOtherKeys = -1;
+struct PassKeys {
+  uint32_t n;
+  uint32_t k[kPassKeys][4];   // src, dst, sport | dport << 16, proto
+};
+__device__ __forceinline__ void pass_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <bool kSpec>
 __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
                                                 uint32_t k, uint64_t q0, uint64_t hi, uint64_t bound, Cache &c,
-                                                bool &aborted, bool dense = false, uint64_t *tfirst = nullptr) {
+                                                bool &aborted, bool dense = false, uint64_t *tfirst = nullptr,
+                                                PassKeys *pk = nullptr, int pass = kAllKeys, uint64_t *unk = nullptr) {
+  (void)tfirst;                                     // (measurement builds only)
   const uint32_t lane = threadIdx.x;
   const uint64_t last = b.n - 1;
   const uint64_t lim = bound < b.n ? bound : b.n;
@@ -1127,6 +1152,32 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
     const uint64_t rm = __ballot(inrun);           // the run's records: a prefix of the chunk
     const uint32_t m = rm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~rm));
     uint32_t u0 = 0;
+    bool part = true;                               // this lane's record belongs to the pass
+    if (pass != kAllKeys) {
+      const uint32_t rp = uint32_t(r.sport) | uint32_t(r.dport) << 16;
+      if (pk->n == 0) {                             // the pass-0 connection: the run's first record
+        if (lane == 0) {
+          pk->k[0][0] = r.src;
+          pk->k[0][1] = r.dst;
+          pk->k[0][2] = rp;
+          pk->k[0][3] = r.proto;
+          pk->n = 1;
+        }
+        pass_fence();
+      }
+      const uint32_t nk = pk->n;
+      int kid = -1;
+#pragma unroll
+      for (int j = 0; j < kPassKeys; ++j)
+        if (j < static_cast<int>(nk) && r.src == pk->k[j][0] && r.dst == pk->k[j][1] && rp == pk->k[j][2] &&
+            r.proto == pk->k[j][3])
+          kid = j;
+      part = pass >= 0 ? kid == pass : kid < 0;
+      if (pass >= 0 && *unk == ~0ull) {
+        const uint64_t um = __ballot(lane < m && kid < 0);
+        if (um) *unk = base + __builtin_ctzll(um);
+      }
+    }
 #if PCN_CT_DBG
     ++dbg_chunks;
     dbg_recs += m;
@@ -1148,10 +1199,10 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
       // (the round's last record: the next round starts from its result);
       // 2: needs the table itself (another key of the bucket, a slot to claim,
       // no cached key yet) and takes step() on lane 0.
-      int cls = 2;
+      int cls = part ? 2 : 0;                      // another connection's record: nothing to do here
       int32_t o = 0;
       Cache cc{};
-      if (lane >= u0 && lane < m && (sv & 1) && r.src == ks && r.dst == kd &&
+      if (part && lane >= u0 && lane < m && (sv & 1) && r.src == ks && r.dst == kd &&
           (uint32_t(r.sport) | uint32_t(r.dport) << 16) == kp && r.proto == (kx & 0xff)) {
         cc.k = Key{ks, kd, static_cast<uint16_t>(kp), static_cast<uint16_t>(kp >> 16), static_cast<uint8_t>(kx)};
         cc.e = (sv & 4) ? t.slots : nullptr;          // never dereferenced under kSpec
@@ -1171,12 +1222,14 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
       const uint32_t cnt = em == ~0ull >> u0 ? 64u - u0 : static_cast<uint32_t>(__builtin_ctzll(~em));
       const uint32_t end = u0 + cnt < m ? u0 + cnt : m;
       const bool mine = lane >= u0 && lane < end;
-      if (mine) put_outcome(b, w, o, dense);
+      if (mine && part) put_outcome(b, w, o, dense);
       const bool anyd = __ballot(mine && cls == 0 && cc.dirty) != 0;
       if (lane == 0 && anyd) c.dirty = true;
       // the LRU touch: records that leave the connection as it is touch it if it is live
-      const uint32_t lidx = __shfl(w.idx, end > u0 ? end - 1 : u0);
-      if (lane == 0 && end > u0 && (sv & 2)) c.touch = lidx + 1;
+      const uint64_t rng = end > u0 ? (end == 64 ? ~0ull : (1ull << end) - 1) & ~((1ull << u0) - 1) : 0ull;
+      const uint64_t pm = __ballot(part) & rng;      // the last of them that is the pass's
+      const uint32_t lidx = __shfl(w.idx, pm ? 63 - __builtin_clzll(pm) : u0);
+      if (lane == 0 && pm && (sv & 2)) c.touch = lidx + 1;
       u0 = end;
       if (u0 < m) {
         const int ecls = __shfl(cls, u0);
@@ -1292,17 +1345,51 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
   }
   Cache c{};
   bool ab;
+  __shared__ PassKeys pk;
+  const bool passes = bound == ~0ull;               // no segment continues this walk
+  if (passes) {
+    if (threadIdx.x == 0) pk.n = 0;
+    pass_fence();
+  }
+  uint64_t unk = ~0ull;
+  // pass 0, then the bucket's other connections, one pass each from their
+  // first record (one call site: each inlined copy of the walk costs registers)
+  uint64_t stop = 0, from = q0;
+  int pass = passes ? 0 : kAllKeys;
 #if PCN_CT_DBG_T
   const uint64_t dt0 = wall_clock64();
   uint64_t dt1 = 0;
-  const uint64_t stop = walk_chunks<false>(b, t, wrec, k, q0, hi, bound, c, ab, false, &dt1);
+#endif
+  for (;;) {
+#if PCN_CT_DBG_T
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, &dt1, &pk, pass, &unk);
+#else
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, nullptr, &pk, pass, &unk);
+#endif
+    if (from == q0) stop = st;                       // every pass stops there (the run's end, or hi)
+    if (unk == ~0ull) break;
+    from = unk;
+    unk = ~0ull;
+    if (++pass < kPassKeys) {
+      const WalkRec x = wrec.at(from);
+      if (threadIdx.x == 0) {
+        pk.k[pass][0] = x.r.src;
+        pk.k[pass][1] = x.r.dst;
+        pk.k[pass][2] = uint32_t(x.r.sport) | uint32_t(x.r.dport) << 16;
+        pk.k[pass][3] = x.r.proto;
+        pk.n = pass + 1;
+      }
+      pass_fence();
+    } else {
+      pass = kOtherKeys;                            // the rest as one sequence (sets no unk)
+    }
+  }
+#if PCN_CT_DBG_T
   if (threadIdx.x == 0 && vb < kDbgWaves) {
     g_walk_t[4 * vb + 1] = dt0;
     g_walk_t[4 * vb + 2] = dt1;
     g_walk_t[4 * vb + 3] = wall_clock64() | (stop - q0) << 48;
   }
-#else
-  const uint64_t stop = walk_chunks<false>(b, t, wrec, k, q0, hi, bound, c, ab);
 #endif
   bool cont = false;
   if (stop == bound) {                           // (an active cut: the key goes on there)

@@ -594,3 +594,64 @@ def test_long_runs_in_speculative_segments(dev):
         assert_tables(o, ipt)
     assert_counters(o, ipt, n=len(rules) + 1)
     assert_ae(o, ipt)
+
+
+def _key_bucket(a, b, pa, pb, proto, kbits):
+    """conntrack.hip key_hash % (2^kbits - 1) of a connection's ordered key
+    (ConntrackLabel_dp.c:200-228: lower IP first, lower port first, each compared
+    as the little-endian load of its network-order bytes), numpy u64."""
+    a = a.astype(np.uint32).byteswap().astype(np.uint64)
+    b = b.astype(np.uint32).byteswap().astype(np.uint64)
+    pa = pa.astype(np.uint16).byteswap().astype(np.uint64)
+    pb = pb.astype(np.uint16).byteswap().astype(np.uint64)
+    src, dst = np.minimum(a, b), np.maximum(a, b)
+    sp, dp = np.minimum(pa, pb), np.maximum(pa, pb)
+    with np.errstate(over="ignore"):
+        h = ((src << np.uint64(32)) | dst) * np.uint64(0x9E3779B97F4A7C15)
+        h ^= ((np.uint64(proto) << np.uint64(32)) | (sp << np.uint64(16)) | dp) * np.uint64(0xC2B2AE3D27D4EB4F)
+        h ^= h >> np.uint64(29)
+        h *= np.uint64(0xBF58476D1CE4E5B9)
+        h ^= h >> np.uint64(32)
+    return h % np.uint64((1 << kbits) - 1)
+
+
+def test_long_runs_of_colliding_connections(dev):
+    """One key bucket holding several long connections (hash collisions): the
+    head wave walks them one pass per connection (conntrack.hip PassKeys), and
+    past kPassKeys (4) takes the rest as one sequence.  Buckets of 6, 3 and 2
+    colliding TCP/UDP flows of 150 packets each, over three batches that open
+    them, continue them and close some mid-run.  Bit-exact vs the oracle:
+    verdicts, rule ids, counters, the table (and its LRU stamps' order)."""
+    rng = np.random.default_rng(61)
+    rules = CT_RULES + synth.config_rules(2).rules()
+    o, ipt = ct_pair({1: rules}, {1: "ACCEPT"}, cap_log2=16, jit=1)
+    per, groups = 150, (6, 3, 2)
+    n = per * sum(groups)
+    kbits = 8
+    while (1 << kbits) < 2 * n:
+        kbits += 1
+    flows = []
+    for g, size in enumerate(groups):
+        proto = synth.TCP if g != 1 else synth.UDP
+        m = 1 << 18
+        a = rng.integers(1, 2**32, size=m, dtype=np.uint64)
+        b = rng.integers(1, 2**32, size=m, dtype=np.uint64)
+        pa = rng.integers(1024, 65535, size=m)
+        pb = rng.integers(1, 1024, size=m)
+        bk = _key_bucket(a, b, pa, pb, proto, kbits)
+        target = np.bincount(bk.astype(np.int64)).argmax()
+        pick = np.nonzero(bk == target)[0][:size]
+        assert len(pick) == size
+        for j in pick:
+            flows.append((proto, int(a[j]), int(b[j]), int(pa[j]), int(pb[j]),
+                          int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32))))
+    phases = [("open", {}), ("data", {}), ("data", {0: 0.3, 4: 0.6, 9: 0.5})]
+    for k, (phase, close) in enumerate(phases):
+        ipt.ct_set_time(NOW + k * 10**9)
+        o.ct_set_time(NOW + k * 10**9)
+        f = _elephants(rng, flows, phase, per, close_at=close)
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, f.reshape(-1), n)
+        assert_same(v_o, r_o, v_g, r_g)
+        assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_ae(o, ipt)

@@ -65,6 +65,13 @@ def main():
     for k, x in ph.items():
         q = np.percentile(x / 100.0, [10, 50, 90, 99])
         print(f"  {k:34s} us p10 {q[0]:8.1f} p50 {q[1]:8.1f} p90 {q[2]:8.1f} p99 {q[3]:8.1f} mean {x.mean() / 100:8.1f}")
+    life = end - tt[:, 0]
+    top = np.argsort(life)[::-1][:24]
+    print("  longest class-0 waves (vb, records, entry us, life us, first chunk us):")
+    vbs = np.nonzero(ran)[0]
+    for j in top:
+        print(f"    vb {vbs[j]:6d} recs {recs[j]:6d} entry {(tt[j, 0] - e0) / 100:7.1f} life {life[j] / 100:7.1f} "
+              f"first {(tt[j, 2] - tt[j, 1]) / 100:7.1f}")
     grid = np.linspace(0, (end.max() - e0), 11)
     inflight = [int(((tt[:, 0] - e0 <= g) & (end - e0 > g)).sum()) for g in grid]
     print("  class-0 waves in flight at 0..100 % of the span:", inflight)
