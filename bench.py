@@ -38,12 +38,54 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_frames(n, rs, seed, chunk=1 << 22, protos=(6, 17)):
+DATA = {
+    2: "synthetic (seeded synth.config_rules(2) + synth.make_headers, UDP only; no captured traffic)",
+    3: "synthetic (seeded synth.config_rules(3) + synth.make_headers, 50/50 TCP/UDP; no captured traffic)",
+    5: "synthetic (seeded synth.config_rules(5) + synth.imix_frames; no captured traffic)",
+}
+# the sources that decide what the classify kernel reads per launch: a PMC
+# traffic figure (profiles/pmc_traffic.json) is reported only for the build it
+# was measured on
+KERNEL_SOURCES = ("polycube_amd/csrc/classify.hip", "polycube_amd/csrc/devchain.h", "polycube_amd/csrc/image.cpp")
+
+
+def kernel_src_hash():
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def traffic_key(cfg, hook):
+    return f"config{cfg}" + ("_tc" if hook else "")
+
+
+def load_traffic(cfg, hook, n):
+    """(HBM bytes per launch, note) from profiles/pmc_traffic.json when it was measured on this
+    build's kernel sources and this batch size; (None, why) otherwise."""
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(tf):
+        return None, "no profiles/pmc_traffic.json"
+    with open(tf) as fh:
+        pm = json.load(fh).get("configs", {}).get(traffic_key(cfg, hook))
+    if not pm:
+        return None, f"no PMC entry for {traffic_key(cfg, hook)}"
+    if pm.get("src_hash") != kernel_src_hash():
+        return None, f"PMC entry measured on kernel sources {pm.get('src_hash')}, this build is {kernel_src_hash()}"
+    if pm.get("frames") != n:
+        return None, f"PMC entry measured at {pm.get('frames')} frames, this run has {n}"
+    return pm["hbm_bytes_per_launch"], (f"rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE on kernel sources {pm['src_hash']} "
+                                        f"({pm.get('profile', '')})")
+
+
+def gen_frames(n, rs, seed, chunk=1 << 22, protos=(6, 17), hit_frac=0.5):
     from polycube_amd import synth
     out = np.empty((n, 64), np.uint8)
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
-        cols = synth.make_headers(rs, m, seed + s // chunk, protos=protos)
+        cols = synth.make_headers(rs, m, seed + s // chunk, protos=protos, hit_frac=hit_frac)
         out[s:s + m] = synth.build_frames(*cols, frame_len=64)
     return out.reshape(-1)
 
@@ -300,6 +342,135 @@ def fw_rate(rules, frames, n, dev, s_ptr, jit, steps=20, horus=False, settle=0.5
     return n / (ms * 1e-3) / 1e6, ms, info
 
 
+def timed_calls(fn, steps, stream, settle=0.3):
+    """Kernel ms per call: `settle` seconds of untimed calls, then one HIP event pair on the
+    launch stream around `steps` calls (as the headline is timed)."""
+    import torch
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < settle:
+        for _ in range(16):
+            fn()
+        torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(steps):
+        fn()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / steps
+
+
+def hit_rate_sweep(ipt, chain, rs, n, dev, stream, base_ms, seed, steps=20, hits=(0.0, 1.0)):
+    """The headline chain over batches built with other rule-hit shares (synth.make_headers
+    hit_frac: that share of the frames is built from a random rule's fields, the rest uniform),
+    the same kernel timing as the headline.  Reports kernel ms, Gpkt/s, the roofline fraction
+    and the share of frames that matched a rule (from the counters)."""
+    import torch
+    alt = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    v = torch.empty(n, dtype=torch.uint8, device=dev)
+    s_ptr = stream.cuda_stream
+    out = {"0.5": {"kernel_ms": round(base_ms, 4), "gpkt_s": round(n / base_ms / 1e6, 2),
+                   "frac": round(BYTES_PER_PKT * n / (base_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "what": "the headline batch (timed above)"}}
+    for h in hits:
+        alt.copy_(torch.from_numpy(gen_frames(n, rs, seed, hit_frac=h)))
+        ms = timed_calls(lambda: ipt.classify(alt, n=n, verdicts=v, rule_ids=False, stream=s_ptr), steps, stream)
+        chain.read_counters(len(rs.rules()), flush=True)
+        ipt.classify(alt, n=n, verdicts=v, rule_ids=False, stream=s_ptr)
+        torch.cuda.synchronize()
+        pk, _, dp, _ = chain.read_counters(len(rs.rules()), flush=True)
+        out[str(h)] = {"kernel_ms": round(ms, 4), "gpkt_s": round(n / ms / 1e6, 2),
+                       "frac": round(BYTES_PER_PKT * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "matched_rule_share": round(sum(pk) / max(1, sum(pk) + dp), 4)}
+    del alt
+    return out
+
+
+def rule_update_latency(dev, log):
+    """Rule-update latency, the analogue of the reference's per-update timer
+    (Chain::updateChain, Chain.cpp:436,920-928: rule compile, bcc compile + load of the
+    chain's eBPF programs, map pushes).  Here, per config (1k and 10k rules):
+      apply_ms       pcn_ipt_chain_apply_rules of the whole chain (rule compiler, table image,
+                     upload to the inactive slot, flip), non-interactive mode
+      compile_ms     pcn_ipt_chain_program_compile: the chain program (hiprtc) for the launch shape
+      first_ms       the first classify launch after that (program load) until its verdicts are in
+      append_ms      one more rule appended in interactive mode (Chain::append -> updateChain):
+                     the whole chain recompiled and uploaded
+      append_first_ms  the next launch (jit=0: the generic kernel runs while the new chain
+                     program compiles in the background, as pcn_ipt_config.jit = 0 does)
+      append_program_ms  until that background compile is ready"""
+    import torch
+    from polycube_amd import Iptables, synth
+    out = {}
+    for cfg in (3, 5):
+        rs = synth.config_rules(cfg)
+        rules = rs.rules()
+        big = dict(max_rules=16384, max_counted_rules=10000, max_action_rules=10000) if cfg == 5 else {}
+        m = 1 << 16
+        kw = {}
+        if cfg == 5:
+            buf, off, ln = synth.imix_frames(rs, m, synth.CONFIG_SEEDS[5])
+            frames = torch.from_numpy(buf).to(dev)
+            kw = dict(offsets=torch.from_numpy(off.view(np.int32)).to(dev),
+                      lens=torch.from_numpy(ln.view(np.int16)).to(dev))
+        else:
+            frames = torch.from_numpy(gen_frames(m, rs, synth.CONFIG_SEEDS[3])).to(dev)
+        v = torch.empty(m, dtype=torch.uint8, device=dev)
+        ipt = Iptables(device=dev.index, jit=1, **big)
+        ipt.interactive = False
+        ch = ipt.chain("FORWARD")
+        for r in rules:
+            ch.append(**r)
+        ch.default = "DROP"
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        ch.apply_rules()
+        apply_ms = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
+        ch.compile_program()
+        compile_ms = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
+        ipt.classify(frames, n=m, verdicts=v, rule_ids=False, **kw)
+        ipt.synchronize()
+        first_ms = (time.perf_counter() - t) * 1e3
+        ready0 = ipt.jit_info()["programs_ready"]
+        ipt.close()
+        # interactive one-rule update on a jit=0 context (background compiles)
+        ipt = Iptables(device=dev.index, jit=0, **big)
+        ipt.interactive = False
+        ch = ipt.chain("FORWARD")
+        for r in rules:
+            ch.append(**r)
+        ch.default = "DROP"
+        ch.apply_rules()
+        ch.compile_program()
+        ipt.classify(frames, n=m, verdicts=v, rule_ids=False, **kw)
+        ipt.synchronize()
+        ipt.interactive = True
+        ready = ipt.jit_info()["programs_ready"]
+        t = time.perf_counter()
+        ch.append(**dict(rules[len(rules) // 2], action="ACCEPT"))
+        append_ms = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
+        ipt.classify(frames, n=m, verdicts=v, rule_ids=False, **kw)
+        ipt.synchronize()
+        append_first_ms = (time.perf_counter() - t) * 1e3
+        prog_ms = None
+        while time.perf_counter() - t < 30:
+            if ipt.jit_info()["programs_ready"] > ready:
+                prog_ms = (time.perf_counter() - t) * 1e3
+                break
+            time.sleep(0.005)
+        ipt.close()
+        out[f"config{cfg}"] = {"rules": len(rules), "apply_ms": round(apply_ms, 2), "compile_ms": round(compile_ms, 1),
+                               "first_ms": round(first_ms, 2), "programs_ready": ready0,
+                               "append_ms": round(append_ms, 2), "append_first_ms": round(append_first_ms, 2),
+                               "append_program_ms": None if prog_ms is None else round(prog_ms, 1)}
+        log(f"[bench] rule update config {cfg}: {out[f'config{cfg}']}")
+    out["what"] = rule_update_latency.__doc__.split("\n", 1)[1].strip()
+    return out
+
+
 def spawn_ranks(n):
     """Run this script as N ranks (torch.distributed.run, one process per GPU,
     rendezvous on 127.0.0.1); rank 0 prints the JSON line."""
@@ -331,6 +502,8 @@ def main():
                     help="attach-point semantics (tc: outer VLAN tags stripped before classification)")
     ap.add_argument("--no-ct", action="store_true", help="skip the stateful-conntrack leg")
     ap.add_argument("--no-fw", action="store_true", help="skip the pcn-firewall leg")
+    ap.add_argument("--no-hits", action="store_true", help="skip the hit-rate 0 / 1 sweep (config 3)")
+    ap.add_argument("--no-update", action="store_true", help="skip the rule-update latency leg")
     ap.add_argument("--jit", type=int, default=1,
                     help="chain programs: 1 compiled before the first launch (default), 0 background, -1 off")
     ap.add_argument("--settle", type=float, default=1.0,
@@ -419,16 +592,20 @@ def main():
         ipt.classify(frames, n=n, verdicts=verdicts, rule_ids=rid, offsets=offsets, lens=lens, stream=s_ptr,
                      hook=hook)
 
+    host_ex = [0.0]   # seconds spent in the gloo fallback's host exchange
+
     def exchange():
         if world == 1:
             return
         if use_rccl:
             ipt.sync_counters(s_ptr)
         else:   # fallback: the same per-step exchange, the blocks moved through the host by gloo
+            t = time.perf_counter()
             blk = ipt.snapshot_counters("FORWARD", stream=s_ptr).cpu()
             parts = [torch.empty_like(blk) for _ in range(world)]
             dist.all_gather(parts, blk)
             ipt.sum_counter_blocks("FORWARD", torch.stack(parts).to(dev), stream=s_ptr)
+            host_ex[0] += time.perf_counter() - t
 
     def step():
         classify()
@@ -459,6 +636,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    cinfo0 = ipt.comm_info() if use_rccl else None    # folds the settle/warmup gathers' times in
+    host_ex[0] = 0.0
     t0 = time.perf_counter()
     if args.step_events:
         for k in range(args.steps):
@@ -481,6 +660,32 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = (float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.step_events
                else ev[0][0].elapsed_time(ev[0][1]) / args.steps)
+    multi = None
+    if world > 1:
+        # per rank: device ordinal and PCI bus id (each rank must hold its own GPU unless the
+        # one-GPU test hook put them on one), the RCCL that serves the calls, the exchange time
+        ci = ipt.comm_info()
+        if use_rccl:
+            g = ci["gathers_timed"] - cinfo0["gathers_timed"]
+            ex_ms = (ci["gather_ms_total"] - cinfo0["gather_ms_total"]) / max(1, g)
+        else:
+            g, ex_ms = args.steps, host_ex[0] / args.steps * 1e3
+        mine = {"rank": rank, "local_rank": local, "device": ci["device"], "pci_bus_id": ci["pci_bus_id"],
+                "exchange_ms_per_step": round(ex_ms, 4), "steps_timed": g}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        shared = "PCN_BENCH_DEVICE" in os.environ
+        distinct = len({r["pci_bus_id"] for r in ranks}) == world
+        if not shared and not distinct:
+            raise SystemExit(f"[rank {rank}] ranks share a GPU: {ranks}")
+        multi = {"rccl_version": ci["rccl_version"], "rccl_path": ci["rccl_path"], "ranks": ranks,
+                 "devices_distinct": distinct,
+                 "devices_shared_by_test_hook": shared,
+                 "exchange_ms_per_step_max": max(r["exchange_ms_per_step"] for r in ranks),
+                 "exchange_what": ("RCCL all-gather + device rank sum on the communicator stream (an event pair per "
+                                   "step there; it overlaps the next step's classify)" if use_rccl else
+                                   "gloo fallback: host wall time of snapshot + gloo all_gather + device sum per "
+                                   "step (on the classify path)")}
     if world > 1:
         tt = torch.tensor([elapsed])
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -501,13 +706,7 @@ def main():
     value = n * world * args.steps / elapsed / 1e6
     bytes_per_pkt = BYTES_PER_PKT + (6 if cfg == 5 else 0)   # + offset and length per frame (§8d)
     achieved = bytes_per_pkt * n / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        with open(tf) as fh:
-            pm = json.load(fh)
-        if pm.get("frames") == n and cfg == 3:
-            traffic = pm.get("hbm_bytes_per_launch")
+    traffic, traffic_note = load_traffic(cfg, hook, n)
 
     jit_info = ipt.jit_info()
     kernel = (f"pcn_classify_jit (chain program, config-{cfg} layout baked in)"
@@ -524,7 +723,7 @@ def main():
             "metric": METRIC if world == 1 else METRIC.replace("1 GPU", f"{world} GPUs"), "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded synth.config_rules(3) + make_headers; no captured traffic)",
+            "data": DATA[cfg],
             "config": {"workload": WORKLOADS[cfg] + (", TC hook" if hook else ""),
                        "rules": len(rules), "frames_per_gpu": n,
                        "frame_bytes": "IMIX 64/576/1500 (7:4:1)" if cfg == 5 else 64,
@@ -536,6 +735,7 @@ def main():
                        "collective": collective if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_from": traffic_note, "kernel_src_hash": kernel_src_hash(),
                          "kernel": kernel, "kernel_ms": round(kern_ms, 4),
                          "kernel_ms_from": ("a HIP event pair around each timed step" if args.step_events else
                                             "one HIP event pair around the K timed steps on the launch stream "
@@ -546,6 +746,14 @@ def main():
             "settle": {"seconds": round(settle_s, 2), "steps": settle_steps,
                        "what": "untimed steps before the warmup steps, until the GPU clocks reach steady state"},
         }
+        if multi:
+            line["multi_gpu"] = multi
+        else:
+            from polycube_amd.iptables import comm_info
+            ci = comm_info()
+            line["rccl"] = {"version": ci["rccl_version"], "path": ci["rccl_path"]}
+        if world == 1 and cfg == 3 and not args.no_hits:
+            line["hit_rates"] = hit_rate_sweep(ipt, fw, rs, n, dev, stream, kern_ms, synth.CONFIG_SEEDS[3])
         if cfg == 5:
             line["roofline"]["gather_ceiling"] = gather_ceiling(frames, offsets, lens, n, s_ptr, kern_ms)
         if world == 1 and not args.no_cpu:
@@ -580,6 +788,8 @@ def main():
                 "what": f"same chain with the connection table on (pcn_ipt_ct_enable): 2^{args.log2n} 64B frames of "
                         f"2^16 interleaved flows, labels from and updates to the HBM table in batch order "
                         f"({live} live entries after the run)"}
+        if world == 1 and cfg == 3 and not args.no_update:
+            line["rule_update"] = rule_update_latency(dev, log)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

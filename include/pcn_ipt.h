@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 7
+#define PCN_IPT_ABI_VERSION 8
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -200,6 +200,19 @@ typedef struct {
   uint32_t programs_failed;   /* compiles or module loads that failed          */
 } pcn_ipt_jit_info;
 int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out);
+/* Test hook: the number of guard words past the classify kernel's stale-port
+ * group words (one per 64-frame group + 1, used while a Horus program keys on
+ * ports) that no longer hold their pattern; 0 = no write past the groups.
+ * With PCN_IPT_DEBUG_STALE_CANARY=1 in the environment every word past the
+ * last batch's groups is a guard word, else only those past the largest
+ * batch's.  -ENOENT before the first such batch.  Synchronises the device. */
+int pcn_ipt_debug_stale_canary(pcn_ipt *ctx);
+/* Test hook: how often the stateful walk went past its first pass over a key
+ * bucket since the last reset (device-wide): out[0] passes over a bucket's
+ * 2nd to 4th connection, out[1] walks of its remaining connections as one
+ * sequence (conntrack.hip walk_long).  reset != 0 zeroes them after the read.
+ * Synchronises the device. */
+int pcn_ipt_debug_ct_walk_passes(pcn_ipt *ctx, uint64_t out[2], int reset);
 /* Compile the chain program of `chain` for its usual launch shape (fixed
  * 64-byte stride, ingress/egress alone, image in LDS) now and wait for it —
  * the blocking compile the reference does in Chain::updateChain.  Needs no
@@ -283,7 +296,12 @@ int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain);
  * least recently touched live entries are deleted down to max_entries
  * (pcn_ipt_ct_set_max_entries: 65536 by default, 0 = unbounded), counted in
  * pcn_ipt_ct_info.evicted.  Within a batch nothing is evicted (the kernel's
- * own LRU is approximate: per-CPU lists, reference bits).  Independently of
+ * own LRU is approximate: per-CPU lists, reference bits).  One touch per
+ * packet: an echo reply that falls through to ICMP_MISS also looks up the key
+ * of the header it quotes (ConntrackLabel_dp.c:450-531), and in the kernel's
+ * lru_hash that lookup would refresh the quoted entry too; here (GPU and
+ * oracle alike) it does not, so eviction order can differ from the kernel's
+ * there.  No reference fixture covers it (parity unpinned).  Independently of
  * that, an insert that finds no free slot within 512 slots of the key's home
  * slot (a full or nearly full table: 2^capacity_log2 slots, deleted keys keep
  * theirs) is dropped and counted (inserts_lost), which bounds every lookup at
@@ -434,6 +452,23 @@ int pcn_ipt_comm_init(pcn_ipt *ctx, int nranks, int rank, const uint8_t uid[128]
 /* All-gather every rank's per-rule/default counters over RCCL and sum them
  * into the scope=1 view.  Stream-ordered. */
 int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream);
+/* Facts about the exchange, for a scaling run's record: the RCCL that serves
+ * the calls (its ncclGetVersion and the file dladdr resolves ncclCommInitRank
+ * to: a process may hold more than one librccl), the context's device and PCI
+ * bus id (ranks must not share one), and the summed duration of the
+ * all-gather steps (all-gather + rank sum, an event pair on the communicator
+ * stream per pcn_ipt_sync_counters call; waits for the ones still running).
+ * ctx may be NULL: then only nccl_version and rccl_path are filled. */
+typedef struct {
+  int nccl_version;          /* e.g. 22606 = 2.26.6 */
+  int nranks, rank;          /* 0, 0 before pcn_ipt_comm_init */
+  int device;                /* HIP ordinal, -1 without a device */
+  char pci_bus_id[32];
+  char rccl_path[256];
+  uint64_t gathers_timed;
+  double gather_ms_total;
+} pcn_ipt_comm_info;
+int pcn_ipt_comm_get_info(pcn_ipt *ctx, pcn_ipt_comm_info *out);
 /* The two halves of pcn_ipt_sync_counters, for a caller that moves the counter
  * blocks over its own transport (gloo, MPI, a test), or reads them raw.  The
  * reference's only reduction is the control plane's sum over per-CPU counters

@@ -1116,6 +1116,11 @@ __device__ __forceinline__ WalkRec shfl_rec(const WalkRec &w, uint32_t from) {
 // whose walk a segment continues).
 constexpr int kPassKeys = 4;
 constexpr int kAllKeys = -2, kOtherKeys = -1;
+// How often walk_long went past its first pass: [0] passes for a bucket's 2nd..
+// kPassKeys-th connection, [1] "the rest as one sequence" walks.  Only bucket
+// collisions get there (a global atomic each); read by the tests through
+// pcn_ipt_debug_ct_walk_stats to see that the path they mean to cover ran.
+__device__ unsigned long long g_walk_passes[2];
 struct PassKeys {
   uint32_t n;
   uint32_t k[kPassKeys][4];   // src, dst, sport | dport << 16, proto
@@ -1373,6 +1378,7 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
     if (++pass < kPassKeys) {
       const WalkRec x = wrec.at(from);
       if (threadIdx.x == 0) {
+        atomicAdd(&g_walk_passes[0], 1ull);
         pk.k[pass][0] = x.r.src;
         pk.k[pass][1] = x.r.dst;
         pk.k[pass][2] = uint32_t(x.r.sport) | uint32_t(x.r.dport) << 16;
@@ -1382,6 +1388,7 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
       pass_fence();
     } else {
       pass = kOtherKeys;                            // the rest as one sequence (sets no unk)
+      if (threadIdx.x == 0) atomicAdd(&g_walk_passes[1], 1ull);
     }
   }
 #if PCN_CT_DBG_T
@@ -2333,6 +2340,18 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs, cchunk);
   CT_CHECK(hipGetLastError());
   return hipSuccess;
+}
+
+int ct_walk_passes(uint64_t out[2], bool reset) {
+  unsigned long long v[2];
+  hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_walk_passes), sizeof(v), 0, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[2] = {0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_walk_passes), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  out[0] = v[0];
+  out[1] = v[1];
+  return static_cast<int>(e);
 }
 
 int ct_ae_fixup(const CtBatch &b, void *stream) {

@@ -94,6 +94,8 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
 // counters), as ConntrackLabel_dp.c:580-616 takes ESTABLISHED packets there
 // before the chain runs.  rule_ids may be null.
 int ct_ae_fixup(const CtBatch &b, void *stream);
+// walk_long's extra passes since the last reset (g_walk_passes, current device; a hipError_t)
+int ct_walk_passes(uint64_t out[2], bool reset);
 
 // Flow-affinity split (pcn_ipt_flow_owner / pcn_ipt_flow_split): the owner
 // rank of every frame, from its unordered IPv4 address pair (an ICMP error's

@@ -6,10 +6,12 @@
 // The datapath half owns the chain images in HBM (double-buffered per chain),
 // the counters, and launches the HIP classify kernel (classify.hip).
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -157,6 +159,14 @@ struct pcn_ipt {
   hipEvent_t ev_staged = nullptr, ev_gathered = nullptr;
   bool gather_pending = false;
   int nranks = 1, rank = 0;
+  // timing of the all-gather steps on the communicator stream: a ring of
+  // event pairs, folded into the sum once complete (pcn_ipt_comm_get_info)
+  static constexpr int kGatherEv = 8;
+  hipEvent_t ev_g0[kGatherEv] = {}, ev_g1[kGatherEv] = {};
+  bool ev_g_live[kGatherEv] = {};
+  int ev_g_next = 0;
+  uint64_t gathers_timed = 0;
+  double gather_ms = 0.0;
   JitCache jit;                                // chain programs (per launch shape)
   uint64_t launches_generic = 0, launches_jit = 0;
   // accept-established optimization per chain (Iptables.h accept_established_enabled_*)
@@ -184,6 +194,7 @@ struct pcn_ipt {
   // the classify kernel's stale-port groups (classify.hip stale_lookback)
   uint64_t *d_stale_desc = nullptr;            // one word per 64-frame group
   size_t stale_groups = 0;
+  size_t stale_guard_from = 0;                 // first guard word (pcn_ipt_debug_stale_canary)
   uint32_t stale_epoch = 0;                    // bumped per launch (24 bits)
   uint32_t *d_chunk_ctr = nullptr;
 };
@@ -197,6 +208,29 @@ namespace {
 
 void device_guard(pcn_ipt *ctx) {
   if (ctx->has_device) hip_check(hipSetDevice(ctx->cfg.device), "hipSetDevice");
+}
+
+// Guard words past the stale-port groups: a kernel that published a group
+// past its batch would overwrite one (pcn_ipt_debug_stale_canary).
+constexpr size_t kStaleCanary = 16;
+constexpr int kStaleCanaryByte = 0xA5;
+// PCN_IPT_DEBUG_STALE_CANARY=1: guard every word past each batch's groups
+// (a memset per launch that is smaller than the largest; tests only, read at
+// every launch so a test can set it)
+bool debug_stale_canary() {
+  const char *e = std::getenv("PCN_IPT_DEBUG_STALE_CANARY");
+  return e && *e == '1';
+}
+
+// Add the duration of all-gather step k (its event pair on the communicator
+// stream) to the context's total; waits for it if it is still running.
+void fold_gather_time(pcn_ipt *ctx, int k) {
+  hip_check(hipEventSynchronize(ctx->ev_g1[k]), "hipEventSynchronize");
+  float ms = 0.f;
+  hip_check(hipEventElapsedTime(&ms, ctx->ev_g0[k], ctx->ev_g1[k]), "hipEventElapsedTime");
+  ctx->gather_ms += ms;
+  ++ctx->gathers_timed;
+  ctx->ev_g_live[k] = false;
 }
 
 uint32_t counted(const pcn_ipt *ctx, uint32_t nrules) {
@@ -213,6 +247,20 @@ void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
   cs.desc_words.insert(cs.desc_words.end(), {img.nrw, img.nsw, img.present, img.all_cls});
   cs.info = pcn_ipt_chain_info{img.nrules, img.nrw, img.nsw, img.nvec, img.ngroups, img.present,
                                img.lay.bytes, img.part_bytes};
+  DevChain d{};
+  d.lay = img.lay;
+  d.nrules = img.nrules;
+  d.nrw = img.nrw;
+  d.nsw = img.nsw;
+  d.present = img.present;
+  d.nvec = img.nvec;
+  d.all_cls = img.all_cls;
+  d.ncounted = counted(ctx, img.nrules);
+  d.max_action = ctx->cfg.max_action_rules;
+  d.default_action = img.default_action;
+  d.lds_image = 0;
+  d.lds_bins = -1;
+  d.lds_nrules = 0;
   if (ctx->has_device) {
     device_guard(ctx);
     // every batch queued before this call must not see a half-written slot
@@ -226,25 +274,13 @@ void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
     // default counters live in shared maps and persist (Iptables_Parser_dp.c:47-58)
     hip_check(hipMemset(cs.ctr + 2, 0, (ctx->ctr_words - 2) * sizeof(unsigned long long)),
               "hipMemset(counters)");
-    DevChain d{};
-    d.lay = img.lay;
     d.image = static_cast<const uint8_t *>(s.tables);
     d.ctr = cs.ctr;
-    d.nrules = img.nrules;
-    d.nrw = img.nrw;
-    d.nsw = img.nsw;
-    d.present = img.present;
-    d.nvec = img.nvec;
-    d.all_cls = img.all_cls;
-    d.ncounted = counted(ctx, img.nrules);
-    d.max_action = ctx->cfg.max_action_rules;
-    d.default_action = img.default_action;
-    d.lds_image = 0;
-    d.lds_bins = -1;
-    d.lds_nrules = 0;
-    cs.desc = d;
     cs.active = next;
   }
+  // (without a device the descriptor still describes the chain: a chain
+  // program can be planned and compiled, pcn_ipt_chain_program_compile)
+  cs.desc = d;
   cs.tables = std::move(tables);
 }
 
@@ -564,6 +600,10 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
     if (ctx->ev_staged) (void)hipEventDestroy(ctx->ev_staged);
     if (ctx->ev_gathered) (void)hipEventDestroy(ctx->ev_gathered);
+    for (int k = 0; k < pcn_ipt::kGatherEv; ++k) {
+      if (ctx->ev_g0[k]) (void)hipEventDestroy(ctx->ev_g0[k]);
+      if (ctx->ev_g1[k]) (void)hipEventDestroy(ctx->ev_g1[k]);
+    }
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
     for (void *p : {static_cast<void *>(ctx->hz[0].d_tab), static_cast<void *>(ctx->hz[0].d_ctr),
                     static_cast<void *>(ctx->hz[1].d_tab), static_cast<void *>(ctx->hz[1].d_ctr),
@@ -796,11 +836,14 @@ struct StageA {
 // carry_out (stateless batches that track the stale ports): when the kernel
 // computes them itself (has_stale), its last workgroup writes the carry there
 // and *carried becomes true; otherwise the caller advances the carry.
+// plan (pcn_ipt_chain_program_compile): compute the launch as usual, then set
+// *plan to the chain program's spec ("" when no chain program would run) and
+// return before anything is allocated, requested or launched.
 int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const StageA *sa, const uint32_t *carry,
-                 uint32_t *carry_out = nullptr, bool *carried = nullptr) {
+                 uint32_t *carry_out = nullptr, bool *carried = nullptr, std::string *plan = nullptr) {
   {
     if (!b) return fail(-EINVAL, "null batch");
-    if (!ctx->has_device) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
+    if (!ctx->has_device && !plan) return fail(-ENODEV, "context has no HIP device (created with device=-1)");
     if (b->n == 0) return 0;
     if (!b->frames || !b->verdicts) return fail(-EINVAL, "frames and verdicts are required");
     if (b->direction != PCN_IPT_INGRESS && b->direction != PCN_IPT_EGRESS) return fail(-EINVAL, "bad direction");
@@ -968,7 +1011,9 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
         if (ctx->fw_ct_mode == PCN_FW_CT_DISABLED) a.horus_flags |= kHzMissDrops;   // :170-174
       }
       a.fast_chain = -1;                               // the lookup lives in the general path
-      if (carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) {
+      if (plan && carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) {
+        a.has_stale = 1;
+      } else if (carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) {
         // the key reads ports: stale ones (Q4) computed in the kernel
         // one word per 64-frame group of the batch (+1 for the look-back from
         // the end); the kernel publishes only groups that hold frames
@@ -976,11 +1021,19 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
         if (ctx->stale_groups < groups) {
           if (ctx->d_stale_desc) hip_check(hipFree(ctx->d_stale_desc), "hipFree");
           ctx->d_stale_desc = nullptr;
-          hip_check(hipMalloc(&ctx->d_stale_desc, groups * 8), "hipMalloc(stale groups)");
+          // + kStaleCanary guard words past the groups (pcn_ipt_debug_stale_canary)
+          hip_check(hipMalloc(&ctx->d_stale_desc, (groups + kStaleCanary) * 8), "hipMalloc(stale groups)");
           hip_check(hipMemset(ctx->d_stale_desc, 0, groups * 8), "hipMemset(stale groups)");
+          hip_check(hipMemset(ctx->d_stale_desc + groups, kStaleCanaryByte, kStaleCanary * 8), "hipMemset(canary)");
           ctx->stale_groups = groups;
           ctx->stale_epoch = 0;
         }
+        if (debug_stale_canary() && groups < ctx->stale_groups)
+          // test hook: guard every word past this batch's groups, not only those
+          // past the largest batch so far
+          hip_check(hipMemsetAsync(ctx->d_stale_desc + groups, kStaleCanaryByte, (ctx->stale_groups - groups) * 8,
+                                   static_cast<hipStream_t>(stream)), "hipMemset(canary)");
+        ctx->stale_guard_from = debug_stale_canary() ? groups : ctx->stale_groups;
         if (!ctx->d_chunk_ctr) {   // zero from here on: each launch's last workgroup resets it
           hip_check(hipMalloc(&ctx->d_chunk_ctr, 64), "hipMalloc(chunk counter)");
           hip_check(hipMemset(ctx->d_chunk_ctr, 0, 64), "hipMemset(chunk counter)");
@@ -1003,7 +1056,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     const int ns = ch < 3 ? static_cast<int>(a.ch[ch].lay.nslots) : 6;
     // chain program for this launch shape (jit.hpp), when enabled and ready
     void *fn = nullptr;
-    if (ch < 3 && (reach_fw || reach_in || reach_out) && ctx->cfg.jit >= 0) {
+    if (plan) plan->clear();
+    if (ch < 3 && (reach_fw || reach_in || reach_out) && (ctx->cfg.jit >= 0 || plan)) {
       ChainState &cs = ctx->chains[ch];
       JitShape shape;
       shape.fixed = fixed;
@@ -1023,9 +1077,14 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
         cs.jit_shape = shape;
         cs.jit_spec = jit_spec(key, shape);
       }
+      if (plan) {
+        *plan = cs.jit_spec;
+        return 0;
+      }
       ctx->jit.request(cs.jit_spec, ctx->cfg.jit == 1);
       fn = ctx->jit.function(cs.jit_spec, ctx->cfg.device);
     }
+    if (plan) return 0;
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
     int rc = launch_classify(a, fixed, ch, ns, ctx->num_cus, fn, static_cast<hipStream_t>(stream));
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
@@ -1188,39 +1247,28 @@ int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out) {
 int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
   return guarded(ctx, [&] {
     if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
-    const ChainState &cs = ctx->chains[chain];
-    if (cs.info.nrules == 0) return fail(-ENOENT, "chain has no rules");
-    // the descriptor classify builds when this chain alone runs rules
-    DevChain d{};
-    std::memcpy(&d.lay, cs.desc_words.data(), sizeof(TableLayout));
-    d.nrules = cs.info.nrules;
-    d.nrw = cs.info.nrw;
-    d.nsw = cs.info.nsw;
-    d.present = cs.info.present;
-    d.nvec = cs.info.nvec;
-    d.all_cls = cs.desc_words[sizeof(TableLayout) / 4 + 3];
-    d.ncounted = counted(ctx, cs.info.nrules);
-    d.max_action = ctx->cfg.max_action_rules;
-    d.default_action = cs.default_action;
-    d.lds_image = kLdsDescBytes;
-    d.lds_bins = d.ncounted <= kMaxLdsRuleBins ? 3 : -1;
-    d.lds_nrules = d.lds_bins >= 0 ? d.ncounted : 0;
-    const uint32_t nbins = 3 + d.lds_nrules;
-    const uint32_t tail = (nbins * 4 + 15) / 16 * 16 + (uint32_t(ctx->localip.size()) * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * wave_region_bytes(true);
-    d.lds_limit = kLdsDescBytes + d.lay.bytes + tail <= kLdsBudget   ? d.lay.bytes
-                  : kLdsDescBytes + d.lay.pbase + tail <= kLdsBudget ? d.lay.pbase
-                                                                     : 0;
-    if (d.lds_bins < 0) {          // as launch_batch: bins for the lowest rule ids in the LDS left over
-      d.lds_nrules = partial_rule_bins(kLdsDescBytes + d.lds_limit + tail, 4, d.ncounted);
-      if (d.lds_nrules) d.lds_bins = 3;
-    }
-    JitShape shape;
-    shape.fixed = true;
-    shape.lds = d.lds_limit > 0;
-    shape.ch = chain;
-    shape.ns = static_cast<int>(d.lay.nslots);
-    const std::string spec = jit_spec(d, shape);
+    if (ctx->chains[chain].info.nrules == 0) return fail(-ENOENT, "chain has no rules");
+    // the usual launch shape: a stateless fixed-stride batch of 64-byte
+    // frames in the chain's direction, planned by the launch code itself (so
+    // the descriptor has the same LDS placement, counter bins -- Horus bins
+    // included -- and side inputs as the launches it is compiled for)
+    pcn_ipt_batch b{};
+    uint8_t *const never_read = reinterpret_cast<uint8_t *>(uintptr_t(1) << 12);   // a plan reads no buffer
+    b.frames = never_read;
+    b.n = uint64_t(1) << 20;
+    b.stride = 64;
+    b.fixed_len = 64;
+    b.frames_bytes = b.n * b.stride;
+    b.verdicts = never_read;
+    b.direction = chain == PCN_IPT_OUTPUT ? PCN_IPT_EGRESS : PCN_IPT_INGRESS;
+    const HorusProg *hz = horus_of_batch(ctx, b.direction);
+    const bool track = ctx->hz_enabled || ctx->ct_on;
+    const bool want_stale = hz && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT));
+    const uint32_t *stale = want_stale && track ? (ctx->ct_on ? ctx->ct.carry : ctx->d_hz_carry) : nullptr;
+    std::string spec;
+    int rc = launch_batch(ctx, &b, nullptr, nullptr, stale, nullptr, nullptr, &spec);
+    if (rc) return rc;
+    if (spec.empty()) return fail(-ENOENT, "no chain program runs this chain's rules in its usual launch");
     ctx->jit.request(spec, true);
     if (!ctx->jit.ready(spec)) return fail(-EIO, "chain program compile failed: " + ctx->jit.last_log());
     return 0;
@@ -1383,6 +1431,14 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
     hip_check(hipEventRecord(ctx->ev_staged, s), "hipEventRecord");
     hipStream_t cs_ = ctx->comm_stream;
     hip_check(hipStreamWaitEvent(cs_, ctx->ev_staged, 0), "hipStreamWaitEvent");
+    // time the exchange on the communicator stream (all-gather + rank sum):
+    // reuse the oldest pair of the ring, folding its duration in first
+    const int ge = ctx->ev_g_next;
+    ctx->ev_g_next = (ge + 1) % pcn_ipt::kGatherEv;
+    if (ctx->ev_g_live[ge]) fold_gather_time(ctx, ge);
+    if (!ctx->ev_g0[ge]) hip_check(hipEventCreate(&ctx->ev_g0[ge]), "hipEventCreate");
+    if (!ctx->ev_g1[ge]) hip_check(hipEventCreate(&ctx->ev_g1[ge]), "hipEventCreate");
+    hip_check(hipEventRecord(ctx->ev_g0[ge], cs_), "hipEventRecord");
     ncclResult_t r = ncclGroupStart();
     for (int c = 0; c < PCN_IPT_NCHAINS && r == ncclSuccess; ++c)
       r = ncclAllGather(ctx->chains[c].stage, ctx->chains[c].gather, count[c], ncclUint64, ctx->comm, cs_);
@@ -1394,8 +1450,64 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
       int rc = launch_sum_ranks(cs.gather, cs.ctr_global, count[c], ctx->nranks, cs_);
       if (rc != hipSuccess) return fail(-EIO, "sum_ranks launch failed");
     }
+    hip_check(hipEventRecord(ctx->ev_g1[ge], cs_), "hipEventRecord");
+    ctx->ev_g_live[ge] = true;
     hip_check(hipEventRecord(ctx->ev_gathered, cs_), "hipEventRecord");
     ctx->gather_pending = true;
+    return 0;
+  });
+}
+
+int pcn_ipt_debug_ct_walk_passes(pcn_ipt *ctx, uint64_t out[2], int reset) {
+  return guarded(ctx, [&] {
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (!out) return fail(-EINVAL, "null out");
+    device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    hip_check(static_cast<hipError_t>(ct_walk_passes(out, reset != 0)), "ct_walk_passes");
+    return 0;
+  });
+}
+
+int pcn_ipt_debug_stale_canary(pcn_ipt *ctx) {
+  return guarded(ctx, [&] {
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (!ctx->d_stale_desc) return fail(-ENOENT, "no stale-port groups allocated");
+    device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    const size_t from = ctx->stale_guard_from, words = ctx->stale_groups + kStaleCanary - from;
+    std::vector<uint64_t> w(words);
+    hip_check(hipMemcpy(w.data(), ctx->d_stale_desc + from, words * 8, hipMemcpyDeviceToHost), "hipMemcpy(canary)");
+    uint64_t pat;
+    std::memset(&pat, kStaleCanaryByte, 8);
+    int bad = 0;
+    for (uint64_t x : w) bad += x != pat;
+    return bad;
+  });
+}
+
+int pcn_ipt_comm_get_info(pcn_ipt *ctx, pcn_ipt_comm_info *out) {
+  if (!out) return fail(-EINVAL, "null out");
+  std::memset(out, 0, sizeof(*out));
+  int v = 0;
+  if (ncclGetVersion(&v) == ncclSuccess) out->nccl_version = v;
+  Dl_info di{};
+  if (dladdr(reinterpret_cast<void *>(&ncclCommInitRank), &di) && di.dli_fname)
+    std::snprintf(out->rccl_path, sizeof(out->rccl_path), "%s", di.dli_fname);
+  out->device = -1;
+  if (!ctx) return 0;
+  return guarded(ctx, [&] {
+    out->nranks = ctx->comm ? ctx->nranks : 0;
+    out->rank = ctx->comm ? ctx->rank : 0;
+    if (!ctx->has_device) return 0;
+    device_guard(ctx);
+    out->device = ctx->cfg.device;
+    hip_check(hipDeviceGetPCIBusId(out->pci_bus_id, sizeof(out->pci_bus_id), ctx->cfg.device),
+              "hipDeviceGetPCIBusId");
+    for (int k = 0; k < pcn_ipt::kGatherEv; ++k)
+      if (ctx->ev_g_live[k]) fold_gather_time(ctx, k);
+    out->gathers_timed = ctx->gathers_timed;
+    out->gather_ms_total = ctx->gather_ms;
     return 0;
   });
 }

@@ -82,13 +82,19 @@ class CtInfo(C.Structure):
                 ("inserts_lost", C.c_uint64), ("max_entries", C.c_uint64), ("evicted", C.c_uint64)]
 
 
+class CommInfo(C.Structure):
+    _fields_ = [("nccl_version", C.c_int), ("nranks", C.c_int), ("rank", C.c_int), ("device", C.c_int),
+                ("pci_bus_id", C.c_char * 32), ("rccl_path", C.c_char * 256), ("gathers_timed", C.c_uint64),
+                ("gather_ms_total", C.c_double)]
+
+
 class HorusInfo(C.Structure):
     _fields_ = [("enabled", C.c_uint32), ("runtime", C.c_uint32), ("entries", C.c_uint32), ("fields", C.c_uint32),
                 ("conntrack", C.c_uint32)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
-ABI_VERSION = 7            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
+ABI_VERSION = 8            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
 
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
@@ -117,6 +123,8 @@ SIGNATURES = {
     "pcn_ipt_classify": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p]),
     "pcn_ipt_synchronize": (C.c_int, [C.c_void_p]),
     "pcn_ipt_get_jit_info": (C.c_int, [C.c_void_p, C.POINTER(JitInfo)]),
+    "pcn_ipt_debug_stale_canary": (C.c_int, [C.c_void_p]),
+    "pcn_ipt_debug_ct_walk_passes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "pcn_ipt_chain_program_compile": (C.c_int, [C.c_void_p, C.c_int]),
     "pcn_ipt_read_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64),
@@ -139,6 +147,7 @@ SIGNATURES = {
     "pcn_ipt_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "pcn_ipt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
     "pcn_ipt_sync_counters": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pcn_ipt_comm_get_info": (C.c_int, [C.c_void_p, C.POINTER(CommInfo)]),
     "pcn_ipt_counter_block_words": (C.c_int, [C.c_void_p, C.c_int]),
     "pcn_ipt_snapshot_counters": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "pcn_ipt_sum_counter_blocks": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_uint64,

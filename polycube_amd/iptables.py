@@ -52,6 +52,18 @@ def _enc(v):
     return None if v is None else str(v).encode()
 
 
+def comm_info(handle=None):
+    """pcn_ipt_comm_get_info as a dict; without a context handle only the RCCL facts."""
+    out = ffi.CommInfo()
+    _check(ffi.lib().pcn_ipt_comm_get_info(handle, C.byref(out)))
+    d = {k: getattr(out, k) for k, _ in ffi.CommInfo._fields_}
+    for k in ("pci_bus_id", "rccl_path"):
+        d[k] = d[k].decode(errors="replace")
+    v = d["nccl_version"]
+    d["rccl_version"] = f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v else None
+    return d
+
+
 def make_rule(src=None, dst=None, l4proto=None, sport=None, dport=None, tcpflags=None,
               in_iface=None, out_iface=None, conntrack=None, action=None):
     """Build a pcn_ipt_rule from REST-style fields (None = not set)."""
@@ -325,6 +337,11 @@ class Iptables:
 
     def sync_counters(self, stream=None):
         _check(ffi.lib().pcn_ipt_sync_counters(self._h, stream))
+
+    def comm_info(self):
+        """RCCL version and library path, device ordinal and PCI bus id, and the all-gather steps'
+        summed duration on the communicator stream (pcn_ipt_comm_get_info)."""
+        return comm_info(self._h)
 
     def counter_block_words(self, chain):
         """u64 words of `chain`'s counter block [dp, db, p0, b0, ...] (pcn_ipt_counter_block_words)."""

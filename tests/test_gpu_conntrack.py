@@ -3,6 +3,8 @@
 Bit-exact on verdicts, rule ids, per-rule / default / accept-established
 counters and the whole session table (keys, states, sequence numbers, ttl),
 with state carried across batches.  One process, one MI355X (`pytest -m gpu`)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -619,13 +621,20 @@ def test_long_runs_of_colliding_connections(dev):
     """One key bucket holding several long connections (hash collisions): the
     head wave walks them one pass per connection (conntrack.hip PassKeys), and
     past kPassKeys (4) takes the rest as one sequence.  Buckets of 6, 3 and 2
-    colliding TCP/UDP flows of 150 packets each, over three batches that open
+    colliding TCP/UDP flows of 80 packets each, over three batches that open
     them, continue them and close some mid-run.  Bit-exact vs the oracle:
-    verdicts, rule ids, counters, the table (and its LRU stamps' order)."""
+    verdicts, rule ids, counters, the table (and its LRU stamps' order).
+    The batch (880 records) is shorter than a speculative segment cut needs
+    (kSeg = 512 records on both sides), so every bucket is walked by its head
+    wave in passes; the walk's pass counters say that both the per-connection
+    passes and the rest-as-one-sequence walk ran."""
     rng = np.random.default_rng(61)
     rules = CT_RULES + synth.config_rules(2).rules()
     o, ipt = ct_pair({1: rules}, {1: "ACCEPT"}, cap_log2=16, jit=1)
-    per, groups = 150, (6, 3, 2)
+    from polycube_amd import ffi
+    per, groups = 80, (6, 3, 2)
+    stats = (ctypes.c_uint64 * 2)()
+    assert ffi.lib().pcn_ipt_debug_ct_walk_passes(ipt._h, stats, 1) == 0   # reset
     n = per * sum(groups)
     kbits = 8
     while (1 << kbits) < 2 * n:
@@ -653,5 +662,9 @@ def test_long_runs_of_colliding_connections(dev):
         v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, f.reshape(-1), n)
         assert_same(v_o, r_o, v_g, r_g)
         assert_tables(o, ipt)
+        assert ffi.lib().pcn_ipt_debug_ct_walk_passes(ipt._h, stats, 1) == 0
+        # buckets of 6 / 3 / 2 connections: passes for their 2nd-4th / 2nd-3rd / 2nd, and the
+        # 6-bucket's 5th and 6th as one sequence
+        assert stats[0] >= 3 + 2 + 1 and stats[1] >= 1, (k, list(stats))
     assert_counters(o, ipt, n=len(rules) + 1)
     assert_ae(o, ipt)

@@ -519,3 +519,37 @@ def test_stale_ports_ragged_batches(dev, fixed):
         v_o, r_o, v_g, r_g = go(o, ipt, dev, pk)
         assert_same(v_o, r_o, v_g, r_g)
     assert_horus_counters(o, ipt)
+
+
+@pytest.mark.parametrize("fixed", [False, True], ids=["lens", "fixed"])
+def test_stale_groups_stay_inside_their_words(dev, fixed, monkeypatch):
+    """No stale-port group word is written past the n / 64 + 1 words the host
+    holds for a batch (pcn_ipt.cpp sizes them, classify.hip publishes them):
+    guard words past them keep their pattern (pcn_ipt_debug_stale_canary), for
+    n = 100 and 2^20 + 1 on a fresh context, then for smaller batches after the
+    large one with every word past each batch guarded.  The large batch tiles
+    4096 probe packets."""
+    from polycube_amd import ffi
+    monkeypatch.setenv("PCN_IPT_DEBUG_STALE_CANARY", "1")
+    rules = rule_sets()["proto_ports"]
+    rng = np.random.default_rng(17)
+    pk = traffic(rng, 4096, ADDRS, key_ports(rules), rules)[:4096]
+    f0, lens0, ports0, _ = probe_frames(pk)
+    for sizes in ((100,), ((1 << 20) + 1, 100, 193, 64, 1)):
+        o, ipt = setup(rules)
+        for n in sizes:
+            reps = -(-n // 4096)
+            f = np.tile(f0.reshape(4096, -1), (reps, 1))[:n].reshape(-1)
+            lens = np.tile(lens0, reps)[:n]
+            ports = np.tile(ports0, reps)[:n]
+            kw = dict(stride=128, fixed_len=64) if fixed else dict(stride=128, fixed_len=128)
+            lo = {} if fixed else dict(lens=lens)
+            v_o, r_o = o.classify(f, n=n, in_port=ports, **lo, **kw)
+            lg = {} if fixed else dict(lens=torch.from_numpy(lens.view(np.int16)).to(dev))
+            v_g, r_g = ipt.classify(torch.from_numpy(f).to(dev), n=n,
+                                    in_port=torch.from_numpy(ports.view(np.int16)).to(dev), **lg, **kw)
+            torch.cuda.synchronize()
+            assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
+            assert ffi.lib().pcn_ipt_debug_stale_canary(ipt._h) == 0, f"guard word overwritten at n={n}"
+        assert_horus_counters(o, ipt)
+        ipt.close()

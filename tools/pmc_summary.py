@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--traffic", action="store_true")
     ap.add_argument("--frames", type=int, default=1 << 24)
     ap.add_argument("--out", default="")
+    ap.add_argument("--key", default="config3", help="pmc_traffic.json entry: config2 / config3 / config5 / config5_tc")
+    ap.add_argument("--profile", default="", help="where the passes' summaries are committed (profiles/...)")
     a = ap.parse_args()
     s = collect(a.tag_dir)
     if "FETCH_SIZE" in s:
@@ -57,15 +59,27 @@ def main():
         with open(a.out, "w") as fh:
             json.dump(s, fh, indent=1)
     if a.traffic and "FETCH_SIZE" in s:
+        # bench.py reports this entry as roofline.traffic only while the kernel sources
+        # hash the same (bench.kernel_src_hash) and the batch has the same size
+        import sys
+        sys.path.insert(0, ROOT)
+        from bench import kernel_src_hash
         t = {"frames": a.frames, "hbm_bytes_per_launch": round(s["hbm_read_bytes_per_launch"]
                                                                + s.get("hbm_write_bytes_per_launch", 0)),
              "read_bytes": round(s["hbm_read_bytes_per_launch"]),
              "write_bytes": round(s.get("hbm_write_bytes_per_launch", 0)),
-             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over the classify kernel the product runs, "
-                       "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count correction)"}
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
-            json.dump(t, fh, indent=1)
-
+             "read_bytes_per_frame": round(s["hbm_read_bytes_per_launch"] / a.frames, 3),
+             "src_hash": kernel_src_hash(), "profile": a.profile,
+             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over the classify kernel the product "
+                       "runs, FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count correction), WRITE_SIZE KiB x 1024"}
+        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        doc = {}
+        if os.path.exists(path):
+            with open(path) as fh:
+                doc = json.load(fh)
+        doc.setdefault("configs", {})[a.key] = t
+        with open(path, "w") as fh:
+            json.dump({"configs": doc["configs"]}, fh, indent=1)
 
 if __name__ == "__main__":
     main()
