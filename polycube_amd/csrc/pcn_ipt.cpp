@@ -222,6 +222,17 @@ bool debug_stale_canary() {
   return e && *e == '1';
 }
 
+// Measurement knob (tools/ablate.py): PCN_IPT_DEBUG_GRID_CUS=k sizes the
+// classify grid as if the device had k CUs (the grid is min(frames / 1024,
+// CUs x workgroups per CU)).
+int classify_grid_cus(int num_cus) {
+  static const int v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_GRID_CUS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v > 0 ? v : num_cus;
+}
+
 // Add the duration of all-gather step k (its event pair on the communicator
 // stream) to the context's total; waits for it if it is still running.
 void fold_gather_time(pcn_ipt *ctx, int k) {
@@ -1086,7 +1097,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     }
     if (plan) return 0;
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
-    int rc = launch_classify(a, fixed, ch, ns, ctx->num_cus, fn, static_cast<hipStream_t>(stream));
+    int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, static_cast<hipStream_t>(stream));
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
     return 0;
   }

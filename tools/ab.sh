@@ -20,7 +20,7 @@ mkdir -p "$R/gpurun_out"
 PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 STATEFUL="tests/test_gpu_conntrack.py tests/test_gpu_firewall.py tests/test_gpu_flow_split.py"
 
-lib_of() { if [ "$1" = default ]; then echo "$R/polycube_amd/libpcn_ipt.so"; else echo "$R/polycube_amd/ab/libpcn_ipt_ct_$1.so"; fi; }
+lib_of() { if [ "$1" = default ]; then echo "$R/polycube_amd/libpcn_ipt.so"; else echo "$R/polycube_amd/build/ab/libpcn_ipt_ct_$1.so"; fi; }
 
 case $mode in
 tests)

@@ -59,7 +59,9 @@ def child(lib, hit, log2n, iters, cfg, jit):
         b.record()
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    info = fw.info()
     print(json.dumps({"lib": os.path.basename(lib or "product"), "jit": ipt.jit_info()["launches_jit"] > 0,
+                      "cfg": cfg, "log2n": log2n, "image_bytes": info["table_bytes"], "slots_info": info,
                       "defs": os.environ.get("PCN_IPT_JIT_DEFS", ""),
                       "knobs": {k[14:]: v for k, v in os.environ.items() if k.startswith("PCN_IPT_DEBUG_")},
                       "hit": hit, "ms": ms,

@@ -1,0 +1,62 @@
+#!/bin/bash
+# Helpers for one GPU-box session script (source it; run the script through gpurun
+# from the repo root).  Every GPU step runs under its own timeout; `run` ends the
+# session at the first crash, abort or time limit (124/134/137/139) and, unless
+# KEEP_GOING=1, at any failure.  Logs go to gpurun_out/$TAG/.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+TAG=${TAG:-s}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+
+run() {   # run <name> <timeout s> <cmd...>: stdout+stderr -> $O/<name>.log
+  local name=$1 t=$2
+  shift 2
+  local t0=$(date +%s)
+  timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc ($(( $(date +%s) - t0 )) s)"
+  tail -4 "$O/$name.log"
+  case $rc in
+    0) ;;
+    124|134|137|139) echo "fatal rc=$rc in $name: stopping"; exit $rc ;;
+    *) [ "${KEEP_GOING:-0}" = 1 ] || exit $rc ;;
+  esac
+}
+
+pytest_gpu() {   # pytest_gpu <name> <timeout> <pytest args...>
+  local name=$1 t=$2
+  shift 2
+  run "$name" "$t" python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu "$@"
+}
+
+# PMC passes of the classify kernel, one counter group per rocprofv3 run:
+# pmc <name> <cfg> <log2n> [hook]   -> $O/<name>/p1 (FETCH_SIZE), p2 (WRITE_SIZE)
+pmc() {
+  local name=$1 cfg=$2 log2n=$3 hook=${4:-xdp}
+  mkdir -p "$O/$name"
+  local k=0
+  for grp in FETCH_SIZE WRITE_SIZE; do
+    k=$((k + 1))
+    ( cd /tmp && CFG5_HOOK=$hook timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
+        -d "$O/$name/p$k" -o run -- python3 "$R/tools/ablate.py" --child --lib "" --hit 0.5 --iters 5 \
+        --log2n "$log2n" --cfg "$cfg" --jit 1 > "$O/$name/p$k.log" 2>&1 )
+    local rc=$?
+    echo "== pmc $name $grp rc=$rc"
+    case $rc in 0) ;; *) tail -5 "$O/$name/p$k.log"; exit $rc ;; esac
+  done
+}
+
+# kernel trace + stats of one ablate child: ktrace <name> <cfg> <log2n> [iters] [hook]
+ktrace() {
+  local name=$1 cfg=$2 log2n=$3 iters=${4:-50} hook=${5:-xdp}
+  ( cd /tmp && CFG5_HOOK=$hook timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$O/$name" -o run -- python3 "$R/tools/ablate.py" --child --lib "" --hit 0.5 --iters "$iters" \
+      --log2n "$log2n" --cfg "$cfg" --jit 1 > "$O/$name.log" 2>&1 )
+  local rc=$?
+  echo "== ktrace $name rc=$rc"
+  tail -2 "$O/$name.log"
+  case $rc in 0) ;; *) exit $rc ;; esac
+}
