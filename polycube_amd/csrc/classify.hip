@@ -22,6 +22,9 @@
 #endif
 
 #include <cstdint>
+#ifndef __HIPCC_RTC__
+#include <cstdlib>
+#endif
 
 #include "devchain.h"
 #include "pcn_ipt.h"
@@ -438,15 +441,24 @@ __device__ __forceinline__ void pin_regs(u32x4 (&r)[N]) {
   else asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]));
 }
 
+// Two items per worker lane (a deal window of 128 candidates): a wave with
+// more than 64 candidates (hit rate 1) pays one deal pass, not two -- the
+// second item's dependent LDS chain runs in the shadow of the first's.
+// Fixed-stride launches only (their wave region is the 3 KB transpose buffer).
+#ifndef PCN_DEAL2
+#define PCN_DEAL2 0
+#endif
 struct WaveScratch {
-  u32x4 item[64];        // (owner lane << 16 | candidate word, the owner's classes as u16 pairs)
   uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
+  u32x4 item[64];        // (owner lane << 16 | candidate word, the owner's classes as u16 pairs)
 #if !PCN_ITEM_CLS
   u32x4 cls[64];         // each owner's classes
 #endif
 };
 static_assert(sizeof(WaveScratch) <= PCN_WAVE_SCRATCH_BYTES && PCN_WAVE_SCRATCH_BYTES <= PCN_WAVE_LDS_BYTES,
               "scratch fits the per-wave region");
+static_assert(!PCN_DEAL2 || (64 * 4 + 128 * 16 <= PCN_WAVE_LDS_BYTES && PCN_ITEM_CLS),
+              "a 128-item window fits the fixed-stride wave region");
 
 // ---- rule-chain stage, part 2 (whole wave, converged) ----
 // Lanes with `active` AND their class summaries into a candidate-word mask,
@@ -458,9 +470,15 @@ static_assert(sizeof(WaveScratch) <= PCN_WAVE_SCRATCH_BYTES && PCN_WAVE_SCRATCH_
 // owner's class records, ANDs the partial words of its one word and folds the
 // matched entry into the owner's slot with an LDS atomic min.  Returns the
 // owner's best entry.
-template <bool LDS, int NS>
+template <int K>
+struct IntK {
+  static constexpr int value = K;
+};
+
+template <bool LDS, int NS, uint32_t W = 64>
 __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[NS],
                                                      WaveScratch *ws) {
+  static_assert(W == 64 || W == 128, "deal window");
   const uint32_t lane = __lane_id();
   if (__ballot(active) == 0) return kNoRule;
   const Tab<LDS> t{ch.image, ch.lds_image, ch.lds_limit};
@@ -468,69 +486,101 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
   const uint32_t nrw = ch.nrw, nsw = ch.nsw;
   bool staged = false;  // best slots written (only once some lane has a candidate)
   uint64_t mseen = 0;   // PCN_ABLATE == 3 only
+  u32x4 *const items = ws->item;   // W entries (a 128 window runs past the struct into the wave region)
+  // One worker lane's K queued items (K = 2: the second item's chain of
+  // dependent LDS reads issues alongside the first's; a duplicate item is
+  // harmless, its atomicMin repeats the same value).
+  auto work = [&](auto kk, const uint32_t (&idx)[decltype(kk)::value]) {
+    constexpr int K = decltype(kk)::value;
+    u32x4 it[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      if (PCN_ITEM_CLS) {
+        it[q] = items[idx[q]];
+      } else {
+        const uint32_t x = reinterpret_cast<const uint32_t *>(items)[idx[q]];
+#if !PCN_ITEM_CLS
+        it[q] = ws->cls[x >> 16];
+#endif
+        it[q].x = x;
+      }
+    }
+    uint32_t owner[K], w[K], k[K], bit[K], oc[K][NS];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      owner[q] = it[q].x >> 16;
+      w[q] = it[q].x & 0xffff;
+      k[q] = w[q] >> 6;
+      bit[q] = w[q] & 63;
+      const uint32_t packed[3] = {it[q].y, it[q].z, it[q].w};
+#pragma unroll
+      for (int f = 0; f < NS; ++f) oc[q][f] = (packed[f / 2] >> (16 * (f & 1))) & 0xffff;
+    }
+    // At a candidate word every field's summary bit is set, so a field is
+    // PARTIAL there iff its PM bit is set; one 16-byte read gives PM and
+    // PBASE.  Straight-line on purpose: every record read, then every word
+    // read, issue back to back.  A FULL field reads POOL[0], the all-ones
+    // word (indexed PART: through the zero cell, index 0).
+    uint32_t at[K][NS];   // LDS/image offset of each field's u64 word
+    u32x4 recs[K][NS];
+    if (!lay.part_dense) {
+      // all records in flight together: one LDS round trip (left to itself
+      // the compiler recycles two record registers and waits between pairs)
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+#pragma unroll
+        for (int f = 0; f < NS; ++f) recs[q][f] = t.u128(lay.pbase, 16 * (oc[q][f] * nsw + k[q]));
+      if (PCN_REC_PIN && K == 1) pin_regs<NS>(recs[0]);
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      const uint64_t below = (1ull << bit[q]) - 1;
+#pragma unroll
+      for (int f = 0; f < NS; ++f) {
+        if (lay.part_dense) {
+          const uint32_t cell = oc[q][f] * nrw + w[q];
+          at[q][f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
+          continue;
+        }
+        const u32x4 r = recs[q][f];
+        const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;
+        const uint32_t j = r.z + static_cast<uint32_t>(__builtin_popcountll(pm & below));
+        const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit[q]) & 1);   // ~0: partial
+        if (lay.part_direct) {
+          at[q][f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));
+        } else {
+          const bool wide = lay.part_wide;
+          const uint32_t ia = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
+          at[q][f] = lay.pool + 8 * (wide ? t.u32(lay.part, ia - lay.part) : t.u16(lay.part, ia - lay.part));
+        }
+      }
+    }
+    uint64_t acc[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      acc[q] = ~0ull;
+#pragma unroll
+      for (int f = 0; f < NS; ++f) acc[q] &= t.u64(lay.pool, at[q][f] - lay.pool);   // (PART and POOL are on the same side of the limit)
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      if (acc[q]) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
+        const uint32_t e = t.u16(lay.perm, 2 * (w[q] * 63 + static_cast<uint32_t>(__builtin_ctzll(acc[q]))));
+        atomicMin(&ws->best[owner[q]], e);
+      }
+    }
+  };
   // worker side: the first `cnt` queued items
   auto drain = [&](uint32_t cnt) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < cnt) {
-      u32x4 it;
-      if (PCN_ITEM_CLS) {
-        it = ws->item[lane];
-      } else {
-        const uint32_t x = reinterpret_cast<const uint32_t *>(ws->item)[lane];
-#if !PCN_ITEM_CLS
-        it = ws->cls[x >> 16];
-#endif
-        it.x = x;
-      }
-      const uint32_t owner = it.x >> 16, w = it.x & 0xffff, k = w >> 6, bit = w & 63;
-      const uint64_t below = (1ull << bit) - 1;
-      const uint32_t packed[3] = {it.y, it.z, it.w};
-      uint32_t oc[NS];
-#pragma unroll
-      for (int f = 0; f < NS; ++f) oc[f] = (packed[f / 2] >> (16 * (f & 1))) & 0xffff;
-      // At a candidate word every field's summary bit is set, so a field is
-      // PARTIAL there iff its PM bit is set; one 16-byte read gives PM and
-      // PBASE.  Straight-line on purpose: every record read, then every word
-      // read, issue back to back.  A FULL field reads POOL[0], the all-ones
-      // word (indexed PART: through the zero cell, index 0).
-      uint32_t at[NS];   // LDS/image offset of each field's u64 word
-      u32x4 recs[NS];
-      if (!lay.part_dense) {
-        // all NS records in flight together: one LDS round trip (left to
-        // itself the compiler recycles two record registers and waits
-        // between pairs)
-#pragma unroll
-        for (int f = 0; f < NS; ++f) recs[f] = t.u128(lay.pbase, 16 * (oc[f] * nsw + k));
-        if (PCN_REC_PIN) pin_regs<NS>(recs);
-      }
-#pragma unroll
-      for (int f = 0; f < NS; ++f) {
-        if (lay.part_dense) {
-          const uint32_t cell = oc[f] * nrw + w;
-          at[f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
-          continue;
-        }
-        const u32x4 r = recs[f];
-        const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;
-        const uint32_t j = r.z + static_cast<uint32_t>(__builtin_popcountll(pm & below));
-        const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit) & 1);   // ~0: partial
-        if (lay.part_direct) {
-          at[f] = lay.pool + (part_mask & (lay.part + 8 * j - lay.pool));
-        } else {
-          const bool wide = lay.part_wide;
-          const uint32_t ia = lay.zero + (part_mask & (lay.part + (wide ? 4 * j : 2 * j) - lay.zero));
-          at[f] = lay.pool + 8 * (wide ? t.u32(lay.part, ia - lay.part) : t.u16(lay.part, ia - lay.part));
-        }
-      }
-      uint64_t acc = ~0ull;
-#pragma unroll
-      for (int f = 0; f < NS; ++f) acc &= t.u64(lay.pool, at[f] - lay.pool);   // (PART and POOL are on the same side of the limit)
-      if (acc) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
-        const uint32_t e = t.u16(lay.perm, 2 * (w * 63 + static_cast<uint32_t>(__builtin_ctzll(acc))));
-        atomicMin(&ws->best[owner], e);
-      }
+    if (W > 64 && cnt > 64) {        // wave-uniform: two items per lane
+      const uint32_t idx[2] = {lane, lane + 64 < cnt ? lane + 64 : lane};
+      work(IntK<2>{}, idx);
+    } else if (lane < cnt) {
+      const uint32_t idx[1] = {lane};
+      work(IntK<1>{}, idx);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -545,7 +595,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     mine.z = pk[1];
     mine.w = pk[2];
   }
-  uint32_t qn = 0;      // items queued, not yet dealt (wave-uniform, < 64)
+  uint32_t qn = 0;      // items queued, not yet dealt (wave-uniform, < W)
   for (uint32_t k = 0; k < nsw; ++k) {
     const uint32_t live = nrw - k * 64;
     uint64_t m = 0;
@@ -578,23 +628,23 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
 #endif
     }
     // this block's items go to queue positions [qn, qn + total): each owner
-    // writes those that fall in the current window of 64, which is dealt
+    // writes those that fall in the current window of W, which is dealt
     // when it is full or after the last block (one call site: a chain of one
     // block runs the code of a plain per-block deal)
     uint32_t p = qn + pos, end = qn + total;
     for (;;) {
-      while (m && p < 64) {
+      while (m && p < W) {
         mine.x = (lane << 16) | (k * 64 + static_cast<uint32_t>(__builtin_ctzll(m)));
-        if (PCN_ITEM_CLS) ws->item[p] = mine;
-        else reinterpret_cast<uint32_t *>(ws->item)[p] = mine.x;
+        if (PCN_ITEM_CLS) items[p] = mine;
+        else reinterpret_cast<uint32_t *>(items)[p] = mine.x;
         m &= m - 1;
         ++p;
       }
-      if (end < 64 && !last_block) { qn = end; break; }
-      drain(end < 64 ? end : 64u);
-      if (end <= 64) { qn = 0; break; }
-      p -= 64;
-      end -= 64;
+      if (end < W && !last_block) { qn = end; break; }
+      drain(end < W ? end : W);
+      if (end <= W) { qn = 0; break; }
+      p -= W;
+      end -= W;
     }
   }
   if (PCN_ABLATE == 3) return mseen ? 0u : kNoRule;
@@ -612,7 +662,7 @@ __device__ __forceinline__ uint32_t chain_finish(const DevChain &ch, uint32_t be
 
 // One chain through the three parts; `mine` = lanes whose packet runs it.
 // Called with the wave converged.
-template <bool LDS, int NS>
+template <bool LDS, int NS, uint32_t W = 64>
 __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const Parsed &p, uint32_t port,
                                           WaveScratch *ws, uint32_t &verdict, int32_t &rid) {
   uint32_t cls[NS];
@@ -620,7 +670,7 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
   if (mine) need = chain_classes<LDS, NS>(ch, p, port, cls, verdict, rid);
   // the wave gets issue priority while it deals candidates through LDS
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(PCN_CAND_PRIO >= 0 ? PCN_CAND_PRIO : 0);
-  const uint32_t best = chain_candidates<LDS, NS>(ch, need, cls, ws);
+  const uint32_t best = chain_candidates<LDS, NS, W>(ch, need, cls, ws);
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(0);
   if (need) verdict = chain_finish(ch, best, rid);
 }
@@ -651,6 +701,7 @@ __device__ __forceinline__ DevChain chain_desc(const LaunchArgs &a) {
 template <bool FIXED, bool LDS, int CH, int NS, bool JIT>
 __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   const DevChain run_ch = chain_desc<JIT, CH>(a);   // the chain that runs rules (CH < 3)
+  constexpr uint32_t kDealW = PCN_DEAL2 && FIXED ? 128 : 64;   // candidate deal window
   // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
   // frames per workgroup so neither can wrap; the flush widens to u64)
   uint32_t *bins = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);
@@ -1113,15 +1164,15 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
     if (CH < 3) {
-      run_chain<LDS, NS>(run_ch, chain >= 0, p, port, ws, verdict, rid);
+      run_chain<LDS, NS, kDealW>(run_ch, chain >= 0, p, port, ws, verdict, rid);
       if (chain >= 0) cchain = chain;
     } else {
       if (__ballot(chain == PCN_IPT_FORWARD)) {
-        run_chain<LDS, NS>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, verdict, rid);
+        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, verdict, rid);
         if (chain == PCN_IPT_FORWARD) cchain = PCN_IPT_FORWARD;
       }
       if (__ballot(chain == PCN_IPT_INPUT)) {
-        run_chain<LDS, NS>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, verdict, rid);
+        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, verdict, rid);
         if (chain == PCN_IPT_INPUT) cchain = PCN_IPT_INPUT;
       }
     }
@@ -1191,8 +1242,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
           else atomicAdd(&bins[b], 1u);
           if (!FIXED) atomicAdd(&byte_bins[b], L);
         } else {
-          atomicAdd(&ch.ctr[2 + 2 * rid], 1ull);
-          atomicAdd(&ch.ctr[3 + 2 * rid], static_cast<unsigned long long>(L));
+          unsigned long long *const cr = ch.ctr + (blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;
+          atomicAdd(&cr[2 + 2 * rid], 1ull);
+          atomicAdd(&cr[3 + 2 * rid], static_cast<unsigned long long>(L));
         }
       }
     }
@@ -1235,6 +1287,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // starts at its own rotation of the bins so the global atomics of
   // concurrent flushes mostly land on different addresses.
   const uint32_t rot = PCN_FLUSH_ROT ? (blockIdx.x * 97u) % a.nbins : 0u;
+  const uint64_t rep = static_cast<uint64_t>(blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;   // this copy
   for (uint32_t b0 = threadIdx.x; b0 < a.nbins; b0 += blockDim.x) {
     const uint32_t b = b0 + rot < a.nbins ? b0 + rot : b0 + rot - a.nbins;
     const unsigned long long pk = bins[b];
@@ -1242,14 +1295,14 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     if (!pk) continue;
     unsigned long long *dst = nullptr;
     if (b < 3) {
-      dst = a.ch[b].ctr;
+      dst = a.ch[b].ctr + rep;
     } else {
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const DevChain &ch = c == CH ? run_ch : a.ch[c];
         if (ch.lds_bins >= 0 && b >= static_cast<uint32_t>(ch.lds_bins) &&
             b < static_cast<uint32_t>(ch.lds_bins) + ch.lds_nrules)
-          dst = ch.ctr + 2 + 2 * (b - static_cast<uint32_t>(ch.lds_bins));
+          dst = ch.ctr + rep + 2 + 2 * (b - static_cast<uint32_t>(ch.lds_bins));
       }
       if (a.hz_bins >= 0 && b >= static_cast<uint32_t>(a.hz_bins) && a.horus_ctr)
         dst = a.horus_ctr + 2 * (b - static_cast<uint32_t>(a.hz_bins));
@@ -1305,7 +1358,12 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
   if (a.n == 0) return hipSuccess;
   const size_t lds = a.lds_bytes;
   const bool in_lds = a.lds_images_bytes > 0;
-  const size_t max_per_cu = 2048 / kBlock;   // 32 waves per CU
+  // (PCN_IPT_DEBUG_WG_PER_CU: measurement A/B of the workgroups per CU)
+  static const size_t max_per_cu = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_WG_PER_CU");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return v >= 1 && v <= 2 ? static_cast<size_t>(v) : size_t(2048 / kBlock);   // 32 waves per CU
+  }();
   size_t per_cu = lds ? (160 * 1024) / lds : max_per_cu;
   if (per_cu > max_per_cu) per_cu = max_per_cu;
   if (per_cu < 1) per_cu = 1;
@@ -1352,6 +1410,26 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
     if (e != hipSuccess) return static_cast<int>(e);
   }
   return hipSuccess;
+}
+
+// Fold counter copies 1..reps-1 into copy 0 and zero them (LaunchArgs::ctr_rep_mask).
+__global__ void fold_reps_kernel(unsigned long long *ctr, uint64_t words, uint64_t stride, uint32_t reps) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= words) return;
+  // atomics: a classify on another stream may be adding to the copies meanwhile
+  unsigned long long s = 0;
+  for (uint32_t r = 1; r < reps; ++r) {
+    unsigned long long *p = ctr + r * stride + i;
+    if (*p) s += atomicExch(p, 0ull);
+  }
+  if (s) atomicAdd(&ctr[i], s);
+}
+
+int launch_fold_reps(unsigned long long *ctr, uint64_t words, uint64_t stride, uint32_t reps, hipStream_t stream) {
+  if (reps <= 1 || words == 0) return hipSuccess;
+  const unsigned grid = static_cast<unsigned>((words + 255) / 256);
+  hipLaunchKernelGGL(fold_reps_kernel, dim3(grid), dim3(256), 0, stream, ctr, words, stride, reps);
+  return static_cast<int>(hipGetLastError());
 }
 
 // Sum `nranks` gathered counter blocks into `out` (u64 element-wise).

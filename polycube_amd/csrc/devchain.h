@@ -188,6 +188,13 @@ struct LaunchArgs {
   uint32_t stale_epoch;          // this batch's publication epoch (24 bits, never 0)
   uint32_t *carry_out;           // non-null on a batch's last launch: its last workgroup writes the
                                  // ports the batch leaves to the next one (the carry, Q4)
+  // Counter replicas: workgroup b adds its counters into the copy of every
+  // chain's block at ch[c].ctr + (b & ctr_rep_mask) * ctr_rep_words; the host
+  // folds the copies into copy 0 before it reads a block (pcn_ipt.cpp).
+  // Workgroups of a short launch finish together, and their flushes, all on
+  // one block, serialised on the same few lines.
+  uint32_t ctr_rep_mask;         // copies - 1 (a power of two; 0: one copy)
+  uint32_t ctr_rep_words;        // u64 words between copies
 };
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)

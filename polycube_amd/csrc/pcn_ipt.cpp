@@ -30,6 +30,7 @@ namespace pcn {
 int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream);
 int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint64_t count, int nranks,
                      hipStream_t stream);
+int launch_fold_reps(unsigned long long *ctr, uint64_t words, uint64_t stride, uint32_t reps, hipStream_t stream);
 }  // namespace pcn
 
 namespace pcn {
@@ -152,6 +153,7 @@ struct pcn_ipt {
   bool has_device = false;
   int num_cus = 256;
   size_t ctr_words = 0;
+  uint32_t ctr_reps = 1;                       // counter copies per chain (LaunchArgs::ctr_rep_mask)
   ncclComm_t comm = nullptr;
   // the counter all-gather runs on its own stream, off the classify stream's
   // critical path: the classify stream only snapshots the counters
@@ -248,6 +250,22 @@ uint32_t counted(const pcn_ipt *ctx, uint32_t nrules) {
   return std::min(nrules, ctx->cfg.max_counted_rules);
 }
 
+// Counter copies per chain block (LaunchArgs::ctr_rep_mask): 16, or
+// PCN_IPT_DEBUG_CTR_REPS (a power of two, measurement A/B).
+uint32_t ctr_reps_default() {
+  const char *e = std::getenv("PCN_IPT_DEBUG_CTR_REPS");
+  const long v = e ? std::strtol(e, nullptr, 10) : 16;
+  return v >= 1 && v <= 256 && (v & (v - 1)) == 0 ? static_cast<uint32_t>(v) : 16u;
+}
+
+// Fold a chain's counter copies 1.. into copy 0 (= cs.ctr), stream-ordered;
+// every read, snapshot or clear of a block does this first.
+void fold_counters(pcn_ipt *ctx, const ChainState &cs, size_t words, hipStream_t s) {
+  if (ctx->ctr_reps <= 1 || !cs.ctr) return;
+  const int rc = launch_fold_reps(cs.ctr, words, ctx->ctr_words, ctx->ctr_reps, s);
+  if (rc != hipSuccess) throw HipError(std::string("counter fold: ") + hipGetErrorString(hipError_t(rc)));
+}
+
 // Upload a compiled chain into the inactive slot, then flip (Chain.cpp:441-457,924).
 void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
   ChainState &cs = ctx->chains[chain];
@@ -283,6 +301,7 @@ void load_tables(pcn_ipt *ctx, int chain, ChainTables tables) {
               "hipMemcpy(chain tables)");
     // a new ActionLookup program starts with zeroed per-rule counters; the
     // default counters live in shared maps and persist (Iptables_Parser_dp.c:47-58)
+    fold_counters(ctx, cs, ctx->ctr_words, nullptr);
     hip_check(hipMemset(cs.ctr + 2, 0, (ctx->ctr_words - 2) * sizeof(unsigned long long)),
               "hipMemset(counters)");
     d.image = static_cast<const uint8_t *>(s.tables);
@@ -328,6 +347,7 @@ void fetch_stats(pcn_ipt *ctx, int chain) {
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   uint32_t n = counted(ctx, cs.desc.nrules);
   std::vector<unsigned long long> buf(2 + 2 * size_t(n));
+  fold_counters(ctx, cs, buf.size(), nullptr);
   hip_check(hipMemcpy(buf.data(), cs.ctr, buf.size() * 8, hipMemcpyDeviceToHost), "hipMemcpy(counters)");
   for (uint32_t id = 0; id < n && id < cs.stats.size(); ++id) {
     cs.stats[id].first += buf[2 + 2 * id];
@@ -543,6 +563,7 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
   if (ctx->cfg.max_rules > 32767) return fail(-EINVAL, "max_rules > 32767");
   if (ctx->cfg.jit < -1 || ctx->cfg.jit > 1) return fail(-EINVAL, "jit must be -1, 0 or 1");
   ctx->ctr_words = 2 + 2 * size_t(ctx->cfg.max_counted_rules);
+  ctx->ctr_reps = ctr_reps_default();
   if (cfg->device >= 0) {
     try {
       int ndev = 0;
@@ -569,8 +590,8 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
       hip_check(hipMalloc(&ctx->d_hz_carry, 64), "hipMalloc(horus carry)");
       hip_check(hipMemset(ctx->d_hz_carry, 0, 64), "hipMemset(horus carry)");
       for (auto &cs : ctx->chains) {
-        hip_check(hipMalloc(&cs.ctr, ctx->ctr_words * 8), "hipMalloc(counters)");
-        hip_check(hipMemset(cs.ctr, 0, ctx->ctr_words * 8), "hipMemset(counters)");
+        hip_check(hipMalloc(&cs.ctr, ctx->ctr_reps * ctx->ctr_words * 8), "hipMalloc(counters)");
+        hip_check(hipMemset(cs.ctr, 0, ctx->ctr_reps * ctx->ctr_words * 8), "hipMemset(counters)");
         hip_check(hipMalloc(&cs.ctr_global, ctx->ctr_words * 8), "hipMalloc(counters)");
         hip_check(hipMemset(cs.ctr_global, 0, ctx->ctr_words * 8), "hipMemset(counters)");
       }
@@ -983,6 +1004,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.rule_ids = sa ? sa->rule_ids : b->rule_ids;
     if (sa)
       for (int c = 0; c < PCN_IPT_NCHAINS; ++c) a.ch[c].ctr = ctx->ctr_scratch + c * ctx->ctr_words;
+    a.ctr_rep_mask = sa ? 0u : ctx->ctr_reps - 1;   // (stage A's scratch counters are one copy)
+    a.ctr_rep_words = static_cast<uint32_t>(ctx->ctr_words);
     a.localip = ctx->d_localip;
     a.n = b->n;
     a.stride = b->stride;
@@ -1205,6 +1228,8 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       // `serial`): the accept-established counter move is an atomic exchange
       // and add on d_ae, so interleaved batches neither lose nor double counts.
       device_guard(ctx);
+      for (int c = 0; c < PCN_IPT_NCHAINS; ++c)   // rule 0's counts, wherever the flushes put them
+        if ((ae_mask >> c) & 1) fold_counters(ctx, ctx->chains[c], 4, st);
       const int e = ct_ae_fixup(ct_batch(ctx, b, ae_mask), st);
       if (e != hipSuccess) return fail(-EIO, std::string("accept-established fixup: ") + hipGetErrorString(hipError_t(e)));
       return mark();
@@ -1325,6 +1350,7 @@ int pcn_ipt_read_counters(pcn_ipt *ctx, int chain, uint64_t *pkts, uint64_t *byt
     if (ctx->has_device) {
       device_guard(ctx);
       hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      fold_counters(ctx, cs, ctx->ctr_words, nullptr);
       hip_check(hipMemcpy(buf.data(), scope ? cs.ctr_global : cs.ctr, buf.size() * 8, hipMemcpyDeviceToHost),
                 "hipMemcpy(counters)");
     }
@@ -1370,6 +1396,7 @@ int pcn_ipt_chain_reset_counters(pcn_ipt *ctx, int chain) {
       hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
       // pcn-firewall also flushes the DefaultAction counters (pcn-firewall Chain.cpp:154-155)
       const size_t from = ctx->service == PCN_IPT_SERVICE_FIREWALL ? 0 : 2;
+      fold_counters(ctx, cs, ctx->ctr_words, nullptr);
       hip_check(hipMemset(cs.ctr + from, 0, (ctx->ctr_words - from) * 8), "hipMemset(counters)");
       // ... and the chain's Horus counters of its rule ids (pcn-firewall Chain.cpp:139-152)
       const int k = horus_slot(ctx, chain);
@@ -1423,9 +1450,11 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
     device_guard(ctx);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (!ctx->comm) {
-      for (auto &cs : ctx->chains)
+      for (auto &cs : ctx->chains) {
+        fold_counters(ctx, cs, ctx->ctr_words, s);
         hip_check(hipMemcpyAsync(cs.ctr_global, cs.ctr, ctx->ctr_words * 8, hipMemcpyDeviceToDevice, s),
                   "hipMemcpyAsync(counters)");
+      }
       return 0;
     }
     // The classify stream snapshots each chain's live prefix (defaults +
@@ -1437,6 +1466,7 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
     for (int c = 0; c < PCN_IPT_NCHAINS; ++c) {
       ChainState &cs = ctx->chains[c];
       count[c] = 2 + 2 * size_t(cs.desc.ncounted);
+      fold_counters(ctx, cs, count[c], s);
       hip_check(hipMemcpyAsync(cs.stage, cs.ctr, count[c] * 8, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(stage)");
     }
     hip_check(hipEventRecord(ctx->ev_staged, s), "hipEventRecord");
@@ -1538,6 +1568,7 @@ int pcn_ipt_snapshot_counters(pcn_ipt *ctx, int chain, uint64_t *block, void *st
     device_guard(ctx);
     ChainState &cs = ctx->chains[chain];
     const size_t words = 2 + 2 * size_t(cs.desc.ncounted);
+    fold_counters(ctx, cs, words, static_cast<hipStream_t>(stream));
     hip_check(hipMemcpyAsync(block, cs.ctr, words * 8, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)),
               "hipMemcpyAsync(snapshot)");
     return 0;
