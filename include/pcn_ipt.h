@@ -255,7 +255,13 @@ typedef struct {
   uint16_t const_in_port;
   uint16_t direction;     /* PCN_IPT_INGRESS / PCN_IPT_EGRESS */
   uint16_t hook;          /* PCN_IPT_HOOK_XDP / PCN_IPT_HOOK_TC */
-  uint16_t reserved2;
+  /* Header-only transfer (fixed stride only): 0 copies whole frames; else only
+   * the first hdr_bytes of each frame cross PCIe (a strided copy into a
+   * hdr_bytes-stride device batch), fixed_len / lens still give the frames'
+   * lengths.  A multiple of 16, <= stride, and at least what the classify
+   * path reads: 48 at the XDP hook, 64 at the TC hook (an outer VLAN tag
+   * shifts the window), 80 with the connection table on (ICMP quoted headers). */
+  uint16_t hdr_bytes;
 } pcn_ipt_ring_batch;
 int pcn_ipt_ring_create(pcn_ipt *ctx, const pcn_ipt_ring_config *cfg, pcn_ipt_ring **out);
 void pcn_ipt_ring_destroy(pcn_ipt_ring *ring);

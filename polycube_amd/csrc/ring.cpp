@@ -171,11 +171,23 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   if (b->n > r->cfg.slot_frames) return ring_fail(-EINVAL, "more frames than the slot holds");
   const uint64_t bytes = b->frames_bytes ? b->frames_bytes : b->n * uint64_t(b->stride);
   if (bytes > r->cfg.slot_bytes) return ring_fail(-EINVAL, "frame bytes exceed the slot");
+  const uint32_t hb = b->hdr_bytes;
+  if (hb) {
+    pcn_ipt_ct_info ci{};
+    const bool ct = pcn_ipt_ct_get_info(r->ctx, &ci) == 0 && ci.enabled;
+    const uint32_t need = ct ? 80u : b->hook == PCN_IPT_HOOK_TC ? 64u : 48u;
+    if (b->use_offsets) return ring_fail(-EINVAL, "a header-only transfer needs a fixed stride");
+    if (hb % 16 || hb > b->stride || hb < need)
+      return ring_fail(-EINVAL, "hdr_bytes must be a multiple of 16, <= stride and >= " + std::to_string(need));
+  }
   if (hipSetDevice(r->device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
   hipStream_t st = r->streams[slot % r->streams.size()];
   const size_t n = b->n;
-  // PCIe in: frames and the per-frame arrays the batch uses
-  bool ok = hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+  // PCIe in: frames (or their first hb bytes: a strided copy, hb-byte rows
+  // packed on the device) and the per-frame arrays the batch uses
+  bool ok = hb ? hipMemcpy2DAsync(s.d_frames, hb, s.h_frames, b->stride, hb, n, hipMemcpyHostToDevice, st) ==
+                     hipSuccess
+               : hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
   if (ok && b->use_offsets) ok = hipMemcpyAsync(s.d_offsets, s.h_offsets, 4 * n, hipMemcpyHostToDevice, st) == hipSuccess;
   if (ok && b->use_lens) ok = hipMemcpyAsync(s.d_lens, s.h_lens, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
   if (ok && b->use_in_port) ok = hipMemcpyAsync(s.d_in_port, s.h_in_port, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
@@ -189,10 +201,10 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   if (!ok) return quiesce(-EIO, "hipMemcpyAsync (H2D) failed");
   pcn_ipt_batch batch{};
   batch.frames = s.d_frames;
-  batch.frames_bytes = bytes;
+  batch.frames_bytes = hb ? n * hb : bytes;
   batch.offsets = b->use_offsets ? s.d_offsets : nullptr;
   batch.lens = b->use_lens ? s.d_lens : nullptr;
-  batch.stride = b->stride;
+  batch.stride = hb ? hb : b->stride;
   batch.fixed_len = b->fixed_len;
   batch.in_port = b->use_in_port ? s.d_in_port : nullptr;
   batch.const_in_port = b->const_in_port;

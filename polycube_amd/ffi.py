@@ -68,7 +68,7 @@ class RingBatch(C.Structure):
     _fields_ = [("n", C.c_uint64), ("frames_bytes", C.c_uint64), ("stride", C.c_uint32), ("fixed_len", C.c_uint32),
                 ("use_offsets", C.c_uint8), ("use_lens", C.c_uint8), ("use_in_port", C.c_uint8),
                 ("reserved", C.c_uint8), ("const_in_port", C.c_uint16), ("direction", C.c_uint16),
-                ("hook", C.c_uint16), ("reserved2", C.c_uint16)]
+                ("hook", C.c_uint16), ("hdr_bytes", C.c_uint16)]
 
 
 class ChainInfo(C.Structure):

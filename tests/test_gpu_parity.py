@@ -384,6 +384,46 @@ def test_ingest_ring_parity(dev):
     assert_counters(o, ipt)
 
 
+@pytest.mark.parametrize("hook,hdr", [(0, 48), (1, 64)], ids=["xdp48", "tc64"])
+def test_ingest_ring_header_only(dev, hook, hdr):
+    """pcn_ipt_ring_batch.hdr_bytes: only each frame's first hdr bytes cross
+    PCIe (a strided copy, packed on the device) while the lengths still come
+    from fixed_len / lens: equal to the oracle on the whole frames.  64-byte
+    frames at a 64-byte stride (the bench's slots, the fixed-stride kernel),
+    fuzz frames (every protocol, edge lengths) at a 96-byte stride and up to
+    1536-byte frames; too few header bytes and offsets batches are refused."""
+    from polycube_amd import IptablesError
+    rs = synth.config_rules(3)
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
+    ring = ipt.ring(slots=2, slot_frames=1 << 13, slot_bytes=(1 << 13) * 1536, rule_ids=True)
+    for k, stride in enumerate((64, 96, 1536)):
+        slot, frames, offsets, lens, in_port = ring.acquire()
+        n = (1 << 13) - 5 * k
+        if stride == 64:
+            f = synth.config_frames(3, n, rs, seed=k).reshape(-1)
+            ln, kw = None, {}
+        else:
+            f, ln = synth.fuzz_frames(n, 70 + k, rs, stride=stride)
+            f = f.reshape(-1)
+            lens[:n] = ln
+            kw = dict(lens=True)
+        frames[:f.size] = f
+        ring.submit(slot, n, stride=stride, fixed_len=stride, hook=hook, hdr_bytes=hdr, **kw)
+        v_o, r_o = o.classify(f, n=n, lens=ln, stride=stride, fixed_len=stride, hook=hook, nthreads=NTHREADS)
+        done, v, r = ring.complete()
+        assert done == slot
+        assert_same(v_o, r_o, v.copy(), r.copy())
+        ring.release(done)
+    slot = ring.acquire()[0]
+    for bad in (dict(hdr_bytes=hdr - 16), dict(hdr_bytes=hdr + 8), dict(hdr_bytes=hdr, offsets=True)):
+        with pytest.raises(IptablesError) as e:
+            ring.submit(slot, 16, stride=128, fixed_len=128, hook=hook, **bad)
+        assert e.value.code == -22
+    ring.release(slot)
+    ring.close()
+    assert_counters(o, ipt)
+
+
 @JIT
 def test_ragged_batch_sizes_fixed_stride(dev, jit):
     """Batches that end inside a wave's 64-frame group and inside a workgroup's
