@@ -37,7 +37,8 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 // Measurement-only ablation builds (tools/ablate.py; never the product .so):
 // 1 parse only, 2 + field lookups, 3 + summary AND, 4 full minus counters,
 // 5 full minus the end-of-launch counter flush, 6 full minus the per-rule
-// counter bins, 7 per-rule bins by plain stores (wrong counts; cost of the atomic).
+// counter bins, 7 per-rule bins by plain stores (wrong counts; cost of the atomic),
+// 8 full minus the global atomics of the rule ids past the LDS bins.
 #ifndef PCN_ABLATE
 #define PCN_ABLATE 0
 #endif
@@ -124,6 +125,7 @@ constexpr uint32_t kHashMul = 0x9E3779B1u;
 constexpr uint32_t kNoRule = 0xFFFFFFFFu;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 #ifndef PCN_HDR_ASM_MEM
 #define PCN_HDR_ASM_MEM 0   // 1: the asm chunk loads ordered against the compiler's memory operations (A/B: slower)
 #endif
@@ -162,6 +164,7 @@ struct Tab {
   __device__ __forceinline__ uint32_t u8(uint32_t tbl, uint32_t off) const { return ld<uint8_t>(tbl, off); }
   __device__ __forceinline__ uint64_t u64(uint32_t tbl, uint32_t off) const { return ld<uint64_t>(tbl, off); }
   __device__ __forceinline__ u32x4 u128(uint32_t tbl, uint32_t off) const { return ld<u32x4>(tbl, off); }
+  __device__ __forceinline__ u32x3 u96(uint32_t tbl, uint32_t off) const { return ld<u32x3>(tbl, off); }
 };
 
 // Header window as little-endian dwords: bytes 0..47 (the fixed-stride path)
@@ -444,10 +447,12 @@ __device__ __forceinline__ void pin_regs(u32x4 (&r)[N]) {
 // Two items per worker lane (a deal window of 128 candidates): a wave with
 // more than 64 candidates (hit rate 1) pays one deal pass, not two -- the
 // second item's dependent LDS chain runs in the shadow of the first's.
-// Fixed-stride launches only (their wave region is the 3 KB transpose buffer).
+// 1: fixed-stride launches (their wave region is the 3 KB transpose buffer);
+// 2: every launch whose wave region holds the 128 items (LaunchArgs::wave_bytes).
 #ifndef PCN_DEAL2
 #define PCN_DEAL2 0
 #endif
+constexpr uint32_t kDeal2Bytes = 64 * 4 + 128 * 16;   // best[64] + item[128]
 struct WaveScratch {
   uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
   u32x4 item[64];        // (owner lane << 16 | candidate word, the owner's classes as u16 pairs)
@@ -457,7 +462,7 @@ struct WaveScratch {
 };
 static_assert(sizeof(WaveScratch) <= PCN_WAVE_SCRATCH_BYTES && PCN_WAVE_SCRATCH_BYTES <= PCN_WAVE_LDS_BYTES,
               "scratch fits the per-wave region");
-static_assert(!PCN_DEAL2 || (64 * 4 + 128 * 16 <= PCN_WAVE_LDS_BYTES && PCN_ITEM_CLS),
+static_assert(!PCN_DEAL2 || (kDeal2Bytes <= PCN_WAVE_LDS_BYTES && PCN_ITEM_CLS),
               "a 128-item window fits the fixed-stride wave region");
 
 // ---- rule-chain stage, part 2 (whole wave, converged) ----
@@ -475,10 +480,13 @@ struct IntK {
   static constexpr int value = K;
 };
 
-template <bool LDS, int NS, uint32_t W = 64>
+template <bool LDS, int NS, uint32_t WMAX = 64>
 __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[NS],
-                                                     WaveScratch *ws) {
-  static_assert(W == 64 || W == 128, "deal window");
+                                                     WaveScratch *ws, uint32_t wave_bytes) {
+  static_assert(WMAX == 64 || WMAX == 128, "deal window");
+  // the window: 128 items when the build has the two-item workers and the
+  // wave's LDS region holds them (wave-uniform), else 64
+  const uint32_t W = WMAX > 64 && wave_bytes >= kDeal2Bytes ? 128u : 64u;
   const uint32_t lane = __lane_id();
   if (__ballot(active) == 0) return kNoRule;
   const Tab<LDS> t{ch.image, ch.lds_image, ch.lds_limit};
@@ -522,15 +530,14 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     // read, issue back to back.  A FULL field reads POOL[0], the all-ones
     // word (indexed PART: through the zero cell, index 0).
     uint32_t at[K][NS];   // LDS/image offset of each field's u64 word
-    u32x4 recs[K][NS];
+    u32x3 recs[K][NS];    // {PM lo, PM hi, PBASE} (the record's 4th dword is padding)
     if (!lay.part_dense) {
       // all records in flight together: one LDS round trip (left to itself
       // the compiler recycles two record registers and waits between pairs)
 #pragma unroll
       for (int q = 0; q < K; ++q)
 #pragma unroll
-        for (int f = 0; f < NS; ++f) recs[q][f] = t.u128(lay.pbase, 16 * (oc[q][f] * nsw + k[q]));
-      if (PCN_REC_PIN && K == 1) pin_regs<NS>(recs[0]);
+        for (int f = 0; f < NS; ++f) recs[q][f] = t.u96(lay.pbase, 16 * (oc[q][f] * nsw + k[q]));
     }
 #pragma unroll
     for (int q = 0; q < K; ++q) {
@@ -542,7 +549,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
           at[q][f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
           continue;
         }
-        const u32x4 r = recs[q][f];
+        const u32x3 r = recs[q][f];
         const uint64_t pm = static_cast<uint64_t>(r.y) << 32 | r.x;
         const uint32_t j = r.z + static_cast<uint32_t>(__builtin_popcountll(pm & below));
         const uint32_t part_mask = 0u - static_cast<uint32_t>((pm >> bit[q]) & 1);   // ~0: partial
@@ -575,7 +582,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (W > 64 && cnt > 64) {        // wave-uniform: two items per lane
+    if (WMAX > 64 && cnt > 64) {     // wave-uniform: two items per lane
       const uint32_t idx[2] = {lane, lane + 64 < cnt ? lane + 64 : lane};
       work(IntK<2>{}, idx);
     } else if (lane < cnt) {
@@ -664,13 +671,13 @@ __device__ __forceinline__ uint32_t chain_finish(const DevChain &ch, uint32_t be
 // Called with the wave converged.
 template <bool LDS, int NS, uint32_t W = 64>
 __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const Parsed &p, uint32_t port,
-                                          WaveScratch *ws, uint32_t &verdict, int32_t &rid) {
+                                          WaveScratch *ws, uint32_t wave_bytes, uint32_t &verdict, int32_t &rid) {
   uint32_t cls[NS];
   bool need = false;
   if (mine) need = chain_classes<LDS, NS>(ch, p, port, cls, verdict, rid);
   // the wave gets issue priority while it deals candidates through LDS
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(PCN_CAND_PRIO >= 0 ? PCN_CAND_PRIO : 0);
-  const uint32_t best = chain_candidates<LDS, NS, W>(ch, need, cls, ws);
+  const uint32_t best = chain_candidates<LDS, NS, W>(ch, need, cls, ws, wave_bytes);
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(0);
   if (need) verdict = chain_finish(ch, best, rid);
 }
@@ -701,7 +708,7 @@ __device__ __forceinline__ DevChain chain_desc(const LaunchArgs &a) {
 template <bool FIXED, bool LDS, int CH, int NS, bool JIT>
 __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   const DevChain run_ch = chain_desc<JIT, CH>(a);   // the chain that runs rules (CH < 3)
-  constexpr uint32_t kDealW = PCN_DEAL2 && FIXED ? 128 : 64;   // candidate deal window
+  constexpr uint32_t kDealW = PCN_DEAL2 >= 2 || (PCN_DEAL2 && FIXED) ? 128 : 64;   // candidate deal window (max)
   // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
   // frames per workgroup so neither can wrap; the flush widens to u64)
   uint32_t *bins = reinterpret_cast<uint32_t *>(pcn_smem + a.bins_offset);
@@ -1164,15 +1171,15 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
     if (CH < 3) {
-      run_chain<LDS, NS, kDealW>(run_ch, chain >= 0, p, port, ws, verdict, rid);
+      run_chain<LDS, NS, kDealW>(run_ch, chain >= 0, p, port, ws, a.wave_bytes, verdict, rid);
       if (chain >= 0) cchain = chain;
     } else {
       if (__ballot(chain == PCN_IPT_FORWARD)) {
-        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, verdict, rid);
+        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, a.wave_bytes, verdict, rid);
         if (chain == PCN_IPT_FORWARD) cchain = PCN_IPT_FORWARD;
       }
       if (__ballot(chain == PCN_IPT_INPUT)) {
-        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, verdict, rid);
+        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, a.wave_bytes, verdict, rid);
         if (chain == PCN_IPT_INPUT) cchain = PCN_IPT_INPUT;
       }
     }
@@ -1241,7 +1248,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
           if (PCN_ABLATE == 7) bins[b] = 1u;   // measurement: a plain store instead of the atomic
           else atomicAdd(&bins[b], 1u);
           if (!FIXED) atomicAdd(&byte_bins[b], L);
-        } else {
+        } else if (PCN_ABLATE != 8) {   // (8: measurement, no global atomics for the ids past the bins)
           unsigned long long *const cr = ch.ctr + (blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;
           atomicAdd(&cr[2 + 2 * rid], 1ull);
           atomicAdd(&cr[3 + 2 * rid], static_cast<unsigned long long>(L));
@@ -1362,7 +1369,11 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
   static const size_t max_per_cu = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_WG_PER_CU");
     const long v = e ? std::strtol(e, nullptr, 10) : 0;
-    return v >= 1 && v <= 2 ? static_cast<size_t>(v) : size_t(2048 / kBlock);   // 32 waves per CU
+    // default one: the kernel's ~110 VGPRs allow 4 waves per SIMD, i.e. one
+    // 1024-thread workgroup per CU; a second one per CU could only run after
+    // the first (config 2, whose small image allowed two: 2^20 frames 28.4 ->
+    // 21.7 us, 2^24 203 -> 195 us, profiles/r04_s2/)
+    return v >= 1 && v <= 2 ? static_cast<size_t>(v) : size_t(1);
   }();
   size_t per_cu = lds ? (160 * 1024) / lds : max_per_cu;
   if (per_cu > max_per_cu) per_cu = max_per_cu;

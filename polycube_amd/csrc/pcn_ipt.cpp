@@ -86,7 +86,12 @@ uint32_t wave_region_bytes(bool fixed) {
     return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : uint32_t(PCN_WAVE_LDS_BYTES);
   }();
   // only the fixed-stride path transposes headers through the region
-  return fixed ? v : uint32_t(PCN_WAVE_SCRATCH_BYTES);
+  // (PCN_IPT_DEBUG_WAVE_BYTES_GENERIC: a larger candidate scratch elsewhere, A/B)
+  static const uint32_t g = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_WAVE_BYTES_GENERIC");
+    return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : uint32_t(PCN_WAVE_SCRATCH_BYTES);
+  }();
+  return fixed ? v : g;
 }
 
 struct ImageSlot {
@@ -250,12 +255,14 @@ uint32_t counted(const pcn_ipt *ctx, uint32_t nrules) {
   return std::min(nrules, ctx->cfg.max_counted_rules);
 }
 
-// Counter copies per chain block (LaunchArgs::ctr_rep_mask): 16, or
-// PCN_IPT_DEBUG_CTR_REPS (a power of two, measurement A/B).
+// Counter copies per chain block (LaunchArgs::ctr_rep_mask): 64, or
+// PCN_IPT_DEBUG_CTR_REPS (a power of two, measurement A/B).  A/B on config 2 at
+// 2^20 frames, 1 / 16 / 64 copies: 43.5 / 28.4 / 27.4 us a launch; config 3:
+// 213 / 209 / 207 us; config 5: 166 / 162 us (profiles/r04_s2/).
 uint32_t ctr_reps_default() {
   const char *e = std::getenv("PCN_IPT_DEBUG_CTR_REPS");
-  const long v = e ? std::strtol(e, nullptr, 10) : 16;
-  return v >= 1 && v <= 256 && (v & (v - 1)) == 0 ? static_cast<uint32_t>(v) : 16u;
+  const long v = e ? std::strtol(e, nullptr, 10) : 64;
+  return v >= 1 && v <= 256 && (v & (v - 1)) == 0 ? static_cast<uint32_t>(v) : 64u;
 }
 
 // Fold a chain's counter copies 1.. into copy 0 (= cs.ctr), stream-ordered;
