@@ -114,6 +114,12 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 #ifndef PCN_GEN_QUAD
 #define PCN_GEN_QUAD 1
 #endif
+// Offsets batches: a frame's offset is loaded one prefetch ahead of its
+// header, so the header loads of a prefetch do not first wait on the offset
+// load (two dependent memory round trips per frame otherwise).
+#ifndef PCN_OFF_AHEAD
+#define PCN_OFF_AHEAD 1
+#endif
 // Tuning switches (tools/ablate.py builds experiment variants with -D...).
 
 namespace pcn {
@@ -688,7 +694,8 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
 // and field set into the code as immediates; only its pointers stay kernargs.
 #ifdef PCN_JIT
 constexpr DevChain kJitChain = PCN_JIT_CHAIN;
-constexpr int kJitInputs = PCN_JIT_INPUTS;   // bit 0: in_port array, bits 1-2: ct_status (array / stage-A label)
+constexpr int kJitInputs = PCN_JIT_INPUTS;   // bit 0: in_port array, bits 1-2: ct_status (array / stage-A label),
+                                             // 3 stale ports, 4 Horus, 5 offsets array, 6 lens array
 #else
 constexpr DevChain kJitChain{};
 constexpr int kJitInputs = 7;
@@ -792,6 +799,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     u32x4 g[5];     // generic path, quad gather: the chunks this lane fetched (see prefetch)
     uint32_t sh;    // generic path: the frame start's offset in its 16-byte chunk
     bool quad;      // generic path: g[0..3] hold other frames' chunks (transpose in process)
+    uint32_t offn;  // generic path, PCN_OFF_AHEAD: the offset of the frame this stage fetches next
     uint32_t L, port, ct;
   };
   const uint32_t lane = threadIdx.x & 63;
@@ -808,6 +816,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // per-frame side inputs a chain program knows it does not have are never loaded
   constexpr bool kLoadPort = !JIT || (kJitInputs & 1);
   constexpr bool kLoadCt = !JIT || (kJitInputs & 6);
+  // offsets / lens arrays: constants of a chain program, runtime otherwise
+  const bool has_off = JIT ? (kJitInputs & 32) != 0 : a.offsets != nullptr;
+  const bool has_lens = JIT ? (kJitInputs & 64) != 0 : a.lens != nullptr;
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   constexpr int PF = FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
   Stage st[PF];
@@ -842,10 +853,18 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         x.c[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.frames + f * a.stride) + q);
     } else if (PCN_GEN_QUAD) {
       const uint64_t jf = j < a.n ? j : last;
-      const uint64_t at = reinterpret_cast<uintptr_t>(a.frames) + (a.offsets ? uint64_t(a.offsets[jf]) : jf * a.stride);
+      uint64_t off;
+      if (PCN_OFF_AHEAD && has_off) {
+        off = x.offn;                                // loaded one prefetch ago
+        const uint64_t jn = j + PF * step;           // the frame this stage fetches next
+        x.offn = a.offsets[jn < a.n ? jn : last];
+      } else {
+        off = has_off ? uint64_t(a.offsets[jf]) : jf * a.stride;
+      }
+      const uint64_t at = reinterpret_cast<uintptr_t>(a.frames) + off;
       const uint64_t end = reinterpret_cast<uintptr_t>(a.frames) + a.frames_bytes;
       const uint64_t abase = at & ~uint64_t(15);
-      x.L = a.lens ? a.lens[jf] : a.fixed_len;
+      x.L = has_lens ? a.lens[jf] : a.fixed_len;
       x.sh = static_cast<uint32_t>(at & 15);
       uint64_t group = j - lane;                 // wave-uniform
       group = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(group >> 32))) << 32) |
@@ -883,6 +902,13 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     x.port = kLoadPort ? a.in_port[jc & a.in_port_mask] : 0u;
     x.ct = kLoadCt ? a.ct_status[jc & a.ct_mask] : 0u;
   };
+  if (!FIXED && PCN_GEN_QUAD && PCN_OFF_AHEAD && has_off) {
+#pragma unroll
+    for (int d = 0; d < PF; ++d) {
+      const uint64_t j = first + d * step;
+      st[d].offn = a.offsets[j < a.n ? j : last];
+    }
+  }
 #pragma unroll
   for (int d = 0; d < PF; ++d) prefetch(st[d], first + d * step);
   if (PCN_STAGE_FAST) stage_images();

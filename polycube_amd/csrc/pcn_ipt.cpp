@@ -1106,7 +1106,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.ch = ch;
       shape.ns = ns;
       shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0) |
-                     (a.horus_fields ? 16 : 0);
+                     (a.horus_fields ? 16 : 0) | (a.offsets ? 32 : 0) | (a.lens ? 64 : 0);
       DevChain key = a.ch[ch];
       key.image = nullptr;
       key.ctr = nullptr;

@@ -73,7 +73,7 @@ def main():
     a = ap.parse_args()
     tmp = tempfile.mkdtemp()
     with open(os.path.join(tmp, "pcn_jit_spec.h"), "w") as fh:
-        fh.write(spec_for(a.cfg, a.imix, a.inputs))
+        fh.write(spec_for(a.cfg, a.imix, a.inputs | (96 if a.imix else 0)))   # + offsets and lens arrays
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", f"-I{ROOT}/include", f"-I{ROOT}/polycube_amd/csrc",
            f"-I{tmp}", "-DPCN_JIT", *a.defs.split(), "--offload-arch=gfx950", "-x", "hip", "--cuda-device-only",
            "-S", f"{ROOT}/polycube_amd/csrc/classify.hip", "-o", a.out, "-Rpass-analysis=kernel-resource-usage"]
