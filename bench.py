@@ -198,7 +198,8 @@ def parity_sample(o_rules, frames, v_dev, r_dev, offsets=None, lens=None, hook=0
     return bool(np.array_equal(v, v_dev[:k]) and np.array_equal(r, r_dev[:k]))
 
 
-def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3, stride=64, frame_len=64, hdr_bytes=0):
+def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3, stride=64, frame_len=64, hdr_bytes=0,
+             zero_copy=False):
     """Host ingest ring (pcn_ipt_ring_*): pinned slots -> hipMemcpyAsync H2D ->
     classify -> D2H verdicts, `slots` slots in flight over as many streams.
     The frames are placed in the pinned slots once, as a NIC's RX DMA would
@@ -206,7 +207,7 @@ def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3, stride=64, fra
     slots and waits for every verdict to be back in host memory.  hdr_bytes:
     only each frame's first hdr_bytes cross PCIe (a strided hipMemcpy2DAsync)."""
     from polycube_amd import IptablesError
-    ring = ipt.ring(slots=slots, slot_frames=chunk, slot_bytes=stride * chunk)
+    ring = ipt.ring(slots=slots, slot_frames=chunk, slot_bytes=stride * chunk, zero_copy=zero_copy)
     held = [ring.acquire() for _ in range(slots)]
     m = frames_host.size // stride
     for k, (slot, frames, _, _, _) in enumerate(held):
@@ -245,24 +246,26 @@ def e2e_legs(ipt, frames_host, n, rs, log):
     1536-byte stride) of the same traffic."""
     from polycube_amd import synth
     out = {}
-    for name, hb in (("whole_frames", 0), ("header_only_48", 48)):
-        out[name] = round(e2e_rate(ipt, frames_host, n, hdr_bytes=hb), 2)
+    legs = (("whole_frames", 0, False), ("header_only_48", 48, False), ("zero_copy", 0, True))
+    for name, hb, zc in legs:
+        out[name] = round(e2e_rate(ipt, frames_host, n, hdr_bytes=hb, zero_copy=zc), 2)
         log(f"[bench] e2e 64B {name}: {out[name]} Mpkt/s")
     m = 1 << 16
     cols = synth.make_headers(rs, m, synth.CONFIG_SEEDS[3] + 1)
     big = synth.build_frames(*cols, frame_len=1536).reshape(-1)
     out["frames_1500"] = {}
-    for name, hb in (("whole_frames", 0), ("header_only_64", 64)):
+    for name, hb, zc in (("whole_frames", 0, False), ("header_only_64", 64, False), ("zero_copy", 0, True)):
         out["frames_1500"][name] = round(e2e_rate(ipt, big, 1 << 20, chunk=m, stride=1536, frame_len=1500,
-                                                  hdr_bytes=hb), 2)
+                                                  hdr_bytes=hb, zero_copy=zc), 2)
         log(f"[bench] e2e 1500B {name}: {out['frames_1500'][name]} Mpkt/s")
-    out["value"] = max(out["whole_frames"], out["header_only_48"])
-    out["kept"] = "header_only_48" if out["header_only_48"] > out["whole_frames"] else "whole_frames"
+    out["kept"] = max((k for k, _, _ in legs), key=lambda k: out[k])
+    out["value"] = out[out["kept"]]
     out["unit"] = "Mpkt/s"
     out["what"] = ("host ingest ring (pcn_ipt_ring): pinned slots -> H2D -> classify -> D2H verdicts, 4 slots x 2^21 "
                    "64-byte frames in flight over 4 streams; whole frames vs. only each frame's first 48 bytes over "
-                   "PCIe (pcn_ipt_ring_batch.hdr_bytes, a strided copy); frames_1500: 4 slots x 2^16 1500-byte frames "
-                   "at a 1536-byte stride, whole vs. the first 64 bytes")
+                   "PCIe (pcn_ipt_ring_batch.hdr_bytes, a strided copy) vs. zero copy (PCN_IPT_RING_ZERO_COPY: the "
+                   "classify kernel reads the pinned slots over PCIe); frames_1500: 4 slots x 2^16 1500-byte frames "
+                   "at a 1536-byte stride, the same three")
     return out
 
 

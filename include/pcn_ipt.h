@@ -232,6 +232,11 @@ int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain);
  * bumped as by pcn_ipt_classify.  Destroy rings before their context. */
 typedef struct pcn_ipt_ring pcn_ipt_ring;
 #define PCN_IPT_RING_RULE_IDS 1u     /* also return matched rule ids */
+/* The classify kernel reads each slot's frames (and offsets / lens / in_port)
+ * where they lie, in pinned host memory, over PCIe: no copy in, and only the
+ * bytes the kernel reads cross the bus (a frame's header window, not its
+ * payload).  Verdicts still come back by copy.  Not with hdr_bytes. */
+#define PCN_IPT_RING_ZERO_COPY 2u
 typedef struct {
   uint32_t slots;         /* pinned slots, >= 2 */
   uint32_t slot_frames;   /* frames per slot, at most */

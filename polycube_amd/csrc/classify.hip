@@ -502,9 +502,10 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
   uint64_t mseen = 0;   // PCN_ABLATE == 3 only
   u32x4 *const items = ws->item;   // W entries (a 128 window runs past the struct into the wave region)
   // One worker lane's K queued items (K = 2: the second item's chain of
-  // dependent LDS reads issues alongside the first's; a duplicate item is
-  // harmless, its atomicMin repeats the same value).
-  auto work = [&](auto kk, const uint32_t (&idx)[decltype(kk)::value]) {
+  // dependent LDS reads issues alongside the first's).  A lane without a
+  // second item reads item 0 in its place -- the same addresses in every such
+  // lane, LDS broadcasts -- and folds nothing (`two`).
+  auto work = [&](auto kk, const uint32_t (&idx)[decltype(kk)::value], bool two) {
     constexpr int K = decltype(kk)::value;
     u32x4 it[K];
 #pragma unroll
@@ -577,7 +578,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     }
 #pragma unroll
     for (int q = 0; q < K; ++q) {
-      if (acc[q]) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
+      if (acc[q] && (q == 0 || two)) {   // an all-FULL word has acc == ~0: its lowest valid bit is bit 0
         const uint32_t e = t.u16(lay.perm, 2 * (w[q] * 63 + static_cast<uint32_t>(__builtin_ctzll(acc[q]))));
         atomicMin(&ws->best[owner[q]], e);
       }
@@ -589,11 +590,12 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (WMAX > 64 && cnt > 64) {     // wave-uniform: two items per lane
-      const uint32_t idx[2] = {lane, lane + 64 < cnt ? lane + 64 : lane};
-      work(IntK<2>{}, idx);
+      const bool two = lane + 64 < cnt;
+      const uint32_t idx[2] = {lane, two ? lane + 64 : 0u};
+      work(IntK<2>{}, idx, two);
     } else if (lane < cnt) {
       const uint32_t idx[1] = {lane};
-      work(IntK<1>{}, idx);
+      work(IntK<1>{}, idx, false);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

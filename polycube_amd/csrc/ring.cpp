@@ -41,6 +41,10 @@ struct Slot {
   int32_t *d_rule_ids = nullptr;
   hipEvent_t done = nullptr;
   uint64_t n = 0;
+  // PCN_IPT_RING_ZERO_COPY: device addresses of the pinned buffers (not owned)
+  uint8_t *z_frames = nullptr;
+  uint32_t *z_offsets = nullptr;
+  uint16_t *z_lens = nullptr, *z_in_port = nullptr;
 };
 
 }  // namespace
@@ -90,12 +94,20 @@ bool alloc_slot(Slot &s, const pcn_ipt_ring_config &c) {
             hipHostMalloc(reinterpret_cast<void **>(&s.h_lens), 2 * f, hipHostMallocDefault) == hipSuccess &&
             hipHostMalloc(reinterpret_cast<void **>(&s.h_in_port), 2 * f, hipHostMallocDefault) == hipSuccess &&
             hipHostMalloc(reinterpret_cast<void **>(&s.h_verdicts), f, hipHostMallocDefault) == hipSuccess &&
-            hipMalloc(reinterpret_cast<void **>(&s.d_frames), c.slot_bytes) == hipSuccess &&
-            hipMalloc(reinterpret_cast<void **>(&s.d_offsets), 4 * f) == hipSuccess &&
-            hipMalloc(reinterpret_cast<void **>(&s.d_lens), 2 * f) == hipSuccess &&
-            hipMalloc(reinterpret_cast<void **>(&s.d_in_port), 2 * f) == hipSuccess &&
             hipMalloc(reinterpret_cast<void **>(&s.d_verdicts), f) == hipSuccess &&
             hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+  if (ok && (c.flags & PCN_IPT_RING_ZERO_COPY)) {
+    // the kernel reads the pinned buffers themselves, through their device addresses
+    ok = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.z_frames), s.h_frames, 0) == hipSuccess &&
+         hipHostGetDevicePointer(reinterpret_cast<void **>(&s.z_offsets), s.h_offsets, 0) == hipSuccess &&
+         hipHostGetDevicePointer(reinterpret_cast<void **>(&s.z_lens), s.h_lens, 0) == hipSuccess &&
+         hipHostGetDevicePointer(reinterpret_cast<void **>(&s.z_in_port), s.h_in_port, 0) == hipSuccess;
+  } else if (ok) {
+    ok = hipMalloc(reinterpret_cast<void **>(&s.d_frames), c.slot_bytes) == hipSuccess &&
+         hipMalloc(reinterpret_cast<void **>(&s.d_offsets), 4 * f) == hipSuccess &&
+         hipMalloc(reinterpret_cast<void **>(&s.d_lens), 2 * f) == hipSuccess &&
+         hipMalloc(reinterpret_cast<void **>(&s.d_in_port), 2 * f) == hipSuccess;
+  }
   if (ok && (c.flags & PCN_IPT_RING_RULE_IDS))
     ok = hipHostMalloc(reinterpret_cast<void **>(&s.h_rule_ids), 4 * f, hipHostMallocDefault) == hipSuccess &&
          hipMalloc(reinterpret_cast<void **>(&s.d_rule_ids), 4 * f) == hipSuccess;
@@ -113,7 +125,8 @@ int pcn_ipt_ring_create(pcn_ipt *ctx, const pcn_ipt_ring_config *cfg, pcn_ipt_ri
   if (device < 0) return ring_fail(-ENODEV, "context has no HIP device (created with device=-1)");
   if (cfg->slots < 2 || cfg->slot_frames == 0 || cfg->slot_bytes == 0)
     return ring_fail(-EINVAL, "need >= 2 slots of >= 1 frame and >= 1 byte");
-  if (cfg->flags & ~uint32_t(PCN_IPT_RING_RULE_IDS)) return ring_fail(-EINVAL, "unknown ring flags");
+  if (cfg->flags & ~uint32_t(PCN_IPT_RING_RULE_IDS | PCN_IPT_RING_ZERO_COPY))
+    return ring_fail(-EINVAL, "unknown ring flags");
   if (hipSetDevice(device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
   auto *r = new pcn_ipt_ring();
   r->ctx = ctx;
@@ -172,6 +185,8 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   const uint64_t bytes = b->frames_bytes ? b->frames_bytes : b->n * uint64_t(b->stride);
   if (bytes > r->cfg.slot_bytes) return ring_fail(-EINVAL, "frame bytes exceed the slot");
   const uint32_t hb = b->hdr_bytes;
+  const bool zc = r->cfg.flags & PCN_IPT_RING_ZERO_COPY;
+  if (hb && zc) return ring_fail(-EINVAL, "hdr_bytes with a zero-copy ring (the kernel reads only the headers anyway)");
   if (hb) {
     pcn_ipt_ct_info ci{};
     const bool ct = pcn_ipt_ct_get_info(r->ctx, &ci) == 0 && ci.enabled;
@@ -185,12 +200,14 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   const size_t n = b->n;
   // PCIe in: frames (or their first hb bytes: a strided copy, hb-byte rows
   // packed on the device) and the per-frame arrays the batch uses
-  bool ok = hb ? hipMemcpy2DAsync(s.d_frames, hb, s.h_frames, b->stride, hb, n, hipMemcpyHostToDevice, st) ==
-                     hipSuccess
-               : hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
-  if (ok && b->use_offsets) ok = hipMemcpyAsync(s.d_offsets, s.h_offsets, 4 * n, hipMemcpyHostToDevice, st) == hipSuccess;
-  if (ok && b->use_lens) ok = hipMemcpyAsync(s.d_lens, s.h_lens, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
-  if (ok && b->use_in_port) ok = hipMemcpyAsync(s.d_in_port, s.h_in_port, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+  bool ok = true;
+  if (!zc) {
+    ok = hb ? hipMemcpy2DAsync(s.d_frames, hb, s.h_frames, b->stride, hb, n, hipMemcpyHostToDevice, st) == hipSuccess
+            : hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+    if (ok && b->use_offsets) ok = hipMemcpyAsync(s.d_offsets, s.h_offsets, 4 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+    if (ok && b->use_lens) ok = hipMemcpyAsync(s.d_lens, s.h_lens, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+    if (ok && b->use_in_port) ok = hipMemcpyAsync(s.d_in_port, s.h_in_port, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+  }
   // a failed submit leaves the slot kFilling (the caller may release and
   // refill it): wait until nothing queued on the stream still reads it
   auto quiesce = [&](int code, const std::string &msg) {
@@ -200,13 +217,13 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   };
   if (!ok) return quiesce(-EIO, "hipMemcpyAsync (H2D) failed");
   pcn_ipt_batch batch{};
-  batch.frames = s.d_frames;
+  batch.frames = zc ? s.z_frames : s.d_frames;
   batch.frames_bytes = hb ? n * hb : bytes;
-  batch.offsets = b->use_offsets ? s.d_offsets : nullptr;
-  batch.lens = b->use_lens ? s.d_lens : nullptr;
+  batch.offsets = b->use_offsets ? (zc ? s.z_offsets : s.d_offsets) : nullptr;
+  batch.lens = b->use_lens ? (zc ? s.z_lens : s.d_lens) : nullptr;
   batch.stride = hb ? hb : b->stride;
   batch.fixed_len = b->fixed_len;
-  batch.in_port = b->use_in_port ? s.d_in_port : nullptr;
+  batch.in_port = b->use_in_port ? (zc ? s.z_in_port : s.d_in_port) : nullptr;
   batch.const_in_port = b->const_in_port;
   batch.direction = b->direction;
   batch.hook = b->hook;

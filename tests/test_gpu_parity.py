@@ -344,14 +344,16 @@ def test_localip_input_output_from_lds(dev):
     assert_counters(o, ipt)
 
 
-def test_ingest_ring_parity(dev):
-    """Host ingest ring: frames filled into pinned slots, copied in, classified
-    and the verdicts / rule ids copied back -- fixed-stride slots and IMIX
-    slots (offsets, lens, in_port, TC hook) interleaved; equal to the oracle,
+@pytest.mark.parametrize("zero_copy", [False, True], ids=["copy", "zero_copy"])
+def test_ingest_ring_parity(dev, zero_copy):
+    """Host ingest ring: frames filled into pinned slots, copied in (or, zero
+    copy, read by the kernel in the pinned slots over PCIe), classified and the
+    verdicts / rule ids copied back -- fixed-stride slots and IMIX slots
+    (offsets, lens, in_port, TC hook) interleaved; equal to the oracle,
     counters included."""
     rs = synth.config_rules(2)
     o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
-    ring = ipt.ring(slots=3, slot_frames=1 << 14, slot_bytes=(1 << 14) * 1600, rule_ids=True)
+    ring = ipt.ring(slots=3, slot_frames=1 << 14, slot_bytes=(1 << 14) * 1600, rule_ids=True, zero_copy=zero_copy)
     expect = {}
     for k in range(8):
         slot, frames, offsets, lens, in_port = ring.acquire()
