@@ -16,5 +16,9 @@ pmcq sq_cfg3_parse 3 24 0.5 "$SQ" -DPCN_ABLATE=1
 pmcq sq_cfg5 5 22 0.5 "$SQ"
 pmcq sq_cfg5_parse 5 22 0.5 "$SQ" -DPCN_ABLATE=1
 pmcq sq_cfg5_lookups 5 22 0.5 "$SQ" -DPCN_ABLATE=2
+TCC="TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum"
+pmcq tcc_cfg5 5 22 0.5 "$TCC"
+pmcq tcc_cfg5_lookups 5 22 0.5 "$TCC" -DPCN_ABLATE=2
+pmcq tcc_cfg3 3 24 0.5 "$TCC"
 run bench 600 python bench.py --steps 50 --warmup 10 --no-cpu
 exit 0
