@@ -115,10 +115,6 @@ struct TableLayout {
   uint32_t pool;           // u64[]: distinct partial words; POOL[0] is all-ones
   uint32_t zero;           // 16 zero bytes (the PART cell a FULL field reads: index 0)
   uint32_t perm;           // u16[nrw * 63]
-  uint32_t dense_pm;       // dense PART only, != 0: u64[nvec][nsw], PM (bit w: word w partial) per
-                           // class and block, in the LDS prefix; a candidate field that is FULL at
-                           // its word then reads no PART cell from L2.  PERM then follows PART
-                           // (past the prefix: one L2 read per candidate word that matches)
 };
 
 struct DevChain {

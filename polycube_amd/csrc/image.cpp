@@ -39,14 +39,6 @@ bool ip_search_only() {
   static const bool v = std::getenv("PCN_IPT_DEBUG_IPSEARCH") != nullptr;
   return v;
 }
-// PCN_IPT_DEBUG_DENSE_PM=0: dense PART images without the PM masks (A/B).
-bool dense_pm_masks() {
-  static const bool v = [] {
-    const char *e = std::getenv("PCN_IPT_DEBUG_DENSE_PM");
-    return !e || *e != '0';
-  }();
-  return v;
-}
 int forced_join() {
   static const int v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_JOIN");
@@ -550,29 +542,15 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     // field costs one L2 read rather than a record read and an index read.
     lay.pool = blob.add(words);
     lay.zero = blob.add(std::vector<uint32_t>(4, 0));
+    lay.perm = blob.add(perm.perm);
     const size_t iw = lay.part_wide ? 4 : 2;
-    const size_t indexed_bytes = blob.bytes.size() + perm.perm.size() * 2 + cand.size() * 4 + part.size() * iw +
-                                 3 * kAlign;
+    const size_t indexed_bytes = blob.bytes.size() + cand.size() * 4 + part.size() * iw + 2 * kAlign;
     lay.part_dense = indexed_bytes > kDenseMinBytes && dense.size() * iw <= kDenseMaxBytes && !compact_images();
-    if (lay.part_dense && dense_pm_masks()) {
-      // {PM} per class and block in the LDS prefix: a FULL field's PART cell
-      // (index 0, POOL[0]) is not read at all (config 5: 2.3 of a candidate's
-      // 5 fields are partial).  PERM moves past PART, out of the prefix: read
-      // once per matching candidate word, it buys back most of the masks' LDS.
-      std::vector<uint64_t> pmv(nrec);
-      for (size_t r = 0; r < nrec; ++r) pmv[r] = uint64_t(cand[4 * r + 1]) << 32 | cand[4 * r];
-      lay.dense_pm = blob.add(pmv);
-      if (lay.part_wide) lay.part = blob.add(dense);
-      else lay.part = blob.add(std::vector<uint16_t>(dense.begin(), dense.end()));
-      lay.pbase = lay.part;
-      lay.perm = blob.add(perm.perm);
-    } else if (lay.part_dense) {
-      lay.perm = blob.add(perm.perm);
+    if (lay.part_dense) {
       if (lay.part_wide) lay.part = blob.add(dense);
       else lay.part = blob.add(std::vector<uint16_t>(dense.begin(), dense.end()));
       lay.pbase = lay.part;
     } else {
-      lay.perm = blob.add(perm.perm);
       lay.pbase = blob.add(cand);
       if (lay.part_wide) lay.part = blob.add(part);
       else lay.part = blob.add(std::vector<uint16_t>(part.begin(), part.end()));
