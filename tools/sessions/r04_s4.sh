@@ -1,15 +1,11 @@
 #!/bin/bash
-# Round 4, session 4: ring zero-copy + header-only tests and bench legs; config-5 PM masks A/B; the
+# Round 4, session 4: ring zero-copy + header-only tests and bench legs; the
 # two-item deal with broadcast filler items; SQ counters of the candidate stage
 # (config 3 at hit 0.5 / 1, config 5) against the parse-only build.
 TAG=r04_s4
 source "$(dirname "$0")/../gpu_lib.sh"
 KEEP_GOING=1
-pytest_gpu tests_parity 400 tests/test_gpu_parity.py
-run ab_cfg5_pm 900 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
-  --variants "jit,jit@DENSE_PM=0,jit:-DPCN_DEAL2=2@WAVE_BYTES_GENERIC=2304,jit,jit@DENSE_PM=0,jit:-DPCN_DEAL2=2@WAVE_BYTES_GENERIC=2304"
-CFG5_HOOK=tc run ab_cfg5_pm_tc 900 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
-  --variants "jit,jit@DENSE_PM=0,jit:-DPCN_DEAL2=2@WAVE_BYTES_GENERIC=2304,jit,jit@DENSE_PM=0"
+pytest_gpu tests_ring 300 tests/test_gpu_parity.py -k "ring"
 run ab_cfg3_deal2 900 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0.5,1 --iters 30 \
   --variants "jit,jit:-DPCN_DEAL2=1,jit,jit:-DPCN_DEAL2=1"
 SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT"
