@@ -61,15 +61,19 @@ ktrace() {
   case $rc in 0) ;; *) exit $rc ;; esac
 }
 
-# One PMC pass (any counters) of one ablate child, kernel trace only:
-# pmcq <name> <cfg> <log2n> <hit> "<counters>" [jit defs] [hook]  -> $O/<name>/
+# One PMC pass (any counters) of one ablate child, kernel trace only, then
+# summarised on the box (tools/pmc_summary.py: per-dispatch averages of the
+# classify kernel) and the raw CSVs dropped (they exceed gpurun's copy-back):
+# pmcq <name> <cfg> <log2n> <hit> "<counters>" [jit defs] [hook]  -> $O/<name>.json
 pmcq() {
   local name=$1 cfg=$2 log2n=$3 hit=$4 ctrs=$5 defs=${6:-} hook=${7:-xdp}
   mkdir -p "$O/$name"
-  ( cd /tmp && PCN_IPT_JIT_DEFS="$defs" CFG5_HOOK=$hook timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-trace \
-      --output-format csv -d "$O/$name" -o run -- python3 "$R/tools/ablate.py" --child --lib "" --hit "$hit" --iters 5 \
-      --log2n "$log2n" --cfg "$cfg" --jit 1 > "$O/$name.log" 2>&1 )
+  ( cd /tmp && SETTLE=0.05 PCN_IPT_JIT_DEFS="$defs" CFG5_HOOK=$hook timeout -s KILL 120 rocprofv3 --pmc $ctrs \
+      --kernel-trace --output-format csv -d "$O/$name/p1" -o run -- python3 "$R/tools/ablate.py" --child --lib "" \
+      --hit "$hit" --iters 5 --log2n "$log2n" --cfg "$cfg" --jit 1 > "$O/$name.log" 2>&1 )
   local rc=$?
   echo "== pmcq $name rc=$rc"
   case $rc in 0) ;; *) tail -5 "$O/$name.log"; exit $rc ;; esac
+  python3 "$R/tools/pmc_summary.py" "$O/$name" --frames $((1 << log2n)) --out "$O/$name.json" > /dev/null && \
+    rm -rf "$O/$name"
 }

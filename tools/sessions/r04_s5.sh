@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 4, session 5: SQ / TCC counters of the candidate stage (config 3 at hit
+# 0.5 / 1, with and without the two-item deal; config 5) against the parse-only
+# and lookups-only builds.
+TAG=r04_s5
+source "$(dirname "$0")/../gpu_lib.sh"
+SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT"
+TCC="TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum"
+pmcq sq_cfg3_h05 3 24 0.5 "$SQ"
+pmcq sq_cfg3_h1 3 24 1 "$SQ"
+pmcq sq_cfg3_h1_deal2 3 24 1 "$SQ" -DPCN_DEAL2=1
+pmcq sq_cfg3_h05_deal2 3 24 0.5 "$SQ" -DPCN_DEAL2=1
+pmcq sq_cfg3_parse 3 24 0.5 "$SQ" -DPCN_ABLATE=1
+pmcq sq_cfg5 5 22 0.5 "$SQ"
+pmcq sq_cfg5_parse 5 22 0.5 "$SQ" -DPCN_ABLATE=1
+pmcq sq_cfg5_lookups 5 22 0.5 "$SQ" -DPCN_ABLATE=2
+pmcq tcc_cfg5 5 22 0.5 "$TCC"
+pmcq tcc_cfg5_lookups 5 22 0.5 "$TCC" -DPCN_ABLATE=2
+pmcq tcc_cfg3 3 24 0.5 "$TCC"
+exit 0
