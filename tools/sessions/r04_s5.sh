@@ -17,4 +17,7 @@ pmcq sq_cfg5_lookups 5 22 0.5 "$SQ" -DPCN_ABLATE=2
 pmcq tcc_cfg5 5 22 0.5 "$TCC"
 pmcq tcc_cfg5_lookups 5 22 0.5 "$TCC" -DPCN_ABLATE=2
 pmcq tcc_cfg3 3 24 0.5 "$TCC"
+KEEP_GOING=1
+run ab_cfg3_stages 900 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0,0.5 --iters 30 \
+  --variants "jit1,jit2,jit3,jit4,jit5,jit"
 exit 0
