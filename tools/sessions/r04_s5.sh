@@ -20,4 +20,6 @@ pmcq tcc_cfg3 3 24 0.5 "$TCC"
 KEEP_GOING=1
 run ab_cfg3_stages 900 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0,0.5 --iters 30 \
   --variants "jit1,jit2,jit3,jit4,jit5,jit"
+CFG5_HOOK=xdp run ab_cfg5_pf2 600 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
+  --variants "jit,jit:-DPCN_PREFETCH_GENERIC=2,jit,jit:-DPCN_PREFETCH_GENERIC=2"
 exit 0
