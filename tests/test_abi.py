@@ -93,3 +93,34 @@ def test_null_context_is_an_error():
     cfg = ffi.Config(-1, 0, 0, 70000)
     h = C.c_void_p()
     assert ffi.lib().pcn_ipt_create(C.byref(cfg), C.byref(h)) < 0
+
+
+def test_comm_info_without_a_device():
+    """pcn_ipt_comm_get_info with no context: the RCCL that would serve the
+    calls (version and library), no device, no gathers."""
+    from polycube_amd.iptables import comm_info
+    ci = comm_info()
+    assert ci["nccl_version"] > 20000 and ci["rccl_version"].count(".") == 2
+    assert "rccl" in ci["rccl_path"]
+    assert ci["device"] == -1 and ci["gathers_timed"] == 0 and ci["nranks"] == 0
+
+
+def test_bench_traffic_needs_the_measured_build(tmp_path, monkeypatch):
+    """bench.py reports roofline.traffic only for the kernel sources (and batch
+    size) the PMC entry was measured on, and says why not otherwise."""
+    import json
+    import bench
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    (tmp_path / "profiles").mkdir()
+    for rel in bench.KERNEL_SOURCES:
+        (tmp_path / rel).parent.mkdir(parents=True, exist_ok=True)
+        (tmp_path / rel).write_text(rel)
+    h = bench.kernel_src_hash()
+    entry = {"frames": 1024, "hbm_bytes_per_launch": 70000, "src_hash": h, "profile": "p"}
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"configs": {"config3": entry}}))
+    assert bench.load_traffic(3, 0, 1024)[0] == 70000
+    assert bench.load_traffic(3, 0, 2048)[0] is None                 # another batch size
+    assert bench.load_traffic(5, 1, 1024)[0] is None                 # no entry for config 5 / TC
+    (tmp_path / bench.KERNEL_SOURCES[0]).write_text("changed kernel")
+    t, why = bench.load_traffic(3, 0, 1024)
+    assert t is None and h in why                                    # sources changed since the PMC run
