@@ -17,6 +17,9 @@ pmcq sq_cfg5_lookups 5 22 0.5 "$SQ" -DPCN_ABLATE=2
 pmcq tcc_cfg5 5 22 0.5 "$TCC"
 pmcq tcc_cfg5_lookups 5 22 0.5 "$TCC" -DPCN_ABLATE=2
 pmcq tcc_cfg3 3 24 0.5 "$TCC"
+TCP="TCP_PERF_SEL_TOTAL_READ_sum TCP_PERF_SEL_TOTAL_HIT_LRU_READ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_CC_READ_REQ_sum"
+pmcq tcp_cfg5 5 22 0.5 "$TCP"
+pmcq tcp_cfg5_lookups 5 22 0.5 "$TCP" -DPCN_ABLATE=2
 KEEP_GOING=1
 run ab_cfg3_stages 900 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0,0.5 --iters 30 \
   --variants "jit1,jit2,jit3,jit4,jit5,jit"
