@@ -17,12 +17,13 @@ pmcq sq_cfg5_lookups 5 22 0.5 "$SQ" -DPCN_ABLATE=2
 pmcq tcc_cfg5 5 22 0.5 "$TCC"
 pmcq tcc_cfg5_lookups 5 22 0.5 "$TCC" -DPCN_ABLATE=2
 pmcq tcc_cfg3 3 24 0.5 "$TCC"
-TCP="TCP_PERF_SEL_TOTAL_READ_sum TCP_PERF_SEL_TOTAL_HIT_LRU_READ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_CC_READ_REQ_sum"
-pmcq tcp_cfg5 5 22 0.5 "$TCP"
-pmcq tcp_cfg5_lookups 5 22 0.5 "$TCP" -DPCN_ABLATE=2
 KEEP_GOING=1
 run ab_cfg3_stages 900 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0,0.5 --iters 30 \
   --variants "jit1,jit2,jit3,jit4,jit5,jit"
 CFG5_HOOK=xdp run ab_cfg5_pf2 600 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
   --variants "jit,jit:-DPCN_PREFETCH_GENERIC=2,jit,jit:-DPCN_PREFETCH_GENERIC=2"
+# (last: counter names not checked on this pool before)
+TCP="TCP_PERF_SEL_TOTAL_READ_sum TCP_PERF_SEL_TOTAL_HIT_LRU_READ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_CC_READ_REQ_sum"
+pmcq tcp_cfg5 5 22 0.5 "$TCP"
+pmcq tcp_cfg5_lookups 5 22 0.5 "$TCP" -DPCN_ABLATE=2
 exit 0
