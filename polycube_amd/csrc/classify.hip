@@ -538,6 +538,13 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     // word (indexed PART: through the zero cell, index 0).
     uint32_t at[K][NS];   // LDS/image offset of each field's u64 word
     u32x3 recs[K][NS];    // {PM lo, PM hi, PBASE} (the record's 4th dword is padding)
+    uint64_t pmw[K][NS];  // dense PART with PM masks: each field's PM word (LDS)
+    if (lay.part_dense && lay.dense_pm) {
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+#pragma unroll
+        for (int f = 0; f < NS; ++f) pmw[q][f] = t.u64(lay.dense_pm, 8 * (oc[q][f] * nsw + k[q]));
+    }
     if (!lay.part_dense) {
       // all records in flight together: one LDS round trip (left to itself
       // the compiler recycles two record registers and waits between pairs)
@@ -553,7 +560,10 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       for (int f = 0; f < NS; ++f) {
         if (lay.part_dense) {
           const uint32_t cell = oc[q][f] * nrw + w[q];
-          at[q][f] = lay.pool + 8 * (lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell));
+          uint32_t qi = 0;   // POOL index (0: all-ones, a FULL field)
+          if (!lay.dense_pm || ((pmw[q][f] >> bit[q]) & 1))
+            qi = lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell);
+          at[q][f] = lay.pool + 8 * qi;
           continue;
         }
         const u32x3 r = recs[q][f];

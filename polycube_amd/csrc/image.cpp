@@ -39,6 +39,23 @@ bool ip_search_only() {
   static const bool v = std::getenv("PCN_IPT_DEBUG_IPSEARCH") != nullptr;
   return v;
 }
+// PCN_IPT_DEBUG_DENSE_PM=1: dense PART images with the PM masks (A/B);
+// PCN_IPT_DEBUG_IP_BITS=b: IP bucket tables of at most 2^b entries (A/B).
+bool dense_pm_masks() {
+  static const bool v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_DENSE_PM");
+    return e && *e == '1';
+  }();
+  return v;
+}
+uint32_t ip_bits_max() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_IP_BITS");
+    const long b = e ? std::strtol(e, nullptr, 10) : 0;
+    return b >= 4 && b <= PCN_IP_BUCKET_BITS_MAX ? static_cast<uint32_t>(b) : uint32_t(PCN_IP_BUCKET_BITS_MAX);
+  }();
+  return v;
+}
 int forced_join() {
   static const int v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_JOIN");
@@ -278,7 +295,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     // (one dependent read instead of a search).  A prefix's two boundaries
     // usually share a bucket, so this is the common case.
     uint32_t bits = 0, win = 0;
-    const uint32_t max_bits = compact_images() ? 10 : PCN_IP_BUCKET_BITS_MAX;
+    const uint32_t max_bits = compact_images() ? 10 : ip_bits_max();
     for (uint32_t b = 4; b <= max_bits && !bits && !compact_images() && !ip_search_only(); ++b)
       if (max_count(first_of(b)) <= kIpWindowMax) bits = b;
     if (bits) {
@@ -540,12 +557,20 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     // indexed PART would exceed LDS anyway, PART is stored dense instead (a
     // POOL index per class and word, larger but L2-resident), so a candidate
     // field costs one L2 read rather than a record read and an index read.
+    const size_t iw = lay.part_wide ? 4 : 2;
+    const size_t indexed_bytes = blob.bytes.size() + words.size() * 8 + perm.perm.size() * 2 + cand.size() * 4 +
+                                 part.size() * iw + 5 * kAlign;
+    lay.part_dense = indexed_bytes > kDenseMinBytes && dense.size() * iw <= kDenseMaxBytes && !compact_images();
+    if (lay.part_dense && dense_pm_masks()) {
+      // PM per class and block in the LDS prefix (A/B): a field FULL at a
+      // candidate word (index 0: POOL[0]) reads no PART cell from L2
+      std::vector<uint64_t> pmv(nrec);
+      for (size_t r = 0; r < nrec; ++r) pmv[r] = uint64_t(cand[4 * r + 1]) << 32 | cand[4 * r];
+      lay.dense_pm = blob.add(pmv);
+    }
     lay.pool = blob.add(words);
     lay.zero = blob.add(std::vector<uint32_t>(4, 0));
     lay.perm = blob.add(perm.perm);
-    const size_t iw = lay.part_wide ? 4 : 2;
-    const size_t indexed_bytes = blob.bytes.size() + cand.size() * 4 + part.size() * iw + 2 * kAlign;
-    lay.part_dense = indexed_bytes > kDenseMinBytes && dense.size() * iw <= kDenseMaxBytes && !compact_images();
     if (lay.part_dense) {
       if (lay.part_wide) lay.part = blob.add(dense);
       else lay.part = blob.add(std::vector<uint16_t>(dense.begin(), dense.end()));

@@ -22,6 +22,12 @@ run ab_cfg3_stages 900 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0,0.5
   --variants "jit1,jit2,jit3,jit4,jit5,jit"
 CFG5_HOOK=xdp run ab_cfg5_pf2 600 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
   --variants "jit,jit:-DPCN_PREFETCH_GENERIC=2,jit,jit:-DPCN_PREFETCH_GENERIC=2"
+pytest_gpu tests_cfg5 300 tests/test_gpu_parity.py -k "imix or config"
+PCN_IPT_DEBUG_DENSE_PM=1 PCN_IPT_DEBUG_IP_BITS=8 pytest_gpu tests_cfg5_pm 300 tests/test_gpu_parity.py -k "imix or config"
+run ab_cfg5_lds 900 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
+  --variants "jit,jit@IP_BITS=8,jit@DENSE_PM=1;IP_BITS=8,jit,jit@IP_BITS=8,jit@DENSE_PM=1;IP_BITS=8"
+CFG5_HOOK=tc run ab_cfg5_lds_tc 900 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
+  --variants "jit,jit@IP_BITS=8,jit@DENSE_PM=1;IP_BITS=8,jit,jit@IP_BITS=8,jit@DENSE_PM=1;IP_BITS=8"
 # (last: counter names not checked on this pool before)
 TCP="TCP_PERF_SEL_TOTAL_READ_sum TCP_PERF_SEL_TOTAL_HIT_LRU_READ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_CC_READ_REQ_sum"
 pmcq tcp_cfg5 5 22 0.5 "$TCP"
