@@ -1135,7 +1135,8 @@ template <bool kSpec>
 __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
                                                 uint32_t k, uint64_t q0, uint64_t hi, uint64_t bound, Cache &c,
                                                 bool &aborted, bool dense = false, uint64_t *tfirst = nullptr,
-                                                PassKeys *pk = nullptr, int pass = kAllKeys, uint64_t *unk = nullptr) {
+                                                PassKeys *pk = nullptr, int pass = kAllKeys, uint64_t *unk = nullptr,
+                                                int64_t idx0 = -1) {
   (void)tfirst;                                     // (measurement builds only)
   const uint32_t lane = threadIdx.x;
   const uint64_t last = b.n - 1;
@@ -1143,7 +1144,9 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
   uint64_t base = q0;
   aborted = false;
   auto cl = [&](uint64_t r) -> uint64_t { return r < last ? r : last; };
-  WalkRec w = wrec.load(wrec.sidx[cl(base + lane)], cl(base + lane));
+  // idx0 >= 0: the first chunk's batch index, loaded by the caller (walk_long
+  // issues it before it reads the run's key and cuts)
+  WalkRec w = wrec.load(idx0 >= 0 ? static_cast<uint32_t>(idx0) : wrec.sidx[cl(base + lane)], cl(base + lane));
   uint32_t nidx = wrec.sidx[cl(base + 64 + lane)];   // the next chunk's indices, a chunk ahead
 #if PCN_CT_DBG
   uint32_t dbg_chunks = 0, dbg_rounds = 0, dbg_changes = 0, dbg_steps = 0, dbg_recs = 0;
@@ -1341,8 +1344,15 @@ __device__ __forceinline__ uint32_t cache_px(const Cache &c) {
 __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
                           const uint32_t *skeys, uint32_t p, uint32_t *cursor, uint32_t vb, uint64_t hi, int first,
                           HeadExit *hx) {
-  const uint32_t k = wrec.key(p);
   const uint64_t q0 = first ? p : cursor[vb];
+  // the first chunk's batch indices in flight with the key, before the cut
+  // checks and the pass setup: the head's dependent loads are heads -> {key,
+  // sorted index} -> record -> slot, not heads -> key -> cuts -> sorted index
+  // -> record -> slot (the records themselves would hold 14 more VGPRs
+  // across the setup: 136, three waves per SIMD instead of four)
+  const uint64_t last = b.n - 1;
+  const uint32_t i0 = wrec.sidx[q0 + threadIdx.x < last ? q0 + threadIdx.x : last];
+  const uint32_t k = wrec.key(p);
   uint64_t bound = ~0ull;
   if (first != 0 && kSeg != 0) {
     const uint64_t B1 = (p / (kSeg ? kSeg : 1) + 1) * kSeg;
@@ -1367,9 +1377,11 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
 #endif
   for (;;) {
 #if PCN_CT_DBG_T
-    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, &dt1, &pk, pass, &unk);
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, &dt1, &pk, pass, &unk,
+                                           from == q0 ? int64_t(i0) : int64_t(-1));
 #else
-    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, nullptr, &pk, pass, &unk);
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, nullptr, &pk, pass, &unk,
+                                           from == q0 ? int64_t(i0) : int64_t(-1));
 #endif
     if (from == q0) stop = st;                       // every pass stops there (the run's end, or hi)
     if (unk == ~0ull) break;
