@@ -11,6 +11,7 @@
 // (one dependent table access per packet of a run), the sort is hipCUB's
 // onesweep radix sort on a key-bucket id.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -1135,8 +1136,7 @@ template <bool kSpec>
 __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
                                                 uint32_t k, uint64_t q0, uint64_t hi, uint64_t bound, Cache &c,
                                                 bool &aborted, bool dense = false, uint64_t *tfirst = nullptr,
-                                                PassKeys *pk = nullptr, int pass = kAllKeys, uint64_t *unk = nullptr,
-                                                int64_t idx0 = -1) {
+                                                PassKeys *pk = nullptr, int pass = kAllKeys, uint64_t *unk = nullptr) {
   (void)tfirst;                                     // (measurement builds only)
   const uint32_t lane = threadIdx.x;
   const uint64_t last = b.n - 1;
@@ -1144,9 +1144,7 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
   uint64_t base = q0;
   aborted = false;
   auto cl = [&](uint64_t r) -> uint64_t { return r < last ? r : last; };
-  // idx0 >= 0: the first chunk's batch index, loaded by the caller (walk_long
-  // issues it before it reads the run's key and cuts)
-  WalkRec w = wrec.load(idx0 >= 0 ? static_cast<uint32_t>(idx0) : wrec.sidx[cl(base + lane)], cl(base + lane));
+  WalkRec w = wrec.load(wrec.sidx[cl(base + lane)], cl(base + lane));
   uint32_t nidx = wrec.sidx[cl(base + 64 + lane)];   // the next chunk's indices, a chunk ahead
 #if PCN_CT_DBG
   uint32_t dbg_chunks = 0, dbg_rounds = 0, dbg_changes = 0, dbg_steps = 0, dbg_recs = 0;
@@ -1344,15 +1342,8 @@ __device__ __forceinline__ uint32_t cache_px(const Cache &c) {
 __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
                           const uint32_t *skeys, uint32_t p, uint32_t *cursor, uint32_t vb, uint64_t hi, int first,
                           HeadExit *hx) {
-  const uint64_t q0 = first ? p : cursor[vb];
-  // the first chunk's batch indices in flight with the key, before the cut
-  // checks and the pass setup: the head's dependent loads are heads -> {key,
-  // sorted index} -> record -> slot, not heads -> key -> cuts -> sorted index
-  // -> record -> slot (the records themselves would hold 14 more VGPRs
-  // across the setup: 136, three waves per SIMD instead of four)
-  const uint64_t last = b.n - 1;
-  const uint32_t i0 = wrec.sidx[q0 + threadIdx.x < last ? q0 + threadIdx.x : last];
   const uint32_t k = wrec.key(p);
+  const uint64_t q0 = first ? p : cursor[vb];
   uint64_t bound = ~0ull;
   if (first != 0 && kSeg != 0) {
     const uint64_t B1 = (p / (kSeg ? kSeg : 1) + 1) * kSeg;
@@ -1377,11 +1368,9 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
 #endif
   for (;;) {
 #if PCN_CT_DBG_T
-    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, &dt1, &pk, pass, &unk,
-                                           from == q0 ? int64_t(i0) : int64_t(-1));
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, &dt1, &pk, pass, &unk);
 #else
-    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, nullptr, &pk, pass, &unk,
-                                           from == q0 ? int64_t(i0) : int64_t(-1));
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, nullptr, &pk, pass, &unk);
 #endif
     if (from == q0) stop = st;                       // every pass stops there (the run's end, or hi)
     if (unk == ~0ull) break;
@@ -2174,6 +2163,17 @@ static hipError_t sort_pairs(void *temp, size_t &bytes, const uint32_t *kin, uin
                                                  static_cast<unsigned int>(n), 0u, kbits, st);
 }
 
+// PCN_IPT_DEBUG_CT_KBITS=b (16..30): key buckets of at most b bits, whatever
+// the batch size (A/B of fewer sort passes against more bucket collisions)
+static uint32_t debug_key_bits() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_CT_KBITS");
+    const long b = e ? std::strtol(e, nullptr, 10) : 0;
+    return b >= 16 && b <= 30 ? static_cast<uint32_t>(b) : 30u;
+  }();
+  return v;
+}
+
 static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4, hipStream_t st) {
   if (lab4 && s.ox_cap < n) {                  // only batches with four labels read it
     if (s.ox) CT_CHECK(hipFree(s.ox));
@@ -2283,6 +2283,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   hipStream_t st = static_cast<hipStream_t>(stream);
   uint32_t kbits = 8;
   while (kbits < 30 && (uint64_t(1) << kbits) < 2 * b.n) ++kbits;
+  kbits = std::min(kbits, debug_key_bits());
   const uint32_t sentinel = (1u << kbits) - 1;
   CT_CHECK(grow(s, b.n, kbits, b.nlab == 4, st));
   const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
