@@ -77,3 +77,24 @@ pmcq() {
   python3 "$R/tools/pmc_summary.py" "$O/$name" --frames $((1 << log2n)) --out "$O/$name.json" > /dev/null && \
     rm -rf "$O/$name"
 }
+
+# HBM traffic of the classify kernel for bench.py's roofline.traffic:
+# pmct <key> <cfg> <log2n> [hook] -> FETCH_SIZE and WRITE_SIZE passes, summarised on the
+# box into $O/pmc_<key>.json and into profiles/pmc_traffic.json (copied to $O), raw CSVs dropped
+pmct() {
+  local key=$1 cfg=$2 log2n=$3 hook=${4:-xdp}
+  local d="$O/pmc_$key"
+  mkdir -p "$d"
+  local k=0
+  for grp in FETCH_SIZE WRITE_SIZE; do
+    k=$((k + 1))
+    ( cd /tmp && CFG5_HOOK=$hook timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
+        -d "$d/p$k" -o run -- python3 "$R/tools/ablate.py" --child --lib "" --hit 0.5 --iters 5 \
+        --log2n "$log2n" --cfg "$cfg" --jit 1 > "$d.p$k.log" 2>&1 )
+    local rc=$?
+    echo "== pmct $key $grp rc=$rc"
+    case $rc in 0) ;; *) tail -5 "$d.p$k.log"; exit $rc ;; esac
+  done
+  python3 "$R/tools/pmc_summary.py" "$d" --frames $((1 << log2n)) --out "$d.json" --traffic --key "$key" \
+    --profile "profiles/$TAG/pmc_$key.json" > /dev/null && rm -rf "$d" && cp "$R/profiles/pmc_traffic.json" "$O/"
+}
