@@ -38,7 +38,9 @@ extern __shared__ __attribute__((aligned(16))) uint8_t pcn_smem[];
 // 1 parse only, 2 + field lookups, 3 + summary AND, 4 full minus counters,
 // 5 full minus the end-of-launch counter flush, 6 full minus the per-rule
 // counter bins, 7 per-rule bins by plain stores (wrong counts; cost of the atomic),
-// 8 full minus the global atomics of the rule ids past the LDS bins.
+// 8 full minus the global atomics of the rule ids past the LDS bins,
+// 9 global counter adds (flush and ids past the bins) without the byte word
+// (wrong byte counts; what one packed atomic per counter pair would save).
 #ifndef PCN_ABLATE
 #define PCN_ABLATE 0
 #endif
@@ -1289,7 +1291,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         } else if (PCN_ABLATE != 8) {   // (8: measurement, no global atomics for the ids past the bins)
           unsigned long long *const cr = ch.ctr + (blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;
           atomicAdd(&cr[2 + 2 * rid], 1ull);
-          atomicAdd(&cr[3 + 2 * rid], static_cast<unsigned long long>(L));
+          if (PCN_ABLATE != 9) atomicAdd(&cr[3 + 2 * rid], static_cast<unsigned long long>(L));
         }
       }
     }
@@ -1354,7 +1356,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       if (!dst) continue;
     }
     atomicAdd(dst, pk);
-    atomicAdd(dst + 1, by);
+    if (PCN_ABLATE != 9) atomicAdd(dst + 1, by);
   }
 }
 
