@@ -20,13 +20,6 @@ ktrace ktrace_cfg3_24 3 24 30
 ktrace ktrace_cfg2_20 2 20 100
 ktrace ktrace_cfg5_22 5 22 30 xdp
 ktrace ktrace_cfg5_22_tc 5 22 30 tc
-# one atomic per counter pair instead of two: the upper bound of the saving (wrong byte counts)
-run ab_ctr_cfg5 300 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
-  --variants "jit,jit:-DPCN_ABLATE=9,jit:-DPCN_ABLATE=5,jit,jit:-DPCN_ABLATE=9"
-run ab_ctr_cfg3 300 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0.5 --iters 30 \
-  --variants "jit,jit:-DPCN_ABLATE=9,jit:-DPCN_ABLATE=5,jit,jit:-DPCN_ABLATE=9"
-run ab_ctr_cfg2 300 python -u tools/ablate.py --cfg 2 --log2n 20 --hits 0.5 --iters 50 \
-  --variants "jit,jit:-DPCN_ABLATE=9,jit:-DPCN_ABLATE=5,jit,jit:-DPCN_ABLATE=9"
 ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_bench" -o run \
     -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu > "$O/prof_bench.log" 2>&1 )
 echo "== prof_bench rc=$?"
