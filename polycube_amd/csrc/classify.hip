@@ -1289,9 +1289,14 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
           else atomicAdd(&bins[b], 1u);
           if (!FIXED) atomicAdd(&byte_bins[b], L);
         } else if (PCN_ABLATE != 8) {   // (8: measurement, no global atomics for the ids past the bins)
-          unsigned long long *const cr = ch.ctr + (blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;
-          atomicAdd(&cr[2 + 2 * rid], 1ull);
-          if (PCN_ABLATE != 9) atomicAdd(&cr[3 + 2 * rid], static_cast<unsigned long long>(L));
+          if (a.ctr_pack_off) {         // one packed pair into this workgroup's copy
+            unsigned long long *const cp =
+                ch.ctr + a.ctr_pack_off + static_cast<uint64_t>(blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;
+            atomicAdd(&cp[1 + rid], (1ull << kCtrPackShift) | L);
+          } else {
+            atomicAdd(&ch.ctr[2 + 2 * rid], 1ull);
+            if (PCN_ABLATE != 9) atomicAdd(&ch.ctr[3 + 2 * rid], static_cast<unsigned long long>(L));
+          }
         }
       }
     }
@@ -1334,29 +1339,40 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // starts at its own rotation of the bins so the global atomics of
   // concurrent flushes mostly land on different addresses.
   const uint32_t rot = PCN_FLUSH_ROT ? (blockIdx.x * 97u) % a.nbins : 0u;
-  const uint64_t rep = static_cast<uint64_t>(blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;   // this copy
+  const uint64_t rep = a.ctr_pack_off + static_cast<uint64_t>(blockIdx.x & a.ctr_rep_mask) * a.ctr_rep_words;
   for (uint32_t b0 = threadIdx.x; b0 < a.nbins; b0 += blockDim.x) {
     const uint32_t b = b0 + rot < a.nbins ? b0 + rot : b0 + rot - a.nbins;
     const unsigned long long pk = bins[b];
     const unsigned long long by = FIXED ? pk * a.fixed_len : byte_bins[b];
     if (!pk) continue;
-    unsigned long long *dst = nullptr;
+    unsigned long long *blk = nullptr;   // a chain's counter block, pair `pair` (0: default)
+    uint32_t pair = 0;
     if (b < 3) {
-      dst = a.ch[b].ctr + rep;
+      blk = a.ch[b].ctr;
     } else {
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const DevChain &ch = c == CH ? run_ch : a.ch[c];
         if (ch.lds_bins >= 0 && b >= static_cast<uint32_t>(ch.lds_bins) &&
-            b < static_cast<uint32_t>(ch.lds_bins) + ch.lds_nrules)
-          dst = ch.ctr + rep + 2 + 2 * (b - static_cast<uint32_t>(ch.lds_bins));
+            b < static_cast<uint32_t>(ch.lds_bins) + ch.lds_nrules) {
+          blk = ch.ctr;
+          pair = 1 + (b - static_cast<uint32_t>(ch.lds_bins));
+        }
       }
-      if (a.hz_bins >= 0 && b >= static_cast<uint32_t>(a.hz_bins) && a.horus_ctr)
-        dst = a.horus_ctr + 2 * (b - static_cast<uint32_t>(a.hz_bins));
-      if (!dst) continue;
+      if (a.hz_bins >= 0 && b >= static_cast<uint32_t>(a.hz_bins) && a.horus_ctr) {   // Horus: one plain block
+        unsigned long long *const dst = a.horus_ctr + 2 * (b - static_cast<uint32_t>(a.hz_bins));
+        atomicAdd(dst, pk);
+        atomicAdd(dst + 1, by);
+        continue;
+      }
+      if (!blk) continue;
     }
-    atomicAdd(dst, pk);
-    if (PCN_ABLATE != 9) atomicAdd(dst + 1, by);
+    if (a.ctr_pack_off) {
+      atomicAdd(blk + rep + pair, pk << kCtrPackShift | by);
+    } else {
+      atomicAdd(blk + 2 * pair, pk);
+      if (PCN_ABLATE != 9) atomicAdd(blk + 2 * pair + 1, by);
+    }
   }
 }
 
@@ -1401,7 +1417,8 @@ void launch_ns(const LaunchArgs &a, int ch, int, unsigned grid, size_t lds, hipS
 // reach the rule stage (0..2) or 3 for INPUT+FORWARD.  `jit` (a hipFunction_t
 // or null) is the chain program compiled for exactly this launch shape
 // (jit.cpp); null runs the generic variant.  Returns a hipError_t.
-int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream) {
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream,
+                    CopyBound *cb) {
   if (a.n == 0) return hipSuccess;
   const size_t lds = a.lds_bytes;
   const bool in_lds = a.lds_images_bytes > 0;
@@ -1422,14 +1439,34 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
   const uint64_t cap = static_cast<uint64_t>(num_cus) * per_cu;
   const unsigned grid = static_cast<unsigned>(want < cap ? want : cap);
   // u32 histogram bins: at most 2^32-1 bytes per workgroup per launch, so a
-  // batch whose workgroups could exceed that is split into launches.
+  // batch whose workgroups could exceed that is split into launches; so is
+  // one that could fill more than half of a packed counter copy's fields
+  // (each copy takes the flushes of `wpc` workgroups).
   const uint64_t max_len = a.lens ? 65535u : (a.fixed_len ? a.fixed_len : 1u);
+  const uint64_t wpc = (grid + uint64_t(a.ctr_rep_mask)) / (uint64_t(a.ctr_rep_mask) + 1);
   // (a workgroup takes whole kBlock-frame rows of the grid stride)
-  const uint64_t per_block = 0xFFFFFFFFull / max_len / kBlock * kBlock;
+  uint64_t per_block = 0xFFFFFFFFull / max_len;
+  if (cb && a.ctr_pack_off) {
+    per_block = std::min<uint64_t>(per_block, (cb->max_pkts / 2) / wpc);
+    per_block = std::min<uint64_t>(per_block, (cb->max_bytes / 2) / (wpc * max_len));
+  }
+  per_block = std::max<uint64_t>(per_block / kBlock * kBlock, kBlock);
   const uint64_t chunk = per_block * grid;
   for (uint64_t base = 0; base < a.n; base += chunk) {
     LaunchArgs c = a;
     c.n = a.n - base < chunk ? a.n - base : chunk;
+    if (cb && a.ctr_pack_off) {
+      // the most any one copy takes from this launch; fold first if the copies
+      // could overflow (cb->fold resets the bound)
+      const uint64_t fw = (c.n + uint64_t(grid) * kBlock - 1) / (uint64_t(grid) * kBlock) * kBlock;
+      const uint64_t pk = wpc * fw, by = pk * max_len;
+      if (cb->pkts + pk > cb->max_pkts || cb->bytes + by > cb->max_bytes) {
+        const int e = cb->fold(cb->ctx, static_cast<void *>(stream));
+        if (e != hipSuccess) return e;
+      }
+      cb->pkts += pk;
+      cb->bytes += by;
+    }
     if (a.has_stale) {   // contiguous chunks per workgroup, claimed in start order
       c.gbase = base;
       c.chunk_frames = (c.n + uint64_t(grid) * kBlock - 1) / (uint64_t(grid) * kBlock) * kBlock;
@@ -1463,23 +1500,31 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
   return hipSuccess;
 }
 
-// Fold counter copies 1..reps-1 into copy 0 and zero them (LaunchArgs::ctr_rep_mask).
-__global__ void fold_reps_kernel(unsigned long long *ctr, uint64_t words, uint64_t stride, uint32_t reps) {
+// Fold the packed counter copies (LaunchArgs::ctr_pack_off) into the plain
+// block: pair i of every copy is taken with an atomic exchange (a classify on
+// another stream may be adding meanwhile) and unpacked on its own (the sum of
+// the copies could overflow a field), then added to pair i of the block.
+__global__ void fold_reps_kernel(unsigned long long *ctr, uint64_t pairs, uint64_t pack_off, uint64_t stride,
+                                 uint32_t reps) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= words) return;
-  // atomics: a classify on another stream may be adding to the copies meanwhile
-  unsigned long long s = 0;
-  for (uint32_t r = 1; r < reps; ++r) {
-    unsigned long long *p = ctr + r * stride + i;
-    if (*p) s += atomicExch(p, 0ull);
+  if (i >= pairs) return;
+  unsigned long long pk = 0, by = 0;
+  for (uint32_t r = 0; r < reps; ++r) {
+    unsigned long long *p = ctr + pack_off + r * stride + i;
+    if (!*p) continue;
+    const unsigned long long w = atomicExch(p, 0ull);
+    pk += w >> kCtrPackShift;
+    by += w & kCtrPackBytesMask;
   }
-  if (s) atomicAdd(&ctr[i], s);
+  if (pk) atomicAdd(&ctr[2 * i], pk);
+  if (by) atomicAdd(&ctr[2 * i + 1], by);
 }
 
-int launch_fold_reps(unsigned long long *ctr, uint64_t words, uint64_t stride, uint32_t reps, hipStream_t stream) {
-  if (reps <= 1 || words == 0) return hipSuccess;
-  const unsigned grid = static_cast<unsigned>((words + 255) / 256);
-  hipLaunchKernelGGL(fold_reps_kernel, dim3(grid), dim3(256), 0, stream, ctr, words, stride, reps);
+int launch_fold_reps(unsigned long long *ctr, uint64_t pairs, uint64_t pack_off, uint64_t stride, uint32_t reps,
+                     hipStream_t stream) {
+  if (pairs == 0) return hipSuccess;
+  const unsigned grid = static_cast<unsigned>((pairs + 255) / 256);
+  hipLaunchKernelGGL(fold_reps_kernel, dim3(grid), dim3(256), 0, stream, ctr, pairs, pack_off, stride, reps);
   return static_cast<int>(hipGetLastError());
 }
 

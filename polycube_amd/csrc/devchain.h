@@ -191,13 +191,34 @@ struct LaunchArgs {
   uint32_t stale_epoch;          // this batch's publication epoch (24 bits, never 0)
   uint32_t *carry_out;           // non-null on a batch's last launch: its last workgroup writes the
                                  // ports the batch leaves to the next one (the carry, Q4)
-  // Counter replicas: workgroup b adds its counters into the copy of every
-  // chain's block at ch[c].ctr + (b & ctr_rep_mask) * ctr_rep_words; the host
-  // folds the copies into copy 0 before it reads a block (pcn_ipt.cpp).
+  // Counter replicas: workgroup b adds each (packets, bytes) pair of its
+  // counters as ONE u64, packets << kCtrPackShift | bytes, into word p (p = 0
+  // default, 1 + rule id) of copy b & ctr_rep_mask at ch[c].ctr + ctr_pack_off
+  // + (b & ctr_rep_mask) * ctr_rep_words.  The host folds the copies into the
+  // plain block at ch[c].ctr before it reads one, and often enough that no
+  // field of a copy can overflow (pcn_ipt.cpp, fold_counters / pack_bound).
   // Workgroups of a short launch finish together, and their flushes, all on
-  // one block, serialised on the same few lines.
+  // one block, serialised on the same few lines; the packed pair halves the
+  // global atomics of the flush and of the rule ids past the LDS bins.
+  // ctr_pack_off 0: plain pairs straight into ch[c].ctr (stage A's scratch).
   uint32_t ctr_rep_mask;         // copies - 1 (a power of two; 0: one copy)
-  uint32_t ctr_rep_words;        // u64 words between copies
+  uint32_t ctr_rep_words;        // u64 words between packed copies
+  uint32_t ctr_pack_off;         // u64 words from ch[c].ctr to packed copy 0; 0: unpacked
+};
+
+// Packed counter pair: packets in bits 38-63, bytes in bits 0-37.
+constexpr uint32_t kCtrPackShift = 38;
+constexpr unsigned long long kCtrPackBytesMask = (1ull << kCtrPackShift) - 1;
+constexpr unsigned long long kCtrPackPktsMax = (1ull << (64 - kCtrPackShift)) - 1;
+
+// Host side of the packed copies (launch_classify): upper bounds of what any
+// one copy holds since the last fold, and the fold to run before a launch
+// that could overflow a field (it resets both bounds).
+struct CopyBound {
+  unsigned long long pkts, bytes;
+  unsigned long long max_pkts, max_bytes;   // the fields' capacity (lower: a test hook)
+  int (*fold)(void *ctx, void *stream);   // stream: a hipStream_t
+  void *ctx;
 };
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)

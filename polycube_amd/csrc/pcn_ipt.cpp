@@ -27,10 +27,12 @@
 #include "ruleset.hpp"
 
 namespace pcn {
-int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream);
+int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream,
+                    CopyBound *cb);
 int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint64_t count, int nranks,
                      hipStream_t stream);
-int launch_fold_reps(unsigned long long *ctr, uint64_t words, uint64_t stride, uint32_t reps, hipStream_t stream);
+int launch_fold_reps(unsigned long long *ctr, uint64_t pairs, uint64_t pack_off, uint64_t stride, uint32_t reps,
+                     hipStream_t stream);
 }  // namespace pcn
 
 namespace pcn {
@@ -159,6 +161,13 @@ struct pcn_ipt {
   int num_cus = 256;
   size_t ctr_words = 0;
   uint32_t ctr_reps = 1;                       // counter copies per chain (LaunchArgs::ctr_rep_mask)
+  // Packed copies (LaunchArgs::ctr_pack_off): the most any copy can hold since
+  // the last full fold, the streams that launched into them since then, and
+  // the event a full fold uses to wait for those streams' work.
+  // With more than one stream in play each launch records an event on its
+  // stream, and the fold waits on those (no stream handle is used later).
+  CopyBound pack{};
+  std::vector<std::pair<hipStream_t, hipEvent_t>> pack_streams;
   ncclComm_t comm = nullptr;
   // the counter all-gather runs on its own stream, off the classify stream's
   // critical path: the classify stream only snapshots the counters
@@ -255,7 +264,7 @@ uint32_t counted(const pcn_ipt *ctx, uint32_t nrules) {
   return std::min(nrules, ctx->cfg.max_counted_rules);
 }
 
-// Counter copies per chain block (LaunchArgs::ctr_rep_mask): 64, or
+// Packed counter copies per chain block (LaunchArgs::ctr_rep_mask): 64, or
 // PCN_IPT_DEBUG_CTR_REPS (a power of two, measurement A/B).  A/B on config 2 at
 // 2^20 frames, 1 / 16 / 64 copies: 43.5 / 28.4 / 27.4 us a launch; config 3:
 // 213 / 209 / 207 us; config 5: 166 / 162 us (profiles/r04_s2/).
@@ -265,12 +274,53 @@ uint32_t ctr_reps_default() {
   return v >= 1 && v <= 256 && (v & (v - 1)) == 0 ? static_cast<uint32_t>(v) : 64u;
 }
 
-// Fold a chain's counter copies 1.. into copy 0 (= cs.ctr), stream-ordered;
-// every read, snapshot or clear of a block does this first.
+// Fold a chain's packed counter copies into its plain block (cs.ctr, the
+// first ctr_words words; the copies follow it), the pairs of the block's
+// first `words` words, stream-ordered; every read, snapshot or clear of a
+// block does this first.
 void fold_counters(pcn_ipt *ctx, const ChainState &cs, size_t words, hipStream_t s) {
-  if (ctx->ctr_reps <= 1 || !cs.ctr) return;
-  const int rc = launch_fold_reps(cs.ctr, words, ctx->ctr_words, ctx->ctr_reps, s);
+  if (!cs.ctr) return;
+  const int rc = launch_fold_reps(cs.ctr, (words + 1) / 2, ctx->ctr_words, ctx->ctr_words / 2, ctx->ctr_reps, s);
   if (rc != hipSuccess) throw HipError(std::string("counter fold: ") + hipGetErrorString(hipError_t(rc)));
+}
+
+// Every chain's copies folded on `stream` once the work queued so far on the
+// other streams that launched into them has run: the launches queued before
+// this fold are then all in it, so the copies hold at most what launches
+// queued after it add, which is what pcn_ipt::pack counts from zero again.
+// launch_classify calls it before a launch that could overflow a field of a
+// copy (every ~60 launches of 2^22 IMIX frames, ~250 of 2^24 64-byte frames).
+int fold_all_copies(void *c, void *stream) {
+  pcn_ipt *ctx = static_cast<pcn_ipt *>(c);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  try {
+    for (const auto &se : ctx->pack_streams)
+      if (se.first != s && se.second) hip_check(hipStreamWaitEvent(s, se.second, 0), "hipStreamWaitEvent(fold)");
+    for (const ChainState &cs : ctx->chains) fold_counters(ctx, cs, ctx->ctr_words, s);
+  } catch (const HipError &) {
+    return static_cast<int>(hipErrorUnknown);
+  }
+  // the streams stay known (their events are reused); only the bound restarts
+  ctx->pack.pkts = ctx->pack.bytes = 0;
+  return hipSuccess;
+}
+
+// Bookkeeping of a launch into the packed copies on stream s: once a second
+// stream has launched into them, every launch leaves an event behind (the
+// first stream's is recorded when the second one appears).
+void note_pack_stream(pcn_ipt *ctx, hipStream_t s) {
+  auto &v = ctx->pack_streams;
+  auto it = std::find_if(v.begin(), v.end(), [&](const auto &se) { return se.first == s; });
+  if (it == v.end()) {
+    v.emplace_back(s, nullptr);
+    it = v.end() - 1;
+  }
+  if (v.size() < 2) return;
+  for (auto &se : v) {
+    if (se.second && se.first != s) continue;
+    if (!se.second) hip_check(hipEventCreateWithFlags(&se.second, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(se.second, se.first), "hipEventRecord(pack)");
+  }
 }
 
 // Upload a compiled chain into the inactive slot, then flip (Chain.cpp:441-457,924).
@@ -571,6 +621,17 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
   if (ctx->cfg.jit < -1 || ctx->cfg.jit > 1) return fail(-EINVAL, "jit must be -1, 0 or 1");
   ctx->ctr_words = 2 + 2 * size_t(ctx->cfg.max_counted_rules);
   ctx->ctr_reps = ctr_reps_default();
+  ctx->pack.fold = fold_all_copies;
+  ctx->pack.ctx = ctx.get();
+  ctx->pack.max_pkts = kCtrPackPktsMax;
+  ctx->pack.max_bytes = kCtrPackBytesMask;
+  if (const char *e = std::getenv("PCN_IPT_DEBUG_PACK_MAX_PKTS")) {   // test hook: fold every few launches
+    const unsigned long long v = std::strtoull(e, nullptr, 10);
+    if (v >= 4096 && v < kCtrPackPktsMax) {
+      ctx->pack.max_pkts = v;
+      ctx->pack.max_bytes = v * 64;
+    }
+  }
   if (cfg->device >= 0) {
     try {
       int ndev = 0;
@@ -597,8 +658,10 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
       hip_check(hipMalloc(&ctx->d_hz_carry, 64), "hipMalloc(horus carry)");
       hip_check(hipMemset(ctx->d_hz_carry, 0, 64), "hipMemset(horus carry)");
       for (auto &cs : ctx->chains) {
-        hip_check(hipMalloc(&cs.ctr, ctx->ctr_reps * ctx->ctr_words * 8), "hipMalloc(counters)");
-        hip_check(hipMemset(cs.ctr, 0, ctx->ctr_reps * ctx->ctr_words * 8), "hipMemset(counters)");
+        // the plain block, then ctr_reps packed copies of ctr_words / 2 pairs
+        const size_t words = ctx->ctr_words + size_t(ctx->ctr_reps) * (ctx->ctr_words / 2);
+        hip_check(hipMalloc(&cs.ctr, words * 8), "hipMalloc(counters)");
+        hip_check(hipMemset(cs.ctr, 0, words * 8), "hipMemset(counters)");
         hip_check(hipMalloc(&cs.ctr_global, ctx->ctr_words * 8), "hipMalloc(counters)");
         hip_check(hipMemset(cs.ctr_global, 0, ctx->ctr_words * 8), "hipMemset(counters)");
       }
@@ -644,6 +707,8 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
       if (ctx->ev_g1[k]) (void)hipEventDestroy(ctx->ev_g1[k]);
     }
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
+    for (auto &se : ctx->pack_streams)
+      if (se.second) (void)hipEventDestroy(se.second);
     for (void *p : {static_cast<void *>(ctx->hz[0].d_tab), static_cast<void *>(ctx->hz[0].d_ctr),
                     static_cast<void *>(ctx->hz[1].d_tab), static_cast<void *>(ctx->hz[1].d_ctr),
                     static_cast<void *>(ctx->d_hz_carry), static_cast<void *>(ctx->d_stale_desc),
@@ -1011,8 +1076,10 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.rule_ids = sa ? sa->rule_ids : b->rule_ids;
     if (sa)
       for (int c = 0; c < PCN_IPT_NCHAINS; ++c) a.ch[c].ctr = ctx->ctr_scratch + c * ctx->ctr_words;
-    a.ctr_rep_mask = sa ? 0u : ctx->ctr_reps - 1;   // (stage A's scratch counters are one copy)
-    a.ctr_rep_words = static_cast<uint32_t>(ctx->ctr_words);
+    // packed copies after each chain's plain block (stage A's scratch counters: plain adds)
+    a.ctr_rep_mask = sa ? 0u : ctx->ctr_reps - 1;
+    a.ctr_rep_words = static_cast<uint32_t>(ctx->ctr_words / 2);
+    a.ctr_pack_off = sa ? 0u : static_cast<uint32_t>(ctx->ctr_words);
     a.localip = ctx->d_localip;
     a.n = b->n;
     a.stride = b->stride;
@@ -1127,7 +1194,9 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     }
     if (plan) return 0;
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
-    int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, static_cast<hipStream_t>(stream));
+    const hipStream_t hs = static_cast<hipStream_t>(stream);
+    int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, hs, sa ? nullptr : &ctx->pack);
+    if (!rc && !sa) note_pack_stream(ctx, hs);
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
     return 0;
   }

@@ -327,6 +327,36 @@ def test_u32_bins_split_launch_counts_exactly(dev):
     del offsets, lens, v, r
 
 
+def test_packed_counter_copies_fold_across_launches_and_streams(dev, monkeypatch):
+    """Each workgroup adds a counter pair as one packed u64 (packets << 38 |
+    bytes) into its copy of the chain's block; the host folds the copies into
+    the plain block before any field could overflow.  With the test limit of
+    2^14 packets per copy a 2^20-frame launch splits in two and every launch
+    folds first, after waiting for the other stream's launches (two streams
+    alternate).  Every counter must equal the oracle's over all launches."""
+    monkeypatch.setenv("PCN_IPT_DEBUG_PACK_MAX_PKTS", str(1 << 14))
+    rs = synth.config_rules(3)
+    rules = rs.rules()
+    o, ipt = make_pair({1: rules}, {1: "DROP"})
+    n = 1 << 20
+    frames = synth.config_frames(3, n, rs).reshape(-1)
+    tf = torch.from_numpy(frames).to(dev)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k in range(6):
+        outs.append(ipt.classify(tf, n=n, stream=streams[k % 2].cuda_stream))
+        o.classify(frames, n=n, nthreads=NTHREADS)
+    torch.cuda.synchronize()
+    assert_counters(o, ipt, chains=(1,), n=len(rules))
+    # IMIX lengths: the byte field bounds the copies (test limit 2^20 bytes)
+    n5 = 1 << 17
+    buf, offsets, lens = synth.imix_frames(rs, n5, 7)
+    for k in range(4):
+        v_o, r_o, v_g, r_g = run_both(o, ipt, dev, buf, n5, offsets=offsets, lens=lens)
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_counters(o, ipt, chains=(1,), n=len(rules))
+
+
 def test_localip_input_output_from_lds(dev):
     """INPUT/OUTPUT selection by a 200-address localip set staged in LDS."""
     rs = synth.config_rules(2)

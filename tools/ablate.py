@@ -101,6 +101,8 @@ def main():
             env["PCN_IPT_JIT_DEFS"] = f"-DPCN_ABLATE={var[3:]}"
         elif var == "product":
             lib = ""
+        elif var.startswith("lib:"):   # lib:NAME: polycube_amd/build/ab/libpcn_ipt_NAME.so, chain programs on
+            lib, jit = os.path.join(ROOT, "polycube_amd", "build", "ab", f"libpcn_ipt_{var[4:]}.so"), 1
         elif var.startswith("exp_"):   # another build of the product library (A/B), chain programs on
             lib, jit = os.path.join(ROOT, "polycube_amd", "build", f"libpcn_ipt_{var.split(':')[0]}.so"), 1
         else:
