@@ -98,3 +98,19 @@ pmct() {
   python3 "$R/tools/pmc_summary.py" "$d" --frames $((1 << log2n)) --out "$d.json" --traffic --key "$key" \
     --profile "profiles/$TAG/pmc_$key.json" > /dev/null && rm -rf "$d" && cp "$R/profiles/pmc_traffic.json" "$O/"
 }
+
+# One PMC pass over the stateful probe (tools/ct_probe.py), summarised per kernel:
+# pmcct <name> "<counters>" "<kernel substrings...>" -> $O/<name>_<kernel>.json
+pmcct() {
+  local name=$1 ctrs=$2 kernels=$3
+  mkdir -p "$O/$name"
+  ( cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d "$O/$name/p1" -o run \
+      -- python3 "$R/tools/ct_probe.py" --steps 3 > "$O/$name.log" 2>&1 )
+  local rc=$?
+  echo "== pmcct $name rc=$rc"
+  case $rc in 0) ;; *) tail -5 "$O/$name.log"; exit $rc ;; esac
+  for k in $kernels; do
+    python3 "$R/tools/pmc_summary.py" "$O/$name" --kernel "$k" --frames $((1 << 24)) --out "$O/${name}_$k.json" > /dev/null
+  done
+  rm -rf "$O/$name"
+}

@@ -47,12 +47,13 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--key", default="config3", help="pmc_traffic.json entry: config2 / config3 / config5 / config5_tc")
     ap.add_argument("--profile", default="", help="where the passes' summaries are committed (profiles/...)")
+    ap.add_argument("--kernel", default="classify", help="summarise the dispatches whose name contains this")
     a = ap.parse_args()
     if a.tag_dir.endswith(".json"):   # a summary this script wrote on the GPU box (--out)
         with open(a.tag_dir) as fh:
             s = json.load(fh)
     else:
-        s = collect(a.tag_dir)
+        s = collect(a.tag_dir, a.kernel)
     if "FETCH_SIZE" in s:
         s["hbm_read_bytes_per_launch"] = s["FETCH_SIZE"] * 1024 * 2
         s["hbm_read_bytes_per_pkt"] = s["hbm_read_bytes_per_launch"] / a.frames
