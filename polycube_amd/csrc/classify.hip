@@ -255,8 +255,6 @@ __device__ __forceinline__ bool localip_has(const LaunchArgs &a, uint32_t ip) {
 // bits gives the boundaries inside it, then a branchless upper-bound search
 // of `steps` (wave-uniform; unrolled in a chain program) probes finds the
 // interval.
-// A bucket entry is (count << 16) | first boundary, or, when the bucket holds
-// no boundary, the class of the one interval it lies in (count 0).
 // Window mode (win != 0): the bucket's <= win boundaries are read at once
 // and counted; boundaries past the bucket (the next buckets', or the
 // 0xFFFFFFFF padding) exceed every address in it, except that the padding
@@ -265,9 +263,6 @@ template <bool LDS>
 __device__ __forceinline__ uint32_t ip_class(const Tab<LDS> &t, uint32_t bkt, uint32_t shift, uint32_t steps,
                                              uint32_t win, uint32_t bnd, uint32_t cls, uint32_t h) {
   const uint32_t e = t.u32(bkt, 4 * (h >> shift));
-  // a bucket without a boundary is one interval: its entry is that class
-  // (count 0), so those lanes skip the boundary and class reads
-  if ((e >> 16) == 0) return e & 0xFFFFu;
   if (win) {
     const uint32_t first = e & 0xFFFFu;
     uint32_t n = 0;

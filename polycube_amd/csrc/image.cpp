@@ -317,10 +317,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     }
     const uint32_t nb = 1u << bits;
     std::vector<uint32_t> bkt(nb);
-    // a bucket without a boundary holds its interval's class (count 0: the
-    // kernel reads no boundary and no class for it)
-    for (uint32_t b = 0; b < nb; ++b)
-      bkt[b] = first[b + 1] > first[b] ? ((first[b + 1] - first[b]) << 16) | first[b] : uint32_t(cls[first[b]]);
+    for (uint32_t b = 0; b < nb; ++b) bkt[b] = ((first[b + 1] - first[b]) << 16) | first[b];
     lay.ip_shift[side] = 32 - bits;
     lay.ip_steps[side] = steps;
     lay.ip_win[side] = win;

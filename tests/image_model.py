@@ -44,8 +44,6 @@ class ImageModel:
     def ip_class(self, side, h):
         L = self.lay
         e = self.u32(L[f"ip_bkt{side}"] + 4 * (h >> L[f"ip_shift{side}"]))
-        if e >> 16 == 0:                  # a bucket without a boundary: its interval's class
-            return e & 0xFFFF
         win = L[f"ip_win{side}"]
         if win:
             first = e & 0xFFFF

@@ -29,4 +29,9 @@ ktrace ktrace_cfg5_22_tc 5 22 30 tc
     -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu > "$O/prof_bench.log" 2>&1 )
 echo "== prof_bench rc=$?"
 find "$O" -name "*kernel_trace.csv" -delete
+# per-kernel counters of the stateful pipeline (ct_prep, ct_walk, ct_heads, ct_count)
+K="ct_prep ct_walk ct_heads ct_count"
+pmcct ct_fetch "FETCH_SIZE" "$K"
+pmcct ct_write "WRITE_SIZE" "$K"
+pmcct ct_sq "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU" "$K"
 exit 0

@@ -2,8 +2,8 @@
 # Round 4, session 9 + final evidence in one call (GPU boxes are scarce): IP bucket
 # entries that hold the class of a bucket without a boundary -- every GPU test and the
 # smoke on it, A/B against the previous build (build/ab/libpcn_ipt_base.so) on configs
-# 3, 5, 2; then the HEAD evidence: PMC traffic into profiles/pmc_traffic.json, bench
-# lines, 2-rank self-launch, kernel traces, rocprof stats of the bench.
+# 3, 5, 2; then the evidence of that build (not kept: the A/B lost on config 3, so
+# tools/sessions/r04_final.sh reruns the evidence part on the reverted tree).
 TAG=r04_final
 source "$(dirname "$0")/../gpu_lib.sh"
 KEEP_GOING=1
