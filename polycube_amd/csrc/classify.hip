@@ -457,10 +457,14 @@ __device__ __forceinline__ void pin_regs(u32x4 (&r)[N]) {
 // second item's dependent LDS chain runs in the shadow of the first's.
 // 1: fixed-stride launches (their wave region is the 3 KB transpose buffer);
 // 2: every launch whose wave region holds the 128 items (LaunchArgs::wave_bytes).
+// Chain programs of chains with two or more summary blocks get 2 (jit.cpp:
+// config 5's 10k rules deal ~200 candidates a wave), others 0 (config 3 at
+// hit rate 0.5 deals fewer than 64 a wave, and the larger program cost 1.5 %).
 #ifndef PCN_DEAL2
 #define PCN_DEAL2 0
 #endif
 constexpr uint32_t kDeal2Bytes = 64 * 4 + 128 * 16;   // best[64] + item[128]
+static_assert(kDeal2Bytes == PCN_DEAL2_WAVE_BYTES, "the host sizes the wave region for the 128-item window");
 struct WaveScratch {
   uint32_t best[64];     // per owner lane: min (rule id << 1 | action)
   u32x4 item[64];        // (owner lane << 16 | candidate word, the owner's classes as u16 pairs)

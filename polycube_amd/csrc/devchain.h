@@ -47,6 +47,8 @@
                                     // reused as the candidate-stage scratch
 #define PCN_WAVE_SCRATCH_BYTES 1280 // the candidate-stage scratch alone: the whole region of a launch
                                     // without the fixed-stride header transpose
+#define PCN_DEAL2_WAVE_BYTES 2304   // the scratch of a 128-candidate deal window (classify.hip PCN_DEAL2):
+                                    // chain programs of chains with 2+ summary blocks
 
 #if defined(__HIPCC__) || defined(__HIPCC_RTC__)
 #define PCN_HD __host__ __device__

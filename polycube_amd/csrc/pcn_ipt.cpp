@@ -82,7 +82,7 @@ uint32_t partial_rule_bins(uint32_t used, uint32_t per_bin, uint32_t ncounted) {
   return nb < ncounted ? nb : ncounted;
 }
 
-uint32_t wave_region_bytes(bool fixed) {
+uint32_t wave_region_bytes(bool fixed, bool deal2) {
   static const uint32_t v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_WAVE_BYTES");
     return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : uint32_t(PCN_WAVE_LDS_BYTES);
@@ -93,7 +93,8 @@ uint32_t wave_region_bytes(bool fixed) {
     const char *e = std::getenv("PCN_IPT_DEBUG_WAVE_BYTES_GENERIC");
     return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : uint32_t(PCN_WAVE_SCRATCH_BYTES);
   }();
-  return fixed ? v : g;
+  // a chain program with the 128-candidate deal window (jit.cpp) needs its scratch
+  return fixed ? v : deal2 ? std::max<uint32_t>(g, PCN_DEAL2_WAVE_BYTES) : g;
 }
 
 struct ImageSlot {
@@ -1022,8 +1023,10 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.nlocal = static_cast<uint32_t>(ctx->localip.size());
     // counter bins: u32 pkts, plus u32 bytes unless every frame has the same length
     const uint32_t bin_bytes = (fixed ? 4 : 8) * a.nbins;
+    // the chain program of a chain with 2+ summary blocks deals 128 candidates a pass (jit.cpp)
+    const bool deal2 = ch < 3 && any_rules && a.ch[ch].nsw >= 2 && ctx->cfg.jit >= 0;
     const uint32_t tail = (bin_bytes + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * wave_region_bytes(fixed);
+                          (PCN_BLOCK / 64) * wave_region_bytes(fixed, deal2);
     // whole images if they fit, else their per-packet prefix [0, pbase) (the
     // candidate-stage tables are then read from L2/HBM), else nothing
     uint32_t img_bytes = 0;
@@ -1060,7 +1063,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.bins_offset = kLdsDescBytes + img_bytes;
     a.lds_localip = a.bins_offset + (all_bin_bytes + 15) / 16 * 16;
     a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
-    a.wave_bytes = wave_region_bytes(fixed);
+    a.wave_bytes = wave_region_bytes(fixed, deal2);
     a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;

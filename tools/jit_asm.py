@@ -60,7 +60,8 @@ def spec_for(cfg, imix=False, inputs=0):
     limit = lay[LAYOUT.index("pbase")] if imix else lay[0]
     return (f"#pragma once\n#define PCN_JIT_FIXED {'false' if imix else 'true'}\n#define PCN_JIT_LDS true\n#define PCN_JIT_CH 1\n"
             f"#define PCN_JIT_NS {ns}\n#define PCN_JIT_INPUTS {inputs}\n#define PCN_JIT_CHAIN {{{vals}, nullptr, nullptr, {info['nrules']}u, {nrw}u, "
-            f"{nsw}u, {present}u, {info['nvec']}u, {all_cls}u, {ncounted}u, 10000u, 0, 0u, {limit}u, {lds_bins}}}\n")
+            f"{nsw}u, {present}u, {info['nvec']}u, {all_cls}u, {ncounted}u, 10000u, 0, 0u, {limit}u, {lds_bins}}}\n"
+            + ("#ifndef PCN_DEAL2\n#define PCN_DEAL2 2\n#endif\n" if nsw >= 2 else ""))   # as jit.cpp
 
 
 def main():

@@ -9,6 +9,13 @@ source "$(dirname "$0")/../gpu_lib.sh"
 KEEP_GOING=1
 pytest_gpu tests_all 900 tests
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+# the two-item deal for chains of 2+ summary blocks (config 5) against the build
+# without it (build/ab/libpcn_ipt_base.so); config 3 (one block) as a control
+run ab_deal2_cfg5 300 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5,1 --iters 30 \
+  --variants "jit,lib:base,jit,lib:base"
+CFG5_HOOK=tc run ab_deal2_cfg5_tc 300 python -u tools/ablate.py --cfg 5 --log2n 22 --hits 0.5 --iters 30 \
+  --variants "jit,lib:base,jit,lib:base"
+run ab_deal2_cfg3 300 python -u tools/ablate.py --cfg 3 --log2n 24 --hits 0.5 --iters 30 --variants "jit,lib:base"
 KEEP_GOING=0
 pmct config3 3 24
 pmct config2 2 20
