@@ -165,8 +165,8 @@ struct pcn_ipt {
   // Packed copies (LaunchArgs::ctr_pack_off): the most any copy can hold since
   // the last full fold, the streams that launched into them since then, and
   // the event a full fold uses to wait for those streams' work.
-  // Each launch records an event on its stream (one event per stream), and
-  // the fold waits on those (no stream handle is used later).
+  // With more than one stream in play each launch records an event on its
+  // stream, and the fold waits on those (no stream handle is used later).
   CopyBound pack{};
   std::vector<std::pair<hipStream_t, hipEvent_t>> pack_streams;
   ncclComm_t comm = nullptr;
@@ -306,9 +306,9 @@ int fold_all_copies(void *c, void *stream) {
   return hipSuccess;
 }
 
-// Bookkeeping of a launch into the packed copies on stream s: an event
-// recorded after it on its stream, reused per stream, so a later full fold
-// waits on events only and never uses a stream handle that may be gone.
+// Bookkeeping of a launch into the packed copies on stream s: once a second
+// stream has launched into them, every launch leaves an event behind (the
+// first stream's is recorded when the second one appears).
 void note_pack_stream(pcn_ipt *ctx, hipStream_t s) {
   auto &v = ctx->pack_streams;
   auto it = std::find_if(v.begin(), v.end(), [&](const auto &se) { return se.first == s; });
@@ -316,8 +316,12 @@ void note_pack_stream(pcn_ipt *ctx, hipStream_t s) {
     v.emplace_back(s, nullptr);
     it = v.end() - 1;
   }
-  if (!it->second) hip_check(hipEventCreateWithFlags(&it->second, hipEventDisableTiming), "hipEventCreate");
-  hip_check(hipEventRecord(it->second, s), "hipEventRecord(pack)");
+  if (v.size() < 2) return;
+  for (auto &se : v) {
+    if (se.second && se.first != s) continue;
+    if (!se.second) hip_check(hipEventCreateWithFlags(&se.second, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(se.second, se.first), "hipEventRecord(pack)");
+  }
 }
 
 // Upload a compiled chain into the inactive slot, then flip (Chain.cpp:441-457,924).
