@@ -187,7 +187,14 @@ int pcn_ipt_chain_get_image(pcn_ipt *ctx, int chain, uint8_t *buf, uint32_t cap,
                             uint32_t desc_cap);
 
 /* ---- datapath ---------------------------------------------------------- */
-/* Classify a batch (device pointers), stream = hipStream_t (NULL = default). */
+/* Classify a batch (device pointers), stream = hipStream_t (NULL = default).
+ * Batches may come on several streams.  A stream that has carried a batch
+ * must stay valid until a batch on another stream follows it (or the context
+ * is destroyed): the first batch on a second stream records an event on the
+ * earlier one, so a later fold of the per-workgroup counter copies can wait
+ * for its work (pcn_ipt.cpp note_pack_stream).  Each batch afterwards records
+ * one on its own stream; with a single stream none is recorded, since an
+ * event per launch costs ~3-4 us of GPU time (profiles/r04_final2/). */
 int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *batch, void *stream);
 /* Wait for all work this context queued. */
 int pcn_ipt_synchronize(pcn_ipt *ctx);
