@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--p-icmp", type=float, default=0.1)
     ap.add_argument("--p-err", type=float, default=0.02)
     ap.add_argument("--p-noise", type=float, default=0.05)
+    ap.add_argument("--cap-log2", type=int, default=20, help="connection table slots (pcn_ipt_ct_enable)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rs = synth.config_rules(3)
@@ -41,7 +42,7 @@ def main():
                               p_noise=a.p_noise)
     frames = torch.from_numpy(f).to(dev)
     v = torch.empty(n, dtype=torch.uint8, device=dev)
-    ipt.ct_enable(20)
+    ipt.ct_enable(a.cap_log2)
     ipt.ct_set_time(1_700_000_000 * 10**9)
     ipt.classify(frames, n=n, verdicts=v)
     torch.cuda.synchronize()
