@@ -1736,15 +1736,19 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
 // stamp: every stamp shares the bits above their highest difference, so the
 // digit passes start there (a batch's stamps differ in the batch index and a
 // few low bits of the batch sequence: four passes instead of six).  Pass p > 0
-// takes the next 11 bits (fewer at the bottom) below the chosen prefix and
+// takes the next kEvDigit bits (fewer at the bottom) below the chosen prefix and
 // returns at once when nothing is left to choose.  Every workgroup merges its
 // LDS histogram into the global one with one atomic per non-empty bin, and
 // the pass's last workgroup picks the digit with a block-wide scan.  (Six
 // fixed 11-bit passes of 64 workgroups took 26 us each, 0.19 ms a batch:
 // profiles/r03_s24_ev_ab.log.)
-constexpr uint32_t kEvBins = 2048;
-constexpr uint32_t kEvDigit = 11;
-constexpr int kEvPasses = 7;          // pass 0 + up to six 11-bit digits (64 bits)
+#ifndef PCN_CT_EV_DIGIT
+#define PCN_CT_EV_DIGIT 14   // A/B: 11 (seven launches a batch)
+#endif
+constexpr uint32_t kEvDigit = PCN_CT_EV_DIGIT;
+constexpr uint32_t kEvBins = 1u << kEvDigit;
+constexpr int kEvPasses = 1 + (64 + kEvDigit - 1) / kEvDigit;   // pass 0 + the digits of 64 bits
+static_assert(kEvBins % 1024 == 0, "the final scan gives each of the 1024 threads a run of bins");
 constexpr uint32_t kEvBlock = 1024;
 
 __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_t *ctl, uint32_t *hist, int p) {
@@ -1851,12 +1855,15 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
     }
     return;
   }
-  // the digit whose bin holds the k-th smallest matching stamp, by a block-wide scan
+  // the digit whose bin holds the k-th smallest matching stamp, by a block-wide
+  // scan of each thread's run of `per` bins
   const uint32_t k = ctl[kCtlEvK];
-  const uint32_t b0 = 2 * threadIdx.x;                 // this thread's two bins
-  const uint32_t c0 = __hip_atomic_load(&hp[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t c1 = __hip_atomic_load(&hp[b0 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  scan[threadIdx.x] = c0 + c1;
+  constexpr uint32_t per = kEvBins / kEvBlock;
+  const uint32_t b0 = per * threadIdx.x;               // this thread's bins
+  uint32_t mine = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < per; ++j) mine += __hip_atomic_load(&hp[b0 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  scan[threadIdx.x] = mine;
   __syncthreads();
   for (uint32_t o = 1; o < kEvBlock; o <<= 1) {        // inclusive scan
     const uint32_t v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0u;
@@ -1864,10 +1871,15 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
     scan[threadIdx.x] += v;
     __syncthreads();
   }
-  const uint32_t incl = scan[threadIdx.x], excl = incl - c0 - c1;
+  const uint32_t incl = scan[threadIdx.x], excl = incl - mine;
   if (excl < k && k <= incl) {                         // exactly one thread
-    const uint32_t d = excl + c0 >= k ? b0 : b0 + 1;
-    const uint32_t below = d == b0 ? excl : excl + c0;
+    uint32_t below = excl, d = b0;
+    for (;;) {
+      const uint32_t c = __hip_atomic_load(&hp[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (below + c >= k) break;
+      below += c;
+      ++d;
+    }
     ctl[kCtlEvK] = k - below;
     *reinterpret_cast<unsigned long long *>(ctl + kCtlEvPrefix) = prefix | (uint64_t(d) << shift);
     ctl[kCtlEvLow] = shift;
@@ -1896,143 +1908,6 @@ __global__ __launch_bounds__(256) void ct_ev_evict_kernel(CtTable t, const uint3
     ++n;
   }
   if (n) atomicAdd(&t.stats[1], static_cast<unsigned long long>(n));
-}
-
-// A table of at most 2^kLruSmallLog2 slots takes the whole LRU cut in ONE
-// workgroup and one launch: a pass that counts the live entries and finds
-// their oldest and newest stamps, radix-select passes with 14-bit digits whose
-// histograms stay in LDS (no global merge, no last-workgroup hand-off), and the
-// deletion pass.  The multi-workgroup passes above, seven launches plus the
-// eviction, took ~0.14 ms a batch on a 2^17-slot table, nearly all launch
-// gaps and merge atomics; one CU streams 8 bytes a slot per pass instead.
-constexpr uint32_t kLruSmallLog2 = 18;
-#ifndef PCN_CT_LRU_PASSES
-#define PCN_CT_LRU_PASSES 0   // 1: the multi-workgroup passes for every table size (A/B)
-#endif
-constexpr uint32_t kLruDigit = 14;
-constexpr uint32_t kLruBins = 1u << kLruDigit;   // 64 KB of LDS
-__global__ __launch_bounds__(kEvBlock) void ct_lru_small_kernel(CtTable t) {
-  __shared__ uint32_t h[kLruBins];
-  __shared__ uint32_t part[kEvBlock / 64];
-  __shared__ unsigned long long lo_s, hi_s;       // ~oldest, newest live stamp
-  __shared__ unsigned long long prefix_s;
-  __shared__ uint32_t live_s, k_s, n_s;
-  const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const uint64_t pairs = (uint64_t(1) << t.cap_log2) / 2;   // touch[] read as 16-byte pairs
-  const ulonglong2 *tp = reinterpret_cast<const ulonglong2 *>(t.touch);
-  constexpr int U = 8;                                       // loads in flight per thread
-  if (tid == 0) { live_s = 0; lo_s = 0; hi_s = 0; n_s = 0; }
-  __syncthreads();
-  // every stamp of the table, U pairs in flight per thread: f(stamp)
-  auto scan_table = [&](auto &&f) {
-    for (uint64_t i0 = tid; i0 < pairs; i0 += uint64_t(U) * kEvBlock) {
-      ulonglong2 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint64_t i = i0 + uint64_t(u) * kEvBlock;
-        v[u] = i < pairs ? tp[i] : make_ulonglong2(~0ull, ~0ull);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        f(v[u].x);
-        f(v[u].y);
-      }
-    }
-  };
-  uint32_t live = 0;
-  unsigned long long nmin = 0, mx = 0;
-  scan_table([&](unsigned long long key) {
-    if (key == ~0ull) return;
-    ++live;
-    nmin = ~key > nmin ? ~key : nmin;
-    mx = key > mx ? key : mx;
-  });
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    live += __shfl_xor(live, o);
-    const unsigned long long a = __shfl_xor(nmin, o), b = __shfl_xor(mx, o);
-    nmin = a > nmin ? a : nmin;
-    mx = b > mx ? b : mx;
-  }
-  if (lane == 0 && live) {
-    atomicAdd(&live_s, live);
-    atomicMax(&lo_s, nmin);
-    atomicMax(&hi_s, mx);
-  }
-  __syncthreads();
-  if (!t.max_entries || live_s <= t.max_entries) return;     // uniform: nothing to evict
-  // the k-th oldest live stamp (stamps are distinct): digits below the bits
-  // every live stamp shares
-  const uint64_t oldest = ~lo_s, newest = hi_s;
-  uint32_t low = oldest == newest ? 0u : 64u - static_cast<uint32_t>(__builtin_clzll(oldest ^ newest));
-  uint64_t prefix = low >= 64 ? 0ull : oldest & ~((uint64_t(1) << low) - 1);
-  uint32_t k = live_s - static_cast<uint32_t>(t.max_entries);
-  while (low > 0) {                                          // uniform
-    const uint32_t width = low < kLruDigit ? low : kLruDigit, shift = low - width;
-    const uint64_t above = low >= 64 ? 0ull : ~((uint64_t(1) << low) - 1);
-    for (uint32_t b = tid; b < kLruBins; b += kEvBlock) h[b] = 0;
-    __syncthreads();
-    scan_table([&](unsigned long long key) {
-      // LDS atomics on one address serialise, and most stamps can share a
-      // digit: the lanes with the first lane's digit add together
-      const bool in = key != ~0ull && (key & above) == prefix;
-      const uint64_t im = __ballot(in);
-      if (!im) return;
-      const uint32_t d = static_cast<uint32_t>(key >> shift) & ((1u << width) - 1);
-      const int first = static_cast<int>(__builtin_ctzll(im));
-      const uint32_t d0 = __shfl(d, first);
-      const uint64_t same = __ballot(in && d == d0);
-      if (static_cast<int>(lane) == first) atomicAdd(&h[d0], static_cast<uint32_t>(__builtin_popcountll(same)));
-      else if (in && d != d0) atomicAdd(&h[d], 1u);
-    });
-    __syncthreads();
-    // the bin holding the k-th stamp: each thread sums its 16 bins, a block
-    // scan of those sums, then the one thread whose range holds k walks its bins
-    constexpr uint32_t per = kLruBins / kEvBlock;
-    uint32_t mine = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < per; ++j) mine += h[tid * per + j];
-    uint32_t incl = mine;                                    // inclusive scan: waves, then wave totals
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = __shfl_up(incl, o);
-      incl += lane >= static_cast<uint32_t>(o) ? v : 0u;
-    }
-    if (lane == 63) part[tid >> 6] = incl;
-    __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) before += part[w];
-    incl += before;
-    const uint32_t excl = incl - mine;
-    if (excl < k && k <= incl) {                             // exactly one thread
-      uint32_t below = excl, b = tid * per;
-      while (below + h[b] < k) below += h[b++];
-      prefix_s = prefix | (uint64_t(b) << shift);
-      k_s = k - below;
-    }
-    __syncthreads();
-    prefix = prefix_s;
-    k = k_s;
-    low = shift;
-    __syncthreads();                                         // h, part and the shared picks are reused
-  }
-  // delete the live entries at or below the chosen stamp (exactly the oldest
-  // live - max_entries)
-  const uint64_t cut = prefix;
-  uint32_t n = 0;
-  for (uint64_t i = tid; i < (uint64_t(1) << t.cap_log2); i += kEvBlock) {
-    const unsigned long long key = t.touch[i];
-    if (key > cut) continue;                                 // newer, or not live (~0)
-    CtSlot *e = &t.slots[i];
-    ct_u32x4 hi = slot_half(e, 1);
-    hi.w &= ~0xff00u;                                        // valid = 0: connections.delete
-    reinterpret_cast<ct_u32x4 *>(e)[1] = hi;
-    t.touch[i] = ~0ull;
-    ++n;
-  }
-  if (n) atomicAdd(&n_s, n);
-  __syncthreads();
-  if (tid == 0 && n_s) atomicAdd(&t.stats[1], static_cast<unsigned long long>(n_s));
 }
 
 // Long echo replies (K_HARD) into the walk: a reply joins its own key's run
@@ -2471,10 +2346,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.heads, s.ctl, s.th_list,
                      s.cursor);
   CT_CHECK(hipGetLastError());
-  if (t.max_entries && t.cap_log2 <= kLruSmallLog2 && !PCN_CT_LRU_PASSES) {   // one workgroup, one launch
-    hipLaunchKernelGGL(ct_lru_small_kernel, dim3(1), dim3(kEvBlock), 0, st, t);
-    CT_CHECK(hipGetLastError());
-  } else if (t.max_entries) {                  // LRU down to max_entries (no read-back either)
+  if (t.max_entries) {                         // LRU down to max_entries (no read-back either)
     const uint64_t cap = uint64_t(1) << t.cap_log2;
     // few workgroups: each one's merge and finish atomics land on the same few
     // addresses, which serialise at ~0.1 us apiece (256 workgroups: 69 us a pass)
