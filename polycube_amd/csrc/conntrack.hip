@@ -1743,7 +1743,7 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
 // fixed 11-bit passes of 64 workgroups took 26 us each, 0.19 ms a batch:
 // profiles/r03_s24_ev_ab.log.)
 #ifndef PCN_CT_EV_DIGIT
-#define PCN_CT_EV_DIGIT 14   // A/B: 11 (seven launches a batch)
+#define PCN_CT_EV_DIGIT 11   // A/B 14: six launches of 17.8 us against seven of 15.4 (profiles/r04_s14/)
 #endif
 constexpr uint32_t kEvDigit = PCN_CT_EV_DIGIT;
 constexpr uint32_t kEvBins = 1u << kEvDigit;
