@@ -169,6 +169,10 @@ struct pcn_ipt {
   // stream, and the fold waits on those (no stream handle is used later).
   CopyBound pack{};
   std::vector<std::pair<hipStream_t, hipEvent_t>> pack_streams;
+  // per chain: device work that can add to its counters was queued since
+  // fetch_stats last read them (else they are all zero and the read, a device
+  // sync, a fold and a copy per rule append, is skipped)
+  bool ctr_dirty[PCN_IPT_NCHAINS] = {false, false, false};
   ncclComm_t comm = nullptr;
   // the counter all-gather runs on its own stream, off the classify stream's
   // critical path: the classify stream only snapshots the counters
@@ -400,9 +404,10 @@ const HorusProg *horus_of_batch(const pcn_ipt *ctx, int direction) {
 void fetch_stats(pcn_ipt *ctx, int chain) {
   ChainState &cs = ctx->chains[chain];
   cs.stats.resize(cs.rules.size());
-  if (!ctx->has_device || cs.active < 0) return;
+  if (!ctx->has_device || cs.active < 0 || !ctx->ctr_dirty[chain]) return;
   device_guard(ctx);
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  ctx->ctr_dirty[chain] = false;
   uint32_t n = counted(ctx, cs.desc.nrules);
   std::vector<unsigned long long> buf(2 + 2 * size_t(n));
   fold_counters(ctx, cs, buf.size(), nullptr);
@@ -1198,6 +1203,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     if (plan) return 0;
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
     const hipStream_t hs = static_cast<hipStream_t>(stream);
+    for (bool &d : ctx->ctr_dirty) d = true;        // (fetch_stats reads them again)
     int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, hs, sa ? nullptr : &ctx->pack);
     if (!rc && !sa) note_pack_stream(ctx, hs);
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));

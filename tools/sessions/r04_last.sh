@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 4, last check on the committed tree: every GPU test, the smoke, the bench
+# Round 4, last check on the committed tree (rerun after the stats-read skip): every GPU test, the smoke, the bench
 # lines (headline with every leg, configs 2 and 5) and the rocprof kernel stats of
 # the headline bench.  The kernel sources are those of profiles/r04_final/ (PMC
 # traffic hash e076dd6a); conntrack.hip changed since (LRU scan, reverted tries).
-TAG=r04_last
+TAG=r04_last2
 source "$(dirname "$0")/../gpu_lib.sh"
 KEEP_GOING=1
 pytest_gpu tests_all 900 tests
