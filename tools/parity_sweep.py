@@ -23,6 +23,10 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
+BIG = False   # --big: chains of 4100-8000 rules (2+ summary blocks: the two-item deal,
+              # global counter atomics past the LDS bins)
+
+
 def trial(seed, torch, dev):
     from oracle.ffi import Oracle
     from polycube_amd import Firewall, Iptables, synth
@@ -52,11 +56,12 @@ def trial(seed, torch, dev):
     ipt.interactive = False
     nrules = {}
     for c in chains:
-        rules = quirky_rules(int(rng.integers(0, 260)), seed * 7 + c, ct=fw_mode != 0, ifaces=fw_mode < 0)
+        count = int(rng.integers(4100, 8000)) if BIG else int(rng.integers(0, 260))
+        rules = quirky_rules(count, seed * 7 + c, ct=fw_mode != 0, ifaces=fw_mode < 0)
         if fw_mode >= 0:
             for r in rules:
                 r.setdefault("action", "DROP")
-        if rng.random() < 0.15:
+        if rng.random() < 0.15 and not BIG:
             rules = []
         d = "DROP" if rng.random() < 0.5 else "ACCEPT"
         o.set_chain(c, rules, d)
@@ -168,7 +173,10 @@ def main():
     ap.add_argument("--stateful", action="store_true", help="connection-table trials")
     ap.add_argument("--lib", default="", help="another build of the product library (A/B)")
     ap.add_argument("--trials", type=int, default=0, help="stop after this many trials (0: --seconds)")
+    ap.add_argument("--big", action="store_true", help="chains of 4100-8000 rules (2+ summary blocks)")
     a = ap.parse_args()
+    global BIG
+    BIG = a.big
     import torch
     if a.lib:
         from polycube_amd import ffi
