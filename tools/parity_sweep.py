@@ -71,10 +71,10 @@ def trial(seed, torch, dev):
             # the oracle refuses a chain the reference's maps cannot hold (an
             # LPM trie past its 1,024 entries, Iptables_IpLookup_dp.c:54-55):
             # the product must refuse it too
-            for r in rules:
-                ch.append(**r)
-            ch.default = d
             try:
+                for r in rules:
+                    ch.append(**r)
+                ch.default = d
                 ch.apply_rules()
                 refused = False
             except Exception:
