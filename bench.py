@@ -50,12 +50,46 @@ KERNEL_SOURCES = ("polycube_amd/csrc/classify.hip", "polycube_amd/csrc/devchain.
 
 
 def kernel_src_hash():
+    """sha-256 (16 hex digits) of classify.hip + devchain.h + image.cpp as the loaded
+    libpcn_ipt.so carries them (pcn_ipt_embedded_source): the build that runs, not the
+    files on disk (a stale library reports its own hash, see disk_src_hash)."""
+    from polycube_amd.iptables import embedded_kernel_hash
+    return embedded_kernel_hash()
+
+
+def disk_src_hash():
+    """The same hash over the files on disk (differs from kernel_src_hash when the
+    library is stale)."""
     import hashlib
     h = hashlib.sha256()
     for rel in KERNEL_SOURCES:
         with open(os.path.join(ROOT, rel), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+def rccl_libraries():
+    """Every librccl the process has mapped (torch ships its own; libpcn_ipt.so links
+    /opt/rocm/lib's): which RCCL serves a call depends on symbol resolution order."""
+    seen = []
+    try:
+        with open("/proc/self/maps") as fh:
+            for ln in fh:
+                path = ln.split()[-1] if len(ln.split()) >= 6 else ""
+                if "librccl" in path and path not in seen:
+                    seen.append(path)
+    except OSError:
+        pass
+    return seen
+
+
+def torch_rccl():
+    import torch
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as e:   # noqa: BLE001 (a report field, never fatal)
+        return f"unavailable: {e}"
 
 
 def traffic_key(cfg, hook):
@@ -559,6 +593,7 @@ def main():
 
     from polycube_amd import Iptables, synth
     from polycube_amd import dist as pdist
+    from polycube_amd.iptables import build_sha256
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -746,14 +781,21 @@ def main():
     jit_info = ipt.jit_info()
     kernel = (f"pcn_classify_jit (chain program, config-{cfg} layout baked in)"
               if jit_info["launches_jit"] > args.warmup else "classify_kernel (generic)")
+    # every rank: one untimed pass with rule ids, its first 2^16 frames checked against the
+    # oracle (each rank classifies its own shard), then the verdict of all ranks together
+    rid = torch.empty(n, dtype=torch.int32, device=dev)
+    fw.read_counters(len(rules), flush=True)
+    classify(rid)
+    torch.cuda.synchronize()
+    ok = parity_sample(rules, frames_host, verdicts[: 1 << 16].cpu().numpy(), rid[: 1 << 16].cpu().numpy(),
+                       offsets_host, lens_host, hook, big)
+    parity_ranks = [ok]
+    if world > 1:
+        parity_ranks = [None] * world
+        dist.all_gather_object(parity_ranks, bool(ok))
+        ok = all(parity_ranks)
+    program = fw.program_info()
     if rank == 0:
-        # one untimed pass with rule ids for the parity sample
-        rid = torch.empty(n, dtype=torch.int32, device=dev)
-        fw.read_counters(len(rules), flush=True)
-        classify(rid)
-        torch.cuda.synchronize()
-        ok = parity_sample(rules, frames_host, verdicts[: 1 << 16].cpu().numpy(), rid[: 1 << 16].cpu().numpy(),
-                           offsets_host, lens_host, hook, big)
         line = {
             "metric": METRIC if world == 1 else METRIC.replace("1 GPU", f"{world} GPUs"), "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -771,22 +813,35 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_from": traffic_note, "kernel_src_hash": kernel_src_hash(),
+                         "kernel_src_hash_from": "classify.hip + devchain.h + image.cpp text embedded in the loaded "
+                                                 "libpcn_ipt.so (pcn_ipt_embedded_source)",
+                         "disk_src_hash": disk_src_hash(), "library_build_sha256": build_sha256()[:16],
+                         "program": {k: program[k] for k in ("ready", "vgpr_count", "agpr_count", "sgpr_count",
+                                                             "vgpr_spill_count", "sgpr_spill_count", "scratch_bytes",
+                                                             "static_lds_bytes", "dynamic_lds_bytes", "code_bytes",
+                                                             "deal_window", "hdr_asm")},
                          "kernel": kernel, "kernel_ms": round(kern_ms, 4),
                          "kernel_ms_from": ("a HIP event pair around each timed step" if args.step_events else
                                             "one HIP event pair around the K timed steps on the launch stream "
                                             "(includes the launch boundaries)"),
                          "bytes_per_unit": bytes_per_pkt, "units_per_launch": n},
             "parity_sample_vs_oracle": ok,
+            "parity_sample_per_rank": parity_ranks,
+            "parity_sample_what": ("each rank's first 2^16 frames of its own shard, verdicts and rule ids against the "
+                                   "oracle, after the timed loop; the AND over ranks"),
             "counters_summed_over_ranks_ok": sum_ok,
             "settle": {"seconds": round(settle_s, 2), "steps": settle_steps,
                        "what": "untimed steps before the warmup steps, until the GPU clocks reach steady state"},
         }
+        from polycube_amd.iptables import comm_info
+        ci = comm_info()
+        line["rccl"] = {"library_resolved": {"version": ci["rccl_version"], "path": ci["rccl_path"]},
+                        "torch": torch_rccl(), "mapped": rccl_libraries(),
+                        "what": "library_resolved: the RCCL libpcn_ipt.so's ncclCommInitRank binds to (dladdr) and "
+                                "ncclGetVersion reports -- the one that serves pcn_ipt_sync_counters; torch: "
+                                "torch.cuda.nccl.version(); mapped: every librccl in the process"}
         if multi:
             line["multi_gpu"] = multi
-        else:
-            from polycube_amd.iptables import comm_info
-            ci = comm_info()
-            line["rccl"] = {"version": ci["rccl_version"], "path": ci["rccl_path"]}
         if world == 1 and cfg == 3 and not args.no_hits:
             line["hit_rates"] = hit_rate_sweep(ipt, fw, rs, n, dev, stream, kern_ms, synth.CONFIG_SEEDS[3])
         if cfg == 5:

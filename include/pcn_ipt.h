@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 8
+#define PCN_IPT_ABI_VERSION 9
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -189,13 +189,19 @@ int pcn_ipt_chain_get_image(pcn_ipt *ctx, int chain, uint8_t *buf, uint32_t cap,
 /* ---- datapath ---------------------------------------------------------- */
 /* Classify a batch (device pointers), stream = hipStream_t (NULL = default).
  * Batches may come on several streams.  A stream that has carried a batch
- * must stay valid until a batch on another stream follows it (or the context
- * is destroyed): the first batch on a second stream records an event on the
- * earlier one, so a later fold of the per-workgroup counter copies can wait
- * for its work (pcn_ipt.cpp note_pack_stream).  Each batch afterwards records
- * one on its own stream; with a single stream none is recorded, since an
- * event per launch costs ~3-4 us of GPU time (profiles/r04_final2/). */
+ * must stay valid until a batch on another stream follows it, or until
+ * pcn_ipt_release_stream forgets it (or the context is destroyed): the first
+ * batch on a second stream records an event on the earlier one, before it
+ * launches, so a later fold of the per-workgroup counter copies can wait for
+ * its work (pcn_ipt.cpp note_pack_stream).  Each batch afterwards records one
+ * on its own stream; with a single stream none is recorded, since an event per
+ * launch costs ~3-4 us of GPU time (profiles/r04_final2/). */
 int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *batch, void *stream);
+/* Before destroying a stream that carried batches: waits for the work this
+ * context queued on it and drops the context's record of it, so no later
+ * batch touches the handle.  The ingest ring does this for its own streams.
+ * 0 also when the stream never carried a batch. */
+int pcn_ipt_release_stream(pcn_ipt *ctx, void *stream);
 /* Wait for all work this context queued. */
 int pcn_ipt_synchronize(pcn_ipt *ctx);
 
@@ -226,6 +232,30 @@ int pcn_ipt_debug_ct_walk_passes(pcn_ipt *ctx, uint64_t out[2], int reset);
  * device (works with device = -1).  On failure the compiler log is in
  * pcn_ipt_last_error(). */
 int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain);
+/* Resources of the chain program a chain's launches last asked for (or, before
+ * any launch, of its usual launch shape, as pcn_ipt_chain_program_compile plans
+ * it), read from the code object's metadata: what a measurement of that
+ * program should name.  ready: 1 compiled, 0 not compiled (yet), -1 failed;
+ * the other fields are valid only when ready == 1, except dynamic_lds_bytes
+ * (the last launch's, 0 before one). */
+typedef struct {
+  int32_t ready;
+  int32_t vgpr_count, agpr_count, sgpr_count;
+  int32_t vgpr_spill_count, sgpr_spill_count;
+  uint32_t scratch_bytes;        /* .private_segment_fixed_size: scratch per lane */
+  uint32_t static_lds_bytes;     /* .group_segment_fixed_size */
+  uint32_t dynamic_lds_bytes;    /* LDS per workgroup of the chain's last launch */
+  uint32_t code_bytes;           /* code object size */
+  uint32_t deal_window;          /* candidates dealt per pass: 64, or 128 (two per worker lane) */
+  uint32_t hdr_asm;              /* fixed-stride header loads as counted asm (classify.hip PCN_HDR_ASM) */
+} pcn_ipt_program_info;
+int pcn_ipt_get_program_info(pcn_ipt *ctx, int chain, pcn_ipt_program_info *out);
+/* Provenance of the loaded library.  which: 0 classify.hip, 1 devchain.h,
+ * 2 pcn_ipt.h, 3 image.cpp -- the text the library was built from (the first
+ * three are also what chain programs compile); NULL for any other value.
+ * pcn_ipt_build_sha256: sha-256 (hex) of every library source at build time. */
+const char *pcn_ipt_embedded_source(int which);
+const char *pcn_ipt_build_sha256(void);
 
 /* ---- host ingest ring -------------------------------------------------- */
 /* Frames that start in host memory (a NIC / AF_XDP / AF_PACKET RX ring, a
@@ -485,6 +515,8 @@ typedef struct {
   char rccl_path[256];
   uint64_t gathers_timed;
   double gather_ms_total;
+  uint64_t gathers_untimed;  /* steps not timed: their timing slot's earlier step was still
+                                running (the call never waits on the device for it) */
 } pcn_ipt_comm_info;
 int pcn_ipt_comm_get_info(pcn_ipt *ctx, pcn_ipt_comm_info *out);
 /* The two halves of pcn_ipt_sync_counters, for a caller that moves the counter

@@ -1119,8 +1119,11 @@ constexpr int kPassKeys = 4;
 constexpr int kAllKeys = -2, kOtherKeys = -1;
 // How often walk_long went past its first pass: [0] passes for a bucket's 2nd..
 // kPassKeys-th connection, [1] "the rest as one sequence" walks.  Only bucket
-// collisions get there (a global atomic each); read by the tests through
-// pcn_ipt_debug_ct_walk_stats to see that the path they mean to cover ran.
+// collisions get there (a global atomic each, ~64 a batch on the bench
+// traffic); read by the tests through pcn_ipt_debug_ct_walk_passes to see that
+// the path they mean to cover ran.  One pair per DEVICE, not per context: two
+// contexts on one device add into the same counters (a test reads them with a
+// single context).
 __device__ unsigned long long g_walk_passes[2];
 struct PassKeys {
   uint32_t n;

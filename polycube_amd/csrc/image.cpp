@@ -190,7 +190,8 @@ std::vector<LpmEntry> lpm_entries(const FieldMap &m) {
     trie[{len, host_order(m.keys[k]) & prefix_mask(len)}] = static_cast<uint32_t>(k);
   }
   if (trie.size() > kTrieCapacity)
-    throw std::runtime_error("LPM trie full: " + std::to_string(trie.size()) + " prefixes > 1024");
+    throw TableFull("LPM trie full: " + std::to_string(trie.size()) +
+                    " prefixes > 1024 (Table set error: No space left on device)");
   std::vector<LpmEntry> out;
   for (auto &[key, vec] : trie) out.push_back({key.first, key.second, vec});
   return out;   // sorted by (len, prefix): shortest first

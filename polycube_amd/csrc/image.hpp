@@ -3,6 +3,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <stdexcept>
 #include <vector>
 
 #include "devchain.h"
@@ -21,8 +22,16 @@ struct HostImage {
   int default_action = 1;
 };
 
-// Throws std::runtime_error (> 1024 LPM entries per field — the kernel trie
-// capacity of Iptables_IpLookup_dp.c:54-55 — or > 65534 distinct vectors).
+// A table the reference's BPF map could not hold: its map push fails with
+// ENOSPC ("Table set error: No space left on device", libs/polycube/src/
+// table.cpp:61-66) at the verb that runs Chain::updateChain.  The C ABI
+// returns -ENOSPC for it.
+struct TableFull : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// Throws TableFull (> 1024 LPM entries per field — the kernel trie capacity of
+// Iptables_IpLookup_dp.c:54-55) or std::runtime_error (> 65534 distinct vectors).
 HostImage build_image(const ChainTables &t);
 
 // Kernel-LPM view of an IP map (what the BPF trie holds after updateMap):

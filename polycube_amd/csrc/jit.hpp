@@ -37,6 +37,15 @@ struct JitShape {
 // pointers are ignored); doubles as the cache key.
 std::string jit_spec(const DevChain &d, const JitShape &s);
 
+// Resources of a compiled chain program, from its code object's metadata.
+struct ProgramMeta {
+  int vgpr = -1, agpr = -1, sgpr = -1, vgpr_spill = -1, sgpr_spill = -1;
+  int scratch = -1;       // .private_segment_fixed_size (bytes per lane)
+  int static_lds = -1;    // .group_segment_fixed_size
+  uint32_t code_bytes = 0;
+  bool hdr_asm = true;    // built with the counted asm header loads (else rebuilt without, jit.cpp compile)
+};
+
 class JitCache {
  public:
   JitCache() = default;
@@ -51,6 +60,8 @@ class JitCache {
   void *function(const std::string &spec, int device);
   // Compiled successfully (false while compiling or after a failure).
   bool ready(const std::string &spec) const;
+  // 1 and *out filled when compiled, 0 while compiling or never requested, -1 failed.
+  int meta(const std::string &spec, ProgramMeta *out) const;
   // Programs compiled / failed so far (diagnostics).
   int compiled() const;
   int failed() const;
@@ -58,7 +69,9 @@ class JitCache {
 
  private:
   struct Entry {
-    std::shared_future<std::vector<char>> code;   // empty vector: compile failed
+    // empty vector: compile failed; the last byte says whether the counted asm
+    // header loads were kept (1) or the program was rebuilt without (0)
+    std::shared_future<std::vector<char>> code;
     std::map<int, std::pair<void *, void *>> loaded;   // device -> (hipModule_t, hipFunction_t)
     bool bad = false;
   };

@@ -131,6 +131,7 @@ struct ChainState {
   DevChain jit_desc{};
   JitShape jit_shape{};
   std::string jit_spec;
+  uint32_t last_lds_bytes = 0;                 // dynamic LDS of the last launch that ran this chain's rules
 };
 
 // One Horus program (pcn_ipt.h): pcn-iptables has one (ingress, built from
@@ -186,7 +187,7 @@ struct pcn_ipt {
   hipEvent_t ev_g0[kGatherEv] = {}, ev_g1[kGatherEv] = {};
   bool ev_g_live[kGatherEv] = {};
   int ev_g_next = 0;
-  uint64_t gathers_timed = 0;
+  uint64_t gathers_timed = 0, gathers_untimed = 0;
   double gather_ms = 0.0;
   JitCache jit;                                // chain programs (per launch shape)
   uint64_t launches_generic = 0, launches_jit = 0;
@@ -310,19 +311,31 @@ int fold_all_copies(void *c, void *stream) {
   return hipSuccess;
 }
 
-// Bookkeeping of a launch into the packed copies on stream s: once a second
-// stream has launched into them, every launch leaves an event behind (the
-// first stream's is recorded when the second one appears).
-void note_pack_stream(pcn_ipt *ctx, hipStream_t s) {
+// Bookkeeping of the launches into the packed copies, in two halves around a
+// launch on stream s.  Before it (register_pack_stream): s joins the known
+// streams, and when it is a second stream every earlier stream that has no
+// event yet gets one now, at the end of what it has queued -- so a fold inside
+// this very launch (launch_classify, cb->fold) already waits for their work,
+// and no stream handle is ever used after the launch that introduced it.
+// After it (note_pack_stream): once two streams are known, the launch leaves
+// an event behind on s.  With one stream neither records anything.
+void register_pack_stream(pcn_ipt *ctx, hipStream_t s) {
   auto &v = ctx->pack_streams;
-  auto it = std::find_if(v.begin(), v.end(), [&](const auto &se) { return se.first == s; });
-  if (it == v.end()) {
-    v.emplace_back(s, nullptr);
-    it = v.end() - 1;
-  }
+  if (std::find_if(v.begin(), v.end(), [&](const auto &se) { return se.first == s; }) != v.end()) return;
+  v.emplace_back(s, nullptr);
   if (v.size() < 2) return;
   for (auto &se : v) {
-    if (se.second && se.first != s) continue;
+    if (se.first == s || se.second) continue;
+    hip_check(hipEventCreateWithFlags(&se.second, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(se.second, se.first), "hipEventRecord(pack)");
+  }
+}
+
+void note_pack_stream(pcn_ipt *ctx, hipStream_t s) {
+  auto &v = ctx->pack_streams;
+  if (v.size() < 2) return;
+  for (auto &se : v) {
+    if (se.first != s) continue;
     if (!se.second) hip_check(hipEventCreateWithFlags(&se.second, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventRecord(se.second, se.first), "hipEventRecord(pack)");
   }
@@ -602,6 +615,8 @@ int guarded(pcn_ipt *ctx, F &&f) {
     return f();
   } catch (const HipError &e) {
     return fail(-EIO, e.what());
+  } catch (const TableFull &e) {
+    return fail(-ENOSPC, e.what());
   } catch (const std::exception &e) {
     return fail(-EINVAL, e.what());
   }
@@ -999,77 +1014,84 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     auto runs = [&](int c) {
       return any_rules && (ch < 3 ? c == ch : (c == PCN_IPT_FORWARD || c == PCN_IPT_INPUT));
     };
-    uint32_t base = 3;
-    for (int c : order) {
-      uint32_t nc = a.ch[c].ncounted;
-      if (nc && base - 3 + nc <= kMaxLdsRuleBins) {
-        a.ch[c].lds_bins = static_cast<int32_t>(base);
-        a.ch[c].lds_nrules = nc;
-        base += nc;
-      } else {
-        a.ch[c].lds_bins = -1;
-        a.ch[c].lds_nrules = 0;
-      }
-    }
-    // Horus hits count into the same workgroup histogram (a hot key would
-    // otherwise serialize on one global address)
-    const HorusProg *hzb = horus_of_batch(ctx, b->direction);
-    a.hz_bins = -1;
-    if (hzb && !sa && base - 3 + hzb->nids <= kMaxLdsRuleBins) {
-      a.hz_bins = static_cast<int32_t>(base);
-      base += hzb->nids;
-    }
     // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
     // (TC frames may carry a VLAN tag: the 52-byte window of the generic path)
     bool fixed = b->hook == PCN_IPT_HOOK_XDP && !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
                  (reinterpret_cast<uintptr_t>(b->frames) % 16) == 0 &&
                  (b->n - 1) * uint64_t(b->stride) + 48 <= b->frames_bytes;
-    a.nbins = base;
-    a.nlocal = static_cast<uint32_t>(ctx->localip.size());
-    // counter bins: u32 pkts, plus u32 bytes unless every frame has the same length
-    const uint32_t bin_bytes = (fixed ? 4 : 8) * a.nbins;
-    // the chain program of a chain with 2+ summary blocks deals 128 candidates a pass (jit.cpp)
-    const bool deal2 = ch < 3 && any_rules && a.ch[ch].nsw >= 2 && ctx->cfg.jit >= 0;
-    const uint32_t tail = (bin_bytes + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
-                          (PCN_BLOCK / 64) * wave_region_bytes(fixed, deal2);
-    // whole images if they fit, else their per-packet prefix [0, pbase) (the
-    // candidate-stage tables are then read from L2/HBM), else nothing
-    uint32_t img_bytes = 0;
-    for (int mode = 0; mode < 3; ++mode) {
-      img_bytes = 0;
+    // LDS plan (every field below): a chain program of a chain with 2+ summary
+    // blocks deals 128 candidates a pass (jit.cpp) and needs the larger wave
+    // region; the plan is made for it, and made again without it when the
+    // launch falls back to the generic kernel (program still compiling, or
+    // failed), so the generic kernel keeps that LDS for images and bins.
+    auto plan_lds = [&](bool deal2) {
+      uint32_t base = 3;
       for (int c : order) {
-        a.ch[c].lds_image = 0;
-        a.ch[c].lds_limit = 0;
-        if (!runs(c) || mode == 2) continue;
-        a.ch[c].lds_image = kLdsDescBytes + img_bytes;
-        a.ch[c].lds_limit = mode == 0 ? a.ch[c].lay.bytes : a.ch[c].lay.pbase;
-        img_bytes += a.ch[c].lds_limit;
+        uint32_t nc = a.ch[c].ncounted;
+        if (nc && base - 3 + nc <= kMaxLdsRuleBins) {
+          a.ch[c].lds_bins = static_cast<int32_t>(base);
+          a.ch[c].lds_nrules = nc;
+          base += nc;
+        } else {
+          a.ch[c].lds_bins = -1;
+          a.ch[c].lds_nrules = 0;
+        }
       }
-      if (mode == 2 || kLdsDescBytes + img_bytes + tail <= kLdsBudget) break;
-    }
-    // A chain that runs rules here but got no bin per rule (more rules than
-    // the histogram budget): bins for its lowest rule ids in the LDS the
-    // images leave over, the rest counted with global atomics.  Placed after
-    // the choice above, so no image loses its place in LDS to them.
-    for (int c : order) {
-      if (!runs(c) || a.ch[c].lds_bins >= 0 || !a.ch[c].ncounted) continue;
-      const uint32_t nb = partial_rule_bins(kLdsDescBytes + img_bytes + tail, fixed ? 4 : 8, a.ch[c].ncounted);
-      if (nb) {                    // before the Horus bins, which the flush takes to run to the end
-        a.ch[c].lds_bins = a.hz_bins >= 0 ? a.hz_bins : static_cast<int32_t>(base);
-        a.ch[c].lds_nrules = nb;
-        if (a.hz_bins >= 0) a.hz_bins += static_cast<int32_t>(nb);
-        base += nb;
-        a.nbins = base;
+      // Horus hits count into the same workgroup histogram (a hot key would
+      // otherwise serialize on one global address)
+      const HorusProg *hzb = horus_of_batch(ctx, b->direction);
+      a.hz_bins = -1;
+      if (hzb && !sa && base - 3 + hzb->nids <= kMaxLdsRuleBins) {
+        a.hz_bins = static_cast<int32_t>(base);
+        base += hzb->nids;
       }
-      break;
-    }
-    const uint32_t all_bin_bytes = (fixed ? 4 : 8) * a.nbins;
-    a.lds_images_bytes = img_bytes;
-    a.bins_offset = kLdsDescBytes + img_bytes;
-    a.lds_localip = a.bins_offset + (all_bin_bytes + 15) / 16 * 16;
-    a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
-    a.wave_bytes = wave_region_bytes(fixed, deal2);
-    a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
+      a.nbins = base;
+      a.nlocal = static_cast<uint32_t>(ctx->localip.size());
+      // counter bins: u32 pkts, plus u32 bytes unless every frame has the same length
+      const uint32_t bin_bytes = (fixed ? 4 : 8) * a.nbins;
+      const uint32_t tail = (bin_bytes + 15) / 16 * 16 + (a.nlocal * 4 + 15) / 16 * 16 +
+                            (PCN_BLOCK / 64) * wave_region_bytes(fixed, deal2);
+      // whole images if they fit, else their per-packet prefix [0, pbase) (the
+      // candidate-stage tables are then read from L2/HBM), else nothing
+      uint32_t img_bytes = 0;
+      for (int mode = 0; mode < 3; ++mode) {
+        img_bytes = 0;
+        for (int c : order) {
+          a.ch[c].lds_image = 0;
+          a.ch[c].lds_limit = 0;
+          if (!runs(c) || mode == 2) continue;
+          a.ch[c].lds_image = kLdsDescBytes + img_bytes;
+          a.ch[c].lds_limit = mode == 0 ? a.ch[c].lay.bytes : a.ch[c].lay.pbase;
+          img_bytes += a.ch[c].lds_limit;
+        }
+        if (mode == 2 || kLdsDescBytes + img_bytes + tail <= kLdsBudget) break;
+      }
+      // A chain that runs rules here but got no bin per rule (more rules than
+      // the histogram budget): bins for its lowest rule ids in the LDS the
+      // images leave over, the rest counted with global atomics.  Placed after
+      // the choice above, so no image loses its place in LDS to them.
+      for (int c : order) {
+        if (!runs(c) || a.ch[c].lds_bins >= 0 || !a.ch[c].ncounted) continue;
+        const uint32_t nb = partial_rule_bins(kLdsDescBytes + img_bytes + tail, fixed ? 4 : 8, a.ch[c].ncounted);
+        if (nb) {                    // before the Horus bins, which the flush takes to run to the end
+          a.ch[c].lds_bins = a.hz_bins >= 0 ? a.hz_bins : static_cast<int32_t>(base);
+          a.ch[c].lds_nrules = nb;
+          if (a.hz_bins >= 0) a.hz_bins += static_cast<int32_t>(nb);
+          base += nb;
+          a.nbins = base;
+        }
+        break;
+      }
+      const uint32_t all_bin_bytes = (fixed ? 4 : 8) * a.nbins;
+      a.lds_images_bytes = img_bytes;
+      a.bins_offset = kLdsDescBytes + img_bytes;
+      a.lds_localip = a.bins_offset + (all_bin_bytes + 15) / 16 * 16;
+      a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
+      a.wave_bytes = wave_region_bytes(fixed, deal2);
+      a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
+    };
+    bool deal2 = ch < 3 && any_rules && a.ch[ch].nsw >= 2 && ctx->cfg.jit >= 0;
+    plan_lds(deal2);
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
     a.offsets = b->offsets;
@@ -1199,11 +1221,18 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       }
       ctx->jit.request(cs.jit_spec, ctx->cfg.jit == 1);
       fn = ctx->jit.function(cs.jit_spec, ctx->cfg.device);
+      // the generic kernel deals 64 a pass: give the 128-item region back
+      if (!fn && deal2) {
+        deal2 = false;
+        plan_lds(false);
+      }
+      cs.last_lds_bytes = a.lds_bytes;
     }
     if (plan) return 0;
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
     const hipStream_t hs = static_cast<hipStream_t>(stream);
     for (bool &d : ctx->ctr_dirty) d = true;        // (fetch_stats reads them again)
+    if (!sa) register_pack_stream(ctx, hs);
     int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, hs, sa ? nullptr : &ctx->pack);
     if (!rc && !sa) note_pack_stream(ctx, hs);
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
@@ -1365,14 +1394,13 @@ int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out) {
   });
 }
 
-int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
-  return guarded(ctx, [&] {
-    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
-    if (ctx->chains[chain].info.nrules == 0) return fail(-ENOENT, "chain has no rules");
-    // the usual launch shape: a stateless fixed-stride batch of 64-byte
-    // frames in the chain's direction, planned by the launch code itself (so
-    // the descriptor has the same LDS placement, counter bins -- Horus bins
-    // included -- and side inputs as the launches it is compiled for)
+namespace {
+// The chain program spec of a chain's usual launch shape: a stateless
+// fixed-stride batch of 64-byte frames in the chain's direction, planned by
+// the launch code itself (so the descriptor has the same LDS placement,
+// counter bins -- Horus bins included -- and side inputs as the launches it is
+// compiled for).  0, or a negative errno (with the error set).
+int usual_spec(pcn_ipt *ctx, int chain, std::string &spec) {
     pcn_ipt_batch b{};
     uint8_t *const never_read = reinterpret_cast<uint8_t *>(uintptr_t(1) << 12);   // a plan reads no buffer
     b.frames = never_read;
@@ -1386,15 +1414,85 @@ int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
     const bool track = ctx->hz_enabled || ctx->ct_on;
     const bool want_stale = hz && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT));
     const uint32_t *stale = want_stale && track ? (ctx->ct_on ? ctx->ct.carry : ctx->d_hz_carry) : nullptr;
-    std::string spec;
     int rc = launch_batch(ctx, &b, nullptr, nullptr, stale, nullptr, nullptr, &spec);
     if (rc) return rc;
     if (spec.empty()) return fail(-ENOENT, "no chain program runs this chain's rules in its usual launch");
+    return 0;
+}
+}  // namespace
+
+int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    if (ctx->chains[chain].info.nrules == 0) return fail(-ENOENT, "chain has no rules");
+    std::string spec;
+    if (int rc = usual_spec(ctx, chain, spec)) return rc;
     ctx->jit.request(spec, true);
     if (!ctx->jit.ready(spec)) return fail(-EIO, "chain program compile failed: " + ctx->jit.last_log());
     return 0;
   });
 }
+
+int pcn_ipt_get_program_info(pcn_ipt *ctx, int chain, pcn_ipt_program_info *out) {
+  if (!out) return fail(-EINVAL, "null out");
+  std::memset(out, 0, sizeof(*out));
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    const ChainState &cs = ctx->chains[chain];
+    out->dynamic_lds_bytes = cs.last_lds_bytes;
+    std::string spec = cs.jit_spec;
+    if (spec.empty()) {
+      if (cs.info.nrules == 0) return 0;
+      if (int rc = usual_spec(ctx, chain, spec)) return rc;
+    }
+    ProgramMeta m;
+    out->ready = ctx->jit.meta(spec, &m);
+    if (out->ready != 1) return 0;
+    out->vgpr_count = m.vgpr;
+    out->agpr_count = m.agpr;
+    out->sgpr_count = m.sgpr;
+    out->vgpr_spill_count = m.vgpr_spill;
+    out->sgpr_spill_count = m.sgpr_spill;
+    out->scratch_bytes = m.scratch < 0 ? 0u : static_cast<uint32_t>(m.scratch);
+    out->static_lds_bytes = m.static_lds < 0 ? 0u : static_cast<uint32_t>(m.static_lds);
+    out->code_bytes = m.code_bytes;
+    out->deal_window = spec.find("#define PCN_DEAL2 2") != std::string::npos ? 128u : 64u;
+    out->hdr_asm = m.hdr_asm;
+    return 0;
+  });
+}
+
+int pcn_ipt_release_stream(pcn_ipt *ctx, void *stream) {
+  return guarded(ctx, [&] {
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    auto &v = ctx->pack_streams;
+    auto it = std::find_if(v.begin(), v.end(), [&](const auto &se) { return se.first == s; });
+    if (it == v.end()) return 0;
+    device_guard(ctx);
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (it->second) hip_check(hipEventDestroy(it->second), "hipEventDestroy");
+    v.erase(it);
+    return 0;
+  });
+}
+
+extern const char pcn_jit_src_classify[];
+extern const char pcn_jit_src_devchain[];
+extern const char pcn_jit_src_pcn_ipt[];
+extern const char pcn_src_image[];
+extern const char pcn_build_src_sha256[];
+
+const char *pcn_ipt_embedded_source(int which) {
+  switch (which) {
+    case 0: return pcn_jit_src_classify;
+    case 1: return pcn_jit_src_devchain;
+    case 2: return pcn_jit_src_pcn_ipt;
+    case 3: return pcn_src_image;
+    default: return nullptr;
+  }
+}
+
+const char *pcn_ipt_build_sha256(void) { return pcn_build_src_sha256; }
 
 int pcn_ipt_chain_get_info(pcn_ipt *ctx, int chain, pcn_ipt_chain_info *out) {
   return guarded(ctx, [&] {
@@ -1559,12 +1657,28 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
     hip_check(hipStreamWaitEvent(cs_, ctx->ev_staged, 0), "hipStreamWaitEvent");
     // time the exchange on the communicator stream (all-gather + rank sum):
     // reuse the oldest pair of the ring, folding its duration in first
+    // reuse the oldest pair of the ring once its step has run, folding its
+    // duration in first; while it still runs this step goes untimed (the call
+    // never waits on the device)
     const int ge = ctx->ev_g_next;
-    ctx->ev_g_next = (ge + 1) % pcn_ipt::kGatherEv;
-    if (ctx->ev_g_live[ge]) fold_gather_time(ctx, ge);
-    if (!ctx->ev_g0[ge]) hip_check(hipEventCreate(&ctx->ev_g0[ge]), "hipEventCreate");
-    if (!ctx->ev_g1[ge]) hip_check(hipEventCreate(&ctx->ev_g1[ge]), "hipEventCreate");
-    hip_check(hipEventRecord(ctx->ev_g0[ge], cs_), "hipEventRecord");
+    bool timed = true;
+    if (ctx->ev_g_live[ge]) {
+      const hipError_t q = hipEventQuery(ctx->ev_g1[ge]);
+      if (q == hipSuccess) {
+        fold_gather_time(ctx, ge);
+      } else if (q == hipErrorNotReady) {
+        timed = false;
+        ++ctx->gathers_untimed;
+      } else {
+        hip_check(q, "hipEventQuery");
+      }
+    }
+    if (timed) {
+      ctx->ev_g_next = (ge + 1) % pcn_ipt::kGatherEv;
+      if (!ctx->ev_g0[ge]) hip_check(hipEventCreate(&ctx->ev_g0[ge]), "hipEventCreate");
+      if (!ctx->ev_g1[ge]) hip_check(hipEventCreate(&ctx->ev_g1[ge]), "hipEventCreate");
+      hip_check(hipEventRecord(ctx->ev_g0[ge], cs_), "hipEventRecord");
+    }
     ncclResult_t r = ncclGroupStart();
     for (int c = 0; c < PCN_IPT_NCHAINS && r == ncclSuccess; ++c)
       r = ncclAllGather(ctx->chains[c].stage, ctx->chains[c].gather, count[c], ncclUint64, ctx->comm, cs_);
@@ -1576,8 +1690,10 @@ int pcn_ipt_sync_counters(pcn_ipt *ctx, void *stream) {
       int rc = launch_sum_ranks(cs.gather, cs.ctr_global, count[c], ctx->nranks, cs_);
       if (rc != hipSuccess) return fail(-EIO, "sum_ranks launch failed");
     }
-    hip_check(hipEventRecord(ctx->ev_g1[ge], cs_), "hipEventRecord");
-    ctx->ev_g_live[ge] = true;
+    if (timed) {
+      hip_check(hipEventRecord(ctx->ev_g1[ge], cs_), "hipEventRecord");
+      ctx->ev_g_live[ge] = true;
+    }
     hip_check(hipEventRecord(ctx->ev_gathered, cs_), "hipEventRecord");
     ctx->gather_pending = true;
     return 0;
@@ -1634,6 +1750,7 @@ int pcn_ipt_comm_get_info(pcn_ipt *ctx, pcn_ipt_comm_info *out) {
       if (ctx->ev_g_live[k]) fold_gather_time(ctx, k);
     out->gathers_timed = ctx->gathers_timed;
     out->gather_ms_total = ctx->gather_ms;
+    out->gathers_untimed = ctx->gathers_untimed;
     return 0;
   });
 }

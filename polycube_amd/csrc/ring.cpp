@@ -155,6 +155,9 @@ void pcn_ipt_ring_destroy(pcn_ipt_ring *r) {
   (void)hipSetDevice(r->device);
   for (hipStream_t st : r->streams) (void)hipStreamSynchronize(st);
   for (auto &s : r->slots) free_slot(s);
+  // the context keeps a record of every stream that carried a batch (its
+  // counter-copy bookkeeping): drop ours before the handles die
+  for (hipStream_t st : r->streams) (void)pcn_ipt_release_stream(r->ctx, st);
   for (hipStream_t st : r->streams) (void)hipStreamDestroy(st);
   delete r;
 }

@@ -85,7 +85,7 @@ class CtInfo(C.Structure):
 class CommInfo(C.Structure):
     _fields_ = [("nccl_version", C.c_int), ("nranks", C.c_int), ("rank", C.c_int), ("device", C.c_int),
                 ("pci_bus_id", C.c_char * 32), ("rccl_path", C.c_char * 256), ("gathers_timed", C.c_uint64),
-                ("gather_ms_total", C.c_double)]
+                ("gather_ms_total", C.c_double), ("gathers_untimed", C.c_uint64)]
 
 
 class HorusInfo(C.Structure):
@@ -93,8 +93,15 @@ class HorusInfo(C.Structure):
                 ("conntrack", C.c_uint32)]
 
 
+class ProgramInfo(C.Structure):
+    _fields_ = [("ready", C.c_int32), ("vgpr_count", C.c_int32), ("agpr_count", C.c_int32),
+                ("sgpr_count", C.c_int32), ("vgpr_spill_count", C.c_int32), ("sgpr_spill_count", C.c_int32),
+                ("scratch_bytes", C.c_uint32), ("static_lds_bytes", C.c_uint32), ("dynamic_lds_bytes", C.c_uint32),
+                ("code_bytes", C.c_uint32), ("deal_window", C.c_uint32), ("hdr_asm", C.c_uint32)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
-ABI_VERSION = 8            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
+ABI_VERSION = 9            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
 
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),
@@ -126,6 +133,10 @@ SIGNATURES = {
     "pcn_ipt_debug_stale_canary": (C.c_int, [C.c_void_p]),
     "pcn_ipt_debug_ct_walk_passes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "pcn_ipt_chain_program_compile": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_get_program_info": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ProgramInfo)]),
+    "pcn_ipt_embedded_source": (C.c_char_p, [C.c_int]),
+    "pcn_ipt_build_sha256": (C.c_char_p, []),
+    "pcn_ipt_release_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pcn_ipt_read_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.c_int, C.c_int]),

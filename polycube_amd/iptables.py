@@ -64,6 +64,22 @@ def comm_info(handle=None):
     return d
 
 
+def embedded_kernel_hash():
+    """sha-256 (16 hex digits) of classify.hip + devchain.h + image.cpp as the LOADED
+    library carries them (pcn_ipt_embedded_source): what decides the bytes a classify
+    launch reads, taken from the build that runs, not from the files on disk."""
+    import hashlib
+    h = hashlib.sha256()
+    for which in (0, 1, 3):
+        h.update(ffi.lib().pcn_ipt_embedded_source(which))
+    return h.hexdigest()[:16]
+
+
+def build_sha256():
+    """sha-256 of every library source at the loaded library's build time."""
+    return ffi.lib().pcn_ipt_build_sha256().decode()
+
+
 def make_rule(src=None, dst=None, l4proto=None, sport=None, dport=None, tcpflags=None,
               in_iface=None, out_iface=None, conntrack=None, action=None):
     """Build a pcn_ipt_rule from REST-style fields (None = not set)."""
@@ -159,6 +175,13 @@ class Chain:
         _check(ffi.lib().pcn_ipt_chain_get_info(self._h(), self.id, C.byref(out)))
         return {k: getattr(out, k) for k, _ in ffi.ChainInfo._fields_}
 
+    def program_info(self):
+        """Resources of this chain's chain program (pcn_ipt_get_program_info): VGPRs,
+        SGPRs, scratch and LDS bytes, deal window; ready = 1 once compiled."""
+        out = ffi.ProgramInfo()
+        _check(ffi.lib().pcn_ipt_get_program_info(self._h(), self.id, C.byref(out)))
+        return {k: getattr(out, k) for k, _ in ffi.ProgramInfo._fields_}
+
     def compile_program(self):
         """Compile this chain's chain program now (pcn_ipt_chain_program_compile)."""
         _check(ffi.lib().pcn_ipt_chain_program_compile(self._h(), self.id))
@@ -200,6 +223,10 @@ class Iptables:
             self.close()
         except Exception:
             pass
+
+    def release_stream(self, stream):
+        """pcn_ipt_release_stream: before destroying a stream that carried batches."""
+        _check(ffi.lib().pcn_ipt_release_stream(self._h, stream))
 
     def add_port(self, name, index):
         _check(ffi.lib().pcn_ipt_add_port(self._h, name.encode(), index))

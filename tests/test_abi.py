@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert ffi.lib().pcn_ipt_abi_version() == ffi.ABI_VERSION == 8
+    assert ffi.lib().pcn_ipt_abi_version() == ffi.ABI_VERSION == 9
 
 
 def test_classify_fails_loudly_without_device():
@@ -107,20 +107,50 @@ def test_comm_info_without_a_device():
 
 def test_bench_traffic_needs_the_measured_build(tmp_path, monkeypatch):
     """bench.py reports roofline.traffic only for the kernel sources (and batch
-    size) the PMC entry was measured on, and says why not otherwise."""
+    size) the PMC entry was measured on -- the sources embedded in the LOADED
+    library, not the files on disk -- and says why not otherwise."""
     import json
     import bench
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     (tmp_path / "profiles").mkdir()
-    for rel in bench.KERNEL_SOURCES:
-        (tmp_path / rel).parent.mkdir(parents=True, exist_ok=True)
-        (tmp_path / rel).write_text(rel)
     h = bench.kernel_src_hash()
     entry = {"frames": 1024, "hbm_bytes_per_launch": 70000, "src_hash": h, "profile": "p"}
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({"configs": {"config3": entry}}))
     assert bench.load_traffic(3, 0, 1024)[0] == 70000
     assert bench.load_traffic(3, 0, 2048)[0] is None                 # another batch size
     assert bench.load_traffic(5, 1, 1024)[0] is None                 # no entry for config 5 / TC
-    (tmp_path / bench.KERNEL_SOURCES[0]).write_text("changed kernel")
+    monkeypatch.setattr(bench, "kernel_src_hash", lambda: "0123456789abcdef")   # another build loaded
     t, why = bench.load_traffic(3, 0, 1024)
-    assert t is None and h in why                                    # sources changed since the PMC run
+    assert t is None and h in why and "0123456789abcdef" in why
+
+
+def test_loaded_library_carries_its_sources():
+    """The kernel text the library embeds (and compiles chain programs from) is the
+    text on disk when the build is fresh, and the build hash covers every source."""
+    import bench
+    from polycube_amd.iptables import build_sha256
+    assert bench.kernel_src_hash() == bench.disk_src_hash()
+    for which, rel in ((0, "classify.hip"), (1, "devchain.h"), (3, "image.cpp")):
+        with open(os.path.join(bench.ROOT, "polycube_amd", "csrc", rel), "rb") as fh:
+            assert ffi.lib().pcn_ipt_embedded_source(which) == fh.read()
+    assert ffi.lib().pcn_ipt_embedded_source(4) is None
+    assert len(build_sha256()) == 64
+
+
+def test_program_info_names_the_chain_program():
+    """pcn_ipt_get_program_info: the usual launch shape's chain program, compiled on
+    the CPU (no device), reports its registers, scratch and deal window."""
+    from polycube_amd import Iptables, synth
+    ipt = Iptables(device=-1)
+    ipt.interactive = False
+    fw = ipt.chain("FORWARD")
+    for r in synth.config_rules(2).rules():
+        fw.append(**r)
+    fw.apply_rules()
+    assert fw.program_info()["ready"] == 0
+    fw.compile_program()
+    pi = fw.program_info()
+    assert pi["ready"] == 1 and 0 < pi["vgpr_count"] <= 128 and pi["sgpr_count"] > 0
+    assert pi["vgpr_spill_count"] == 0 and pi["deal_window"] == 64 and pi["code_bytes"] > 1000
+    assert ipt.chain("INPUT").program_info()["ready"] == 0          # no rules: no program
+    ipt.close()

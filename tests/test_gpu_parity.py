@@ -374,6 +374,38 @@ def test_packed_counter_copies_fold_across_launches_and_streams(dev, monkeypatch
     assert_counters(o, ipt, chains=(1,), n=len(rules))
 
 
+def test_stream_of_a_closed_ring_is_never_touched(dev, monkeypatch):
+    """A ring whose one stream carried batches, closed (its stream destroyed), then
+    batches on the NULL stream and on a new stream: the context must not record an
+    event on the dead stream (pcn_ipt_ring_destroy releases it first), and every
+    counter still equals the oracle's -- with a fold before every launch (test
+    limit), so the folds wait on the streams that remain."""
+    monkeypatch.setenv("PCN_IPT_DEBUG_PACK_MAX_PKTS", str(1 << 13))
+    rs = synth.config_rules(2)
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
+    ring = ipt.ring(slots=2, slot_frames=1 << 14, slot_bytes=(1 << 14) * 64, streams=1)
+    for k in range(3):
+        slot, frames, _, _, _ = ring.acquire()
+        f = synth.config_frames(2, 1 << 14, rs, seed=k).reshape(-1)
+        frames[:f.size] = f
+        ring.submit(slot, 1 << 14)
+        o.classify(f, n=1 << 14, nthreads=NTHREADS)
+        done, _, _ = ring.complete()
+        ring.release(done)
+    ring.close()
+    n = 1 << 16
+    frames = synth.config_frames(2, n, rs, seed=9).reshape(-1)
+    tf = torch.from_numpy(frames).to(dev)
+    side = torch.cuda.Stream()
+    for stream in (None, side.cuda_stream, None):
+        v_g, r_g = ipt.classify(tf, n=n, stream=stream)
+        v_o, r_o = o.classify(frames, n=n, nthreads=NTHREADS)
+        torch.cuda.synchronize()
+        assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
+    ipt.release_stream(side.cuda_stream)
+    assert_counters(o, ipt, chains=(1,), n=len(rs.rules()))
+
+
 def test_localip_input_output_from_lds(dev):
     """INPUT/OUTPUT selection by a 200-address localip set staged in LDS."""
     rs = synth.config_rules(2)

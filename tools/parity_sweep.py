@@ -11,6 +11,7 @@ per trial plus a summary; exits non-zero on the first mismatch.
   python tools/parity_sweep.py --seconds 150 > gpurun_out/parity_sweep.log
 """
 import argparse
+import errno
 import json
 import os
 import sys
@@ -29,7 +30,7 @@ BIG = False   # --big: chains of 4100-8000 rules (2+ summary blocks: the two-ite
 
 def trial(seed, torch, dev):
     from oracle.ffi import Oracle
-    from polycube_amd import Firewall, Iptables, synth
+    from polycube_amd import Firewall, Iptables, IptablesError, synth
     from rulegen import PORTS, quirky_rules
     rng = np.random.default_rng(seed)
     fw_mode = int(rng.integers(-1, 3))           # -1: pcn-iptables, else firewall conntrack mode
@@ -70,19 +71,23 @@ def trial(seed, torch, dev):
         except ValueError as e:
             # the oracle refuses a chain the reference's maps cannot hold (an
             # LPM trie past its 1,024 entries, Iptables_IpLookup_dp.c:54-55):
-            # the product must refuse it too
+            # the product must refuse it too, for the same reason and at the
+            # verb that pushes the maps (non-interactive: apply_rules; the
+            # reference's RawTable::set throws "Table set error: No space left
+            # on device", libs/polycube/src/table.cpp:61-66)
+            refused, why = False, ""
+            for r in rules:
+                ch.append(**r)             # staged: no map push, must not fail
+            ch.default = d
             try:
-                for r in rules:
-                    ch.append(**r)
-                ch.default = d
                 ch.apply_rules()
-                refused = False
-            except Exception:
-                refused = True
+            except IptablesError as pe:
+                why = str(pe)
+                refused = pe.code == -errno.ENOSPC and "LPM trie full" in why
             ipt.close()
             return {"seed": seed, "service": "iptables" if fw_mode < 0 else f"firewall/ct{fw_mode}",
                     "rules": len(rules), "oracle_refused": str(e), "product_refused": refused,
-                    "mismatches": 0 if refused else 1, "counters_equal": refused}
+                    "product_error": why, "mismatches": 0 if refused else 1, "counters_equal": refused}
         if fw_mode < 0:
             o.apply_accept_established(c)
         for r in rules:
