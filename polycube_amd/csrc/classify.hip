@@ -116,6 +116,15 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 #ifndef PCN_GEN_QUAD
 #define PCN_GEN_QUAD 1
 #endif
+// Offsets / lengths batches: the next header prefetch is issued after the
+// candidate stage instead of before the parse.  vmcnt completes in order, so
+// the candidate stage's L2 reads of a dense PART (config 5) wait for every
+// load issued before them: a prefetch issued before the stage is forced to
+// land by it, half an iteration after its issue.  Issued after the stage, at
+// depth 2, each header has about one iteration before a wait forces it.
+#ifndef PCN_PF_LATE
+#define PCN_PF_LATE 0
+#endif
 // Offsets batches: a frame's offset is loaded one prefetch ahead of its
 // header, so the header loads of a prefetch do not first wait on the offset
 // load (two dependent memory round trips per frame otherwise).
@@ -494,7 +503,7 @@ struct IntK {
 
 template <bool LDS, int NS, uint32_t WMAX = 64>
 __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[NS],
-                                                     WaveScratch *ws, uint32_t wave_bytes) {
+                                                     WaveScratch *ws, uint32_t wave_bytes, uint32_t &wide) {
   static_assert(WMAX == 64 || WMAX == 128, "deal window");
   // the window: 128 items when the build has the two-item workers and the
   // wave's LDS region holds them (wave-uniform), else 64
@@ -627,6 +636,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     mine.w = pk[2];
   }
   uint32_t qn = 0;      // items queued, not yet dealt (wave-uniform, < W)
+  uint32_t queued = 0;  // candidates over all blocks (wave-uniform)
   for (uint32_t k = 0; k < nsw; ++k) {
     const uint32_t live = nrw - k * 64;
     uint64_t m = 0;
@@ -650,6 +660,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       if (__ballot(c >> (b + 1)) == 0) break;
     }
     const bool last_block = k + 1 == nsw;
+    queued += total;
     if (total == 0 && (!last_block || qn == 0)) continue;
     if (!staged) {
       staged = true;
@@ -679,6 +690,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     }
   }
   if (PCN_ABLATE == 3) return mseen ? 0u : kNoRule;
+  wide += queued > 64 ? 1u : 0u;   // a 64-candidate window needed a second pass
   return staged ? ws->best[lane] : kNoRule;
 }
 
@@ -695,13 +707,14 @@ __device__ __forceinline__ uint32_t chain_finish(const DevChain &ch, uint32_t be
 // Called with the wave converged.
 template <bool LDS, int NS, uint32_t W = 64>
 __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const Parsed &p, uint32_t port,
-                                          WaveScratch *ws, uint32_t wave_bytes, uint32_t &verdict, int32_t &rid) {
+                                          WaveScratch *ws, uint32_t wave_bytes, uint32_t &verdict, int32_t &rid,
+                                          uint32_t &wide) {
   uint32_t cls[NS];
   bool need = false;
   if (mine) need = chain_classes<LDS, NS>(ch, p, port, cls, verdict, rid);
   // the wave gets issue priority while it deals candidates through LDS
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(PCN_CAND_PRIO >= 0 ? PCN_CAND_PRIO : 0);
-  const uint32_t best = chain_candidates<LDS, NS, W>(ch, need, cls, ws, wave_bytes);
+  const uint32_t best = chain_candidates<LDS, NS, W>(ch, need, cls, ws, wave_bytes, wide);
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(0);
   if (need) verdict = chain_finish(ch, best, rid);
 }
@@ -935,6 +948,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   for (uint32_t b = threadIdx.x; b < (FIXED ? 1u : 2u) * a.nbins; b += blockDim.x) bins[b] = 0;
   for (uint32_t k = threadIdx.x; k < a.nlocal; k += blockDim.x)
     reinterpret_cast<uint32_t *>(pcn_smem + a.lds_localip)[k] = a.localip[k];
+  uint32_t *const lds_stats = reinterpret_cast<uint32_t *>(pcn_smem + a.lds_stats);
+  if (threadIdx.x == 0) *lds_stats = 0;
+  uint32_t wide = 0;   // this wave's rule stages that dealt more than 64 candidates (wave-uniform)
   __syncthreads();
   // Stage d always holds the frames i with (i - first) / step == d (mod
   // PF): the loop is unrolled PF times so no stage is
@@ -1031,7 +1047,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
     uint32_t L = FIXED ? a.fixed_len : cur.L;
     const uint32_t cur_port = cur.port, cur_ct = cur.ct;
-    prefetch(cur, i + PF * step);
+    constexpr bool kLate = PCN_PF_LATE && !FIXED;
+    if (!kLate) prefetch(cur, i + PF * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
     int32_t cchain = -1;    // chain whose counters this packet bumps
@@ -1215,18 +1232,21 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
     if (CH < 3) {
-      run_chain<LDS, NS, kDealW>(run_ch, chain >= 0, p, port, ws, a.wave_bytes, verdict, rid);
+      run_chain<LDS, NS, kDealW>(run_ch, chain >= 0, p, port, ws, a.wave_bytes, verdict, rid, wide);
       if (chain >= 0) cchain = chain;
     } else {
       if (__ballot(chain == PCN_IPT_FORWARD)) {
-        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, a.wave_bytes, verdict, rid);
+        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_FORWARD], chain == PCN_IPT_FORWARD, p, port, ws, a.wave_bytes, verdict, rid,
+                                   wide);
         if (chain == PCN_IPT_FORWARD) cchain = PCN_IPT_FORWARD;
       }
       if (__ballot(chain == PCN_IPT_INPUT)) {
-        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, a.wave_bytes, verdict, rid);
+        run_chain<LDS, NS, kDealW>(a.ch[PCN_IPT_INPUT], chain == PCN_IPT_INPUT, p, port, ws, a.wave_bytes, verdict, rid,
+                                   wide);
         if (chain == PCN_IPT_INPUT) cchain = PCN_IPT_INPUT;
       }
     }
+    if (kLate) prefetch(cur, i + PF * step);
     if (valid) {
       a.verdicts[i] = static_cast<uint8_t>(verdict);
       if (a.rule_ids) a.rule_ids[i] = rid;
@@ -1312,7 +1332,12 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   }
   // the last stages' (unused) asm chunk loads land before the wave moves on
   if (PCN_HDR_ASM && FIXED && PCN_HDR_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.deal_stats && lane == 0 && wide) atomicAdd(lds_stats, wide);
   __syncthreads();
+  // the workgroup's deal statistics, stored into host-mapped memory (a plain
+  // system-scope vector store; the host reads whatever has landed)
+  if (a.deal_stats && threadIdx.x == 0)
+    __hip_atomic_store(&a.deal_stats[blockIdx.x], *lds_stats, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (chunked) {
     // The launch's last workgroup to finish zeroes the start counter for the
     // next launch (no memset per launch) and, on the batch's last launch,

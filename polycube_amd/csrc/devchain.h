@@ -206,6 +206,12 @@ struct LaunchArgs {
   uint32_t ctr_rep_mask;         // copies - 1 (a power of two; 0: one copy)
   uint32_t ctr_rep_words;        // u64 words between packed copies
   uint32_t ctr_pack_off;         // u64 words from ch[c].ctr to packed copy 0; 0: unpacked
+  // Deal statistics (pcn_ipt.cpp, the adaptive deal window): each workgroup
+  // stores, in host-mapped memory, how many of its waves' rule stages dealt
+  // more than 64 candidates -- the passes a 128-candidate window saves.  The
+  // host picks the next launch's chain program from them without a sync.
+  uint32_t *deal_stats;          // [grid] host-mapped u32 per workgroup; null: not counted
+  uint32_t lds_stats;            // byte offset of the workgroup's u32 counter in LDS
 };
 
 // Packed counter pair: packets in bits 38-63, bytes in bits 0-37.

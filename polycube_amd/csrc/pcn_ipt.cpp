@@ -82,6 +82,17 @@ uint32_t partial_rule_bins(uint32_t used, uint32_t per_bin, uint32_t ncounted) {
   return nb < ncounted ? nb : ncounted;
 }
 
+// Adaptive deal window (launch_batch): 1 on (default), 0 off (the 64-candidate
+// chain program always), 2 the 128 one always (A/B): PCN_IPT_DEBUG_DEAL_ADAPT.
+int deal_adapt() {
+  static const int v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_DEAL_ADAPT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+constexpr uint32_t kDealStatsSlots = 1024;   // workgroups a counted launch may have
+
 uint32_t wave_region_bytes(bool fixed, bool deal2) {
   static const uint32_t v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_WAVE_BYTES");
@@ -132,6 +143,8 @@ struct ChainState {
   JitShape jit_shape{};
   std::string jit_spec;
   uint32_t last_lds_bytes = 0;                 // dynamic LDS of the last launch that ran this chain's rules
+  bool deal_wide = false;                      // adaptive deal window: the 128-candidate program in use
+  std::string last_spec;                       // the chain program the last launch ran (empty: generic)
 };
 
 // One Horus program (pcn_ipt.h): pcn-iptables has one (ingress, built from
@@ -219,6 +232,12 @@ struct pcn_ipt {
   size_t stale_guard_from = 0;                 // first guard word (pcn_ipt_debug_stale_canary)
   uint32_t stale_epoch = 0;                    // bumped per launch (24 bits)
   uint32_t *d_chunk_ctr = nullptr;
+  // adaptive deal window (launch_batch): per workgroup of the last launch that
+  // counted, its waves that dealt more than 64 candidates (host-mapped, written
+  // by the kernel); that launch's grid and frames (0: nothing counted since)
+  uint32_t *h_deal_stats = nullptr;
+  uint32_t deal_grid = 0;
+  uint64_t deal_frames = 0;
 };
 
 namespace pcn {
@@ -676,6 +695,9 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
         hip_check(hipMalloc(&h.d_ctr, PCN_IPT_HORUS_MAX * 16), "hipMalloc(horus counters)");
         hip_check(hipMemset(h.d_ctr, 0, PCN_IPT_HORUS_MAX * 16), "hipMemset(horus counters)");
       }
+      hip_check(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_deal_stats), kDealStatsSlots * 4, hipHostMallocDefault),
+                "hipHostMalloc(deal statistics)");
+      std::memset(ctx->h_deal_stats, 0, kDealStatsSlots * 4);
       hip_check(hipMalloc(&ctx->d_hz_carry, 64), "hipMalloc(horus carry)");
       hip_check(hipMemset(ctx->d_hz_carry, 0, 64), "hipMemset(horus carry)");
       for (auto &cs : ctx->chains) {
@@ -728,6 +750,7 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
       if (ctx->ev_g1[k]) (void)hipEventDestroy(ctx->ev_g1[k]);
     }
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
+    if (ctx->h_deal_stats) (void)hipHostFree(ctx->h_deal_stats);
     for (auto &se : ctx->pack_streams)
       if (se.second) (void)hipEventDestroy(se.second);
     for (void *p : {static_cast<void *>(ctx->hz[0].d_tab), static_cast<void *>(ctx->hz[0].d_ctr),
@@ -861,7 +884,14 @@ int pcn_ipt_chain_set_default(pcn_ipt *ctx, int chain, int action) {
     // its DefaultAction program (pcn-firewall Chain.cpp:60-82): no chain
     // update, so its Horus program stays in place.
     fetch_stats(ctx, chain);
-    update_chain(ctx, chain, ctx->service != PCN_IPT_SERVICE_FIREWALL);
+    try {
+      update_chain(ctx, chain, ctx->service != PCN_IPT_SERVICE_FIREWALL);
+    } catch (const TableFull &e) {
+      // the reference catches the reload's runtime_error, logs "Can't reload
+      // the code for default action" and returns normally (Chain.cpp:123-129);
+      // the chain keeps its last image, the next update reports the overflow
+      g_last_error = std::string("Can't reload the code for default action. Error: ") + e.what();
+    }
     return 0;
   });
 }
@@ -1086,7 +1116,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       a.lds_images_bytes = img_bytes;
       a.bins_offset = kLdsDescBytes + img_bytes;
       a.lds_localip = a.bins_offset + (all_bin_bytes + 15) / 16 * 16;
-      a.lds_scratch = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;
+      a.lds_stats = (a.lds_localip + a.nlocal * 4 + 15) / 16 * 16;   // the deal statistics' counter
+      a.lds_scratch = a.lds_stats + 16;
       a.wave_bytes = wave_region_bytes(fixed, deal2);
       a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
     };
@@ -1221,13 +1252,48 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       }
       ctx->jit.request(cs.jit_spec, ctx->cfg.jit == 1);
       fn = ctx->jit.function(cs.jit_spec, ctx->cfg.device);
+      cs.last_spec = fn ? cs.jit_spec : std::string();
       // the generic kernel deals 64 a pass: give the 128-item region back
       if (!fn && deal2) {
         deal2 = false;
         plan_lds(false);
       }
       cs.last_lds_bytes = a.lds_bytes;
+      // Adaptive deal window (fixed-stride chains of one summary block, whose
+      // chain program deals 64 candidates a pass): with the previous launch's
+      // waves mostly holding more than 64 candidates (hit rate near 1: two
+      // passes each) the program with the 128-candidate window (classify.hip
+      // PCN_DEAL2 = 1, the same 3 KB wave region) runs instead; where no wave
+      // needs a second pass the 64 one stays (its smaller program is ~1.5 %
+      // faster).  The counts come from the kernel itself through
+      // host-mapped memory, read without a sync: whatever has landed.
+      const int adapt = deal_adapt();
+      if (fn && fixed && !sa && a.ch[ch].nsw == 1 && adapt && ctx->h_deal_stats) {
+        const std::string spec128 = cs.jit_spec + "#ifndef PCN_DEAL2\n#define PCN_DEAL2 1\n#endif\n";
+        ctx->jit.request(spec128, false);
+        bool wide = adapt == 2 || cs.deal_wide;
+        if (adapt == 1 && ctx->deal_frames) {
+          uint64_t sum = 0;
+          for (uint32_t k = 0; k < ctx->deal_grid; ++k) sum += reinterpret_cast<volatile uint32_t *>(ctx->h_deal_stats)[k];
+          const uint64_t waves = (ctx->deal_frames + 63) / 64;
+          if (!wide && sum * 8 > waves) wide = true;          // more than 1/8 of the waves: switch to 128
+          else if (wide && sum * 32 < waves) wide = false;    // fewer than 1/32: back to 64
+        }
+        cs.deal_wide = wide;
+        if (void *f128 = wide ? ctx->jit.function(spec128, ctx->cfg.device) : nullptr) {
+          fn = f128;
+          cs.last_spec = spec128;
+        }
+        const uint64_t grid = std::min<uint64_t>((b->n + PCN_BLOCK - 1) / PCN_BLOCK,
+                                                 uint64_t(classify_grid_cus(ctx->num_cus)));
+        if (grid <= kDealStatsSlots) {
+          a.deal_stats = ctx->h_deal_stats;
+          ctx->deal_grid = static_cast<uint32_t>(grid);
+          ctx->deal_frames = b->n;
+        }
+      }
     }
+    if (!a.deal_stats && !sa && !plan) ctx->deal_frames = 0;   // this launch counts nothing: forget the old counts
     if (plan) return 0;
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
     const hipStream_t hs = static_cast<hipStream_t>(stream);
@@ -1440,7 +1506,7 @@ int pcn_ipt_get_program_info(pcn_ipt *ctx, int chain, pcn_ipt_program_info *out)
     if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
     const ChainState &cs = ctx->chains[chain];
     out->dynamic_lds_bytes = cs.last_lds_bytes;
-    std::string spec = cs.jit_spec;
+    std::string spec = !cs.last_spec.empty() ? cs.last_spec : cs.jit_spec;
     if (spec.empty()) {
       if (cs.info.nrules == 0) return 0;
       if (int rc = usual_spec(ctx, chain, spec)) return rc;
@@ -1456,7 +1522,9 @@ int pcn_ipt_get_program_info(pcn_ipt *ctx, int chain, pcn_ipt_program_info *out)
     out->scratch_bytes = m.scratch < 0 ? 0u : static_cast<uint32_t>(m.scratch);
     out->static_lds_bytes = m.static_lds < 0 ? 0u : static_cast<uint32_t>(m.static_lds);
     out->code_bytes = m.code_bytes;
-    out->deal_window = spec.find("#define PCN_DEAL2 2") != std::string::npos ? 128u : 64u;
+    out->deal_window = spec.find("#define PCN_DEAL2 2") != std::string::npos ||
+                               (spec.find("#define PCN_DEAL2 1") != std::string::npos && cs.jit_shape.fixed)
+                           ? 128u : 64u;
     out->hdr_asm = m.hdr_asm;
     return 0;
   });

@@ -374,6 +374,41 @@ def test_packed_counter_copies_fold_across_launches_and_streams(dev, monkeypatch
     assert_counters(o, ipt, chains=(1,), n=len(rules))
 
 
+def test_adaptive_deal_window_follows_the_traffic(dev):
+    """A one-block chain's chain program deals 64 candidates a pass; when the
+    previous launch's waves mostly held more (hit rate 1: 64-110 candidate words
+    per wave) the 128-candidate program runs instead, and the 64 one again once
+    the traffic falls back (hit rate 0.5: never more than 63).  The choice reads
+    the kernel's own per-workgroup counts from host-mapped memory; results are
+    identical either way."""
+    import time
+    rs = synth.config_rules(3)
+    rules = rs.rules()
+    o, ipt = make_pair({1: rules}, {1: "DROP"}, jit=1)
+    chain = ipt.chain("FORWARD")
+    n = 1 << 20
+    frames = {}
+    for h in (1.0, 0.5):
+        cols = synth.make_headers(rs, n, 33, hit_frac=h)
+        frames[h] = synth.build_frames(*cols, frame_len=64).reshape(-1)
+    windows = []
+    for h in (1.0, 0.5):
+        tf = torch.from_numpy(frames[h]).to(dev)
+        for k in range(8):
+            v_g, r_g = ipt.classify(tf, n=n)
+            torch.cuda.synchronize()
+            if k in (0, 7):
+                v_o, r_o = o.classify(frames[h], n=n, nthreads=NTHREADS)
+                assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
+            else:
+                o.classify(frames[h], n=n, nthreads=NTHREADS)
+            if k == 3:
+                time.sleep(1.0)       # the 128-candidate program compiles in the background
+        windows.append(chain.program_info()["deal_window"])
+    assert windows == [128, 64], windows
+    assert_counters(o, ipt, chains=(1,), n=len(rules))
+
+
 def test_stream_of_a_closed_ring_is_never_touched(dev, monkeypatch):
     """A ring whose one stream carried batches, closed (its stream destroyed), then
     batches on the NULL stream and on a new stream: the context must not record an
