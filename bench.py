@@ -233,15 +233,18 @@ def parity_sample(o_rules, frames, v_dev, r_dev, offsets=None, lens=None, hook=0
 
 
 def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3, stride=64, frame_len=64, hdr_bytes=0,
-             zero_copy=False):
+             zero_copy=False, host_pack=False, pack_threads=0):
     """Host ingest ring (pcn_ipt_ring_*): pinned slots -> hipMemcpyAsync H2D ->
     classify -> D2H verdicts, `slots` slots in flight over as many streams.
     The frames are placed in the pinned slots once, as a NIC's RX DMA would
     write them (not timed); each timed pass submits n frames in chunk-frame
     slots and waits for every verdict to be back in host memory.  hdr_bytes:
-    only each frame's first hdr_bytes cross PCIe (a strided hipMemcpy2DAsync)."""
+    only each frame's first hdr_bytes cross PCIe (a strided hipMemcpy2DAsync, or with
+    host_pack the windows packed on pack_threads host threads, then one contiguous copy;
+    the pack runs inside each timed submit)."""
     from polycube_amd import IptablesError
-    ring = ipt.ring(slots=slots, slot_frames=chunk, slot_bytes=stride * chunk, zero_copy=zero_copy)
+    ring = ipt.ring(slots=slots, slot_frames=chunk, slot_bytes=stride * chunk, zero_copy=zero_copy,
+                    host_pack=host_pack, pack_threads=pack_threads)
     held = [ring.acquire() for _ in range(slots)]
     m = frames_host.size // stride
     for k, (slot, frames, _, _, _) in enumerate(held):
@@ -280,10 +283,14 @@ def e2e_legs(ipt, frames_host, n, rs, log):
     1536-byte stride) of the same traffic."""
     from polycube_amd import synth
     out = {}
-    legs = (("whole_frames", 0, False), ("header_only_48", 48, False), ("zero_copy", 0, True))
-    for name, hb, zc in legs:
-        out[name] = round(e2e_rate(ipt, frames_host, n, hdr_bytes=hb, zero_copy=zc), 2)
+    threads = host_cores()[0]
+    legs = (("whole_frames", 0, False, False), ("header_only_48", 48, False, False), ("zero_copy", 0, True, False),
+            ("header_pack_48", 48, False, True))
+    for name, hb, zc, hp in legs:
+        out[name] = round(e2e_rate(ipt, frames_host, n, hdr_bytes=hb, zero_copy=zc, host_pack=hp,
+                                   pack_threads=min(threads, 16)), 2)
         log(f"[bench] e2e 64B {name}: {out[name]} Mpkt/s")
+    out["pack_threads"] = min(threads, 16)
     m = 1 << 16
     cols = synth.make_headers(rs, m, synth.CONFIG_SEEDS[3] + 1)
     big = synth.build_frames(*cols, frame_len=1536).reshape(-1)
@@ -292,14 +299,16 @@ def e2e_legs(ipt, frames_host, n, rs, log):
         out["frames_1500"][name] = round(e2e_rate(ipt, big, 1 << 20, chunk=m, stride=1536, frame_len=1500,
                                                   hdr_bytes=hb, zero_copy=zc), 2)
         log(f"[bench] e2e 1500B {name}: {out['frames_1500'][name]} Mpkt/s")
-    out["kept"] = max((k for k, _, _ in legs), key=lambda k: out[k])
+    out["kept"] = max((k for k, _, _, _ in legs), key=lambda k: out[k])
     out["value"] = out[out["kept"]]
     out["unit"] = "Mpkt/s"
     out["what"] = ("host ingest ring (pcn_ipt_ring): pinned slots -> H2D -> classify -> D2H verdicts, 4 slots x 2^21 "
                    "64-byte frames in flight over 4 streams; whole frames vs. only each frame's first 48 bytes over "
                    "PCIe (pcn_ipt_ring_batch.hdr_bytes, a strided copy) vs. zero copy (PCN_IPT_RING_ZERO_COPY: the "
-                   "classify kernel reads the pinned slots over PCIe); frames_1500: 4 slots x 2^16 1500-byte frames "
-                   "at a 1536-byte stride, the same three")
+                   "classify kernel reads the pinned slots over PCIe) vs. header pack (PCN_IPT_RING_HOST_PACK: each "
+                   "submit packs the 48-byte windows into contiguous pinned rows on pack_threads host threads, then "
+                   "one contiguous 48-byte-stride copy; the pack is inside the timed loop); frames_1500: 4 slots x "
+                   "2^16 1500-byte frames at a 1536-byte stride, the first three")
     return out
 
 

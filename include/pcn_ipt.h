@@ -274,12 +274,18 @@ typedef struct pcn_ipt_ring pcn_ipt_ring;
  * bytes the kernel reads cross the bus (a frame's header window, not its
  * payload).  Verdicts still come back by copy.  Not with hdr_bytes. */
 #define PCN_IPT_RING_ZERO_COPY 2u
+/* With hdr_bytes: the host packs each frame's first hdr_bytes into a
+ * contiguous pinned staging buffer (pack_threads host threads), then ONE
+ * contiguous copy crosses PCIe, instead of a strided copy of hdr_bytes-byte
+ * rows (which the DMA engine moves one short row per request). */
+#define PCN_IPT_RING_HOST_PACK 4u
 typedef struct {
   uint32_t slots;         /* pinned slots, >= 2 */
   uint32_t slot_frames;   /* frames per slot, at most */
   uint64_t slot_bytes;    /* frame bytes per slot */
   uint32_t streams;       /* HIP streams the slots rotate over (0 => one per slot) */
   uint32_t flags;         /* PCN_IPT_RING_* */
+  uint32_t pack_threads;  /* PCN_IPT_RING_HOST_PACK: host threads that pack (0 => 8) */
 } pcn_ipt_ring_config;
 typedef struct {
   uint32_t slot;

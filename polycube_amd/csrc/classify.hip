@@ -116,14 +116,15 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 #ifndef PCN_GEN_QUAD
 #define PCN_GEN_QUAD 1
 #endif
-// Offsets / lengths batches: the next header prefetch is issued after the
-// candidate stage instead of before the parse.  vmcnt completes in order, so
-// the candidate stage's L2 reads of a dense PART (config 5) wait for every
-// load issued before them: a prefetch issued before the stage is forced to
-// land by it, half an iteration after its issue.  Issued after the stage, at
-// depth 2, each header has about one iteration before a wait forces it.
+// Offsets / lengths batches of a chain program whose PART is dense (read
+// from L2 in the candidate stage: config 5): the next header prefetch is
+// issued after the candidate stage instead of before the parse.  vmcnt
+// completes in order, so the stage's L2 reads wait for every load issued
+// before them, and a prefetch issued first was forced to land there.  A/B
+// on config 5 at 2^22 frames (profiles/r05_s2/ab_cfg5*.log): XDP 153-156 ->
+// 148 us, TC 177.6 -> 174.4 us; at depth 2 (either issue point) no gain.
 #ifndef PCN_PF_LATE
-#define PCN_PF_LATE 0
+#define PCN_PF_LATE 1
 #endif
 // Offsets batches: a frame's offset is loaded one prefetch ahead of its
 // header, so the header loads of a prefetch do not first wait on the offset
@@ -445,6 +446,9 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
 #ifndef PCN_ITEM_CLS
 #define PCN_ITEM_CLS 1   // 1: candidates carry their owner's classes; 0: owners stage class rows
 #endif
+#ifndef PCN_WFIELDS
+#define PCN_WFIELDS 1    // dense PART: read a field's PART cell only where its slot can be partial
+#endif
 #ifndef PCN_REC_PIN
 #define PCN_REC_PIN 0    // 1: candidate records all issued before the first is used (A/B: 1.6 % slower, profiles/r02_ab_recpin.log)
 #endif
@@ -553,12 +557,10 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     // word (indexed PART: through the zero cell, index 0).
     uint32_t at[K][NS];   // LDS/image offset of each field's u64 word
     u32x3 recs[K][NS];    // {PM lo, PM hi, PBASE} (the record's 4th dword is padding)
-    uint64_t pmw[K][NS];  // dense PART with PM masks: each field's PM word (LDS)
-    if (lay.part_dense && lay.dense_pm) {
+    uint32_t wf[K];       // dense PART: the slots that can be partial at the word (LDS)
+    if (lay.part_dense) {
 #pragma unroll
-      for (int q = 0; q < K; ++q)
-#pragma unroll
-        for (int f = 0; f < NS; ++f) pmw[q][f] = t.u64(lay.dense_pm, 8 * (oc[q][f] * nsw + k[q]));
+      for (int q = 0; q < K; ++q) wf[q] = PCN_WFIELDS && lay.wfields ? t.u8(lay.wfields, w[q]) : 0xffu;
     }
     if (!lay.part_dense) {
       // all records in flight together: one LDS round trip (left to itself
@@ -576,7 +578,7 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
         if (lay.part_dense) {
           const uint32_t cell = oc[q][f] * nrw + w[q];
           uint32_t qi = 0;   // POOL index (0: all-ones, a FULL field)
-          if (!lay.dense_pm || ((pmw[q][f] >> bit[q]) & 1))
+          if ((wf[q] >> f) & 1)
             qi = lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell);
           at[q][f] = lay.pool + 8 * qi;
           continue;
@@ -1047,7 +1049,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
     uint32_t L = FIXED ? a.fixed_len : cur.L;
     const uint32_t cur_port = cur.port, cur_ct = cur.ct;
-    constexpr bool kLate = PCN_PF_LATE && !FIXED;
+    constexpr bool kLate = PCN_PF_LATE && !FIXED && JIT && kJitChain.lay.part_dense;
     if (!kLate) prefetch(cur, i + PF * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;

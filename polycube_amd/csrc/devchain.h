@@ -117,9 +117,9 @@ struct TableLayout {
   uint32_t pool;           // u64[]: distinct partial words; POOL[0] is all-ones
   uint32_t zero;           // 16 zero bytes (the PART cell a FULL field reads: index 0)
   uint32_t perm;           // u16[nrw * 63]
-  uint32_t dense_pm;       // dense PART only, != 0: u64[nvec][nsw] in the LDS prefix, PM per class
-                           // and block (bit w: word w partial); a field FULL at a candidate word
-                           // then reads no PART cell from L2
+  uint32_t wfields;        // dense PART only: u8[nrw] in the LDS prefix, bit f set when a class of
+                           // slot f can be partial at word w; a candidate field whose bit is clear
+                           // is FULL there and reads no PART cell from L2
 };
 
 struct DevChain {

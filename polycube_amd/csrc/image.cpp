@@ -39,15 +39,7 @@ bool ip_search_only() {
   static const bool v = std::getenv("PCN_IPT_DEBUG_IPSEARCH") != nullptr;
   return v;
 }
-// PCN_IPT_DEBUG_DENSE_PM=1: dense PART images with the PM masks (A/B);
 // PCN_IPT_DEBUG_IP_BITS=b: IP bucket tables of at most 2^b entries (A/B).
-bool dense_pm_masks() {
-  static const bool v = [] {
-    const char *e = std::getenv("PCN_IPT_DEBUG_DENSE_PM");
-    return e && *e == '1';
-  }();
-  return v;
-}
 uint32_t ip_bits_max() {
   static const uint32_t v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_IP_BITS");
@@ -244,6 +236,8 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
   for (int f = 0; f < PCN_IPT_NFIELDS; ++f)
     if (t.maps[f].present()) img.present |= 1u << f;
 
+  // the classes each slot can hold (wfields below): 0 meta, 1/2 IP, 3.. own-slot key fields
+  std::vector<std::set<uint32_t>> slot_cls(6);
   // vectors visible to the datapath, per field (IP: after the trie collapse)
   std::vector<LpmEntry> lpm[2];
   std::vector<std::vector<const BitVec *>> field_vecs(PCN_IPT_NFIELDS);
@@ -271,6 +265,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     Intervals iv = lpm_intervals(m);
     std::vector<uint16_t> cls;
     for (int32_t c : iv.cls) cls.push_back(c < 0 ? PCN_CLS_MISS : pool.intern(m.vecs[c]));
+    slot_cls[1 + side].insert(cls.begin(), cls.end());
     // Bucket entry (count << 16) | first: the boundaries inside the bucket
     // are bnd[first, first + count).  The kernel runs a branchless upper-bound
     // search of ip_steps[side] steps (a wave-uniform trip count), so the bucket
@@ -456,6 +451,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
       return v ? pool.intern(*v) : PCN_CLS_MISS;
     };
     lay.hash_wild[i] = value(miss_vec[i]);
+    if (!merged[i]) slot_cls[lay.key_slot[i]].insert(lay.hash_wild[i]);
     if (i < 2) lay.key_skip[i] = merged[i] ? K[i].index(&ones) : img.all_cls;
     size_t nk = 0;
     for (size_t k = 0; k < m.keys.size(); ++k)
@@ -475,6 +471,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
         if (tab[h] != PCN_HASH_EMPTY) h = (h + 1) & (size - 1);
         if (tab[h] != PCN_HASH_EMPTY) { ok = false; break; }
         tab[h] = (key << 16) | value(&m.vecs[k]);
+        if (!merged[i]) slot_cls[lay.key_slot[i]].insert(tab[h] & 0xffff);
       }
       if (!ok) continue;
       tab[size] = tab[0];
@@ -499,6 +496,7 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     std::vector<uint16_t> meta;
     meta.reserve(stride);
     for_each_entry(dims, [&](const BitVec *v) { meta.push_back(v ? pool.intern(*v) : PCN_CLS_MISS); });
+    slot_cls[0].insert(meta.begin(), meta.end());
     lay.proto_idx = blob.add(pidx);
     lay.flags_idx = blob.add(fidx);
     lay.ct_idx = blob.add(cidx);
@@ -562,12 +560,18 @@ HostImage build_image_with(const ChainTables &t, uint32_t join) {
     const size_t indexed_bytes = blob.bytes.size() + words.size() * 8 + perm.perm.size() * 2 + cand.size() * 4 +
                                  part.size() * iw + 5 * kAlign;
     lay.part_dense = indexed_bytes > kDenseMinBytes && dense.size() * iw <= kDenseMaxBytes && !compact_images();
-    if (lay.part_dense && dense_pm_masks()) {
-      // PM per class and block in the LDS prefix (A/B): a field FULL at a
-      // candidate word (index 0: POOL[0]) reads no PART cell from L2
-      std::vector<uint64_t> pmv(nrec);
-      for (size_t r = 0; r < nrec; ++r) pmv[r] = uint64_t(cand[4 * r + 1]) << 32 | cand[4 * r];
-      lay.dense_pm = blob.add(pmv);
+    if (lay.part_dense) {
+      // Per word, the slots whose classes can be partial there (a word's rules
+      // constrain ~3 of config 5's 5 slots): a candidate field outside them is
+      // FULL whatever the class, and its PART cell is not read from L2.
+      std::vector<uint8_t> wf(img.nrw, 0);
+      for (uint32_t f = 0; f < lay.nslots; ++f)
+        for (uint32_t c : slot_cls[f]) {
+          if (c >= img.nvec) continue;   // PCN_CLS_MISS: no entry, the packet takes the default
+          for (uint32_t w = 0; w < img.nrw; ++w)
+            if (dense[size_t(c) * img.nrw + w]) wf[w] |= uint8_t(1u << f);
+        }
+      lay.wfields = blob.add(wf);
     }
     lay.pool = blob.add(words);
     lay.zero = blob.add(std::vector<uint32_t>(4, 0));

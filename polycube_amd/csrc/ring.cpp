@@ -10,11 +10,16 @@
 // the classify kernels of other slots.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <condition_variable>
 #include <cerrno>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pcn_ipt.h"
@@ -41,10 +46,80 @@ struct Slot {
   int32_t *d_rule_ids = nullptr;
   hipEvent_t done = nullptr;
   uint64_t n = 0;
+  // PCN_IPT_RING_HOST_PACK: the packed header windows (pinned host), bytes held
+  uint8_t *h_pack = nullptr;
+  size_t pack_cap = 0;
   // PCN_IPT_RING_ZERO_COPY: device addresses of the pinned buffers (not owned)
   uint8_t *z_frames = nullptr;
   uint32_t *z_offsets = nullptr;
   uint16_t *z_lens = nullptr, *z_in_port = nullptr;
+};
+
+// Host threads that pack header windows (PCN_IPT_RING_HOST_PACK): run(fn, k)
+// calls fn(0..k-1) on the pool (and the caller) and returns when all are done.
+class PackPool {
+ public:
+  explicit PackPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  ~PackPool() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : workers_) t.join();
+  }
+  void run(const std::function<void(unsigned)> &fn, unsigned parts) {
+    std::unique_lock<std::mutex> l(mu_);
+    fn_ = &fn;
+    parts_ = parts;
+    next_ = 0;
+    left_ = parts;
+    ++gen_;
+    cv_.notify_all();
+    l.unlock();
+    work();                                    // the caller takes parts too
+    l.lock();
+    done_.wait(l, [&] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      unsigned k;
+      const std::function<void(unsigned)> *fn;
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        if (!fn_ || next_ >= parts_) return;
+        k = next_++;
+        fn = fn_;
+      }
+      (*fn)(k);
+      std::lock_guard<std::mutex> l(mu_);
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)> *fn_ = nullptr;
+  unsigned parts_ = 0, next_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
 };
 
 }  // namespace
@@ -66,6 +141,7 @@ struct pcn_ipt_ring {
   std::vector<hipStream_t> streams;
   std::deque<uint32_t> inflight;   // submission order
   std::mutex mu;
+  std::unique_ptr<PackPool> pack;  // PCN_IPT_RING_HOST_PACK
 };
 
 namespace {
@@ -77,6 +153,7 @@ void free_slot(Slot &s) {
   if (s.h_in_port) (void)hipHostFree(s.h_in_port);
   if (s.h_verdicts) (void)hipHostFree(s.h_verdicts);
   if (s.h_rule_ids) (void)hipHostFree(s.h_rule_ids);
+  if (s.h_pack) (void)hipHostFree(s.h_pack);
   if (s.d_frames) (void)hipFree(s.d_frames);
   if (s.d_offsets) (void)hipFree(s.d_offsets);
   if (s.d_lens) (void)hipFree(s.d_lens);
@@ -125,8 +202,11 @@ int pcn_ipt_ring_create(pcn_ipt *ctx, const pcn_ipt_ring_config *cfg, pcn_ipt_ri
   if (device < 0) return ring_fail(-ENODEV, "context has no HIP device (created with device=-1)");
   if (cfg->slots < 2 || cfg->slot_frames == 0 || cfg->slot_bytes == 0)
     return ring_fail(-EINVAL, "need >= 2 slots of >= 1 frame and >= 1 byte");
-  if (cfg->flags & ~uint32_t(PCN_IPT_RING_RULE_IDS | PCN_IPT_RING_ZERO_COPY))
+  if (cfg->flags & ~uint32_t(PCN_IPT_RING_RULE_IDS | PCN_IPT_RING_ZERO_COPY | PCN_IPT_RING_HOST_PACK))
     return ring_fail(-EINVAL, "unknown ring flags");
+  if ((cfg->flags & PCN_IPT_RING_ZERO_COPY) && (cfg->flags & PCN_IPT_RING_HOST_PACK))
+    return ring_fail(-EINVAL, "PCN_IPT_RING_HOST_PACK packs for a copy: not with PCN_IPT_RING_ZERO_COPY");
+  if (cfg->pack_threads > 64) return ring_fail(-EINVAL, "pack_threads > 64");
   if (hipSetDevice(device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
   auto *r = new pcn_ipt_ring();
   r->ctx = ctx;
@@ -145,6 +225,10 @@ int pcn_ipt_ring_create(pcn_ipt *ctx, const pcn_ipt_ring_config *cfg, pcn_ipt_ri
     (void)hipGetLastError();
     pcn_ipt_ring_destroy(r);
     return ring_fail(-ENOMEM, "ring allocation failed (pinned host or device memory)");
+  }
+  if (r->cfg.flags & PCN_IPT_RING_HOST_PACK) {
+    if (!r->cfg.pack_threads) r->cfg.pack_threads = 8;
+    r->pack = std::make_unique<PackPool>(r->cfg.pack_threads - 1);   // + the submitting thread
   }
   *out = r;
   return 0;
@@ -204,7 +288,32 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   // PCIe in: frames (or their first hb bytes: a strided copy, hb-byte rows
   // packed on the device) and the per-frame arrays the batch uses
   bool ok = true;
-  if (!zc) {
+  if (hb && r->pack && n) {
+    // host pack: the windows into contiguous pinned rows (the slot's last
+    // copy out of them was queued on this slot's stream: wait for it first)
+    if (s.pack_cap < n * hb) {
+      if (hipStreamSynchronize(st) != hipSuccess) return ring_fail(-EIO, "hipStreamSynchronize failed");
+      if (s.h_pack) (void)hipHostFree(s.h_pack);
+      s.h_pack = nullptr;
+      s.pack_cap = 0;
+      if (hipHostMalloc(reinterpret_cast<void **>(&s.h_pack), size_t(r->cfg.slot_frames) * hb, hipHostMallocDefault) !=
+          hipSuccess)
+        return ring_fail(-ENOMEM, "pinned pack buffer");
+      s.pack_cap = size_t(r->cfg.slot_frames) * hb;
+    } else if (hipEventSynchronize(s.done) != hipSuccess) {   // (a released slot: its copies are done already)
+      return ring_fail(-EIO, "hipEventSynchronize failed");
+    }
+    const uint8_t *src = s.h_frames;
+    uint8_t *dst = s.h_pack;
+    const uint32_t stride = b->stride;
+    const unsigned parts = r->cfg.pack_threads * 4;
+    const size_t per = (n + parts - 1) / parts;
+    r->pack->run([&](unsigned k) {
+      const size_t lo = k * per, hi = std::min<size_t>(n, lo + per);
+      for (size_t i = lo; i < hi; ++i) std::memcpy(dst + i * hb, src + i * stride, hb);
+    }, parts);
+    ok = hipMemcpyAsync(s.d_frames, s.h_pack, n * hb, hipMemcpyHostToDevice, st) == hipSuccess;
+  } else if (!zc) {
     ok = hb ? hipMemcpy2DAsync(s.d_frames, hb, s.h_frames, b->stride, hb, n, hipMemcpyHostToDevice, st) == hipSuccess
             : hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
     if (ok && b->use_offsets) ok = hipMemcpyAsync(s.d_offsets, s.h_offsets, 4 * n, hipMemcpyHostToDevice, st) == hipSuccess;

@@ -56,7 +56,7 @@ class JitInfo(C.Structure):
 
 class RingConfig(C.Structure):
     _fields_ = [("slots", C.c_uint32), ("slot_frames", C.c_uint32), ("slot_bytes", C.c_uint64),
-                ("streams", C.c_uint32), ("flags", C.c_uint32)]
+                ("streams", C.c_uint32), ("flags", C.c_uint32), ("pack_threads", C.c_uint32)]
 
 
 class RingSlot(C.Structure):

@@ -317,10 +317,14 @@ class Iptables:
     def synchronize(self):
         _check(ffi.lib().pcn_ipt_synchronize(self._h))
 
-    def ring(self, slots=4, slot_frames=1 << 20, slot_bytes=None, streams=0, rule_ids=False, zero_copy=False):
+    def ring(self, slots=4, slot_frames=1 << 20, slot_bytes=None, streams=0, rule_ids=False, zero_copy=False,
+             host_pack=False, pack_threads=0):
         """Host ingest ring (pcn_ipt_ring_*): pinned slots -> HBM -> classify -> verdicts.
-        zero_copy: the kernel reads the frames in the pinned slots over PCIe (PCN_IPT_RING_ZERO_COPY)."""
-        return IngestRing(self, slots, slot_frames, slot_bytes or 64 * slot_frames, streams, rule_ids, zero_copy)
+        zero_copy: the kernel reads the frames in the pinned slots over PCIe (PCN_IPT_RING_ZERO_COPY);
+        host_pack: header-only submits pack the windows on host threads, one contiguous copy
+        (PCN_IPT_RING_HOST_PACK)."""
+        return IngestRing(self, slots, slot_frames, slot_bytes or 64 * slot_frames, streams, rule_ids, zero_copy,
+                          host_pack, pack_threads)
 
     # ---- stateful connection tracking ----
     def ct_enable(self, capacity_log2=0):
@@ -447,13 +451,15 @@ class IngestRing:
     it; complete() returns the oldest slot's (slot, verdicts[, rule_ids]) views,
     valid until release(slot)."""
 
-    def __init__(self, ipt, slots, slot_frames, slot_bytes, streams, rule_ids, zero_copy=False):
+    def __init__(self, ipt, slots, slot_frames, slot_bytes, streams, rule_ids, zero_copy=False, host_pack=False,
+                 pack_threads=0):
         import numpy as np
         self._np = np
         self._ipt = ipt
         self.slot_frames = slot_frames
         self.slot_bytes = slot_bytes
-        cfg = ffi.RingConfig(slots, slot_frames, slot_bytes, streams, (1 if rule_ids else 0) | (2 if zero_copy else 0))
+        flags = (1 if rule_ids else 0) | (2 if zero_copy else 0) | (4 if host_pack else 0)
+        cfg = ffi.RingConfig(slots, slot_frames, slot_bytes, streams, flags, pack_threads)
         h = C.c_void_p()
         _check(ffi.lib().pcn_ipt_ring_create(ipt._h, C.byref(cfg), C.byref(h)))
         self._h = h

@@ -15,7 +15,7 @@ LAYOUT = ["bytes", "ip_bkt0", "ip_bkt1", "ip_shift0", "ip_shift1", "ip_steps0", 
           "hash0", "hash1", "hash2", "mask0", "mask1", "mask2", "wild0", "wild1", "wild2", "skip0", "skip1",
           "slot0", "slot1", "slot2", "nslots", "proto_idx", "flags_idx", "ct_idx", "flags_skip", "meta",
           "stride_proto", "stride_flags", "stride_ct", "stride_sport", "stride_dport", "stride_iface",
-          "sf", "pbase", "part", "part_wide", "part_direct", "part_dense", "pool", "zero", "perm", "dense_pm"]
+          "sf", "pbase", "part", "part_wide", "part_direct", "part_dense", "pool", "zero", "perm", "wfields"]
 MISS = 0xFFFF
 EMPTY = 0xFFFFFFFF
 

@@ -500,8 +500,9 @@ def test_ingest_ring_parity(dev, zero_copy):
     assert_counters(o, ipt)
 
 
+@pytest.mark.parametrize("pack", [False, True], ids=["strided", "host_pack"])
 @pytest.mark.parametrize("hook,hdr", [(0, 48), (1, 64)], ids=["xdp48", "tc64"])
-def test_ingest_ring_header_only(dev, hook, hdr):
+def test_ingest_ring_header_only(dev, hook, hdr, pack):
     """pcn_ipt_ring_batch.hdr_bytes: only each frame's first hdr bytes cross
     PCIe (a strided copy, packed on the device) while the lengths still come
     from fixed_len / lens: equal to the oracle on the whole frames.  64-byte
@@ -511,8 +512,9 @@ def test_ingest_ring_header_only(dev, hook, hdr):
     from polycube_amd import IptablesError
     rs = synth.config_rules(3)
     o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
-    ring = ipt.ring(slots=2, slot_frames=1 << 13, slot_bytes=(1 << 13) * 1536, rule_ids=True)
-    for k, stride in enumerate((64, 96, 1536)):
+    ring = ipt.ring(slots=2, slot_frames=1 << 13, slot_bytes=(1 << 13) * 1536, rule_ids=True, host_pack=pack,
+                    pack_threads=3)
+    for k, stride in enumerate((64, 96, 1536, 64)):
         slot, frames, offsets, lens, in_port = ring.acquire()
         n = (1 << 13) - 5 * k
         if stride == 64:
