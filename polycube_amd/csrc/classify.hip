@@ -447,7 +447,7 @@ __device__ __forceinline__ bool chain_classes(const DevChain &ch, const Parsed &
 #define PCN_ITEM_CLS 1   // 1: candidates carry their owner's classes; 0: owners stage class rows
 #endif
 #ifndef PCN_WFIELDS
-#define PCN_WFIELDS 1    // dense PART: read a field's PART cell only where its slot can be partial
+#define PCN_WFIELDS 2    // dense PART: read a field's PART cell only where its slot can be partial
 #endif
 #ifndef PCN_REC_PIN
 #define PCN_REC_PIN 0    // 1: candidate records all issued before the first is used (A/B: 1.6 % slower, profiles/r02_ab_recpin.log)
@@ -577,9 +577,19 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
       for (int f = 0; f < NS; ++f) {
         if (lay.part_dense) {
           const uint32_t cell = oc[q][f] * nrw + w[q];
+          // A slot that cannot be partial at the word reads POOL[0] (all-ones)
+          // without a PART read.  PCN_WFIELDS 2: the load stays unconditional
+          // (a conditional load's phi costs an immediate vmcnt(0) wait), every
+          // such lane reading cell 0, one line for all of them; 1: a branch.
+          const bool part = (wf[q] >> f) & 1;
           uint32_t qi = 0;   // POOL index (0: all-ones, a FULL field)
-          if ((wf[q] >> f) & 1)
+          if (PCN_WFIELDS >= 2) {
+            const uint32_t c = part ? cell : 0u;
+            const uint32_t x = lay.part_wide ? t.u32(lay.part, 4 * c) : t.u16(lay.part, 2 * c);
+            qi = part ? x : 0u;
+          } else if (part) {
             qi = lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell);
+          }
           at[q][f] = lay.pool + 8 * qi;
           continue;
         }

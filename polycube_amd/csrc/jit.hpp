@@ -31,6 +31,7 @@ struct JitShape {
   int ch = 1;          // the one chain that runs rules (0..2)
   int ns = 5;          // class slots
   int inputs = 0;      // bit 0: per-frame in_port array, bit 1: per-frame ct_status array
+  bool shallow = false;   // fixed stride, at most 8 frames per lane: header prefetch depth 1
 };
 
 // Source of the generated "pcn_jit_spec.h" for one chain descriptor (its

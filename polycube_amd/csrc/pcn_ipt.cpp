@@ -82,6 +82,16 @@ uint32_t partial_rule_bins(uint32_t used, uint32_t per_bin, uint32_t ncounted) {
   return nb < ncounted ? nb : ncounted;
 }
 
+// PCN_IPT_DEBUG_SHALLOW=0: keep prefetch depth 2 for launches of few frames
+// per lane (A/B of JitShape::shallow)
+bool shallow_prefetch() {
+  static const bool v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_SHALLOW");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 // Adaptive deal window (launch_batch): 1 on (default), 0 off (the 64-candidate
 // chain program always), 2 the 128 one always (A/B): PCN_IPT_DEBUG_DEAL_ADAPT.
 int deal_adapt() {
@@ -1235,13 +1245,19 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.ns = ns;
       shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0) |
                      (a.horus_fields ? 16 : 0) | (a.offsets ? 32 : 0) | (a.lens ? 64 : 0);
+      {
+        const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((b->n + PCN_BLOCK - 1) / PCN_BLOCK,
+                                                                       uint64_t(classify_grid_cus(ctx->num_cus))));
+        shape.shallow = fixed && !plan && (b->n + grid * PCN_BLOCK - 1) / (grid * PCN_BLOCK) <= 8 &&
+                        shallow_prefetch();
+      }
       DevChain key = a.ch[ch];
       key.image = nullptr;
       key.ctr = nullptr;
       if (cs.jit_spec.empty() || std::memcmp(&key, &cs.jit_desc, sizeof(DevChain)) != 0 ||
           shape.fixed != cs.jit_shape.fixed ||
           shape.lds != cs.jit_shape.lds || shape.ch != cs.jit_shape.ch || shape.ns != cs.jit_shape.ns ||
-          shape.inputs != cs.jit_shape.inputs) {
+          shape.inputs != cs.jit_shape.inputs || shape.shallow != cs.jit_shape.shallow) {
         cs.jit_desc = key;
         cs.jit_shape = shape;
         cs.jit_spec = jit_spec(key, shape);
