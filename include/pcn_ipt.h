@@ -226,6 +226,11 @@ int pcn_ipt_debug_stale_canary(pcn_ipt *ctx);
  * sequence (conntrack.hip walk_long).  reset != 0 zeroes them after the read.
  * Synchronises the device. */
 int pcn_ipt_debug_ct_walk_passes(pcn_ipt *ctx, uint64_t out[2], int reset);
+/* Test hook: the stateful pipeline's (key bucket, batch index) sort (radix.hip)
+ * on its own.  keys: n device u32 < 2^kbits (left unchanged); out: the keys
+ * sorted stably and the batch index of each.  Synchronises the device. */
+int pcn_ipt_debug_sort_pairs(pcn_ipt *ctx, const uint32_t *keys, uint64_t n, uint32_t kbits, uint32_t *keys_out,
+                             uint32_t *idx_out);
 /* Compile the chain program of `chain` for its usual launch shape (fixed
  * 64-byte stride, ingress/egress alone, image in LDS) now and wait for it —
  * the blocking compile the reference does in Chain::updateChain.  Needs no

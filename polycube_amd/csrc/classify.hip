@@ -164,6 +164,9 @@ __device__ __forceinline__ uint32_t bswap16u(uint32_t x) { return ((x & 0xff) <<
 // and a table at or past `limit` is read from HBM/L2.  Tables never straddle
 // the limit, so the choice depends on the table's base only: a wave-uniform
 // branch in the generic kernel, a constant in a chain program.
+#ifndef PCN_BUF_LOADS
+#define PCN_BUF_LOADS 1  // dense PART cells through buffer loads (Tab::g16 / g32)
+#endif
 template <bool LDS>
 struct Tab {
   const uint8_t *g;
@@ -176,6 +179,25 @@ struct Tab {
     const uint32_t at = tbl + off;
     return (LDS && tbl < limit) ? *reinterpret_cast<const T *>(pcn_smem + base + at)
                                 : *reinterpret_cast<const T *>(g + at);
+  }
+  // A table past the LDS limit (the dense PART of a large chain) through a
+  // buffer load: a 32-bit offset from the image base in SGPRs, where the
+  // global form spends a 64-bit address computation (3-4 VALU) per load.
+  __device__ __forceinline__ uint32_t g16(uint32_t tbl, uint32_t off) const {
+    if (PCN_BUF_LOADS) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(g), 0, 0x7fffffff,
+                                                                         0x00020000);
+      return __builtin_amdgcn_raw_buffer_load_b16(r, tbl + off, 0, 0);
+    }
+    return *reinterpret_cast<const uint16_t *>(g + (tbl + off));
+  }
+  __device__ __forceinline__ uint32_t g32(uint32_t tbl, uint32_t off) const {
+    if (PCN_BUF_LOADS) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(g), 0, 0x7fffffff,
+                                                                         0x00020000);
+      return __builtin_amdgcn_raw_buffer_load_b32(r, tbl + off, 0, 0);
+    }
+    return *reinterpret_cast<const uint32_t *>(g + (tbl + off));
   }
   __device__ __forceinline__ uint32_t u32(uint32_t tbl, uint32_t off) const { return ld<uint32_t>(tbl, off); }
   __device__ __forceinline__ uint32_t u16(uint32_t tbl, uint32_t off) const { return ld<uint16_t>(tbl, off); }
@@ -505,7 +527,15 @@ struct IntK {
   static constexpr int value = K;
 };
 
-template <bool LDS, int NS, uint32_t WMAX = 64>
+// Chains of 2-4 summary blocks in a chain program (MERGE, PCN_MERGE_BLOCKS):
+// every block's summary words are read and ANDed at once (one LDS round trip),
+// one queue prefix covers all of them and one divergent loop queues a lane's
+// candidates of every block, instead of a summary read, a prefix and a queue
+// loop per block.
+#ifndef PCN_MERGE_BLOCKS
+#define PCN_MERGE_BLOCKS 1
+#endif
+template <bool LDS, int NS, uint32_t WMAX = 64, bool MERGE = false>
 __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool active, const uint32_t cls[NS],
                                                      WaveScratch *ws, uint32_t wave_bytes, uint32_t &wide) {
   static_assert(WMAX == 64 || WMAX == 128, "deal window");
@@ -583,12 +613,13 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
           // such lane reading cell 0, one line for all of them; 1: a branch.
           const bool part = (wf[q] >> f) & 1;
           uint32_t qi = 0;   // POOL index (0: all-ones, a FULL field)
+          // (dense PART is never staged in LDS: past the limit, read from L2)
           if (PCN_WFIELDS >= 2) {
             const uint32_t c = part ? cell : 0u;
-            const uint32_t x = lay.part_wide ? t.u32(lay.part, 4 * c) : t.u16(lay.part, 2 * c);
+            const uint32_t x = lay.part_wide ? t.g32(lay.part, 4 * c) : t.g16(lay.part, 2 * c);
             qi = part ? x : 0u;
           } else if (part) {
-            qi = lay.part_wide ? t.u32(lay.part, 4 * cell) : t.u16(lay.part, 2 * cell);
+            qi = lay.part_wide ? t.g32(lay.part, 4 * cell) : t.g16(lay.part, 2 * cell);
           }
           at[q][f] = lay.pool + 8 * qi;
           continue;
@@ -646,6 +677,58 @@ __device__ __forceinline__ uint32_t chain_candidates(const DevChain &ch, bool ac
     mine.y = pk[0];
     mine.z = pk[1];
     mine.w = pk[2];
+  }
+  if (MERGE && PCN_ABLATE != 3 && nsw >= 2 && nsw <= 4) {
+    constexpr uint32_t kMaxB = 4;
+    uint64_t mk[kMaxB] = {0, 0, 0, 0};
+    if (active) {
+      uint64_t sm[kMaxB][NS];
+#pragma unroll
+      for (uint32_t k = 0; k < kMaxB; ++k)
+        if (k < nsw)
+#pragma unroll
+          for (int f = 0; f < NS; ++f) sm[k][f] = t.u64(lay.sf, 8 * (cls[f] * nsw + k));
+#pragma unroll
+      for (uint32_t k = 0; k < kMaxB; ++k) {
+        if (k >= nsw) continue;
+        const uint32_t live = nrw - k * 64;
+        uint64_t m = live >= 64 ? ~0ull : ((1ull << live) - 1);
+#pragma unroll
+        for (int f = 0; f < NS; ++f) m &= sm[k][f];
+        mk[k] = m;
+      }
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kMaxB; ++k) c += static_cast<uint32_t>(__builtin_popcountll(mk[k]));
+    uint32_t pos = 0, total = 0;
+    for (uint32_t b = 0; b < 9; ++b) {   // c <= 256
+      const uint64_t bm = __ballot((c >> b) & 1);
+      pos += static_cast<uint32_t>(__builtin_popcountll(bm & ((1ull << lane) - 1))) << b;
+      total += static_cast<uint32_t>(__builtin_popcountll(bm)) << b;
+      if (__ballot(c >> (b + 1)) == 0) break;
+    }
+    wide += total > 64 ? 1u : 0u;
+    if (total == 0) return kNoRule;
+    ws->best[lane] = kNoRule;
+    uint32_t p = pos, end = total;
+    for (;;) {
+#pragma unroll
+      for (uint32_t k = 0; k < kMaxB; ++k) {
+        if (k >= nsw) continue;
+        while (mk[k] && p < W) {
+          mine.x = (lane << 16) | (k * 64 + static_cast<uint32_t>(__builtin_ctzll(mk[k])));
+          items[p] = mine;
+          mk[k] &= mk[k] - 1;
+          ++p;
+        }
+      }
+      drain(end < W ? end : W);
+      if (end <= W) break;
+      p -= W;   // (wraps for lanes with nothing left: they write no more)
+      end -= W;
+    }
+    return ws->best[lane];
   }
   uint32_t qn = 0;      // items queued, not yet dealt (wave-uniform, < W)
   uint32_t queued = 0;  // candidates over all blocks (wave-uniform)
@@ -717,7 +800,7 @@ __device__ __forceinline__ uint32_t chain_finish(const DevChain &ch, uint32_t be
 
 // One chain through the three parts; `mine` = lanes whose packet runs it.
 // Called with the wave converged.
-template <bool LDS, int NS, uint32_t W = 64>
+template <bool LDS, int NS, uint32_t W = 64, bool MERGE = false>
 __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const Parsed &p, uint32_t port,
                                           WaveScratch *ws, uint32_t wave_bytes, uint32_t &verdict, int32_t &rid,
                                           uint32_t &wide) {
@@ -726,7 +809,7 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
   if (mine) need = chain_classes<LDS, NS>(ch, p, port, cls, verdict, rid);
   // the wave gets issue priority while it deals candidates through LDS
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(PCN_CAND_PRIO >= 0 ? PCN_CAND_PRIO : 0);
-  const uint32_t best = chain_candidates<LDS, NS, W>(ch, need, cls, ws, wave_bytes, wide);
+  const uint32_t best = chain_candidates<LDS, NS, W, MERGE>(ch, need, cls, ws, wave_bytes, wide);
   if (PCN_CAND_PRIO >= 0) __builtin_amdgcn_s_setprio(0);
   if (need) verdict = chain_finish(ch, best, rid);
 }
@@ -1244,7 +1327,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
     if (CH < 3) {
-      run_chain<LDS, NS, kDealW>(run_ch, chain >= 0, p, port, ws, a.wave_bytes, verdict, rid, wide);
+      run_chain<LDS, NS, kDealW, JIT && PCN_MERGE_BLOCKS>(run_ch, chain >= 0, p, port, ws, a.wave_bytes, verdict, rid,
+                                                          wide);
       if (chain >= 0) cchain = chain;
     } else {
       if (__ballot(chain == PCN_IPT_FORWARD)) {

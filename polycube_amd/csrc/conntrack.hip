@@ -13,13 +13,12 @@
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <cstring>
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <vector>
 
 #include "conntrack.hpp"
+#include "radix.hpp"
 #include "pcn_ipt.h"
 
 #ifndef PCN_CT_FAST
@@ -2101,8 +2100,7 @@ struct CtScratch {
   PackedRec *brec = nullptr;  // walk records, batch order
   ct_u32x4 *ox = nullptr;     // the four stage-A outcomes per packet (batches with four labels)
   uint64_t ox_cap = 0;
-  void *temp = nullptr;
-  size_t temp_bytes = 0;
+  RadixScratch rx;            // the (key bucket, index) sort (radix.hip)
   // ct_advance_carry: 1 + the batch's last port-writing frame
   unsigned long long *zfound = nullptr;
 };
@@ -2115,10 +2113,11 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->keys), static_cast<void *>(s->keys2),
                   static_cast<void *>(s->idx2), static_cast<void *>(s->cursor), static_cast<void *>(s->hard_list),
                   static_cast<void *>(s->ctl), static_cast<void *>(s->brec), static_cast<void *>(s->ox),
-                  static_cast<void *>(s->heads), s->temp,
+                  static_cast<void *>(s->heads),
                   static_cast<void *>(s->zfound), static_cast<void *>(s->th_list), static_cast<void *>(s->bm),
                   static_cast<void *>(s->evh), static_cast<void *>(s->seg), static_cast<void *>(s->hx)})
     if (p) (void)hipFree(p);
+  radix_free(s->rx);
   delete s;
 }
 
@@ -2153,31 +2152,6 @@ void ct_table_free(CtTable &t) {
     if (e_ != hipSuccess) return int(e_);   \
   } while (0)
 
-// The (key bucket, batch index) sort: rocPRIM's onesweep radix sort with
-// PCN_CT_RADIX_BITS bits per pass (its gfx950 default is 8: a 25-bit key
-// took four passes, the last for one bit).
-#ifndef PCN_CT_RADIX_BITS
-#define PCN_CT_RADIX_BITS 9   // A/B 8 / 9 / 11: 0.54 / 0.41 / 0.52 ms a 2^24 batch
-#endif
-#ifndef PCN_CT_SORT_BLOCK
-#define PCN_CT_SORT_BLOCK 1024
-#endif
-#ifndef PCN_CT_SORT_ITEMS
-#define PCN_CT_SORT_ITEMS 8    // A/B 16 / 12 / 8 items per thread: 3.13 / 3.13 / 2.98 ms a 2^24 batch (16 and 12 use scratch)
-#endif
-using CtSortConfig = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<PCN_CT_SORT_BLOCK, PCN_CT_SORT_ITEMS>,
-                                        rocprim::kernel_config<PCN_CT_SORT_BLOCK, PCN_CT_SORT_ITEMS>,
-                                        PCN_CT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
-// The values are the batch indices 0..n-1, generated by the sort's first pass
-// (a counting iterator): nothing writes or reads an index array for them.
-static hipError_t sort_pairs(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout, uint32_t *vout,
-                             uint64_t n, uint32_t kbits, hipStream_t st) {
-  return rocprim::radix_sort_pairs<CtSortConfig>(temp, bytes, kin, kout, rocprim::counting_iterator<uint32_t>(0u), vout,
-                                                 static_cast<unsigned int>(n), 0u, kbits, st);
-}
-
 // PCN_IPT_DEBUG_CT_KBITS=b (16..30): key buckets of at most b bits, whatever
 // the batch size (A/B of fewer sort passes against more bucket collisions)
 static uint32_t debug_key_bits() {
@@ -2189,7 +2163,7 @@ static uint32_t debug_key_bits() {
   return v;
 }
 
-static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4, hipStream_t st) {
+static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4) {
   if (lab4 && s.ox_cap < n) {                  // only batches with four labels read it
     if (s.ox) CT_CHECK(hipFree(s.ox));
     CT_CHECK(hipMalloc(&s.ox, n * sizeof(ct_u32x4)));
@@ -2226,13 +2200,6 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4, hipStream_t
     if (s.bm) CT_CHECK(hipFree(s.bm));
     CT_CHECK(hipMalloc(&s.bm, bmb));
     s.bm_bytes = bmb;
-  }
-  size_t need = 0;
-  CT_CHECK(sort_pairs(nullptr, need, s.keys, s.keys2, s.idx2, n, kbits, st));
-  if (s.temp_bytes < need) {
-    if (s.temp) CT_CHECK(hipFree(s.temp));
-    CT_CHECK(hipMalloc(&s.temp, need));
-    s.temp_bytes = need;
   }
   return hipSuccess;
 }
@@ -2300,7 +2267,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   while (kbits < 30 && (uint64_t(1) << kbits) < 2 * b.n) ++kbits;
   kbits = std::min(kbits, debug_key_bits());
   const uint32_t sentinel = (1u << kbits) - 1;
-  CT_CHECK(grow(s, b.n, kbits, b.nlab == 4, st));
+  CT_CHECK(grow(s, b.n, kbits, b.nlab == 4));
   const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
   // one memset for the control words (long echo replies, run counts per
   // class, ct_prep's chunk counter, ...; kCtl*): each memset is a launch of
@@ -2324,9 +2291,8 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
                      sentinel, s.th_list);
   CT_CHECK(hipGetLastError());
   // (ct_heads advances the carry from ct_prep's published groups)
-  size_t tb;
-  tb = s.temp_bytes;
-  CT_CHECK(sort_pairs(s.temp, tb, s.keys, s.keys2, s.idx2, b.n, kbits, st));
+  // the sort (radix.hip; s.keys is its ping-pong buffer from here on)
+  CT_CHECK(radix_sort_pairs(s.rx, s.keys, s.keys2, s.idx2, b.n, kbits, num_cus, st));
   const RecSrc src{s.brec, s.idx2, s.keys2, s.ox, b.nlab == 4 ? 1u : 0u};
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "conntrack.hpp"
+#include "radix.hpp"
 #include "devchain.h"
 #include "image.hpp"
 #include "jit.hpp"
@@ -1542,6 +1543,26 @@ int pcn_ipt_get_program_info(pcn_ipt *ctx, int chain, pcn_ipt_program_info *out)
                                (spec.find("#define PCN_DEAL2 1") != std::string::npos && cs.jit_shape.fixed)
                            ? 128u : 64u;
     out->hdr_asm = m.hdr_asm;
+    return 0;
+  });
+}
+
+int pcn_ipt_debug_sort_pairs(pcn_ipt *ctx, const uint32_t *keys, uint64_t n, uint32_t kbits, uint32_t *keys_out,
+                             uint32_t *idx_out) {
+  return guarded(ctx, [&] {
+    if (!ctx->has_device) return fail(-ENODEV, "no device");
+    if (!keys || !keys_out || !idx_out || kbits == 0 || kbits > 32) return fail(-EINVAL, "bad argument");
+    device_guard(ctx);
+    RadixScratch rx;
+    uint32_t *tmp = nullptr;
+    hip_check(hipMalloc(&tmp, std::max<uint64_t>(n, 1) * 4), "hipMalloc(sort keys)");
+    hip_check(hipMemcpy(tmp, keys, n * 4, hipMemcpyDeviceToDevice), "hipMemcpy(sort keys)");
+    const int rc = radix_sort_pairs(rx, tmp, keys_out, idx_out, n, kbits, ctx->num_cus, nullptr);
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipFree(tmp);
+    radix_free(rx);
+    if (rc != hipSuccess) return fail(-EINVAL, std::string("radix sort: ") + hipGetErrorString(hipError_t(rc)));
+    hip_check(e, "hipDeviceSynchronize");
     return 0;
   });
 }

@@ -316,6 +316,8 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   } else if (!zc) {
     ok = hb ? hipMemcpy2DAsync(s.d_frames, hb, s.h_frames, b->stride, hb, n, hipMemcpyHostToDevice, st) == hipSuccess
             : hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+  }
+  if (!zc) {   // the per-frame arrays the batch uses
     if (ok && b->use_offsets) ok = hipMemcpyAsync(s.d_offsets, s.h_offsets, 4 * n, hipMemcpyHostToDevice, st) == hipSuccess;
     if (ok && b->use_lens) ok = hipMemcpyAsync(s.d_lens, s.h_lens, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
     if (ok && b->use_in_port) ok = hipMemcpyAsync(s.d_in_port, s.h_in_port, 2 * n, hipMemcpyHostToDevice, st) == hipSuccess;
