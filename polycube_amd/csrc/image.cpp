@@ -48,6 +48,15 @@ uint32_t ip_bits_max() {
   }();
   return v;
 }
+// PCN_IPT_DEBUG_CLUSTER=0: pack a type group's rules into words in rule-id
+// order (A/B of the value clustering in make_permutation)
+bool cluster_rules() {
+  static const bool v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_CLUSTER");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
 int forced_join() {
   static const int v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_JOIN");
@@ -96,7 +105,41 @@ Permutation make_permutation(const ChainTables &t, const std::vector<std::vector
   }
   std::vector<uint32_t> order(n);
   std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return type[a] < type[b]; });
+  // Inside a type group the rules that share a word are free to choose (a
+  // word keeps its bits in ascending rule id, and the packet's rule is the
+  // minimum over its matching words): rules with equal field values are put
+  // next to each other, so a word's rules agree on their values and a field's
+  // summary bits are set for few words of a class -- fewer candidate words
+  // whose fields each match some rule of the word but no rule all of them.
+  // A rule's value in field f is the first map entry whose vector holds it
+  // (its own key; for IP fields its own prefix, the shortest entry holding it).
+  std::vector<std::vector<uint32_t>> first(PCN_IPT_NFIELDS);
+  const int cluster_order[] = {PCN_IPT_F_DPORT, PCN_IPT_F_IPDST, PCN_IPT_F_IPSRC, PCN_IPT_F_L4PROTO,
+                               PCN_IPT_F_SPORT, PCN_IPT_F_TCPFLAGS, PCN_IPT_F_IFACE, PCN_IPT_F_CONNTRACK};
+  if (cluster_rules()) {
+    for (int f : cluster_order) {
+      const auto &vs = field_vecs[f];
+      if (vs.empty()) continue;
+      first[f].assign(n, ~0u);
+      for (size_t e = 0; e < vs.size(); ++e)
+        for (uint32_t w = 0; w < t.nrw && w < vs[e]->size(); ++w) {
+          uint64_t bits = (*vs[e])[w];
+          while (bits) {
+            const uint32_t r = w * kBitsPerWord + static_cast<uint32_t>(__builtin_ctzll(bits));
+            bits &= bits - 1;
+            if (r < n && first[f][r] == ~0u) first[f][r] = static_cast<uint32_t>(e);
+          }
+        }
+    }
+  }
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    if (type[a] != type[b]) return type[a] < type[b];
+    for (int f : cluster_order) {
+      if (first[f].empty()) continue;
+      if (first[f][a] != first[f][b]) return first[f][a] < first[f][b];
+    }
+    return false;
+  });
   std::map<uint32_t, size_t> group_size;
   for (uint32_t r = 0; r < n; ++r) group_size[type[r]]++;
   // Pack type groups into words.  A word mixing types can pass every field's

@@ -32,6 +32,8 @@ struct JitShape {
   int ns = 5;          // class slots
   int inputs = 0;      // bit 0: per-frame in_port array, bit 1: per-frame ct_status array
   bool shallow = false;   // fixed stride, at most 8 frames per lane: header prefetch depth 1
+  bool deal2 = false;     // two candidates per worker lane (a chain of 2+ summary blocks; the launch
+                          // sized the wave region for the 128-candidate window)
 };
 
 // Source of the generated "pcn_jit_spec.h" for one chain descriptor (its

@@ -83,6 +83,16 @@ uint32_t partial_rule_bins(uint32_t used, uint32_t per_bin, uint32_t ncounted) {
   return nb < ncounted ? nb : ncounted;
 }
 
+// PCN_IPT_DEBUG_DEAL2_MULTI=0: chains of 2+ summary blocks deal 64 candidates a
+// pass too (no 128-item wave region: that LDS goes to counter bins); A/B
+bool multi_block_deal2() {
+  static const bool v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_DEAL2_MULTI");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 // PCN_IPT_DEBUG_SHALLOW=0: keep prefetch depth 2 for launches of few frames
 // per lane (A/B of JitShape::shallow)
 bool shallow_prefetch() {
@@ -1132,7 +1142,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       a.wave_bytes = wave_region_bytes(fixed, deal2);
       a.lds_bytes = a.lds_scratch + (PCN_BLOCK / 64) * a.wave_bytes;
     };
-    bool deal2 = ch < 3 && any_rules && a.ch[ch].nsw >= 2 && ctx->cfg.jit >= 0;
+    bool deal2 = ch < 3 && any_rules && a.ch[ch].nsw >= 2 && ctx->cfg.jit >= 0 && multi_block_deal2();
     plan_lds(deal2);
     a.frames = b->frames;
     a.frames_bytes = b->frames_bytes;
@@ -1246,6 +1256,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.ns = ns;
       shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0) |
                      (a.horus_fields ? 16 : 0) | (a.offsets ? 32 : 0) | (a.lens ? 64 : 0);
+      shape.deal2 = deal2;
       {
         const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((b->n + PCN_BLOCK - 1) / PCN_BLOCK,
                                                                        uint64_t(classify_grid_cus(ctx->num_cus))));
@@ -1258,7 +1269,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       if (cs.jit_spec.empty() || std::memcmp(&key, &cs.jit_desc, sizeof(DevChain)) != 0 ||
           shape.fixed != cs.jit_shape.fixed ||
           shape.lds != cs.jit_shape.lds || shape.ch != cs.jit_shape.ch || shape.ns != cs.jit_shape.ns ||
-          shape.inputs != cs.jit_shape.inputs || shape.shallow != cs.jit_shape.shallow) {
+          shape.inputs != cs.jit_shape.inputs || shape.shallow != cs.jit_shape.shallow ||
+          shape.deal2 != cs.jit_shape.deal2) {
         cs.jit_desc = key;
         cs.jit_shape = shape;
         cs.jit_spec = jit_spec(key, shape);

@@ -2,20 +2,22 @@
 // of (key bucket, batch index) pairs, hand-written for gfx950.
 //
 // 1. radix_hist_kernel: one read of the keys, every pass's digit histogram at
-//    once (LDS histograms, one global add per non-empty bin and workgroup; the
-//    keys of packets that need no table -- one "hot" bucket, often most of a
-//    batch -- wave-aggregated).
-// 2. radix_scan_kernel: the global exclusive prefix of each digit's bins, and
-//    the histograms zeroed for the next sort.
+//    once (LDS histograms, one global add per non-empty bin and workgroup into
+//    one of 16 copies; the keys of packets that need no table -- one "hot"
+//    bucket, often most of a batch -- wave-aggregated).
+// 2. radix_scan_kernel: the global exclusive prefix of each digit's bins (the
+//    copies summed), and the histograms zeroed for the next sort.
 // 3. radix_pass_kernel, once per digit (9 / 8 / 8 bits of a 25-bit key): a
-//    tile of 8192 pairs per 1024-thread workgroup, claimed in start order.  Its
-//    items are ranked wave by wave and slot by slot in input order (lanes of
-//    one digit matched with `bits` ballots, a per-wave running count in LDS),
-//    the tile's digit counts are published and the counts of the tiles before
-//    it summed by decoupled look-back (one u64 per tile and digit: epoch,
-//    aggregate / inclusive flag, count), then the tile is ordered by digit in
-//    LDS and written out: consecutive items of a digit go to consecutive
-//    addresses.  The first pass makes the values (batch indices) itself.
+//    tile of 4096 pairs per 512-thread workgroup (three workgroups per CU),
+//    claimed in start order.  Its items are ranked wave by wave and slot by
+//    slot in input order (lanes of one digit matched with `bits` ballots, a
+//    per-wave running count in LDS), the tile's digit counts are published and
+//    the counts of the tiles before it summed by decoupled look-back (one u64
+//    per tile and digit: epoch, aggregate / inclusive flag, count; 16 earlier
+//    tiles read at once -- read one by one, the chain of dependent reads was
+//    the pass's time), then the tile is ordered by digit in LDS and written
+//    out: consecutive items of a digit go to consecutive addresses.  The first
+//    pass makes the values (batch indices) itself.
 // Stability: a tile's items keep input order within a digit (wave, slot, lane
 // order is input order), and tiles are placed in tile order.
 #include "radix.hpp"
@@ -25,17 +27,21 @@
 namespace pcn {
 namespace {
 
-constexpr uint32_t kRBlock = 1024;
+constexpr uint32_t kRBlock = 512;                  // pass workgroups: 3 per CU (46 KB of LDS each)
 constexpr uint32_t kRItems = 8;
-constexpr uint32_t kRTile = kRBlock * kRItems;     // 8192 pairs a tile
-constexpr uint32_t kRWaves = kRBlock / 64;         // 16
+constexpr uint32_t kRTile = kRBlock * kRItems;     // 4096 pairs a tile
+constexpr uint32_t kRWaves = kRBlock / 64;         // 8
 constexpr uint32_t kRMaxBits = 9;
-constexpr uint32_t kRMaxBins = 1u << kRMaxBits;    // 512
+constexpr uint32_t kRMaxBins = 1u << kRMaxBits;    // 512 (= kRBlock: one thread per digit)
 constexpr unsigned long long kFlagAgg = 1ull << 30, kFlagInc = 2ull << 30;
 constexpr uint32_t kCountMask = (1u << 30) - 1;
-// dynamic LDS of a pass: per-wave digit counts, tile counts, tile starts, global
-// bases, the tile's keys and values ordered by digit, the claimed tile id
-constexpr uint32_t kPassLds = (kRWaves * kRMaxBins + 3 * kRMaxBins + 2 * kRTile + 4) * 4;
+constexpr uint32_t kLookWin = 16;                  // earlier tiles read at once in the look-back
+constexpr uint32_t kHistBlock = 1024, kHistCopies = 16;   // histogram workgroups add into copy b % 16
+// dynamic LDS of a pass: per-wave digit counts (u16), tile counts, tile starts,
+// global bases, wave totals, the tile's keys and values ordered by digit, the
+// claimed tile id
+constexpr uint32_t kPassLds = kRWaves * kRMaxBins * 2 + (3 * kRMaxBins + 16 + 2 * kRTile + 4) * 4;
+static_assert(kRMaxBins == kRBlock, "one thread per digit");
 
 constexpr uint32_t kRMaxPass = 4;                  // keys of up to 36 bits
 
@@ -59,10 +65,10 @@ Digits digits_for(uint32_t kbits) {
   return d;
 }
 
-__global__ __launch_bounds__(kRBlock) void radix_hist_kernel(const uint32_t *keys, uint64_t n, Digits dg, uint32_t hot,
-                                                             uint32_t *hist) {
+__global__ __launch_bounds__(kHistBlock) void radix_hist_kernel(const uint32_t *keys, uint64_t n, Digits dg,
+                                                                uint32_t hot, uint32_t *hist) {
   __shared__ uint32_t h[kRMaxPass * kRMaxBins];
-  for (uint32_t i = threadIdx.x; i < kRMaxPass * kRMaxBins; i += kRBlock) h[i] = 0;
+  for (uint32_t i = threadIdx.x; i < kRMaxPass * kRMaxBins; i += kHistBlock) h[i] = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   auto add = [&](uint32_t key, bool valid) {
@@ -76,8 +82,8 @@ __global__ __launch_bounds__(kRBlock) void radix_hist_kernel(const uint32_t *key
       for (uint32_t p = 0; p < dg.npass; ++p) atomicAdd(&h[p * kRMaxBins + ((key >> dg.shift[p]) & ((1u << dg.bits[p]) - 1))], 1u);
   };
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const uint64_t n4 = n / 4, stride = uint64_t(gridDim.x) * kRBlock;
-  for (uint64_t base = uint64_t(blockIdx.x) * kRBlock; base < n4; base += stride) {   // uniform per workgroup
+  const uint64_t n4 = n / 4, stride = uint64_t(gridDim.x) * kHistBlock;
+  for (uint64_t base = uint64_t(blockIdx.x) * kHistBlock; base < n4; base += stride) {   // uniform per workgroup
     const uint64_t q = base + threadIdx.x;
     const bool v = q < n4;
     const u32x4 k4 = v ? reinterpret_cast<const u32x4 *>(keys)[q] : u32x4{0u, 0u, 0u, 0u};
@@ -92,16 +98,23 @@ __global__ __launch_bounds__(kRBlock) void radix_hist_kernel(const uint32_t *key
     add(v ? keys[q] : 0u, v);
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < kRMaxPass * kRMaxBins; i += kRBlock)
-    if (h[i]) atomicAdd(&hist[i], h[i]);
+  // into copy b % 16: the adds of all workgroups to one bin serialised at the
+  // memory side (53 us a sort with one copy and 512 workgroups)
+  uint32_t *const hc = hist + (blockIdx.x % kHistCopies) * (kRMaxPass * kRMaxBins);
+  for (uint32_t i = threadIdx.x; i < kRMaxPass * kRMaxBins; i += kHistBlock)
+    if (h[i]) atomicAdd(&hc[i], h[i]);
 }
 
 __global__ __launch_bounds__(kRMaxBins) void radix_scan_kernel(uint32_t *hist, uint32_t *offs, uint32_t npass) {
   __shared__ uint32_t s[kRMaxBins];
   const uint32_t t = threadIdx.x;
   for (uint32_t p = 0; p < npass; ++p) {
-    const uint32_t x = hist[p * kRMaxBins + t];
-    hist[p * kRMaxBins + t] = 0;           // zero for the next sort
+    uint32_t x = 0;
+    for (uint32_t c = 0; c < kHistCopies; ++c) {
+      uint32_t *const h = hist + c * (kRMaxPass * kRMaxBins) + p * kRMaxBins + t;
+      x += *h;
+      *h = 0;                              // zero for the next sort
+    }
     s[t] = x;
     __syncthreads();
     for (uint32_t off = 1; off < kRMaxBins; off <<= 1) {
@@ -115,22 +128,42 @@ __global__ __launch_bounds__(kRMaxBins) void radix_scan_kernel(uint32_t *hist, u
   }
 }
 
+// Exclusive prefix over the block's 512 threads (one value each); waves scan
+// their 64 values with lane shuffles, then the 8 wave totals.  Two barriers.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wtot) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= static_cast<uint32_t>(o)) inc += y;
+  }
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kRWaves; ++k) before += k < w ? wtot[k] : 0u;
+  __syncthreads();
+  return before + inc - x;
+}
+
 __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
                                                              uint32_t *vout, uint64_t n, uint32_t shift, uint32_t bits,
                                                              const uint32_t *offs, unsigned long long *look,
                                                              unsigned long long *tile_ctr,
                                                              unsigned long long tile_base, uint32_t epoch) {
   extern __shared__ __attribute__((aligned(16))) uint8_t rsm[];
-  uint32_t *const wcnt = reinterpret_cast<uint32_t *>(rsm);   // [wave][digit]
-  uint32_t *const tcnt = wcnt + kRWaves * kRMaxBins;           // the tile's count per digit
+  uint16_t *const wcnt = reinterpret_cast<uint16_t *>(rsm);   // [wave][digit]
+  uint32_t *const tcnt = reinterpret_cast<uint32_t *>(wcnt + kRWaves * kRMaxBins);   // the tile's count per digit
   uint32_t *const dstart = tcnt + kRMaxBins;                   // its digit's first place in the tile
   uint32_t *const dbase = dstart + kRMaxBins;                  // its digit's first place in the output
-  uint32_t *const lk = dbase + kRMaxBins;
+  uint32_t *const wtot = dbase + kRMaxBins;                    // [16] scan scratch
+  uint32_t *const lk = wtot + 16;
   uint32_t *const lv = lk + kRTile;
   uint32_t *const s_tile = lv + kRTile;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t nb = 1u << bits, dmask = nb - 1;
-  for (uint32_t i = tid; i < kRWaves * kRMaxBins; i += kRBlock) wcnt[i] = 0;
+  for (uint32_t i = tid; i < kRWaves * kRMaxBins / 2; i += kRBlock) reinterpret_cast<uint32_t *>(wcnt)[i] = 0;
   if (tid == 0) *s_tile = static_cast<uint32_t>(atomicAdd(tile_ctr, 1ull) - tile_base);
   __syncthreads();
   const uint32_t tile = *s_tile;
@@ -145,7 +178,7 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     val[k] = v ? (vin ? vin[i] : static_cast<uint32_t>(i)) : 0u;
   }
   // ranks within the wave's items of one digit, slot by slot
-  uint32_t *const wc = wcnt + w * kRMaxBins;
+  uint16_t *const wc = wcnt + w * kRMaxBins;
 #pragma unroll
   for (uint32_t k = 0; k < kRItems; ++k) {
     const bool v = t0 + w * (kRItems * 64) + k * 64 + lane < n;
@@ -159,64 +192,73 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     uint32_t old = 0;
     if (v && lane == leader) {
       old = wc[d];
-      wc[d] = old + static_cast<uint32_t>(__builtin_popcountll(m));
+      wc[d] = static_cast<uint16_t>(old + static_cast<uint32_t>(__builtin_popcountll(m)));
     }
     old = __shfl(old, static_cast<int>(leader));
     rnk[k] = old + static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << lane) - 1)));
   }
   __syncthreads();
-  // per digit: the waves' exclusive prefix (in place) and the tile's count
-  if (tid < nb) {
-    uint32_t run = 0;
+  // thread d: the waves' exclusive prefix of digit d (in place) and the tile's count
+  const uint32_t d = tid;
+  uint32_t c = 0;
+  if (d < nb) {
+#pragma unroll
     for (uint32_t ww = 0; ww < kRWaves; ++ww) {
-      const uint32_t c = wcnt[ww * kRMaxBins + tid];
-      wcnt[ww * kRMaxBins + tid] = run;
-      run += c;
+      const uint32_t x = wcnt[ww * kRMaxBins + d];
+      wcnt[ww * kRMaxBins + d] = static_cast<uint16_t>(c);
+      c += x;
     }
-    tcnt[tid] = run;
+    tcnt[d] = c;
   }
-  __syncthreads();
-  // the digits' starts inside the tile (exclusive scan of tcnt)
-  if (tid < kRMaxBins) dstart[tid] = tid < nb ? tcnt[tid] : 0u;
-  __syncthreads();
-  for (uint32_t off = 1; off < kRMaxBins; off <<= 1) {
-    const uint32_t y = (tid < kRMaxBins && tid >= off) ? dstart[tid - off] : 0u;
-    __syncthreads();
-    if (tid < kRMaxBins) dstart[tid] += y;
-    __syncthreads();
-  }
-  if (tid < nb) {
-    const uint32_t c = tcnt[tid];
-    dstart[tid] -= c;
-    // decoupled look-back: the counts of this digit in every earlier tile
+  // the digits' starts inside the tile
+  const uint32_t ds = block_excl_scan(d < nb ? c : 0u, wtot);
+  if (d < nb) {
+    dstart[d] = ds;
+    // decoupled look-back: the counts of digit d in every earlier tile, kLookWin
+    // earlier tiles read at once (a tile's predecessors publish while it reads)
     const unsigned long long tag = static_cast<unsigned long long>(epoch) << 32;
-    unsigned long long *const mine = look + uint64_t(tile) * kRMaxBins + tid;
+    unsigned long long *const mine = look + uint64_t(tile) * kRMaxBins + d;
     uint32_t prefix = 0;
     if (tile == 0) {
       __hip_atomic_store(mine, tag | kFlagInc | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       __hip_atomic_store(mine, tag | kFlagAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t t = tile; t-- > 0;) {
-        unsigned long long x;
-        for (;;) {
-          x = __hip_atomic_load(look + uint64_t(t) * kRMaxBins + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((x >> 32) == epoch) break;   // (an earlier tile: claimed and running, so it publishes)
-          __builtin_amdgcn_s_sleep(1);
+      uint32_t t = tile;        // tiles [0, t) are still to sum
+      bool done = false;
+      while (!done) {
+        unsigned long long x[kLookWin];
+#pragma unroll
+        for (uint32_t j = 0; j < kLookWin; ++j)
+          x[j] = j < t ? __hip_atomic_load(look + uint64_t(t - 1 - j) * kRMaxBins + d, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0ull;
+        uint32_t used = 0;
+        bool stall = false;
+#pragma unroll
+        for (uint32_t j = 0; j < kLookWin; ++j) {
+          if (done || stall || j >= t) continue;
+          if ((x[j] >> 32) != epoch) {   // not yet published (an earlier tile: claimed and running)
+            stall = true;
+            continue;
+          }
+          prefix += static_cast<uint32_t>(x[j]) & kCountMask;
+          ++used;
+          if (x[j] & kFlagInc) done = true;
         }
-        prefix += static_cast<uint32_t>(x) & kCountMask;
-        if (x & kFlagInc) break;
+        t -= used;
+        if (!done && stall) __builtin_amdgcn_s_sleep(1);
       }
       __hip_atomic_store(mine, tag | kFlagInc | (prefix + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    dbase[tid] = offs[tid] + prefix;
+    dbase[d] = offs[d] + prefix;
   }
   __syncthreads();
   // the tile ordered by digit in LDS, then written out run by run
 #pragma unroll
   for (uint32_t k = 0; k < kRItems; ++k) {
     if (t0 + w * (kRItems * 64) + k * 64 + lane < n) {
-      const uint32_t d = (key[k] >> shift) & dmask;
-      const uint32_t pos = dstart[d] + wc[d] + rnk[k];
+      const uint32_t dk = (key[k] >> shift) & dmask;
+      const uint32_t pos = dstart[dk] + wc[dk] + rnk[k];
       lk[pos] = key[k];
       lv[pos] = val[k];
     }
@@ -225,8 +267,8 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
   const uint32_t items = static_cast<uint32_t>(n - t0 < kRTile ? n - t0 : kRTile);
   for (uint32_t j = tid; j < items; j += kRBlock) {
     const uint32_t kk = lk[j];
-    const uint32_t d = (kk >> shift) & dmask;
-    const uint64_t g = uint64_t(dbase[d]) + (j - dstart[d]);
+    const uint32_t dk = (kk >> shift) & dmask;
+    const uint64_t g = uint64_t(dbase[dk]) + (j - dstart[dk]);
     kout[g] = kk;
     vout[g] = lv[j];
   }
@@ -269,18 +311,18 @@ int radix_sort_pairs(RadixScratch &s, uint32_t *keys_in, uint32_t *keys_out, uin
     s.look_tiles = tiles;
   }
   if (!s.hist) {
-    RX_CHECK(hipMalloc(&s.hist, kRMaxPass * kRMaxBins * 4));
+    RX_CHECK(hipMalloc(&s.hist, kHistCopies * kRMaxPass * kRMaxBins * 4));
     RX_CHECK(hipMalloc(&s.offs, kRMaxPass * kRMaxBins * 4));
     RX_CHECK(hipMalloc(&s.tile_ctr, 64));
-    RX_CHECK(hipMemsetAsync(s.hist, 0, kRMaxPass * kRMaxBins * 4, st));
+    RX_CHECK(hipMemsetAsync(s.hist, 0, kHistCopies * kRMaxPass * kRMaxBins * 4, st));
     RX_CHECK(hipMemsetAsync(s.tile_ctr, 0, 64, st));
     s.tiles_issued = 0;
   }
   const Digits dg = digits_for(kbits);
   const uint32_t hot = kbits >= 32 ? ~0u : (1u << kbits) - 1;   // the sentinel bucket (conntrack.hip)
-  const uint64_t hwant = (n / 4 + kRBlock - 1) / kRBlock;
-  const unsigned hgrid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(hwant, uint64_t(num_cus) * 2)));
-  hipLaunchKernelGGL(radix_hist_kernel, dim3(hgrid), dim3(kRBlock), 0, st, keys_in, n, dg, hot, s.hist);
+  const uint64_t hwant = (n / 4 + kHistBlock - 1) / kHistBlock;
+  const unsigned hgrid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(hwant, uint64_t(num_cus))));
+  hipLaunchKernelGGL(radix_hist_kernel, dim3(hgrid), dim3(kHistBlock), 0, st, keys_in, n, dg, hot, s.hist);
   RX_CHECK(hipGetLastError());
   hipLaunchKernelGGL(radix_scan_kernel, dim3(1), dim3(kRMaxBins), 0, st, s.hist, s.offs, dg.npass);
   RX_CHECK(hipGetLastError());
