@@ -229,6 +229,12 @@ int pcn_ipt_debug_ct_walk_passes(pcn_ipt *ctx, uint64_t out[2], int reset);
 /* Test hook: the stateful pipeline's (key bucket, batch index) sort (radix.hip)
  * on its own.  keys: n device u32 < 2^kbits (left unchanged); out: the keys
  * sorted stably and the batch index of each.  Synchronises the device. */
+/* Measurement hook: with PCN_IPT_DEBUG_CLOCKS=1 in the environment each classify
+ * launch records, per workgroup, s_memrealtime (100 MHz) at its start, after its
+ * prologue, after its last frame and after its counter flush; this copies the
+ * last launch's 4 x grid values (when cap allows) and returns the grid.
+ * -ENOENT before such a launch.  Synchronises the device. */
+int pcn_ipt_debug_clocks(pcn_ipt *ctx, uint64_t *out, uint32_t cap);
 int pcn_ipt_debug_sort_pairs(pcn_ipt *ctx, const uint32_t *keys, uint64_t n, uint32_t kbits, uint32_t *keys_out,
                              uint32_t *idx_out);
 /* Compile the chain program of `chain` for its usual launch shape (fixed

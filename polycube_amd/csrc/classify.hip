@@ -841,6 +841,8 @@ __device__ __forceinline__ DevChain chain_desc(const LaunchArgs &a) {
 template <bool FIXED, bool LDS, int CH, int NS, bool JIT>
 __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   const DevChain run_ch = chain_desc<JIT, CH>(a);   // the chain that runs rules (CH < 3)
+  const unsigned long long clk0 = a.dbg_clk ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  unsigned long long clk1 = 0, clk2 = 0;
   constexpr uint32_t kDealW = PCN_DEAL2 >= 2 || (PCN_DEAL2 && FIXED) ? 128 : 64;   // candidate deal window (max)
   // per-workgroup histogram: u32 {pkts, bytes} per bin (the host bounds the
   // frames per workgroup so neither can wrap; the flush widens to u64)
@@ -1047,6 +1049,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   if (threadIdx.x == 0) *lds_stats = 0;
   uint32_t wide = 0;   // this wave's rule stages that dealt more than 64 candidates (wave-uniform)
   __syncthreads();
+  if (a.dbg_clk) clk1 = __builtin_amdgcn_s_memrealtime();
   // Stage d always holds the frames i with (i - first) / step == d (mod
   // PF): the loop is unrolled PF times so no stage is
   // ever copied (a register move of an in-flight load waits for it).
@@ -1430,6 +1433,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   if (PCN_HDR_ASM && FIXED && PCN_HDR_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (a.deal_stats && lane == 0 && wide) atomicAdd(lds_stats, wide);
   __syncthreads();
+  if (a.dbg_clk) clk2 = __builtin_amdgcn_s_memrealtime();
   // the workgroup's deal statistics, stored into host-mapped memory (a plain
   // system-scope vector store; the host reads whatever has landed)
   if (a.deal_stats && threadIdx.x == 0)
@@ -1497,6 +1501,16 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     } else {
       atomicAdd(blk + 2 * pair, pk);
       if (PCN_ABLATE != 9) atomicAdd(blk + 2 * pair + 1, by);
+    }
+  }
+  if (a.dbg_clk) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long *const c = a.dbg_clk + 4ull * blockIdx.x;
+      c[0] = clk0;
+      c[1] = clk1;
+      c[2] = clk2;
+      c[3] = __builtin_amdgcn_s_memrealtime();
     }
   }
 }

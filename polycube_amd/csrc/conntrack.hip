@@ -19,6 +19,16 @@
 
 #include "conntrack.hpp"
 #include "radix.hpp"
+// Measurement builds only (make ct_variant DEFS=-DPCN_CT_ROCPRIM=1): the sort
+// through rocPRIM's onesweep radix sort, as in round 4, for an A/B against the
+// hand-written one (radix.hip) the product runs.
+#ifndef PCN_CT_ROCPRIM
+#define PCN_CT_ROCPRIM 0
+#endif
+#if PCN_CT_ROCPRIM
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#endif
 #include "pcn_ipt.h"
 
 #ifndef PCN_CT_FAST
@@ -2101,6 +2111,10 @@ struct CtScratch {
   ct_u32x4 *ox = nullptr;     // the four stage-A outcomes per packet (batches with four labels)
   uint64_t ox_cap = 0;
   RadixScratch rx;            // the (key bucket, index) sort (radix.hip)
+#if PCN_CT_ROCPRIM
+  void *rp_temp = nullptr;
+  size_t rp_bytes = 0;
+#endif
   // ct_advance_carry: 1 + the batch's last port-writing frame
   unsigned long long *zfound = nullptr;
 };
@@ -2292,7 +2306,28 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipGetLastError());
   // (ct_heads advances the carry from ct_prep's published groups)
   // the sort (radix.hip; s.keys is its ping-pong buffer from here on)
+#if PCN_CT_ROCPRIM
+  {
+    using Cfg = rocprim::radix_sort_config<
+        rocprim::default_config, rocprim::default_config,
+        rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 9,
+                                            rocprim::block_radix_rank_algorithm::match>>;
+    size_t need = 0;
+    auto sort = [&](void *tmp, size_t &bytes) {
+      return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, s.keys, s.keys2, rocprim::counting_iterator<uint32_t>(0u),
+                                            s.idx2, static_cast<unsigned int>(b.n), 0u, kbits, st);
+    };
+    CT_CHECK(sort(nullptr, need));
+    if (s.rp_bytes < need) {
+      if (s.rp_temp) CT_CHECK(hipFree(s.rp_temp));
+      CT_CHECK(hipMalloc(&s.rp_temp, need));
+      s.rp_bytes = need;
+    }
+    CT_CHECK(sort(s.rp_temp, need));
+  }
+#else
   CT_CHECK(radix_sort_pairs(s.rx, s.keys, s.keys2, s.idx2, b.n, kbits, num_cus, st));
+#endif
   const RecSrc src{s.brec, s.idx2, s.keys2, s.ox, b.nlab == 4 ? 1u : 0u};
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;

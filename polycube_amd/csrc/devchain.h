@@ -212,6 +212,10 @@ struct LaunchArgs {
   // host picks the next launch's chain program from them without a sync.
   uint32_t *deal_stats;          // [grid] host-mapped u32 per workgroup; null: not counted
   uint32_t lds_stats;            // byte offset of the workgroup's u32 counter in LDS
+  // Measurement only (PCN_IPT_DEBUG_CLOCKS=1, pcn_ipt_debug_clocks): thread 0 of
+  // workgroup b stores s_memrealtime (100 MHz) at its start, after its prologue,
+  // after its last frame and after its counter flush into dbg_clk[4 b .. 4 b + 3]
+  unsigned long long *dbg_clk;   // null: not recorded
 };
 
 // Packed counter pair: packets in bits 38-63, bytes in bits 0-37.

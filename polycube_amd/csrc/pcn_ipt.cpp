@@ -83,6 +83,17 @@ uint32_t partial_rule_bins(uint32_t used, uint32_t per_bin, uint32_t ncounted) {
   return nb < ncounted ? nb : ncounted;
 }
 
+// PCN_IPT_DEBUG_CLOCKS=1: classify launches record per-workgroup clocks
+// (LaunchArgs::dbg_clk; pcn_ipt_debug_clocks reads the last launch's)
+bool debug_clocks() {
+  static const bool v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_CLOCKS");
+    return e && *e == '1';
+  }();
+  return v;
+}
+constexpr uint32_t kDbgClkGrid = 4096;
+
 // PCN_IPT_DEBUG_DEAL2_MULTI=0: chains of 2+ summary blocks deal 64 candidates a
 // pass too (no 128-item wave region: that LDS goes to counter bins); A/B
 bool multi_block_deal2() {
@@ -259,6 +270,9 @@ struct pcn_ipt {
   uint32_t *h_deal_stats = nullptr;
   uint32_t deal_grid = 0;
   uint64_t deal_frames = 0;
+  // PCN_IPT_DEBUG_CLOCKS=1: per-workgroup clocks of the last classify launch
+  unsigned long long *d_dbg_clk = nullptr;
+  uint32_t dbg_grid = 0;
 };
 
 namespace pcn {
@@ -772,6 +786,7 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     }
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
     if (ctx->h_deal_stats) (void)hipHostFree(ctx->h_deal_stats);
+    if (ctx->d_dbg_clk) (void)hipFree(ctx->d_dbg_clk);
     for (auto &se : ctx->pack_streams)
       if (se.second) (void)hipEventDestroy(se.second);
     for (void *p : {static_cast<void *>(ctx->hz[0].d_tab), static_cast<void *>(ctx->hz[0].d_ctr),
@@ -1327,6 +1342,13 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
     const hipStream_t hs = static_cast<hipStream_t>(stream);
     for (bool &d : ctx->ctr_dirty) d = true;        // (fetch_stats reads them again)
+    if (debug_clocks() && !sa) {
+      if (!ctx->d_dbg_clk) hip_check(hipMalloc(&ctx->d_dbg_clk, kDbgClkGrid * 32), "hipMalloc(debug clocks)");
+      a.dbg_clk = ctx->d_dbg_clk;
+      ctx->dbg_grid = static_cast<uint32_t>(std::min<uint64_t>((b->n + PCN_BLOCK - 1) / PCN_BLOCK,
+                                                               uint64_t(classify_grid_cus(ctx->num_cus))));
+      if (ctx->dbg_grid > kDbgClkGrid) a.dbg_clk = nullptr;
+    }
     if (!sa) register_pack_stream(ctx, hs);
     int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, hs, sa ? nullptr : &ctx->pack);
     if (!rc && !sa) note_pack_stream(ctx, hs);
@@ -1576,6 +1598,17 @@ int pcn_ipt_debug_sort_pairs(pcn_ipt *ctx, const uint32_t *keys, uint64_t n, uin
     if (rc != hipSuccess) return fail(-EINVAL, std::string("radix sort: ") + hipGetErrorString(hipError_t(rc)));
     hip_check(e, "hipDeviceSynchronize");
     return 0;
+  });
+}
+
+int pcn_ipt_debug_clocks(pcn_ipt *ctx, uint64_t *out, uint32_t cap) {
+  return guarded(ctx, [&] {
+    if (!ctx->d_dbg_clk || !ctx->dbg_grid) return fail(-ENOENT, "no launch recorded (PCN_IPT_DEBUG_CLOCKS=1)");
+    if (!out || cap < 4 * ctx->dbg_grid) return static_cast<int>(ctx->dbg_grid);
+    device_guard(ctx);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    hip_check(hipMemcpy(out, ctx->d_dbg_clk, size_t(ctx->dbg_grid) * 32, hipMemcpyDeviceToHost), "hipMemcpy(clocks)");
+    return static_cast<int>(ctx->dbg_grid);
   });
 }
 

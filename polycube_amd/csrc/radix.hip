@@ -8,14 +8,15 @@
 // 2. radix_scan_kernel: the global exclusive prefix of each digit's bins (the
 //    copies summed), and the histograms zeroed for the next sort.
 // 3. radix_pass_kernel, once per digit (9 / 8 / 8 bits of a 25-bit key): a
-//    tile of 4096 pairs per 512-thread workgroup (three workgroups per CU),
-//    claimed in start order.  Its items are ranked wave by wave and slot by
+//    tile of 8192 pairs per 1024-thread workgroup (one per CU), claimed in
+//    start order.  Its items are ranked wave by wave and slot by
 //    slot in input order (lanes of one digit matched with `bits` ballots, a
 //    per-wave running count in LDS), the tile's digit counts are published and
 //    the counts of the tiles before it summed by decoupled look-back (one u64
 //    per tile and digit: epoch, aggregate / inclusive flag, count; 16 earlier
-//    tiles read at once -- read one by one, the chain of dependent reads was
-//    the pass's time), then the tile is ordered by digit in LDS and written
+//    tiles read at once -- read one by one, the chain of dependent reads of
+//    the first tiles, which all start together, was the pass's time), then
+//    the tile is ordered by digit in LDS and written
 //    out: consecutive items of a digit go to consecutive addresses.  The first
 //    pass makes the values (batch indices) itself.
 // Stability: a tile's items keep input order within a digit (wave, slot, lane
@@ -27,12 +28,12 @@
 namespace pcn {
 namespace {
 
-constexpr uint32_t kRBlock = 512;                  // pass workgroups: 3 per CU (46 KB of LDS each)
+constexpr uint32_t kRBlock = 1024;                 // pass workgroups: one per CU (88 KB of LDS)
 constexpr uint32_t kRItems = 8;
-constexpr uint32_t kRTile = kRBlock * kRItems;     // 4096 pairs a tile
-constexpr uint32_t kRWaves = kRBlock / 64;         // 8
+constexpr uint32_t kRTile = kRBlock * kRItems;     // 8192 pairs a tile
+constexpr uint32_t kRWaves = kRBlock / 64;         // 16
 constexpr uint32_t kRMaxBits = 9;
-constexpr uint32_t kRMaxBins = 1u << kRMaxBits;    // 512 (= kRBlock: one thread per digit)
+constexpr uint32_t kRMaxBins = 1u << kRMaxBits;    // 512 (<= kRBlock: one thread per digit)
 constexpr unsigned long long kFlagAgg = 1ull << 30, kFlagInc = 2ull << 30;
 constexpr uint32_t kCountMask = (1u << 30) - 1;
 constexpr uint32_t kLookWin = 16;                  // earlier tiles read at once in the look-back
@@ -40,8 +41,8 @@ constexpr uint32_t kHistBlock = 1024, kHistCopies = 16;   // histogram workgroup
 // dynamic LDS of a pass: per-wave digit counts (u16), tile counts, tile starts,
 // global bases, wave totals, the tile's keys and values ordered by digit, the
 // claimed tile id
-constexpr uint32_t kPassLds = kRWaves * kRMaxBins * 2 + (3 * kRMaxBins + 16 + 2 * kRTile + 4) * 4;
-static_assert(kRMaxBins == kRBlock, "one thread per digit");
+constexpr uint32_t kPassLds = kRWaves * kRMaxBins * 2 + (3 * kRMaxBins + kRWaves + 2 * kRTile + 4) * 4;
+static_assert(kRMaxBins <= kRBlock, "one thread per digit");
 
 constexpr uint32_t kRMaxPass = 4;                  // keys of up to 36 bits
 
@@ -82,15 +83,26 @@ __global__ __launch_bounds__(kHistBlock) void radix_hist_kernel(const uint32_t *
       for (uint32_t p = 0; p < dg.npass; ++p) atomicAdd(&h[p * kRMaxBins + ((key >> dg.shift[p]) & ((1u << dg.bits[p]) - 1))], 1u);
   };
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const uint64_t n4 = n / 4, stride = uint64_t(gridDim.x) * kHistBlock;
-  for (uint64_t base = uint64_t(blockIdx.x) * kHistBlock; base < n4; base += stride) {   // uniform per workgroup
-    const uint64_t q = base + threadIdx.x;
-    const bool v = q < n4;
-    const u32x4 k4 = v ? reinterpret_cast<const u32x4 *>(keys)[q] : u32x4{0u, 0u, 0u, 0u};
-    add(k4.x, v);
-    add(k4.y, v);
-    add(k4.z, v);
-    add(k4.w, v);
+  // four 16-byte loads in flight per thread (one at a time, the kernel waited
+  // a memory round trip per 4 keys)
+  constexpr uint32_t U = 4;
+  const uint64_t n4 = n / 4, stride = uint64_t(gridDim.x) * kHistBlock * U;
+  for (uint64_t base = uint64_t(blockIdx.x) * kHistBlock * U; base < n4; base += stride) {   // uniform per workgroup
+    u32x4 k4[U];
+    bool v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t q = base + u * kHistBlock + threadIdx.x;
+      v[u] = q < n4;
+      k4[u] = v[u] ? reinterpret_cast<const u32x4 *>(keys)[q] : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      add(k4[u].x, v[u]);
+      add(k4[u].y, v[u]);
+      add(k4[u].z, v[u]);
+      add(k4[u].w, v[u]);
+    }
   }
   if (blockIdx.x == 0) {                   // the last n % 4 keys
     const uint64_t q = n4 * 4 + threadIdx.x;
@@ -128,8 +140,8 @@ __global__ __launch_bounds__(kRMaxBins) void radix_scan_kernel(uint32_t *hist, u
   }
 }
 
-// Exclusive prefix over the block's 512 threads (one value each); waves scan
-// their 64 values with lane shuffles, then the 8 wave totals.  Two barriers.
+// Exclusive prefix over the block's threads (one value each); waves scan their
+// 64 values with lane shuffles, then the wave totals.  Two barriers.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wtot) {
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t inc = x;
@@ -157,8 +169,8 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
   uint32_t *const tcnt = reinterpret_cast<uint32_t *>(wcnt + kRWaves * kRMaxBins);   // the tile's count per digit
   uint32_t *const dstart = tcnt + kRMaxBins;                   // its digit's first place in the tile
   uint32_t *const dbase = dstart + kRMaxBins;                  // its digit's first place in the output
-  uint32_t *const wtot = dbase + kRMaxBins;                    // [16] scan scratch
-  uint32_t *const lk = wtot + 16;
+  uint32_t *const wtot = dbase + kRMaxBins;                    // [kRWaves] scan scratch
+  uint32_t *const lk = wtot + kRWaves;
   uint32_t *const lv = lk + kRTile;
   uint32_t *const s_tile = lv + kRTile;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -320,7 +332,7 @@ int radix_sort_pairs(RadixScratch &s, uint32_t *keys_in, uint32_t *keys_out, uin
   }
   const Digits dg = digits_for(kbits);
   const uint32_t hot = kbits >= 32 ? ~0u : (1u << kbits) - 1;   // the sentinel bucket (conntrack.hip)
-  const uint64_t hwant = (n / 4 + kHistBlock - 1) / kHistBlock;
+  const uint64_t hwant = (n / 16 + kHistBlock - 1) / kHistBlock;
   const unsigned hgrid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(hwant, uint64_t(num_cus))));
   hipLaunchKernelGGL(radix_hist_kernel, dim3(hgrid), dim3(kHistBlock), 0, st, keys_in, n, dg, hot, s.hist);
   RX_CHECK(hipGetLastError());

@@ -2,7 +2,7 @@
 // stateful pipeline (conntrack.hip): the key buckets of a batch sorted so each
 // connection's packets form a run in batch order.  Hand-written for gfx950
 // (radix.hip): one histogram pass over the keys for every digit, then one
-// onesweep pass per digit (decoupled look-back between 4096-key tiles).
+// onesweep pass per digit (decoupled look-back between 8192-key tiles).
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -137,6 +137,7 @@ SIGNATURES = {
     "pcn_ipt_embedded_source": (C.c_char_p, [C.c_int]),
     "pcn_ipt_build_sha256": (C.c_char_p, []),
     "pcn_ipt_release_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pcn_ipt_debug_clocks": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]),
     "pcn_ipt_debug_sort_pairs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "pcn_ipt_read_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64),
                                         C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64),
