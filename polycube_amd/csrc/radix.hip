@@ -11,8 +11,9 @@
 //    tile of 8192 pairs per 1024-thread workgroup (one per CU), claimed in
 //    start order.  Its items are ranked wave by wave and slot by
 //    slot in input order (lanes of one digit matched with `bits` ballots, a
-//    per-wave running count in LDS), the tile's digit counts are published and
-//    the counts of the tiles before it summed by decoupled look-back (one u64
+//    per-wave running count in LDS), the tile's digit counts -- counted
+//    first, before the ranking -- are published and the counts of the tiles
+//    before it summed by decoupled look-back (one u64
 //    per tile and digit: epoch, aggregate / inclusive flag, count; 16 earlier
 //    tiles read at once -- read one by one, the chain of dependent reads of
 //    the first tiles, which all start together, was the pass's time), then
@@ -176,6 +177,7 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t nb = 1u << bits, dmask = nb - 1;
   for (uint32_t i = tid; i < kRWaves * kRMaxBins / 2; i += kRBlock) reinterpret_cast<uint32_t *>(wcnt)[i] = 0;
+  if (tid < kRMaxBins) tcnt[tid] = 0;
   if (tid == 0) *s_tile = static_cast<uint32_t>(atomicAdd(tile_ctr, 1ull) - tile_base);
   __syncthreads();
   const uint32_t tile = *s_tile;
@@ -189,45 +191,26 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     key[k] = v ? kin[i] : 0u;
     val[k] = v ? (vin ? vin[i] : static_cast<uint32_t>(i)) : 0u;
   }
-  // ranks within the wave's items of one digit, slot by slot
-  uint16_t *const wc = wcnt + w * kRMaxBins;
+  // The tile's digit counts first (LDS adds; the all-ones digit -- the
+  // batch's "no table" bucket, often most keys -- wave-aggregated), so the
+  // tile publishes its aggregate before it ranks: the tiles after it, which
+  // all start together in the first round, find it early in their look-back.
 #pragma unroll
   for (uint32_t k = 0; k < kRItems; ++k) {
     const bool v = t0 + w * (kRItems * 64) + k * 64 + lane < n;
     const uint32_t d = (key[k] >> shift) & dmask;
-    uint64_t m = __ballot(v);
-    for (uint32_t b = 0; b < bits; ++b) {
-      const uint64_t bb = __ballot((d >> b) & 1);
-      m &= ((d >> b) & 1) ? bb : ~bb;
-    }
-    const uint32_t leader = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lane;
-    uint32_t old = 0;
-    if (v && lane == leader) {
-      old = wc[d];
-      wc[d] = static_cast<uint16_t>(old + static_cast<uint32_t>(__builtin_popcountll(m)));
-    }
-    old = __shfl(old, static_cast<int>(leader));
-    rnk[k] = old + static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << lane) - 1)));
+    const uint64_t hm = __ballot(v && d == dmask);
+    if (hm && lane == static_cast<uint32_t>(__builtin_ctzll(hm)))
+      atomicAdd(&tcnt[dmask], static_cast<uint32_t>(__builtin_popcountll(hm)));
+    if (v && d != dmask) atomicAdd(&tcnt[d], 1u);
   }
   __syncthreads();
-  // thread d: the waves' exclusive prefix of digit d (in place) and the tile's count
   const uint32_t d = tid;
-  uint32_t c = 0;
+  const uint32_t c = d < nb ? tcnt[d] : 0u;
   if (d < nb) {
-#pragma unroll
-    for (uint32_t ww = 0; ww < kRWaves; ++ww) {
-      const uint32_t x = wcnt[ww * kRMaxBins + d];
-      wcnt[ww * kRMaxBins + d] = static_cast<uint16_t>(c);
-      c += x;
-    }
-    tcnt[d] = c;
-  }
-  // the digits' starts inside the tile
-  const uint32_t ds = block_excl_scan(d < nb ? c : 0u, wtot);
-  if (d < nb) {
-    dstart[d] = ds;
     // decoupled look-back: the counts of digit d in every earlier tile, kLookWin
-    // earlier tiles read at once (a tile's predecessors publish while it reads)
+    // earlier tiles read at once (a tile's predecessors publish while it reads);
+    // the waves without a digit rank their items meanwhile
     const unsigned long long tag = static_cast<unsigned long long>(epoch) << 32;
     unsigned long long *const mine = look + uint64_t(tile) * kRMaxBins + d;
     uint32_t prefix = 0;
@@ -264,6 +247,40 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     }
     dbase[d] = offs[d] + prefix;
   }
+  // ranks within the wave's items of one digit, slot by slot
+  uint16_t *const wc = wcnt + w * kRMaxBins;
+#pragma unroll
+  for (uint32_t k = 0; k < kRItems; ++k) {
+    const bool v = t0 + w * (kRItems * 64) + k * 64 + lane < n;
+    const uint32_t dk = (key[k] >> shift) & dmask;
+    uint64_t m = __ballot(v);
+    for (uint32_t b = 0; b < bits; ++b) {
+      const uint64_t bb = __ballot((dk >> b) & 1);
+      m &= ((dk >> b) & 1) ? bb : ~bb;
+    }
+    const uint32_t leader = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lane;
+    uint32_t old = 0;
+    if (v && lane == leader) {
+      old = wc[dk];
+      wc[dk] = static_cast<uint16_t>(old + static_cast<uint32_t>(__builtin_popcountll(m)));
+    }
+    old = __shfl(old, static_cast<int>(leader));
+    rnk[k] = old + static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << lane) - 1)));
+  }
+  __syncthreads();
+  // thread d: the waves' exclusive prefix of digit d (in place)
+  if (d < nb) {
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t ww = 0; ww < kRWaves; ++ww) {
+      const uint32_t x = wcnt[ww * kRMaxBins + d];
+      wcnt[ww * kRMaxBins + d] = static_cast<uint16_t>(run);
+      run += x;
+    }
+  }
+  // the digits' starts inside the tile
+  const uint32_t ds = block_excl_scan(c, wtot);
+  if (d < nb) dstart[d] = ds;
   __syncthreads();
   // the tile ordered by digit in LDS, then written out run by run
 #pragma unroll
