@@ -265,7 +265,7 @@ int pcn_ipt_ring_acquire(pcn_ipt_ring *r, pcn_ipt_ring_slot *out) {
 
 int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch *b) {
   if (!r || !b) return ring_fail(-EINVAL, "null argument");
-  std::lock_guard<std::mutex> l(r->mu);
+  std::unique_lock<std::mutex> l(r->mu);
   if (slot >= r->slots.size() || r->slots[slot].state != kFilling) return ring_fail(-EINVAL, "slot not acquired");
   Slot &s = r->slots[slot];
   if (b->n > r->cfg.slot_frames) return ring_fail(-EINVAL, "more frames than the slot holds");
@@ -308,10 +308,14 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
     const uint32_t stride = b->stride;
     const unsigned parts = r->cfg.pack_threads * 4;
     const size_t per = (n + parts - 1) / parts;
+    // the slot is the producer's (kFilling): the consumer's complete / release
+    // need not wait for the pack
+    l.unlock();
     r->pack->run([&](unsigned k) {
       const size_t lo = k * per, hi = std::min<size_t>(n, lo + per);
       for (size_t i = lo; i < hi; ++i) std::memcpy(dst + i * hb, src + i * stride, hb);
     }, parts);
+    l.lock();
     ok = hipMemcpyAsync(s.d_frames, s.h_pack, n * hb, hipMemcpyHostToDevice, st) == hipSuccess;
   } else if (!zc) {
     ok = hb ? hipMemcpy2DAsync(s.d_frames, hb, s.h_frames, b->stride, hb, n, hipMemcpyHostToDevice, st) == hipSuccess
