@@ -25,6 +25,8 @@
 #include "radix.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 namespace pcn {
 namespace {
@@ -141,6 +143,53 @@ __global__ __launch_bounds__(kRMaxBins) void radix_scan_kernel(uint32_t *hist, u
   }
 }
 
+// Reduce-then-scan, up-sweep: tile t's count of every digit into cnt[t][512].
+__global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, uint64_t n, uint32_t shift,
+                                                           uint32_t bits, uint32_t *cnt) {
+  __shared__ uint32_t h[kRMaxBins];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t dmask = (1u << bits) - 1;
+  if (tid < kRMaxBins) h[tid] = 0;
+  __syncthreads();
+  const uint64_t t0 = uint64_t(blockIdx.x) * kRTile;
+#pragma unroll
+  for (uint32_t k = 0; k < kRItems; ++k) {
+    const uint64_t i = t0 + k * kRBlock + tid;
+    const bool v = i < n;
+    const uint32_t dk = v ? (kin[i] >> shift) & dmask : 0u;
+    const uint64_t hm = __ballot(v && dk == dmask);
+    if (hm && lane == static_cast<uint32_t>(__builtin_ctzll(hm))) atomicAdd(&h[dmask], static_cast<uint32_t>(__builtin_popcountll(hm)));
+    if (v && dk != dmask) atomicAdd(&h[dk], 1u);
+  }
+  __syncthreads();
+  if (tid < kRMaxBins) cnt[uint64_t(blockIdx.x) * kRMaxBins + tid] = h[tid];
+}
+
+// Reduce-then-scan, scan: for 64 digits per workgroup (lane = digit), the
+// exclusive prefix over tiles of cnt[t][d], plus the digit's global base, into
+// pre[t][d].  Wave w takes a contiguous range of tiles.
+__global__ __launch_bounds__(kRBlock) void radix_tscan_kernel(const uint32_t *cnt, uint32_t *pre, uint64_t tiles,
+                                                              uint32_t nb, const uint32_t *offs) {
+  __shared__ uint32_t part[kRWaves][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t d = blockIdx.x * 64 + lane;
+  const uint64_t per = (tiles + kRWaves - 1) / kRWaves;
+  const uint64_t lo = w * per, hi = lo + per < tiles ? lo + per : tiles;
+  uint32_t sum = 0;
+  if (d < nb)
+    for (uint64_t t = lo; t < hi; ++t) sum += cnt[t * kRMaxBins + d];
+  part[w][lane] = sum;
+  __syncthreads();
+  uint32_t run = d < nb ? offs[d] : 0u;
+  for (uint32_t k = 0; k < w; ++k) run += part[k][lane];
+  if (d < nb)
+    for (uint64_t t = lo; t < hi; ++t) {
+      const uint32_t x = cnt[t * kRMaxBins + d];
+      pre[t * kRMaxBins + d] = run;
+      run += x;
+    }
+}
+
 // Exclusive prefix over the block's threads (one value each); waves scan their
 // 64 values with lane shuffles, then the wave totals.  Two barriers.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wtot) {
@@ -164,7 +213,8 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
                                                              uint32_t *vout, uint64_t n, uint32_t shift, uint32_t bits,
                                                              const uint32_t *offs, unsigned long long *look,
                                                              unsigned long long *tile_ctr,
-                                                             unsigned long long tile_base, uint32_t epoch) {
+                                                             unsigned long long tile_base, uint32_t epoch,
+                                                             const uint32_t *pre) {
   extern __shared__ __attribute__((aligned(16))) uint8_t rsm[];
   uint16_t *const wcnt = reinterpret_cast<uint16_t *>(rsm);   // [wave][digit]
   uint32_t *const tcnt = reinterpret_cast<uint32_t *>(wcnt + kRWaves * kRMaxBins);   // the tile's count per digit
@@ -191,6 +241,13 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     key[k] = v ? kin[i] : 0u;
     val[k] = v ? (vin ? vin[i] : static_cast<uint32_t>(i)) : 0u;
   }
+  // Reduce-then-scan mode (pre != null, PCN_IPT_DEBUG_RADIX=rts): the tile's
+  // digit bases come from radix_up_kernel + radix_tscan_kernel; no look-back.
+  const uint32_t d = tid;
+  uint32_t c = 0;
+  if (pre) {
+    if (d < nb) dbase[d] = pre[uint64_t(tile) * kRMaxBins + d];
+  } else {
   // The tile's digit counts first (LDS adds; the all-ones digit -- the
   // batch's "no table" bucket, often most keys -- wave-aggregated), so the
   // tile publishes its aggregate before it ranks: the tiles after it, which
@@ -205,8 +262,7 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     if (v && d != dmask) atomicAdd(&tcnt[d], 1u);
   }
   __syncthreads();
-  const uint32_t d = tid;
-  const uint32_t c = d < nb ? tcnt[d] : 0u;
+  c = d < nb ? tcnt[d] : 0u;
   if (d < nb) {
     // decoupled look-back: the counts of digit d in every earlier tile, kLookWin
     // earlier tiles read at once (a tile's predecessors publish while it reads);
@@ -247,6 +303,7 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     }
     dbase[d] = offs[d] + prefix;
   }
+  }   // (pre)
   // ranks within the wave's items of one digit, slot by slot
   uint16_t *const wc = wcnt + w * kRMaxBins;
 #pragma unroll
@@ -268,7 +325,8 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
     rnk[k] = old + static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << lane) - 1)));
   }
   __syncthreads();
-  // thread d: the waves' exclusive prefix of digit d (in place)
+  // thread d: the waves' exclusive prefix of digit d (in place); the tile's
+  // count of it (reduce-then-scan: not counted before)
   if (d < nb) {
     uint32_t run = 0;
 #pragma unroll
@@ -277,6 +335,7 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
       wcnt[ww * kRMaxBins + d] = static_cast<uint16_t>(run);
       run += x;
     }
+    if (pre) c = run;
   }
   // the digits' starts inside the tile
   const uint32_t ds = block_excl_scan(c, wtot);
@@ -305,8 +364,17 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
 
 }  // namespace
 
+// PCN_IPT_DEBUG_RADIX=rts: reduce-then-scan passes (up-sweep, tile scan,
+// down-sweep) instead of the onesweep look-back (A/B)
+// (read per sort, so a test can flip it; one getenv per batch)
+static bool radix_rts() {
+  const char *e = std::getenv("PCN_IPT_DEBUG_RADIX");
+  return e && std::string(e) == "rts";
+}
+
 void radix_free(RadixScratch &s) {
   for (void *p : {static_cast<void *>(s.tk), static_cast<void *>(s.tv), static_cast<void *>(s.tv2),
+                  static_cast<void *>(s.rts),
                   static_cast<void *>(s.look), static_cast<void *>(s.hist), static_cast<void *>(s.offs),
                   static_cast<void *>(s.tile_ctr)})
     if (p) (void)hipFree(p);
@@ -368,11 +436,30 @@ int radix_sort_pairs(RadixScratch &s, uint32_t *keys_in, uint32_t *keys_out, uin
     kout[p] = last ? keys_out : (p % 2 == 0 ? s.tk : keys_in);
     vout[p] = last ? vals_out : (p % 2 == 0 ? s.tv : s.tv2);
   }
+  const bool rts = radix_rts();
+  if (rts && s.rts_tiles < tiles) {
+    if (s.rts) RX_CHECK(hipFree(s.rts));
+    s.rts = nullptr;
+    RX_CHECK(hipMalloc(&s.rts, 2 * tiles * kRMaxBins * 4));
+    s.rts_tiles = tiles;
+  }
   for (uint32_t p = 0; p < dg.npass; ++p) {
     if (++s.epoch == 0) s.epoch = 1;   // (2^32 passes: the words of epoch 0 are the zeroed ones)
+    uint32_t *pre = nullptr;
+    if (rts) {
+      uint32_t *const cnt = s.rts;
+      pre = s.rts + tiles * kRMaxBins;
+      hipLaunchKernelGGL(radix_up_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kRBlock), 0, st, kin[p], n,
+                         dg.shift[p], dg.bits[p], cnt);
+      RX_CHECK(hipGetLastError());
+      const uint32_t nb = 1u << dg.bits[p];
+      hipLaunchKernelGGL(radix_tscan_kernel, dim3((nb + 63) / 64), dim3(kRBlock), 0, st, cnt, pre, tiles, nb,
+                         s.offs + p * kRMaxBins);
+      RX_CHECK(hipGetLastError());
+    }
     hipLaunchKernelGGL(radix_pass_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kRBlock), kPassLds, st, kin[p],
                        vin[p], kout[p], vout[p], n, dg.shift[p], dg.bits[p], s.offs + p * kRMaxBins, s.look,
-                       s.tile_ctr, s.tiles_issued, s.epoch);
+                       s.tile_ctr, s.tiles_issued, s.epoch, pre);
     RX_CHECK(hipGetLastError());
     s.tiles_issued += tiles;
   }
