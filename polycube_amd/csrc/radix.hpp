@@ -20,8 +20,8 @@ struct RadixScratch {
   unsigned long long *tile_ctr = nullptr;   // tiles claimed so far (monotonic)
   unsigned long long tiles_issued = 0;   // host mirror: the counter's value before a pass
   uint32_t epoch = 0;                    // look-back words of older passes never match
-  uint32_t *rts = nullptr;               // reduce-then-scan A/B: tile counts and prefixes [2][tile][512]
-  uint64_t rts_tiles = 0;
+  uint32_t *seg = nullptr;               // reduce-then-scan: super-tile counts, prefixes [2][group][512], totals [512]
+  uint32_t seg_groups = 0;
 };
 
 // Sort keys_in[0..n) (every key < 2^kbits, kbits <= 36, n < 2^30) stably; the batch

@@ -40,7 +40,7 @@ def _sort(ipt, keys, kbits):
 @pytest.mark.parametrize("n,kbits,hot", [
     (1, 8, 0.0), (5, 9, 0.0), (8191, 13, 0.3), (8192, 18, 0.0), (8193, 18, 0.5), (100_003, 25, 0.6),
     ((1 << 20) + 7, 25, 0.4), (300_000, 27, 0.0), (70_000, 32, 0.1), (1 << 22, 25, 0.9)])
-@pytest.mark.parametrize("mode", ["onesweep", "rts"])
+@pytest.mark.parametrize("mode", ["onesweep", "rts", "rts512"])
 def test_radix_sort_is_a_stable_sort(ipt, n, kbits, hot, mode, monkeypatch):
     monkeypatch.setenv("PCN_IPT_DEBUG_RADIX", mode)
     rng = np.random.default_rng(n ^ kbits)
