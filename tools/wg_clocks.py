@@ -65,6 +65,12 @@ def main():
                                      round(float((us[:, 2] - us[:, 1]).max()), 2)],
                "flush_us_median": round(float(np.median(us[:, 3] - us[:, 2])), 2),
                "program": fw.program_info()["deal_window"]}
+        # workgroups are dispatched round-robin over the 8 XCDs: per XCD (b % 8)
+        # the median frame-loop time and end time
+        xcd = np.arange(grid) % 8
+        loop = us[:, 2] - us[:, 1]
+        out["xcd_frames_us_median"] = [round(float(np.median(loop[xcd == x])), 2) for x in range(8)]
+        out["xcd_end_us_median"] = [round(float(np.median(us[xcd == x, 3])), 2) for x in range(8)]
         print(json.dumps(out), flush=True)
     ipt.close()
 
