@@ -94,6 +94,15 @@ bool debug_clocks() {
 }
 constexpr uint32_t kDbgClkGrid = 4096;
 
+// PCN_IPT_DEBUG_STAGE_A_COUNTS=1: stage A counts into its scratch block again (A/B)
+bool debug_stage_a_counts() {
+  static const bool v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_STAGE_A_COUNTS");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // PCN_IPT_DEBUG_DEAL2_MULTI=0: chains of 2+ summary blocks deal 64 candidates a
 // pass too (no 128-item wave region: that LDS goes to counter bins); A/B
 bool multi_block_deal2() {
@@ -1202,6 +1211,10 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     a.count_mask = b->direction == PCN_IPT_INGRESS
                        ? (1u << PCN_IPT_FORWARD) | (has_local && !firewall ? 1u << PCN_IPT_INPUT : 0u)
                        : (has_local ? 1u << PCN_IPT_OUTPUT : 0u);
+    // stage A counts nothing: ct_count counts every packet from its final
+    // outcome, and stage A's counters went to discarded scratch (their LDS adds,
+    // ballots and the flush into one block were pure cost)
+    if (sa && !debug_stage_a_counts()) a.count_mask = 0;
     // Horus: the program the batch's Parser calls, while one is in place
     if (const HorusProg *hz = horus_of_batch(ctx, b->direction)) {
       a.horus = hz->d_tab;

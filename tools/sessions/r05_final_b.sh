@@ -17,7 +17,7 @@ echo "== prof_bench rc=$?"
     -- python3 "$R/tools/ct_probe.py" --steps 6 > "$O/ct_prof.log" 2>&1 )
 echo "== ct_prof rc=$?"
 find "$O" -name "*kernel_trace.csv" -delete
-K="ct_prep ct_walk ct_heads ct_count radix_pass radix_up"
+K="ct_prep ct_walk ct_heads ct_count radix_pass radix_up pcn_classify_jit"
 pmcct ct_fetch "FETCH_SIZE" "$K"
 pmcct ct_write "WRITE_SIZE" "$K"
 pmcct ct_sq "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU" "$K"
