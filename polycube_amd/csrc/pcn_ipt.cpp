@@ -1325,7 +1325,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       // faster).  The counts come from the kernel itself through
       // host-mapped memory, read without a sync: whatever has landed.
       const int adapt = deal_adapt();
-      if (fn && fixed && !sa && a.ch[ch].nsw == 1 && adapt && ctx->h_deal_stats) {
+      // (stage A too: the stateful traffic is often mostly rule hits)
+      if (fn && fixed && a.ch[ch].nsw == 1 && adapt && ctx->h_deal_stats) {
         const std::string spec128 = cs.jit_spec + "#ifndef PCN_DEAL2\n#define PCN_DEAL2 1\n#endif\n";
         ctx->jit.request(spec128, false);
         bool wide = adapt == 2 || cs.deal_wide;
@@ -1350,7 +1351,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
         }
       }
     }
-    if (!a.deal_stats && !sa && !plan) ctx->deal_frames = 0;   // this launch counts nothing: forget the old counts
+    if (!a.deal_stats && !plan) ctx->deal_frames = 0;   // this launch counts nothing: forget the old counts
     if (plan) return 0;
     ++(fn ? ctx->launches_jit : ctx->launches_generic);
     const hipStream_t hs = static_cast<hipStream_t>(stream);
