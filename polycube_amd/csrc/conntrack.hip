@@ -969,9 +969,23 @@ __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const
   const uint32_t T = per * kHeadsBlock;
   const uint64_t lo = uint64_t(blockIdx.x) * T;
   if (threadIdx.x < kRunClasses) cnt[threadIdx.x] = 0;
-  for (uint32_t j = threadIdx.x; j < T + kLongRun + 1; j += kHeadsBlock) {
-    const uint64_t q = lo + j;                     // tile[j] = key at q - 1 (never a key past the ends)
-    tile[j] = q >= 1 && q - 1 < n ? skeys[q - 1] : 0xffffffffu;
+  // tile[j] = key at q - 1 (never a key past the ends).  Every load of the
+  // tile is issued before the first is used: unconditional (the index clamped
+  // into the batch, the value masked after), where a conditional load per
+  // iteration waited a memory round trip each (17 a workgroup).
+  constexpr uint32_t kTileIt = (kHeadsPer * kHeadsBlock + kLongRun + 1 + kHeadsBlock - 1) / kHeadsBlock;
+  uint32_t tv[kTileIt];
+#pragma unroll
+  for (uint32_t k = 0; k < kTileIt; ++k) {
+    const uint64_t q = lo + threadIdx.x + k * kHeadsBlock;
+    const uint64_t src = q >= 1 ? (q - 1 < n ? q - 1 : n - 1) : 0;
+    tv[k] = skeys[src];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kTileIt; ++k) {
+    const uint32_t j = threadIdx.x + k * kHeadsBlock;
+    const uint64_t q = lo + j;
+    if (j < T + kLongRun + 1) tile[j] = q >= 1 && q - 1 < n ? tv[k] : 0xffffffffu;
   }
   __syncthreads();
   // the class of tile position r (sorted position lo + r); kRunClasses: not a run head

@@ -102,32 +102,45 @@ __global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, 
     if (v && dk != dmask) atomicAdd(&h[dk], 1u);
   };
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  constexpr uint32_t U = 4;   // 16-byte loads in flight per thread
-  // lo is a multiple of 8192: 16-byte aligned.  The next round's loads are
-  // issued before this round's keys are counted.
-  constexpr uint64_t kStep = uint64_t(kRBlock) * 4 * U;
+  constexpr uint32_t U = 16;   // 16-byte loads in flight per thread
+  // lo is a multiple of 8192: 16-byte aligned.  The whole 16-byte vectors
+  // [lo, hi4) are read with unconditional loads (the index clamped, the lanes
+  // past the range masked): a conditional load merges into a phi the compiler
+  // resolves with an immediate vmcnt(0), one round trip per load.  The last
+  // 0-3 keys of an unaligned end are added by the first lanes.
+  const uint64_t lo4 = lo / 4, hi4 = hi / 4;
+  constexpr uint64_t kStep = uint64_t(kRBlock) * U;
+  const u32x4 *const kv = reinterpret_cast<const u32x4 *>(kin);
   auto load = [&](u32x4 *k4, uint64_t base) {
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const uint64_t i = base + 4 * (u * kRBlock + tid);
-      k4[u] = i + 4 <= hi ? *reinterpret_cast<const u32x4 *>(kin + i)
-                          : u32x4{i < hi ? kin[i] : 0u, i + 1 < hi ? kin[i + 1] : 0u, i + 2 < hi ? kin[i + 2] : 0u, 0u};
+      const uint64_t q = base + u * kRBlock + tid;
+      k4[u] = kv[q < hi4 ? q : hi4 - 1];
     }
   };
-  u32x4 cur[U], nxt[U];
-  if (lo < hi) load(cur, lo);
-  for (uint64_t base = lo; base < hi; base += kStep) {   // uniform per workgroup
-    if (base + kStep < hi) load(nxt, base + kStep);
+  auto count = [&](const u32x4 *k4, uint64_t base) {
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const uint64_t i = base + 4 * (u * kRBlock + tid);
-      add(cur[u].x, i < hi);
-      add(cur[u].y, i + 1 < hi);
-      add(cur[u].z, i + 2 < hi);
-      add(cur[u].w, i + 3 < hi);
+      const bool v = base + u * kRBlock + tid < hi4;
+      add(k4[u].x, v);
+      add(k4[u].y, v);
+      add(k4[u].z, v);
+      add(k4[u].w, v);
     }
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) cur[u] = nxt[u];
+  };
+  // A round is 16 loads per thread, all in flight together (256 KB a CU:
+  // a 2^24-key batch is one round per workgroup).  Double-buffered rounds
+  // measured no better: the compiler drains the loads a loop carries at the
+  // loop head anyway.
+  for (uint64_t base = lo4; base < hi4; base += kStep) {   // uniform per workgroup
+    u32x4 k4[U];
+    load(k4, base);
+    count(k4, base);
+  }
+  {
+    const uint64_t i = hi4 * 4 + tid;   // (uniform call: add() ballots)
+    const bool v = tid < 64 && i < hi;
+    add(v ? kin[v ? i : lo] : 0u, v);
   }
   __syncthreads();
   if (tid < kRMaxBins) cnt[uint64_t(blockIdx.x) * kRMaxBins + tid] = h[tid];
@@ -157,10 +170,14 @@ __global__ __launch_bounds__(kRBlock) void radix_colscan_kernel(const uint32_t *
     }
 }
 
-// 4 waves per SIMD.  A sub-tile's values are loaded with its ranking, the next sub-tile's keys
-// while this one is ordered and written; keys and values go out in one loop.
-// On gfx950 vmcnt retires loads and stores in issue order, so a load issued
-// before a sub-tile's stores never waits on them.
+// 4 waves per SIMD.  A sub-tile's values and the next sub-tile's keys are
+// loaded after its ranking, in flight through its scan; keys and values go
+// out in one loop.  On gfx950 vmcnt retires loads and stores in issue order.
+// VIN: the values are read (every pass but the first, whose values are the
+// indices themselves) -- a template parameter, not a branch: loads on one side
+// of a branch and computed values on the other merge into a phi the compiler
+// resolves by waiting for the loads at once.
+template <bool VIN>
 __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin, const uint32_t *vin,
                                                             uint32_t *kout, uint32_t *vout, uint64_t n,
                                                             uint32_t shift, uint32_t bits, uint64_t per,
@@ -207,11 +224,6 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
   if (lo < hi) load(kin, key, lo);
   for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {   // uniform per workgroup
     const uint32_t items = static_cast<uint32_t>(hi - t0 < kTile ? hi - t0 : kTile);
-    uint32_t val[kRItems];   // the first pass's values are the indices themselves
-    if (vin) load(vin, val, t0);
-    else
-#pragma unroll
-      for (uint32_t k = 0; k < kRItems; ++k) val[k] = static_cast<uint32_t>(t0) + li + k * 64;   // (n < 2^30)
     reinterpret_cast<uint4 *>(wcnt)[tid] = uint4{0u, 0u, 0u, 0u};   // kW * 2 KB: 32 bytes a thread
     reinterpret_cast<uint4 *>(wcnt)[tid + SB] = uint4{0u, 0u, 0u, 0u};
     __syncthreads();
@@ -244,7 +256,17 @@ __global__ __launch_bounds__(kRBlock) void radix_pass_kernel(const uint32_t *kin
 #pragma unroll
     for (uint32_t k = 0; k < kRItems; ++k)
       pos[k] = (pos[k] & 0xffffu) + static_cast<uint32_t>(__shfl(old[k], static_cast<int>(pos[k] >> 16)));
-    if (t0 + kTile < hi) load(kin, nkey, t0 + kTile);   // in flight through the rest of this sub-tile
+    // this sub-tile's values, then the next sub-tile's keys: both in flight
+    // through the scan (issued after the ranking, so the wait for this
+    // sub-tile's keys above never counts them)
+    uint32_t val[kRItems];   // the first pass's values are the indices themselves
+    if constexpr (VIN) {
+      load(vin, val, t0);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kRItems; ++k) val[k] = static_cast<uint32_t>(t0) + li + k * 64;   // (n < 2^30)
+    }
+    if (t0 + kTile < hi) load(kin, nkey, t0 + kTile);
     __syncthreads();
     uint32_t c = 0;   // the sub-tile's count of digit d
     if (d < nb) {
@@ -345,8 +367,12 @@ int radix_sort_pairs(RadixScratch &s, uint32_t *keys_in, uint32_t *keys_out, uin
     RX_CHECK(hipGetLastError());
     hipLaunchKernelGGL(radix_colscan_kernel, dim3((nb + 63) / 64), dim3(kRBlock), 0, st, cnt, pre, tot, groups, nb);
     RX_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(radix_pass_kernel, dim3(groups), dim3(kRBlock), kPassLds, st, kin[p], vin[p], kout[p], vout[p],
-                       n, dg.shift[p], dg.bits[p], per, pre, tot);
+    if (vin[p])
+      hipLaunchKernelGGL(radix_pass_kernel<true>, dim3(groups), dim3(kRBlock), kPassLds, st, kin[p], vin[p], kout[p],
+                         vout[p], n, dg.shift[p], dg.bits[p], per, pre, tot);
+    else
+      hipLaunchKernelGGL(radix_pass_kernel<false>, dim3(groups), dim3(kRBlock), kPassLds, st, kin[p], vin[p], kout[p],
+                         vout[p], n, dg.shift[p], dg.bits[p], per, pre, tot);
     RX_CHECK(hipGetLastError());
   }
   return hipSuccess;
