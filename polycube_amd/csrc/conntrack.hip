@@ -1803,13 +1803,17 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
   const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
   uint32_t live = 0;
   unsigned long long nmin = 0, mx = 0;                 // ~oldest, newest
-  for (uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i0 < cap; i0 += 4 * stp) {
-    unsigned long long key[4];
+  // 16 stamps a thread in flight together: unconditional loads (index clamped,
+  // the lanes past the table masked) -- a conditional load merges into a phi
+  // the compiler resolves with an immediate vmcnt(0), one round trip per load
+  constexpr int U = 16;
+  for (uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i0 < cap; i0 += U * stp) {
+    unsigned long long key[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) key[u] = i0 + u * stp < cap ? t.touch[i0 + u * stp] : ~0ull;
+    for (int u = 0; u < U; ++u) key[u] = t.touch[i0 + u * stp < cap ? i0 + u * stp : cap - 1];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const bool in = key[u] != ~0ull && (p == 0 || (key[u] & above) == prefix);
+    for (int u = 0; u < U; ++u) {
+      const bool in = i0 + u * stp < cap && key[u] != ~0ull && (p == 0 || (key[u] & above) == prefix);
       if (p == 0) {
         if (in) {
           ++live;
@@ -1923,17 +1927,31 @@ __global__ __launch_bounds__(256) void ct_ev_evict_kernel(CtTable t, const uint3
   const uint64_t cut = *reinterpret_cast<const unsigned long long *>(ctl + kCtlEvPrefix);
   const uint64_t cap = uint64_t(1) << t.cap_log2;
   uint32_t n = 0;
-  for (uint64_t i = g; i < cap; i += stp) {
-    const unsigned long long key = t.touch[i];
-    if (key > cut) continue;                           // newer, or not live (~0)
-    CtSlot *e = &t.slots[i];
-    ct_u32x4 hi = slot_half(e, 1);
-    hi.w &= ~0xff00u;                                  // valid = 0: connections.delete
-    reinterpret_cast<ct_u32x4 *>(e)[1] = hi;
-    t.touch[i] = ~0ull;
-    ++n;
+  constexpr int U = 4;                                 // stamps in flight together (unconditional loads)
+  for (uint64_t i0 = g; i0 < cap; i0 += U * stp) {
+    unsigned long long key[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) key[u] = t.touch[i0 + u * stp < cap ? i0 + u * stp : cap - 1];
+    uint32_t del = 0;                                  // (all decided before any store: one wait)
+#pragma unroll
+    for (int u = 0; u < U; ++u) del |= (i0 + u * stp < cap && key[u] <= cut ? 1u : 0u) << u;   // newer / not live: kept
+    asm volatile("" : "+v"(del));                      // (opaque: the compares are not sunk into the stores' branches)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!((del >> u) & 1)) continue;
+      const uint64_t i = i0 + u * stp;
+      // valid = 0 (connections.delete): the byte alone -- no read of the
+      // slot (a load per deletion, each waited for before its store)
+      t.slots[i].valid = 0;
+      t.touch[i] = ~0ull;
+      ++n;
+    }
   }
-  if (n) atomicAdd(&t.stats[1], static_cast<unsigned long long>(n));
+  // one atomic per wave on the one counter (one per thread with a deletion
+  // serialised there: ~200 K of them when a batch overflows the table)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(&t.stats[1], static_cast<unsigned long long>(n));
 }
 
 // Long echo replies (K_HARD) into the walk: a reply joins its own key's run

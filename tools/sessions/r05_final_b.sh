@@ -3,7 +3,7 @@
 # the headline bench; per-kernel counters of the stateful pipeline (ct_prep,
 # ct_walk, ct_heads, ct_count and the radix sort's kernels): fetch, write, SQ
 # cycles and the L2 -> memory read requests.
-TAG=r05_final
+TAG=r05_final_b
 source "$(dirname "$0")/../gpu_lib.sh"
 KEEP_GOING=1
 ktrace ktrace_cfg3_24 3 24 30

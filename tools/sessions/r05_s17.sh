@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 5, session 17: the LRU eviction with its deletions decided before any store and the
+# valid byte stored alone (no slot read per deletion).
+TAG=r05_s17
+source "$(dirname "$0")/../gpu_lib.sh"
+pytest_gpu tests_radix 300 tests/test_gpu_radix.py
+pytest_gpu tests_ct 600 tests/test_gpu_conntrack.py
+KEEP_GOING=1
+for r in 1 2; do
+  run ct_probe_$r 300 python tools/ct_probe.py --steps 6
+done
+( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ct_prof" -o run \
+    -- python3 "$R/tools/ct_probe.py" --steps 6 > "$O/ct_prof.log" 2>&1 )
+echo "== ct_prof rc=$?"
+find "$O" -name "*kernel_trace.csv" -delete
+exit 0
