@@ -2451,7 +2451,19 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 // 16-byte aligned fixed-stride batch whose first 48 bytes of every frame lie
 // inside the buffer, read as three 16-byte loads per lane (the scattered
 // dword loads run at ~2.4 TB/s on 64-byte frames, limited by requests).
-__device__ __forceinline__ uint32_t flow_owner_of(const CtBatch &b, uint64_t i, uint32_t nranks, bool vec) {
+// vec: frame i's first 48 bytes as three 16-byte loads
+__device__ __forceinline__ void flow_h12(const CtBatch &b, uint64_t i, uint32_t (&h12)[12]) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(b.frames + i * uint64_t(b.stride));
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint4 v = q[k];
+    h12[4 * k] = v.x; h12[4 * k + 1] = v.y; h12[4 * k + 2] = v.z; h12[4 * k + 3] = v.w;
+  }
+}
+// The owner from frame i's words; vec: h12 holds its first 48 bytes (the
+// caller loaded them, so several frames' loads can be in flight together).
+__device__ __forceinline__ uint32_t flow_owner_core(const CtBatch &b, uint64_t i, uint32_t nranks, bool vec,
+                                                    const uint32_t (&h12)[12]) {
   const uint64_t off = b.offsets ? b.offsets[i] : i * uint64_t(b.stride);
   uint32_t L = b.lens ? b.lens[i] : b.fixed_len;
   const uint64_t base = off & ~uint64_t(3);
@@ -2460,15 +2472,6 @@ __device__ __forceinline__ uint32_t flow_owner_of(const CtBatch &b, uint64_t i, 
     const uint64_t at = base + 4u * k;
     return at + 4 <= b.frames_bytes ? *reinterpret_cast<const uint32_t *>(b.frames + at) : 0u;
   };
-  uint32_t h12[12];
-  if (vec) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(b.frames + off);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const uint4 v = q[k];
-      h12[4 * k] = v.x; h12[4 * k + 1] = v.y; h12[4 * k + 2] = v.z; h12[4 * k + 3] = v.w;
-    }
-  }
   uint32_t s = 0;
   auto W = [&](uint32_t k) {
     if (vec && k + s < 12) return h12[k + s];
@@ -2499,6 +2502,11 @@ __device__ __forceinline__ uint32_t flow_owner_of(const CtBatch &b, uint64_t i, 
   const uint32_t h = fmix32(fmix32(lo ^ 0x9e3779b9u) ^ hi);
   return static_cast<uint32_t>((uint64_t(h) * nranks) >> 32);
 }
+__device__ __forceinline__ uint32_t flow_owner_of(const CtBatch &b, uint64_t i, uint32_t nranks, bool vec) {
+  uint32_t h12[12] = {};
+  if (vec) flow_h12(b, i, h12);
+  return flow_owner_core(b, i, nranks, vec, h12);
+}
 
 __global__ void flow_owner_kernel(CtBatch b, uint32_t nranks, bool vec, uint8_t *owner) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < b.n; i += uint64_t(gridDim.x) * blockDim.x)
@@ -2516,12 +2524,23 @@ __global__ __launch_bounds__(256) void flow_count_kernel(CtBatch b, uint32_t nra
   __shared__ uint32_t wsum[kSplitBlock / 64];
   const uint64_t tile = uint64_t(blockIdx.x) * kSplitTile;
   uint32_t c = 0;
+  // vec: every item's 48 bytes loaded before the first owner is computed
+  // (the index clamped into the batch): behind `if (i < n)` and the owner's
+  // own branches each item's loads waited for the previous item's owner
+  uint32_t h12[kSplitItems][12] = {};
+  if (vec) {
+#pragma unroll
+    for (uint32_t k = 0; k < kSplitItems; ++k) {
+      const uint64_t i = tile + k * kSplitBlock + threadIdx.x;
+      flow_h12(b, i < b.n ? i : b.n - 1, h12[k]);
+    }
+  }
 #pragma unroll
   for (uint32_t k = 0; k < kSplitItems; ++k) {
     const uint64_t i = tile + k * kSplitBlock + threadIdx.x;
     bool f = false;
     if (i < b.n) {
-      f = flow_owner_of(b, i, nranks, vec) == rank;
+      f = flow_owner_core(b, i, nranks, vec, h12[k]) == rank;
       flag[i] = f;
     }
     c += __popcll(__ballot(f));

@@ -1,11 +1,15 @@
 #!/bin/bash
-# Round 5, final evidence (part b): kernel-trace statistics of each config and of
+# Round 5, final evidence (part b), after the flow split's count kernel with its
+# frame loads issued together: its tests and the stateful bench leg; kernel-trace statistics of each config and of
 # the headline bench; per-kernel counters of the stateful pipeline (ct_prep,
 # ct_walk, ct_heads, ct_count and the radix sort's kernels): fetch, write, SQ
 # cycles and the L2 -> memory read requests.
 TAG=r05_final_b
 source "$(dirname "$0")/../gpu_lib.sh"
+# first the flow split with every item's frame words loaded together
+pytest_gpu tests_flow 300 tests/test_gpu_flow_split.py tests/test_gpu_multirank.py
 KEEP_GOING=1
+run bench_ct 400 python bench.py --steps 20 --warmup 5 --no-cpu --no-e2e --no-fw --no-hits --no-update
 ktrace ktrace_cfg3_24 3 24 30
 ktrace ktrace_cfg2_20 2 20 100
 ktrace ktrace_cfg5_22 5 22 30 xdp
