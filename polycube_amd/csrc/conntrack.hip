@@ -2586,9 +2586,16 @@ __global__ __launch_bounds__(256) void flow_write_kernel(CtBatch b, const uint8_
   const uint64_t tile = uint64_t(blockIdx.x) * kSplitTile;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t base = bstart[blockIdx.x];
+  uint8_t fl[kSplitItems];   // every round's flag loaded at once (index clamped, masked below)
+#pragma unroll
   for (uint32_t k = 0; k < kSplitItems; ++k) {
     const uint64_t i = tile + k * kSplitBlock + threadIdx.x;
-    const bool f = i < b.n && flag[i];
+    fl[k] = flag[i < b.n ? i : b.n - 1];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kSplitItems; ++k) {
+    const uint64_t i = tile + k * kSplitBlock + threadIdx.x;
+    const bool f = i < b.n && fl[k];
     const uint64_t m = __ballot(f);
     if (lane == 0) wsum[wave] = __popcll(m);
     __syncthreads();
