@@ -32,7 +32,7 @@ def main():
     import torch
     from polycube_amd import Iptables, ffi, synth
     rs = synth.config_rules(a.cfg)
-    ipt = Iptables(device=0, jit=1)
+    ipt = Iptables(device=0, jit=1, max_rules=16384)
     ipt.interactive = False
     fw = ipt.chain("FORWARD")
     for r in rs.rules():
@@ -40,16 +40,23 @@ def main():
     fw.default = "DROP"
     fw.apply_rules()
     n = 1 << a.log2n
-    cols = synth.make_headers(rs, n, synth.CONFIG_SEEDS[a.cfg], protos=(17,) if a.cfg in (1, 2) else (6, 17))
-    frames = torch.from_numpy(synth.build_frames(*cols).reshape(-1)).cuda()
+    kw = {}
+    if a.cfg == 5:   # IMIX offsets / lens (as tools/ablate.py), TC hook with CFG5_HOOK=tc
+        buf, off, ln = synth.imix_frames(rs, n, synth.CONFIG_SEEDS[5])
+        frames = torch.from_numpy(buf).cuda()
+        kw = dict(offsets=torch.from_numpy(off.view(np.int32)).cuda(), lens=torch.from_numpy(ln.view(np.int16)).cuda(),
+                  hook=1 if os.environ.get("CFG5_HOOK") == "tc" else 0)
+    else:
+        cols = synth.make_headers(rs, n, synth.CONFIG_SEEDS[a.cfg], protos=(17,) if a.cfg in (1, 2) else (6, 17))
+        frames = torch.from_numpy(synth.build_frames(*cols).reshape(-1)).cuda()
     v = torch.empty(n, dtype=torch.uint8, device="cuda")
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
         for _ in range(16):
-            ipt.classify(frames, n=n, verdicts=v, rule_ids=False)
+            ipt.classify(frames, n=n, verdicts=v, rule_ids=False, **kw)
         torch.cuda.synchronize()
     for k in range(a.launches):
-        ipt.classify(frames, n=n, verdicts=v, rule_ids=False)
+        ipt.classify(frames, n=n, verdicts=v, rule_ids=False, **kw)
         grid = ffi.lib().pcn_ipt_debug_clocks(ipt._h, None, 0)
         buf = (C.c_uint64 * (4 * grid))()
         assert ffi.lib().pcn_ipt_debug_clocks(ipt._h, buf, 4 * grid) == grid
