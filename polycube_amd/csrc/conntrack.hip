@@ -35,6 +35,12 @@
 #define PCN_CT_FAST 1   // walk: straight-line step for established TCP / live UDP connections
 #endif
 
+// llvm.amdgcn.struct.ptr.buffer.load (no clang builtin): buffer_load_dwordx4
+// ... idxen, bounds-checked by record index
+typedef int ct_i32x4 __attribute__((ext_vector_type(4)));
+__device__ ct_i32x4 ct_struct_load_v4(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+
 namespace pcn {
 
 namespace {
@@ -312,6 +318,7 @@ __global__ __launch_bounds__(kPrepBlock) PCN_CT_PREP_ATTR void ct_prep_kernel(Ct
                                uint32_t *chunk_ctr, uint32_t chunk_frames) {
   const uint32_t sentinel = (1u << kbits) - 1;
   const uint32_t lane = __lane_id();
+  const bool a0_final = b.nlab == 1 && b.a_rid == b.rule_ids && b.a_verdict == b.verdicts;
   __shared__ uint32_t chunk;
 #if PCN_CT_PREP_LDS
   __shared__ ct_u32x4 prep_stage[(kPrepBlock / 64) * 65 * kPrepRow];
@@ -526,9 +533,12 @@ __global__ __launch_bounds__(kPrepBlock) PCN_CT_PREP_ATTR void ct_prep_kernel(Ct
       // those with no table access (label INVALID for K_INV, else any label);
       // the label-0 one for the rest, which the walk overwrites only where it
       // differs (put_outcome)
+      // (one label: stage A wrote its outcomes into the final arrays themselves)
       const bool l3 = !member && r.kind == K_INV && !pass && b.nlab == 4;
-      b.verdicts[i] = l3 ? b.a_verdict[3 * b.n + i] : ver0;
-      b.rule_ids[i] = l3 ? b.a_rid[3 * b.n + i] : rid0;
+      if (!a0_final) {
+        b.verdicts[i] = l3 ? b.a_verdict[3 * b.n + i] : ver0;
+        b.rule_ids[i] = l3 ? b.a_rid[3 * b.n + i] : rid0;
+      }
     }
 #if PCN_CT_PREP_LDS
     if (fast) {                                         // the wave's records as coalesced chunks
@@ -1089,6 +1099,39 @@ struct RecSrc {
   }
   __device__ __forceinline__ WalkRec at(uint64_t q) const { return load(sidx[q], q); }
   __device__ __forceinline__ uint32_t key(uint64_t q) const { return skeys[q]; }
+  // the batch index / key bucket at sorted position q, clamped into the batch (n >= 1)
+  __device__ __forceinline__ uint32_t idx_at(uint64_t q, uint64_t n) const { return sidx[q < n ? q : n - 1]; }
+  __device__ __forceinline__ uint32_t key_at(uint64_t q, uint64_t n) const { return skeys[q < n ? q : n - 1]; }
+  // The record of batch index i at sorted position q (< n, key bucket kq) if
+  // that is the run's key k; zeros, and no memory request, otherwise: the
+  // index of a structured buffer load (stride 32, n records) is out of range
+  // for the lanes past a run's end.  (Every run's last chunk, and the chunk
+  // prefetched after it, fetched a 128-byte line per lane there: ~70 of the
+  // ~250 records of a bench flow's run, a quarter of the walk's fills.)
+  __device__ __forceinline__ WalkRec load_run(uint32_t i, uint32_t kq, uint32_t k, uint64_t q, uint64_t n) const {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<PackedRec *>(rec), 32, static_cast<uint32_t>(n), 0x00020000);
+    const uint32_t vi = kq == k && q < n ? i : 0xFFFFFFFFu;
+    union {
+      ct_u32x4 v[2];
+      PackedRec p;
+    } u;
+    u.v[0] = __builtin_bit_cast(ct_u32x4, ct_struct_load_v4(rs, static_cast<int>(vi), 0, 0, 0));
+    u.v[1] = __builtin_bit_cast(ct_u32x4, ct_struct_load_v4(rs, static_cast<int>(vi), 16, 0, 0));
+    WalkRec w;
+    w.r = ct_rec(u.p);
+    w.key = kq;
+    w.idx = i;
+    w.o0 = u.p.o0;
+    w.o1 = w.o2 = w.o3 = 0;
+    if (lab4) {
+      const ct_u32x4 v = ox[i];
+      w.o1 = static_cast<int32_t>(v.y);
+      w.o2 = static_cast<int32_t>(v.z);
+      w.o3 = static_cast<int32_t>(v.w);
+    }
+    return w;
+  }
 };
 
 // The walk of one long run's records in chunks of 64, from sorted position q0
@@ -1158,27 +1201,33 @@ __device__ __forceinline__ void pass_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// i0, k0, i1, k1: the batch indices and key buckets of the first two chunks
+// (sorted positions q0 + lane and q0 + 64 + lane, clamped), loaded by the
+// caller: a long run's head wave issues them with the run's key and cut
+// probes, one round trip for all.  Each chunk's indices and keys are loaded a
+// chunk ahead of its records, so that only the run's lanes fetch a record.
 template <bool kSpec>
 __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
-                                                uint32_t k, uint64_t q0, uint64_t hi, uint64_t bound, Cache &c,
-                                                bool &aborted, bool dense = false, uint64_t *tfirst = nullptr,
-                                                PassKeys *pk = nullptr, int pass = kAllKeys, uint64_t *unk = nullptr) {
+                                                uint32_t k, uint64_t q0, uint32_t i0, uint32_t k0, uint32_t i1,
+                                                uint32_t k1, uint64_t hi,
+                                                uint64_t bound, Cache &c, bool &aborted, bool dense = false,
+                                                uint64_t *tfirst = nullptr, PassKeys *pk = nullptr,
+                                                int pass = kAllKeys, uint64_t *unk = nullptr) {
   (void)tfirst;                                     // (measurement builds only)
   const uint32_t lane = threadIdx.x;
-  const uint64_t last = b.n - 1;
   const uint64_t lim = bound < b.n ? bound : b.n;
   uint64_t base = q0;
   aborted = false;
-  auto cl = [&](uint64_t r) -> uint64_t { return r < last ? r : last; };
-  WalkRec w = wrec.load(wrec.sidx[cl(base + lane)], cl(base + lane));
-  uint32_t nidx = wrec.sidx[cl(base + 64 + lane)];   // the next chunk's indices, a chunk ahead
+  WalkRec w = wrec.load_run(i0, k0, k, base + lane, b.n);
+  uint32_t nidx = i1, nkey = k1;                    // the next chunk's indices and keys, a chunk ahead
 #if PCN_CT_DBG
   uint32_t dbg_chunks = 0, dbg_rounds = 0, dbg_changes = 0, dbg_steps = 0, dbg_recs = 0;
   const uint64_t dbg_t0 = wall_clock64();
 #endif
   for (;;) {
-    const WalkRec nx = wrec.load(nidx, cl(base + 64 + lane));
-    nidx = wrec.sidx[cl(base + 128 + lane)];
+    const WalkRec nx = wrec.load_run(nidx, nkey, k, base + 64 + lane, b.n);
+    nidx = wrec.idx_at(base + 128 + lane, b.n);
+    nkey = wrec.key_at(base + 128 + lane, b.n);
     const CtRec &r = w.r;
     const bool inrun = base + lane < lim && w.key == k && w.idx < hi;
     const uint64_t rm = __ballot(inrun);           // the run's records: a prefix of the chunk
@@ -1366,15 +1415,22 @@ __device__ __forceinline__ uint32_t cache_px(const Cache &c) {
 // segments, the first pass stops at the run's first cut if that is active; if
 // the walk gets there, the state is left to ct_seg_fix (no flush, no cursor).
 __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
-                          const uint32_t *skeys, uint32_t p, uint32_t *cursor, uint32_t vb, uint64_t hi, int first,
-                          HeadExit *hx) {
-  const uint32_t k = wrec.key(p);
+                          uint32_t p, uint32_t *cursor, uint32_t vb, uint64_t hi, int first, HeadExit *hx) {
+  // One round trip for the run's key, its first cut's two probes and the
+  // first two chunks' batch indices: every load unconditional (indices
+  // clamped), where the cut's short-circuit test and the key before the
+  // indices made four dependent ones ahead of the first record.
+  const uint32_t lane = threadIdx.x;
+  const uint64_t last = b.n - 1;
   const uint64_t q0 = first ? p : cursor[vb];
-  uint64_t bound = ~0ull;
-  if (first != 0 && kSeg != 0) {
-    const uint64_t B1 = (p / (kSeg ? kSeg : 1) + 1) * kSeg;
-    if (cut_active(skeys, b.n, B1, k)) bound = B1;
-  }
+  const uint32_t k = wrec.key(p);
+  const uint64_t B1 = kSeg ? (p / (kSeg ? kSeg : 1) + 1) * kSeg : 0;
+  // (wrec's sorted keys: ct_tail passes no skeys)
+  const uint32_t kb = wrec.key(B1 - 1 < last ? B1 - 1 : last), ke = wrec.key(B1 + kSeg - 1 < last ? B1 + kSeg - 1 : last);
+  uint32_t i0 = wrec.idx_at(q0 + lane, b.n), i1 = wrec.idx_at(q0 + 64 + lane, b.n);
+  uint32_t k0 = wrec.key_at(q0 + lane, b.n), k1 = wrec.key_at(q0 + 64 + lane, b.n);
+  // cut B1 is active (cut_active): the run holds B1 - 1 and kSeg records from B1 on
+  const uint64_t bound = first != 0 && kSeg != 0 && B1 + kSeg <= b.n && kb == k && ke == k ? B1 : ~0ull;
   Cache c{};
   bool ab;
   __shared__ PassKeys pk;
@@ -1394,14 +1450,20 @@ __device__ void walk_long(const CtBatch &b, const CtTable &t, const RecSrc &wrec
 #endif
   for (;;) {
 #if PCN_CT_DBG_T
-    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, &dt1, &pk, pass, &unk);
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, i0, k0, i1, k1, hi, bound, c, ab, false, &dt1, &pk, pass,
+                                           &unk);
 #else
-    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, hi, bound, c, ab, false, nullptr, &pk, pass, &unk);
+    const uint64_t st = walk_chunks<false>(b, t, wrec, k, from, i0, k0, i1, k1, hi, bound, c, ab, false, nullptr, &pk,
+                                           pass, &unk);
 #endif
     if (from == q0) stop = st;                       // every pass stops there (the run's end, or hi)
     if (unk == ~0ull) break;
     from = unk;
     unk = ~0ull;
+    i0 = wrec.idx_at(from + lane, b.n);
+    i1 = wrec.idx_at(from + 64 + lane, b.n);
+    k0 = wrec.key_at(from + lane, b.n);
+    k1 = wrec.key_at(from + 64 + lane, b.n);
     if (++pass < kPassKeys) {
       const WalkRec x = wrec.at(from);
       if (threadIdx.x == 0) {
@@ -1476,7 +1538,9 @@ __device__ __forceinline__ void walk_seg(const CtBatch &b, const CtTable &t, con
   c.valid = true;
   bool ab;
   const uint64_t bound = cut_active(skeys, b.n, B + kSeg, k) ? B + kSeg : ~0ull;
-  const uint64_t stop = walk_chunks<true>(b, t, wrec, k, B, hi, bound, c, ab);
+  const uint64_t stop = walk_chunks<true>(b, t, wrec, k, B, wrec.idx_at(B + lane, b.n), wrec.key_at(B + lane, b.n),
+                                          wrec.idx_at(B + 64 + lane, b.n), wrec.key_at(B + 64 + lane, b.n), hi, bound, c,
+                                          ab);
   if (lane != 0) return;
   SegRec s{};
   s.src = gk.src;
@@ -1542,30 +1606,42 @@ __device__ __forceinline__ uint64_t walk_hi(const CtBatch &b, const uint32_t *ct
 // shorter runs of one class, one per lane, each from its head (first) or its
 // cursor up to batch index hi.  Every lane returns here (no early exit), so a
 // persistent wave can take the next block.
+// head: heads[vb] (class 0's heads come first), loaded by the caller ahead of
+// the plan's words.
 __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
-                        const uint32_t *skeys, const uint32_t *heads, const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first,
-                        uint32_t vb, HeadExit *hx) {
-  if (vb < plan->blk0[1]) {                       // one wave per long run
-    walk_long(b, t, wrec, skeys, heads[vb], cursor, vb, hi, first, hx);
+                        const uint32_t *heads, const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first,
+                        uint32_t vb, uint32_t head, HeadExit *hx) {
+  const uint32_t b1 = plan->blk0[1];
+  if (vb < b1) {                                  // one wave per long run
+    walk_long(b, t, wrec, head, cursor, vb, hi, first, hx);
     return;
   }
-  uint32_t cls = 1;
-  while (cls + 1 < kRunClasses && vb >= plan->blk0[cls + 1]) ++cls;
-  const uint32_t jj = (vb - plan->blk0[cls]) * 64 + threadIdx.x;
-  if (jj < plan->cnt[cls]) {
+  // the block's class, its first block and run count from the plan's words
+  // read at once (a search reading one word a step was a round trip each)
+  static_assert(kRunClasses == 5, "walk_vb's class selection");
+  const uint32_t b2 = plan->blk0[2], b3 = plan->blk0[3], b4 = plan->blk0[4];
+  const uint32_t c1 = plan->cnt[1], c2 = plan->cnt[2], c3 = plan->cnt[3], c4 = plan->cnt[4];
+  const uint32_t cls = 1u + (vb >= b2 ? 1u : 0u) + (vb >= b3 ? 1u : 0u) + (vb >= b4 ? 1u : 0u);
+  const uint32_t blk = cls == 1 ? b1 : cls == 2 ? b2 : cls == 3 ? b3 : b4;
+  const uint32_t cnt = cls == 1 ? c1 : cls == 2 ? c2 : cls == 3 ? c3 : c4;
+  const uint32_t jj = (vb - blk) * 64 + threadIdx.x;
+  if (jj < cnt) {
     const uint64_t j = class_off(b.n, cls) + jj;
     const uint32_t p = heads[j];
-    const uint32_t k = wrec.key(p);
     uint64_t q = first ? p : cursor[j];
     const uint64_t last = b.n - 1;
     Cache c{};
     // two records in flight in named registers, A/B alternating (a register
     // move of an in-flight load would wait for it), and the batch indices of
-    // the two after them (the record loads never wait on an index load)
+    // the two after them (the record loads never wait on an index load).
+    // The key and all four indices are issued before any record: a record
+    // issued between two index loads made the second one's wait cover it.
     auto cl = [&](uint64_t r) -> uint64_t { return r < last ? r : last; };
-    WalkRec A = wrec.load(wrec.sidx[cl(q)], cl(q));
-    WalkRec B = wrec.load(wrec.sidx[cl(q + 1)], cl(q + 1));
-    uint32_t IA = wrec.sidx[cl(q + 2)], IB = wrec.sidx[cl(q + 3)];
+    const uint32_t k = wrec.key(p);
+    const uint32_t iA = wrec.idx_at(q, b.n), iB = wrec.idx_at(q + 1, b.n);
+    uint32_t IA = wrec.idx_at(q + 2, b.n), IB = wrec.idx_at(q + 3, b.n);
+    WalkRec A = wrec.load(iA, cl(q));
+    WalkRec B = wrec.load(iB, cl(q + 1));
     for (;;) {
       if (q >= b.n || A.key != k || A.idx >= hi) break;
       put_outcome(b, A, step(b, t, c, A), false);
@@ -1615,8 +1691,12 @@ __global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const
 #endif
   const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
   const uint32_t vb = blockIdx.x - nseg;
+  // the head of a long run in flight with the plan's words (the index
+  // clamped into the buffer; a block past the plan returns without using it)
+  const uint64_t hcap = heads_cap(b.n);
+  const uint32_t head = heads[vb < hcap ? vb : 0];
   if (vb >= plan->blk0[kRunClasses]) return;
-  walk_vb(b, t, wrec, skeys, heads, plan, cursor, walk_hi(b, ctl), 1, vb, hx);
+  walk_vb(b, t, wrec, heads, plan, cursor, walk_hi(b, ctl), 1, vb, head, hx);
 }
 
 // One wave per cut j that is its run's first (the head stopped there): chain
@@ -1668,7 +1748,9 @@ __global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, co
       stop = s.stop;
     } else {
       bool ab;
-      stop = walk_chunks<false>(b, t, wrec, k, cut, hi, more ? cut + kSeg : ~0ull, c, ab, true);
+      stop = walk_chunks<false>(b, t, wrec, k, cut, wrec.idx_at(cut + threadIdx.x, b.n), wrec.key_at(cut + threadIdx.x, b.n),
+                                wrec.idx_at(cut + 64 + threadIdx.x, b.n), wrec.key_at(cut + 64 + threadIdx.x, b.n), hi,
+                                more ? cut + kSeg : ~0ull, c, ab, true);
     }
 #if PCN_CT_DBG
     if (threadIdx.x == 0)
@@ -1740,7 +1822,7 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
     nxt = wave_min(nxt);
     const uint64_t hi = nxt == 0xFFFFFFFFu ? b.n : nxt;
     for (uint32_t vb = 0; vb < total; ++vb) {
-      walk_vb(b, t, wrec, nullptr, heads, plan, cursor, hi, 0, vb, nullptr);   // (no cuts)
+      walk_vb(b, t, wrec, heads, plan, cursor, hi, 0, vb, heads[vb], nullptr);   // (no cuts)
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       __syncthreads();
     }

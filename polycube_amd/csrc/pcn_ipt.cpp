@@ -1493,6 +1493,14 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     int32_t *a_rid = static_cast<int32_t *>(ctx->ct_buf);
     int32_t *rids = b->rule_ids ? b->rule_ids : a_rid + nlab * n;
     uint8_t *a_v = reinterpret_cast<uint8_t *>(a_rid + nlab * n + (b->rule_ids ? 0 : n));
+    if (nlab == 1) {
+      // one label: stage A writes straight into the final outcome arrays (every
+      // packet's label-0 outcome is its outcome unless the walk changes it), and
+      // ct_prep, seeing them aliased, does not copy them there (2^24 packets:
+      // 80 MB of writes)
+      a_rid = rids;
+      a_v = b->verdicts;
+    }
     for (uint32_t l = 0; l < nlab; ++l) {
       StageA sa{ctx->d_labels + l, a_v + l * n, a_rid + l * n};
       int rc = launch_batch(ctx, b, stream, &sa, stale);
