@@ -1904,19 +1904,31 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
         }
         continue;
       }
-      // LDS atomics on one address serialise (~20 ns each), and the high
-      // digits put every stamp in one bin: the lanes that share the first
-      // lane's digit add together, the others one by one
+      // LDS atomics on one address serialise (~20 ns each), and a digit's
+      // stamps fall into a few bins (a batch's stamps differ in the batch
+      // index's high bits and the sequence's low ones): the lanes of a digit
+      // find each other by one ballot per digit bit and add once.  (Only the
+      // lanes sharing the first lane's digit added together before; the
+      // rest, most of a wave, added one by one: ~24 us a pass.)
       const uint64_t im = __ballot(in);
       if (!im) continue;
       const uint32_t d = static_cast<uint32_t>(key[u] >> shift) & ((1u << width) - 1);
-      const uint32_t d0 = __shfl(d, static_cast<int>(__builtin_ctzll(im)));
-      const uint64_t same = __ballot(in && d == d0);
-      if ((threadIdx.x & 63) == __builtin_ctzll(im)) atomicAdd(&h[d0], static_cast<uint32_t>(__builtin_popcountll(same)));
-      else if (in && d != d0) atomicAdd(&h[d], 1u);
+      uint64_t peers = im;
+      for (uint32_t bit = 0; bit < width; ++bit) {
+        const uint64_t bb = __ballot((d >> bit) & 1);
+        peers &= ((d >> bit) & 1) ? bb : ~bb;
+      }
+      if (in && (threadIdx.x & 63) == __builtin_ctzll(peers))
+        atomicAdd(&h[d], static_cast<uint32_t>(__builtin_popcountll(peers)));
     }
   }
   uint32_t *hp = hist + p * kEvBins;
+  // The merges are device-scope atomics, which every workgroup's reads of
+  // them (atomic loads) see once they have completed: each wave waits for its
+  // own (returning atomics, the results consumed) before the workgroup
+  // arrives.  No fence: a __threadfence() in all 16 waves (an L2 write-back
+  // and invalidate each) cost ~15 us a pass.
+  uint64_t dep = 0;
   if (p == 0) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {              // one LDS atomic per wave
@@ -1932,21 +1944,20 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
     }
     __syncthreads();
     if (threadIdx.x == 0 && live_s) {
-      atomicAdd(&ctl[kCtlLive], live_s);
-      atomicMax(reinterpret_cast<unsigned long long *>(ctl + kCtlEvNotMin), lo_s);
-      atomicMax(reinterpret_cast<unsigned long long *>(ctl + kCtlEvMax), hi_s);
+      dep += atomicAdd(&ctl[kCtlLive], live_s);
+      dep += atomicMax(reinterpret_cast<unsigned long long *>(ctl + kCtlEvNotMin), lo_s);
+      dep += atomicMax(reinterpret_cast<unsigned long long *>(ctl + kCtlEvMax), hi_s);
     }
   } else {
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < kEvBins; k += blockDim.x)
-      if (h[k]) atomicAdd(&hp[k], h[k]);
+      if (h[k]) dep += atomicAdd(&hp[k], h[k]);
   }
-  __threadfence();
+  asm volatile("" ::"v"(dep));
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(&ctl[kCtlEvDone], 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  __threadfence();
   if (p == 0) {                                        // the last workgroup: evict at all, and from which bit
     if (threadIdx.x == 0) {
       ctl[kCtlEvDone] = 0;
