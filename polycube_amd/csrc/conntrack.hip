@@ -956,7 +956,13 @@ __host__ __device__ constexpr uint64_t heads_cap(uint64_t n) { return class_off(
 // the six keys of a classification from L2, twice, cost 95 us a 2^24 batch.
 // Keys per thread: 16, or fewer (a multiple of 4) so that a smaller batch
 // still gives every CU two workgroups.
-constexpr uint32_t kHeadsBlock = 256;
+// 1024 threads: every workgroup reserves its heads with one global atomic per
+// class, and those land on five addresses (~12 ns apiece, serialised): 4,096
+// workgroups of 256 threads a 2^24 batch spent most of ct_heads' 67 us there.
+#ifndef PCN_CT_HEADS_BLOCK
+#define PCN_CT_HEADS_BLOCK 1024
+#endif
+constexpr uint32_t kHeadsBlock = PCN_CT_HEADS_BLOCK;
 constexpr uint32_t kHeadsPer = 16;
 inline uint32_t heads_per(uint64_t n, int num_cus) {
   const uint64_t p = (n / (uint64_t(kHeadsBlock) * 2 * num_cus) + 3) / 4 * 4;
@@ -2114,6 +2120,9 @@ inline uint64_t count_chunk(uint64_t n, int num_cus) {
   return c < q ? q : c > kCountChunk ? kCountChunk : c;
 }
 
+#ifndef PCN_CT_COUNT_U
+#define PCN_CT_COUNT_U 16
+#endif
 __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) {
   constexpr uint32_t per = 2 + kLdsRules;
   // groups 0-2: the chains; group 3: Horus rule ids (bins 2..).  One u64 LDS
@@ -2124,7 +2133,13 @@ __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) 
   __syncthreads();
   const uint64_t lo = uint64_t(blockIdx.x) * chunk;
   const uint64_t hi = lo + chunk < b.n ? lo + chunk : b.n;
-  constexpr uint32_t U = 4;     // packets per thread whose loads are in flight together
+  // The default rule's packets (half of them on the bench traffic) go to one
+  // bin per chain: as LDS atomics, 32 lanes of an instruction on one address
+  // serialised.  A lane sums them in registers instead (packed as the bins).
+  unsigned long long dflt[3] = {0, 0, 0};
+  // packets per thread whose loads are in flight together (4: a thread's 64
+  // packets of a 2^24 batch took 16 dependent round trips)
+  constexpr uint32_t U = PCN_CT_COUNT_U;
   for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
     int32_t rids[U];
     uint32_t lcv[U];
@@ -2161,7 +2176,8 @@ __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) 
         }
         bin = 2 + uint32_t(rid);
       } else if (rid == PCN_IPT_RID_DEFAULT) {
-        bin = 0;
+        dflt[c] += (1ull << 40) | len;               // (c < 3)
+        continue;
       } else if (rid == -3) {
         bin = 1;
       } else {
@@ -2169,6 +2185,14 @@ __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) 
       }
       atomicAdd(&bins[c * per + bin], (1ull << 40) | len);
     }
+  }
+  // the default bins, summed over the wave: one LDS atomic per wave and chain
+#pragma unroll
+  for (uint32_t c = 0; c < 3; ++c) {
+    unsigned long long v = dflt[c];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&bins[c * per], v);
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) {
