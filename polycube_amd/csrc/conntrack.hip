@@ -2426,8 +2426,14 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   if (b.n == 0) return hipSuccess;
   if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);   // hipCUB item counts are int
   hipStream_t st = static_cast<hipStream_t>(stream);
+  // key buckets: 2^kbits >= n (a 2^24 batch sorts 24-bit keys in three 8-bit
+  // passes; 2^kbits >= 2n gave 25 bits and a 9-bit first pass, +20 us, for half
+  // the bucket collisions between connections, which the walk takes in passes)
+#ifndef PCN_CT_KEY_SLACK
+#define PCN_CT_KEY_SLACK 1
+#endif
   uint32_t kbits = 8;
-  while (kbits < 30 && (uint64_t(1) << kbits) < 2 * b.n) ++kbits;
+  while (kbits < 30 && (uint64_t(1) << kbits) < PCN_CT_KEY_SLACK * b.n) ++kbits;
   kbits = std::min(kbits, debug_key_bits());
   const uint32_t sentinel = (1u << kbits) - 1;
   CT_CHECK(grow(s, b.n, kbits, b.nlab == 4));

@@ -636,8 +636,8 @@ def test_long_runs_of_colliding_connections(dev):
     stats = (ctypes.c_uint64 * 2)()
     assert ffi.lib().pcn_ipt_debug_ct_walk_passes(ipt._h, stats, 1) == 0   # reset
     n = per * sum(groups)
-    kbits = 8
-    while (1 << kbits) < 2 * n:
+    kbits = 8                      # conntrack.hip ct_run: 2^kbits >= n
+    while (1 << kbits) < n:
         kbits += 1
     flows = []
     for g, size in enumerate(groups):
