@@ -956,6 +956,11 @@ __host__ __device__ constexpr uint64_t heads_cap(uint64_t n) { return class_off(
 // the six keys of a classification from L2, twice, cost 95 us a 2^24 batch.
 // Keys per thread: 16, or fewer (a multiple of 4) so that a smaller batch
 // still gives every CU two workgroups.
+#ifndef PCN_CT_SEG
+#define PCN_CT_SEG 512   // records per segment (a power of two >= kLongRun); 0: no segments
+#endif
+constexpr uint64_t kSeg = PCN_CT_SEG;
+static_assert(kSeg == 0 || (kSeg >= kLongRun && (kSeg & (kSeg - 1)) == 0), "PCN_CT_SEG");
 // 1024 threads: every workgroup reserves its heads with one global atomic per
 // class, and those land on five addresses (~12 ns apiece, serialised): 4,096
 // workgroups of 256 threads a 2^24 batch spent most of ct_heads' 67 us there.
@@ -963,6 +968,7 @@ __host__ __device__ constexpr uint64_t heads_cap(uint64_t n) { return class_off(
 #define PCN_CT_HEADS_BLOCK 1024
 #endif
 constexpr uint32_t kHeadsBlock = PCN_CT_HEADS_BLOCK;
+static_assert(kSeg == 0 || (4 * uint64_t(kHeadsBlock)) % (kSeg ? kSeg : 1) == 0, "a heads tile starts at a cut");
 constexpr uint32_t kHeadsPer = 16;
 inline uint32_t heads_per(uint64_t n, int num_cus) {
   const uint64_t p = (n / (uint64_t(kHeadsBlock) * 2 * num_cus) + 3) / 4 * 4;
@@ -975,7 +981,8 @@ inline uint32_t heads_per(uint64_t n, int num_cus) {
 // batch; ct_prep itself doing it put its parse window in scratch.)
 __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads,
                                                                uint32_t *nheads, uint32_t sentinel, uint32_t per,
-                                                               const unsigned long long *desc, uint32_t *carry) {
+                                                               const unsigned long long *desc, uint32_t *carry,
+                                                               uint32_t *cuts, uint32_t *ncuts) {
   __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     const uint32_t c = ports_lookback(desc, (n + 63) / 64, carry);
@@ -1004,6 +1011,17 @@ __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const
     if (j < T + kLongRun + 1) tile[j] = q >= 1 && q - 1 < n ? tv[k] : 0xffffffffu;
   }
   __syncthreads();
+  // The tile's active cuts (the walk's cut_active: the run holds B - 1 and kSeg
+  // records from B on) for the segment waves: rare, one atomic each.
+  if (kSeg != 0 && threadIdx.x < T / (kSeg ? kSeg : 1)) {
+    const uint64_t B = lo + uint64_t(threadIdx.x) * kSeg;
+    if (B >= 1 && B + kSeg <= n) {
+      const uint32_t r = static_cast<uint32_t>(B - lo);
+      const uint32_t k = tile[r + 1];
+      if (k != sentinel && tile[r] == k && skeys[B + kSeg - 1] == k)
+        cuts[atomicAdd(ncuts, 1u)] = static_cast<uint32_t>(B / (kSeg ? kSeg : 1));
+    }
+  }
   // the class of tile position r (sorted position lo + r); kRunClasses: not a run head
   auto run_class_lds = [&](uint32_t r) -> uint32_t {
     const uint32_t k = tile[r + 1], km = tile[r];
@@ -1384,13 +1402,19 @@ __device__ __forceinline__ uint64_t walk_chunks(const CtBatch &b, const CtTable 
 // segment is walked again from the true state, its outcomes overwritten.  A
 // key that keeps its state through the batch has every guess hold; a
 // connection opened or closed mid-run costs re-walked segments from there on.
-#ifndef PCN_CT_SEG
-#define PCN_CT_SEG 512   // records per segment (a power of two >= kLongRun); 0: no segments
-#endif
-constexpr uint64_t kSeg = PCN_CT_SEG;
-static_assert(kSeg == 0 || (kSeg >= kLongRun && (kSeg & (kSeg - 1)) == 0), "PCN_CT_SEG");
+// (kSeg, the records per speculative segment: below, with walk_seg)
 constexpr unsigned long long kTtlUnset = ~0ull;
 __host__ __device__ constexpr uint64_t seg_count(uint64_t n) { return kSeg ? n / (kSeg ? kSeg : 1) + 1 : 0; }
+// Waves for the active cuts (walk_seg, ct_seg_fix), each taking every
+// seg_waves-th: a wave per cut, active or not (32 K at 2^24, nearly all with
+// nothing to do), cost the walk 12 us a batch.
+#ifndef PCN_CT_SEG_WAVES
+#define PCN_CT_SEG_WAVES 64
+#endif
+constexpr uint64_t kSegWaves = PCN_CT_SEG_WAVES;
+__host__ __device__ constexpr uint32_t seg_waves(uint64_t n) {
+  return static_cast<uint32_t>(seg_count(n) < kSegWaves ? seg_count(n) : kSegWaves);
+}
 
 struct alignas(16) SegRec {       // 64 bytes, one per cut j (sorted position j * kSeg)
   uint32_t src, dst, ports, gx;   // the guess: key, proto | state << 8 | rev << 16 | live << 24
@@ -1575,6 +1599,7 @@ struct WalkPlan {
 // stays asynchronous).
 constexpr uint32_t kCtlHard = 0;      // long echo replies (K_HARD) in hard_list
 constexpr uint32_t kCtlClass = 1;     // [1..5] runs per length class (ct_heads)
+constexpr uint32_t kCtlSegN = 6;      // active cuts in CtScratch::cuts (ct_heads)
 constexpr uint32_t kCtlChunk = 8;     // ct_prep's chunk counter
 constexpr uint32_t kCtlTh = 9;        // K_HARD records the walk cannot take (th_list)
 constexpr uint32_t kCtlThFirst = 10;  // 0xFFFFFFFF - the first of them (0: none)
@@ -1672,23 +1697,28 @@ __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
 // blocks past the plan return at once: a workgroup that returns costs the
 // dispatcher next to nothing, where a persistent grid taking blocks from one
 // counter serialised ~10^5 atomics on one address (7.1 vs 2.9 ms a batch).
-// With segments, the first seg_count(n) workgroups are the cuts (walk_seg).
+// With segments, the first seg_waves(n) workgroups walk the active cuts that
+// ct_heads listed (walk_seg), each taking every seg_waves-th of them.
 __global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec,
                                                      const uint32_t *heads, const uint32_t *ctl, uint32_t *cursor,
                                                      const uint32_t *skeys, uint32_t sentinel, SegRec *seg,
-                                                     HeadExit *hx) {
-  const uint32_t nseg = static_cast<uint32_t>(seg_count(b.n));
-#if PCN_CT_DBG
-  const uint64_t dbg_t0 = wall_clock64();
-#endif
+                                                     HeadExit *hx, const uint32_t *cuts) {
+  const uint32_t nseg = seg_waves(b.n);
   if (blockIdx.x < nseg) {
-    walk_seg(b, t, wrec, skeys, sentinel, seg, blockIdx.x, walk_hi(b, ctl));
+    const uint32_t na = ctl[kCtlSegN];
+    for (uint32_t i = blockIdx.x; i < na; i += nseg) {
 #if PCN_CT_DBG
-    const uint64_t dt = wall_clock64() - dbg_t0;
-    if (threadIdx.x == 0 && seg[blockIdx.x].status)
-      printf("seg %u: status %u, walked %u, %llu us\n", blockIdx.x, seg[blockIdx.x].status,
-             seg[blockIdx.x].stop - blockIdx.x * uint32_t(kSeg), (unsigned long long)(dt / 100));
+      const uint64_t dbg_t0 = wall_clock64();
 #endif
+      const uint32_t j = cuts[i];
+      walk_seg(b, t, wrec, skeys, sentinel, seg, j, walk_hi(b, ctl));
+#if PCN_CT_DBG
+      const uint64_t dt = wall_clock64() - dbg_t0;
+      if (threadIdx.x == 0 && seg[j].status)
+        printf("seg %u: status %u, walked %u, %llu us\n", j, seg[j].status, seg[j].stop - j * uint32_t(kSeg),
+               (unsigned long long)(dt / 100));
+#endif
+    }
     return;
   }
   // (the plan is read in place: a local copy indexed by class went to scratch)
@@ -1705,13 +1735,11 @@ __global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const
   walk_vb(b, t, wrec, heads, plan, cursor, walk_hi(b, ctl), 1, vb, head, hx);
 }
 
-// One wave per cut j that is its run's first (the head stopped there): chain
+// For a cut j that is its run's first (the head stopped there): chain
 // the run's segments in order from the head's state, re-walking those whose
 // guess does not hold, then flush the connection and set the run's cursor.
-__global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, const RecSrc wrec,
-                                                        const uint32_t *skeys, const SegRec *seg, const HeadExit *hx,
-                                                        uint32_t *cursor, const uint32_t *ctl) {
-  const uint32_t j = blockIdx.x;
+__device__ void seg_fix_cut(const CtBatch &b, const CtTable &t, const RecSrc &wrec, const uint32_t *skeys,
+                            const SegRec *seg, const HeadExit *hx, uint32_t *cursor, const uint32_t *ctl, uint32_t j) {
   const uint64_t B = uint64_t(j) * kSeg;
   if (j == 0 || B >= b.n || seg[j].status == 0) return;
   const uint32_t k = skeys[B];
@@ -1768,6 +1796,16 @@ __global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, co
     flush(t, c);
     cursor[h.vb] = static_cast<uint32_t>(stop);
   }
+}
+
+// One wave per seg_waves(n)-th active cut (only a run's first cut does work;
+// the bench traffic has such runs: their fixes in ct_tail, one after the other
+// in one wave, took 80 us against this kernel's 22).
+__global__ __launch_bounds__(64) void ct_seg_fix_kernel(CtBatch b, CtTable t, const RecSrc wrec,
+                                                        const uint32_t *skeys, const SegRec *seg, const HeadExit *hx,
+                                                        uint32_t *cursor, const uint32_t *ctl, const uint32_t *cuts) {
+  const uint32_t na = ctl[kCtlSegN];
+  for (uint32_t i = blockIdx.x; i < na; i += gridDim.x) seg_fix_cut(b, t, wrec, skeys, seg, hx, cursor, ctl, cuts[i]);
 }
 
 // An echo reply long enough to quote a header (ConntrackLabel_dp.c:450-531)
@@ -2254,8 +2292,9 @@ struct CtScratch {
   uint32_t *evh = nullptr;                // LRU radix-select histograms (kEvPasses x kEvBins, kept zeroed)
   uint64_t bm_bytes = 0;
   uint32_t *heads = nullptr;
-  SegRec *seg = nullptr;                  // speculative segments of long runs (walk_seg, ct_seg_fix)
+  SegRec *seg = nullptr;                  // speculative segments of long runs (walk_seg, seg_fix_cut)
   HeadExit *hx = nullptr;
+  uint32_t *cuts = nullptr;               // the batch's active cuts (ct_heads; ctl[kCtlSegN] of them)
   PackedRec *brec = nullptr;  // walk records, batch order
   ct_u32x4 *ox = nullptr;     // the four stage-A outcomes per packet (batches with four labels)
   uint64_t ox_cap = 0;
@@ -2278,7 +2317,8 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->ctl), static_cast<void *>(s->brec), static_cast<void *>(s->ox),
                   static_cast<void *>(s->heads),
                   static_cast<void *>(s->zfound), static_cast<void *>(s->th_list), static_cast<void *>(s->bm),
-                  static_cast<void *>(s->evh), static_cast<void *>(s->seg), static_cast<void *>(s->hx)})
+                  static_cast<void *>(s->evh), static_cast<void *>(s->seg), static_cast<void *>(s->hx),
+                  static_cast<void *>(s->cuts)})
     if (p) (void)hipFree(p);
   radix_free(s->rx);
   delete s;
@@ -2348,8 +2388,10 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4) {
     if (kSeg) {
       if (s.seg) CT_CHECK(hipFree(s.seg));
       if (s.hx) CT_CHECK(hipFree(s.hx));
+      if (s.cuts) CT_CHECK(hipFree(s.cuts));
       CT_CHECK(hipMalloc(&s.seg, (seg_count(n) + 1) * sizeof(SegRec)));
       CT_CHECK(hipMalloc(&s.hx, (seg_count(n) + 1) * sizeof(HeadExit)));
+      CT_CHECK(hipMalloc(&s.cuts, (seg_count(n) + 1) * 4));
     }
     if (!s.ctl) CT_CHECK(hipMalloc(&s.ctl, kCtlWords * 4));   // the kCtl* words + the walk plan
     if (!s.evh) {
@@ -2487,19 +2529,20 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
-                     b.n, s.keys2, s.heads, s.ctl + kCtlClass, sentinel, hper, s.pdesc, t.carry);
+                     b.n, s.keys2, s.heads, s.ctl + kCtlClass, sentinel, hper, s.pdesc, t.carry, s.cuts,
+                     s.ctl + kCtlSegN);
   CT_CHECK(hipGetLastError());
   // the walk plan, sized on the device: no read-back, the stream stays asynchronous
   hipLaunchKernelGGL(ct_plan_kernel, dim3(1), dim3(64), 0, st, s.ctl);
   CT_CHECK(hipGetLastError());
   // the cuts of long runs, then the plan's upper bound
-  const unsigned wgrid = static_cast<unsigned>(seg_count(b.n) + b.n / 64 + kRunClasses + 1);
+  const unsigned wgrid = static_cast<unsigned>(seg_waves(b.n) + b.n / 64 + kRunClasses + 1);
   hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.heads, s.ctl, s.cursor,
-                     s.keys2, sentinel, s.seg, s.hx);
+                     s.keys2, sentinel, s.seg, s.hx, s.cuts);
   CT_CHECK(hipGetLastError());
   if (kSeg) {
-    hipLaunchKernelGGL(ct_seg_fix_kernel, dim3(static_cast<unsigned>(seg_count(b.n))), dim3(64), 0, st, b, t, src,
-                       s.keys2, s.seg, s.hx, s.cursor, s.ctl);
+    hipLaunchKernelGGL(ct_seg_fix_kernel, dim3(seg_waves(b.n)), dim3(64), 0, st, b, t, src, s.keys2, s.seg, s.hx,
+                       s.cursor, s.ctl, s.cuts);
     CT_CHECK(hipGetLastError());
   }
   hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.heads, s.ctl, s.th_list,
