@@ -2161,8 +2161,14 @@ inline uint64_t count_chunk(uint64_t n, int num_cus) {
 #ifndef PCN_CT_COUNT_U
 #define PCN_CT_COUNT_U 16
 #endif
-__global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk) {
+// It also leaves the next batch's control words and ports descriptors zeroed
+// (ctl[0, kCtlZero), pdesc[0, ngroups)): two memsets a batch were a launch each.
+__global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk, uint32_t *ctl,
+                                unsigned long long *pdesc, uint64_t ngroups) {
   constexpr uint32_t per = 2 + kLdsRules;
+  for (uint64_t g = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < ngroups; g += uint64_t(gridDim.x) * blockDim.x)
+    pdesc[g] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < kCtlZero) ctl[threadIdx.x] = 0;
   // groups 0-2: the chains; group 3: Horus rule ids (bins 2..).  One u64 LDS
   // atomic per packet: pkts in bits 40-63, bytes in bits 0-39 (a workgroup's
   // <= 2^16 packets of <= 65535 bytes cannot carry out of either field).
@@ -2283,6 +2289,7 @@ unsigned grid_for(uint64_t n, unsigned block, int num_cus) {
 
 struct CtScratch {
   uint64_t cap = 0;
+  bool dirty = false;                     // a batch returned early: ctl / pdesc need zeroing
   unsigned long long *pdesc = nullptr;   // ct_prep: the ports word of every 64-frame group
   uint32_t *keys = nullptr, *keys2 = nullptr;
   uint32_t *lcs = nullptr;                // per packet: len | cinfo << 16 (ct_count)
@@ -2383,6 +2390,7 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4) {
     }
     if (s.pdesc) CT_CHECK(hipFree(s.pdesc));
     CT_CHECK(hipMalloc(&s.pdesc, (n / 64 + 2) * 8));
+    CT_CHECK(hipMemset(s.pdesc, 0, (n / 64 + 2) * 8));
     if (s.brec) CT_CHECK(hipFree(s.brec));
     CT_CHECK(hipMalloc(&s.brec, n * sizeof(PackedRec)));
     if (kSeg) {
@@ -2393,7 +2401,10 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4) {
       CT_CHECK(hipMalloc(&s.hx, (seg_count(n) + 1) * sizeof(HeadExit)));
       CT_CHECK(hipMalloc(&s.cuts, (seg_count(n) + 1) * 4));
     }
-    if (!s.ctl) CT_CHECK(hipMalloc(&s.ctl, kCtlWords * 4));   // the kCtl* words + the walk plan
+    if (!s.ctl) {
+      CT_CHECK(hipMalloc(&s.ctl, kCtlWords * 4));   // the kCtl* words + the walk plan
+      CT_CHECK(hipMemset(s.ctl, 0, kCtlWords * 4));
+    }
     if (!s.evh) {
       CT_CHECK(hipMalloc(&s.evh, kEvPasses * kEvBins * 4));
       CT_CHECK(hipMemset(s.evh, 0, kEvPasses * kEvBins * 4));
@@ -2483,8 +2494,14 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   // one memset for the control words (long echo replies, run counts per
   // class, ct_prep's chunk counter, ...; kCtl*): each memset is a launch of
   // its own (~5 us between kernels)
-  CT_CHECK(hipMemsetAsync(s.ctl, 0, kCtlZero * 4, st));
-  CT_CHECK(hipMemsetAsync(s.pdesc, 0, (b.n / 64 + 1) * 8, st));
+  // ctl's first kCtlZero words and the ports descriptors are zero: from their
+  // allocation, then from the previous batch's ct_count; only a batch that
+  // returned early with an error leaves them to memsets here
+  if (s.dirty) {
+    CT_CHECK(hipMemsetAsync(s.ctl, 0, kCtlZero * 4, st));
+    CT_CHECK(hipMemsetAsync(s.pdesc, 0, (s.cap / 64 + 2) * 8, st));
+  }
+  s.dirty = true;
   const uint32_t pchunk = prep_chunk(b.n, num_cus);
   const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
   hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.ox, s.lcs, s.keys, kbits,
@@ -2564,8 +2581,10 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   ++t.seq;                                     // the next batch's touch stamps are newer
   const uint64_t cchunk = count_chunk(b.n, num_cus);
   const unsigned cgrid = static_cast<unsigned>((b.n + cchunk - 1) / cchunk);
-  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs, cchunk);
+  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs, cchunk, s.ctl, s.pdesc,
+                     b.n / 64 + 1);
   CT_CHECK(hipGetLastError());
+  s.dirty = false;
   return hipSuccess;
 }
 
