@@ -969,7 +969,10 @@ static_assert(kSeg == 0 || (kSeg >= kLongRun && (kSeg & (kSeg - 1)) == 0), "PCN_
 #endif
 constexpr uint32_t kHeadsBlock = PCN_CT_HEADS_BLOCK;
 static_assert(kSeg == 0 || (4 * uint64_t(kHeadsBlock)) % (kSeg ? kSeg : 1) == 0, "a heads tile starts at a cut");
-constexpr uint32_t kHeadsPer = 16;
+#ifndef PCN_CT_HEADS_PER
+#define PCN_CT_HEADS_PER 16
+#endif
+constexpr uint32_t kHeadsPer = PCN_CT_HEADS_PER;
 inline uint32_t heads_per(uint64_t n, int num_cus) {
   const uint64_t p = (n / (uint64_t(kHeadsBlock) * 2 * num_cus) + 3) / 4 * 4;
   return static_cast<uint32_t>(p < 4 ? 4 : p > kHeadsPer ? kHeadsPer : p);
