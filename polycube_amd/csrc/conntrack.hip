@@ -1610,7 +1610,6 @@ constexpr uint32_t kCtlLive = 12;     // LRU: live entries after the batch (ct_e
 constexpr uint32_t kCtlEvict = 13;    //      1 when more than max_entries are live
 constexpr uint32_t kCtlEvK = 14;      //      rank (1-based) of the newest stamp to evict, within the prefix
 constexpr uint32_t kCtlEvDone = 15;   //      workgroups done with the current pass
-constexpr uint32_t kCtlPlan = 16;     // WalkPlan (ct_plan)
 constexpr uint32_t kCtlEvPrefix = 28; // u64: the stamp digits chosen so far
 constexpr uint32_t kCtlEvLow = 30;    //      the stamp bits below this one are still to choose
 constexpr uint32_t kCtlEvNotMin = 32; //      u64: ~(the oldest live stamp) (a max, so zero-initialised)
@@ -1618,17 +1617,21 @@ constexpr uint32_t kCtlEvMax = 34;    //      u64: the newest live stamp
 constexpr uint32_t kCtlZero = 36;     // words zeroed per batch
 constexpr uint32_t kCtlWords = 64;
 
-__global__ void ct_plan_kernel(uint32_t *ctl) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  WalkPlan *plan = reinterpret_cast<WalkPlan *>(ctl + kCtlPlan);
+// The walk plan from ct_heads' class counts, computed where it is used (a
+// kernel of its own, ct_plan, was a launch of ~5 us a batch): in registers,
+// indexed only by constants (a local copy indexed by class went to scratch).
+__device__ __forceinline__ WalkPlan plan_of(const uint32_t *ctl) {
+  WalkPlan plan;
   uint32_t b0 = 0;
+#pragma unroll
   for (uint32_t c = 0; c < kRunClasses; ++c) {
     const uint32_t cnt = ctl[kCtlClass + c];
-    plan->cnt[c] = cnt;
-    plan->blk0[c] = b0;
+    plan.cnt[c] = cnt;
+    plan.blk0[c] = b0;
     b0 += c == 0 ? cnt : (cnt + 63) / 64;      // one wave per long run, one lane per shorter run
   }
-  plan->blk0[kRunClasses] = b0;
+  plan.blk0[kRunClasses] = b0;
+  return plan;
 }
 
 __device__ __forceinline__ uint64_t walk_hi(const CtBatch &b, const uint32_t *ctl) {
@@ -1643,9 +1646,9 @@ __device__ __forceinline__ uint64_t walk_hi(const CtBatch &b, const uint32_t *ct
 // head: heads[vb] (class 0's heads come first), loaded by the caller ahead of
 // the plan's words.
 __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
-                        const uint32_t *heads, const WalkPlan *plan, uint32_t *cursor, uint64_t hi, int first,
+                        const uint32_t *heads, const WalkPlan &plan, uint32_t *cursor, uint64_t hi, int first,
                         uint32_t vb, uint32_t head, HeadExit *hx) {
-  const uint32_t b1 = plan->blk0[1];
+  const uint32_t b1 = plan.blk0[1];
   if (vb < b1) {                                  // one wave per long run
     walk_long(b, t, wrec, head, cursor, vb, hi, first, hx);
     return;
@@ -1653,8 +1656,8 @@ __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
   // the block's class, its first block and run count from the plan's words
   // read at once (a search reading one word a step was a round trip each)
   static_assert(kRunClasses == 5, "walk_vb's class selection");
-  const uint32_t b2 = plan->blk0[2], b3 = plan->blk0[3], b4 = plan->blk0[4];
-  const uint32_t c1 = plan->cnt[1], c2 = plan->cnt[2], c3 = plan->cnt[3], c4 = plan->cnt[4];
+  const uint32_t b2 = plan.blk0[2], b3 = plan.blk0[3], b4 = plan.blk0[4];
+  const uint32_t c1 = plan.cnt[1], c2 = plan.cnt[2], c3 = plan.cnt[3], c4 = plan.cnt[4];
   const uint32_t cls = 1u + (vb >= b2 ? 1u : 0u) + (vb >= b3 ? 1u : 0u) + (vb >= b4 ? 1u : 0u);
   const uint32_t blk = cls == 1 ? b1 : cls == 2 ? b2 : cls == 3 ? b3 : b4;
   const uint32_t cnt = cls == 1 ? c1 : cls == 2 ? c2 : cls == 3 ? c3 : c4;
@@ -1728,13 +1731,13 @@ __global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const
 #if PCN_CT_DBG_T
   if (threadIdx.x == 0 && blockIdx.x >= nseg && blockIdx.x - nseg < kDbgWaves) g_walk_t[4 * (blockIdx.x - nseg)] = wall_clock64();
 #endif
-  const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
+  const WalkPlan plan = plan_of(ctl);
   const uint32_t vb = blockIdx.x - nseg;
   // the head of a long run in flight with the plan's words (the index
   // clamped into the buffer; a block past the plan returns without using it)
   const uint64_t hcap = heads_cap(b.n);
   const uint32_t head = heads[vb < hcap ? vb : 0];
-  if (vb >= plan->blk0[kRunClasses]) return;
+  if (vb >= plan.blk0[kRunClasses]) return;
   walk_vb(b, t, wrec, heads, plan, cursor, walk_hi(b, ctl), 1, vb, head, hx);
 }
 
@@ -1854,8 +1857,8 @@ __global__ __launch_bounds__(64) void ct_tail_kernel(CtBatch b, CtTable t, const
   const uint32_t th = ctl[kCtlThFirst];
   if (!th) return;
   const uint32_t nth = ctl[kCtlTh];
-  const WalkPlan *plan = reinterpret_cast<const WalkPlan *>(ctl + kCtlPlan);
-  const uint32_t total = plan->blk0[kRunClasses];
+  const WalkPlan plan = plan_of(ctl);
+  const uint32_t total = plan.blk0[kRunClasses];
   uint32_t cur = 0xFFFFFFFFu - th;
   for (;;) {
     if (threadIdx.x == 0) hard_step(b, t, brec, cur);
@@ -2552,9 +2555,8 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
                      b.n, s.keys2, s.heads, s.ctl + kCtlClass, sentinel, hper, s.pdesc, t.carry, s.cuts,
                      s.ctl + kCtlSegN);
   CT_CHECK(hipGetLastError());
-  // the walk plan, sized on the device: no read-back, the stream stays asynchronous
-  hipLaunchKernelGGL(ct_plan_kernel, dim3(1), dim3(64), 0, st, s.ctl);
-  CT_CHECK(hipGetLastError());
+  // (the walk plan is computed on the device from ct_heads' counts, in the walk
+  // itself: no read-back, the stream stays asynchronous)
   // the cuts of long runs, then the plan's upper bound
   const unsigned wgrid = static_cast<unsigned>(seg_waves(b.n) + b.n / 64 + kRunClasses + 1);
   hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.heads, s.ctl, s.cursor,
