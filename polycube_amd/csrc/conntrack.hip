@@ -985,7 +985,14 @@ inline uint32_t heads_per(uint64_t n, int num_cus) {
 __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const uint32_t *skeys, uint32_t *heads,
                                                                uint32_t *nheads, uint32_t sentinel, uint32_t per,
                                                                const unsigned long long *desc, uint32_t *carry,
-                                                               uint32_t *cuts, uint32_t *ncuts) {
+                                                               uint32_t *cuts, uint32_t *ncuts, const uint32_t *nhard,
+                                                               uint32_t *bm, uint64_t bm_words) {
+  // the key-bucket bitmap of the long echo replies (ct_hbits_set,
+  // ct_hard_split: both done) left zeroed for the next batch
+  if (*nhard)
+    for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < bm_words;
+         w += uint64_t(gridDim.x) * blockDim.x)
+      bm[w] = 0;
   __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     const uint32_t c = ports_lookback(desc, (n + 63) / 64, carry);
@@ -2101,11 +2108,9 @@ __global__ __launch_bounds__(256) void ct_ev_evict_kernel(CtTable t, const uint3
 // unless its quoted key's bucket holds a packet of the batch (or another
 // reply's own key), which only the tail can order.  Three passes over a
 // bitmap of the batch's key buckets; each returns at once without replies.
-__global__ void ct_hbits_clear_kernel(const uint32_t *ctl, uint32_t *bm, uint64_t words) {
-  if (!ctl[kCtlHard]) return;
-  const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < words; w += stp) bm[w] = 0;
-}
+// The bitmap is zero when a batch starts: from its allocation, then cleared
+// by ct_heads after any batch that set bits (a clearing kernel of its own was
+// a launch a batch).
 
 __device__ __forceinline__ void set_bit(uint32_t *bm, uint32_t k) {
   const uint32_t m = 1u << (k & 31);
@@ -2421,6 +2426,7 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4) {
   if (s.bm_bytes < bmb) {
     if (s.bm) CT_CHECK(hipFree(s.bm));
     CT_CHECK(hipMalloc(&s.bm, bmb));
+    CT_CHECK(hipMemset(s.bm, 0, bmb));          // zero from here on: ct_heads clears what a batch set
     s.bm_bytes = bmb;
   }
   return hipSuccess;
@@ -2506,6 +2512,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   if (s.dirty) {
     CT_CHECK(hipMemsetAsync(s.ctl, 0, kCtlZero * 4, st));
     CT_CHECK(hipMemsetAsync(s.pdesc, 0, (s.cap / 64 + 2) * 8, st));
+    CT_CHECK(hipMemsetAsync(s.bm, 0, s.bm_bytes, st));
   }
   s.dirty = true;
   const uint32_t pchunk = prep_chunk(b.n, num_cus);
@@ -2516,8 +2523,6 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   // long echo replies join their own key's run unless their quoted key's
   // bucket is in the batch (each kernel returns at once without replies)
   const uint64_t bm_words = (uint64_t(1) << kbits) / 32;
-  hipLaunchKernelGGL(ct_hbits_clear_kernel, dim3(grid), dim3(blk), 0, st, s.ctl, s.bm, bm_words);
-  CT_CHECK(hipGetLastError());
   hipLaunchKernelGGL(ct_hbits_set_kernel, dim3(grid), dim3(blk), 0, st, b.n, s.ctl, s.keys, s.hard_list, s.brec, s.bm,
                      sentinel);
   CT_CHECK(hipGetLastError());
@@ -2553,7 +2558,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
                      b.n, s.keys2, s.heads, s.ctl + kCtlClass, sentinel, hper, s.pdesc, t.carry, s.cuts,
-                     s.ctl + kCtlSegN);
+                     s.ctl + kCtlSegN, s.ctl + kCtlHard, s.bm, bm_words);
   CT_CHECK(hipGetLastError());
   // (the walk plan is computed on the device from ct_heads' counts, in the walk
   // itself: no read-back, the stream stays asynchronous)
