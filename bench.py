@@ -96,16 +96,18 @@ def traffic_key(cfg, hook):
     return f"config{cfg}" + ("_tc" if hook else "")
 
 
-def load_traffic(cfg, hook, n):
+def load_traffic(cfg, hook, n, key=None):
     """(HBM bytes per launch, note) from profiles/pmc_traffic.json when it was measured on this
-    build's kernel sources and this batch size; (None, why) otherwise."""
+    build's kernel sources and this batch size; (None, why) otherwise.  key: another entry
+    than the config's own (the frame-size sweep's config3_stride<S>)."""
+    key = key or traffic_key(cfg, hook)
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(tf):
         return None, "no profiles/pmc_traffic.json"
     with open(tf) as fh:
-        pm = json.load(fh).get("configs", {}).get(traffic_key(cfg, hook))
+        pm = json.load(fh).get("configs", {}).get(key)
     if not pm:
-        return None, f"no PMC entry for {traffic_key(cfg, hook)}"
+        return None, f"no PMC entry for {key}"
     if pm.get("src_hash") != kernel_src_hash():
         return None, f"PMC entry measured on kernel sources {pm.get('src_hash')}, this build is {kernel_src_hash()}"
     if pm.get("frames") != n:
@@ -464,6 +466,62 @@ def hit_rate_sweep(ipt, chain, rs, n, dev, stream, base_ms, seed, steps=20, hits
     return out
 
 
+FRAME_SIZES = (64, 128, 256, 576, 1024, 1500)
+
+
+def frame_size_sweep(ipt, rules, frames, n, dev, stream, log, steps=20, sizes=FRAME_SIZES):
+    """north_star's "Mpkt/s on synthetic 64 B-1500 B frames": the headline chain and
+    traffic as fixed-size frames of each size (stride = size, packet_len = size;
+    synth.spread_frames lays the resident 64-byte frames out on the device, IP / UDP
+    lengths rewritten), 2^log2n frames in HBM, timed as the headline (settle, one event
+    pair around `steps` launches).  The roofline is the 64-byte header sector per frame
+    (the Parser reads bytes 0..47, Iptables_Parser_dp.c:126-143): `frac` = 64 B x n /
+    time / peak.  `lines_128b` is the count of 128-byte lines a frame's 48-byte window
+    touches (1500 B: 48 of every 128 windows cross into a second line), the L2's request
+    unit; `traffic` the PMC HBM bytes per frame where profiles/pmc_traffic.json
+    holds an entry for this build.  Each size's first 2^16 frames are checked against
+    the oracle (verdicts and rule ids)."""
+    import torch
+
+    from polycube_amd import synth
+    big = torch.empty(n * max(sizes), dtype=torch.uint8, device=dev)
+    v = torch.empty(n, dtype=torch.uint8, device=dev)
+    rid = torch.empty(n, dtype=torch.int32, device=dev)
+    s_ptr = stream.cuda_stream
+    out = {}
+    from oracle.ffi import Oracle
+    o = Oracle()
+    o.set_chain(1, rules, "DROP")
+    k = 1 << 16
+    for size in sizes:
+        buf = synth.spread_frames(frames, n, size, out=big)
+        ms = timed_calls(lambda: ipt.classify(buf, n=n, verdicts=v, rule_ids=False, stride=size, fixed_len=size,
+                                              stream=s_ptr), steps, stream)
+        ipt.classify(buf, n=n, verdicts=v, rule_ids=rid, stride=size, fixed_len=size, stream=s_ptr)
+        torch.cuda.synchronize()
+        w = min(size, 128)
+        host = buf.view(n, size)[:k, :w].cpu().numpy().reshape(-1)
+        vo, ro = o.classify(host, n=k, stride=w, fixed_len=size, nthreads=4)
+        ok = bool(np.array_equal(vo, v[:k].cpu().numpy()) and np.array_equal(ro, rid[:k].cpu().numpy()))
+        offs = np.arange(n, dtype=np.int64) * size
+        lines = float(np.mean(1 + ((offs + 47) // 128 - offs // 128)))
+        traffic, note = load_traffic(3, 0, n, key=None if size == 64 else f"config3_stride{size}")
+        out[str(size)] = {"kernel_ms": round(ms, 4), "mpkt_s": round(n / ms / 1e3, 1),
+                          "frac": round(BYTES_PER_PKT * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "frame_gb_s": round(size * n / (ms * 1e-3) / 1e9, 1),
+                          "lines_128b_per_frame": round(lines, 4),
+                          "line_gb_s": round(lines * 128 * n / (ms * 1e-3) / 1e9, 1),
+                          "path": "fixed-stride" if size % 16 == 0 else "generic gather (any byte offset)",
+                          "traffic_bytes_per_frame": None if traffic is None else round(traffic / n, 2),
+                          "traffic_from": note, "parity_sample_vs_oracle": ok}
+        log(f"[bench] frame size {size}: {out[str(size)]}")
+    del big
+    torch.cuda.empty_cache()
+    out["frames"] = n
+    out["what"] = frame_size_sweep.__doc__.split("\n", 1)[1].strip()
+    return out
+
+
 def rule_update_latency(dev, log):
     """Rule-update latency, the analogue of the reference's per-update timer
     (Chain::updateChain, Chain.cpp:436,920-928: rule compile, bcc compile + load of the
@@ -582,6 +640,7 @@ def main():
     ap.add_argument("--no-fw", action="store_true", help="skip the pcn-firewall leg")
     ap.add_argument("--no-hits", action="store_true", help="skip the hit-rate 0 / 1 sweep (config 3)")
     ap.add_argument("--no-update", action="store_true", help="skip the rule-update latency leg")
+    ap.add_argument("--no-sizes", action="store_true", help="skip the 64-1500 B frame-size sweep (config 3)")
     ap.add_argument("--jit", type=int, default=1,
                     help="chain programs: 1 compiled before the first launch (default), 0 background, -1 off")
     ap.add_argument("--settle", type=float, default=1.0,
@@ -853,6 +912,8 @@ def main():
             line["multi_gpu"] = multi
         if world == 1 and cfg == 3 and not args.no_hits:
             line["hit_rates"] = hit_rate_sweep(ipt, fw, rs, n, dev, stream, kern_ms, synth.CONFIG_SEEDS[3])
+        if world == 1 and cfg == 3 and not args.no_sizes:
+            line["frame_sizes"] = frame_size_sweep(ipt, rules, frames, n, dev, stream, log)
         if cfg == 5:
             line["roofline"]["gather_ceiling"] = gather_ceiling(frames, offsets, lens, n, s_ptr, kern_ms)
         if world == 1 and not args.no_cpu:

@@ -8,8 +8,8 @@
 //   stale ports (Q4)  Iptables_Parser_dp.c:122-143 (ports written for TCP/UDP only)
 // Everything here is integer work on HBM-resident state: the parse/prep
 // kernels stream the 72-byte header window once, the walk is latency-bound
-// (one dependent table access per packet of a run), the sort is hipCUB's
-// onesweep radix sort on a key-bucket id.
+// (one dependent table access per packet of a run), the sort is the
+// hand-written LSD radix sort of radix.hip on a key-bucket id.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <cstring>
@@ -19,16 +19,6 @@
 
 #include "conntrack.hpp"
 #include "radix.hpp"
-// Measurement builds only (make ct_variant DEFS=-DPCN_CT_ROCPRIM=1): the sort
-// through rocPRIM's onesweep radix sort, as in round 4, for an A/B against the
-// hand-written one (radix.hip) the product runs.
-#ifndef PCN_CT_ROCPRIM
-#define PCN_CT_ROCPRIM 0
-#endif
-#if PCN_CT_ROCPRIM
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#endif
 #include "pcn_ipt.h"
 
 #ifndef PCN_CT_FAST
@@ -1417,13 +1407,17 @@ constexpr unsigned long long kTtlUnset = ~0ull;
 __host__ __device__ constexpr uint64_t seg_count(uint64_t n) { return kSeg ? n / (kSeg ? kSeg : 1) + 1 : 0; }
 // Waves for the active cuts (walk_seg, ct_seg_fix), each taking every
 // seg_waves-th: a wave per cut, active or not (32 K at 2^24, nearly all with
-// nothing to do), cost the walk 12 us a batch.
-#ifndef PCN_CT_SEG_WAVES
-#define PCN_CT_SEG_WAVES 64
+// nothing to do), cost the walk 12 us a batch.  The count is fixed before
+// ct_heads has counted the active cuts (no read-back), so it is sized for the
+// worst case the device can run at once, PCN_CT_SEG_WAVES_PER_CU per CU (a
+// batch of one long connection has a cut every kSeg records: 32 K at 2^24),
+// and waves without a cut return at once.
+#ifndef PCN_CT_SEG_WAVES_PER_CU
+#define PCN_CT_SEG_WAVES_PER_CU 4
 #endif
-constexpr uint64_t kSegWaves = PCN_CT_SEG_WAVES;
-__host__ __device__ constexpr uint32_t seg_waves(uint64_t n) {
-  return static_cast<uint32_t>(seg_count(n) < kSegWaves ? seg_count(n) : kSegWaves);
+__host__ __device__ constexpr uint32_t seg_waves(uint64_t n, int num_cus) {
+  return static_cast<uint32_t>(seg_count(n) < uint64_t(num_cus) * PCN_CT_SEG_WAVES_PER_CU
+                                   ? seg_count(n) : uint64_t(num_cus) * PCN_CT_SEG_WAVES_PER_CU);
 }
 
 struct alignas(16) SegRec {       // 64 bytes, one per cut j (sorted position j * kSeg)
@@ -1710,13 +1704,12 @@ __device__ void walk_vb(const CtBatch &b, const CtTable &t, const RecSrc &wrec,
 // blocks past the plan return at once: a workgroup that returns costs the
 // dispatcher next to nothing, where a persistent grid taking blocks from one
 // counter serialised ~10^5 atomics on one address (7.1 vs 2.9 ms a batch).
-// With segments, the first seg_waves(n) workgroups walk the active cuts that
-// ct_heads listed (walk_seg), each taking every seg_waves-th of them.
+// With segments, the first nseg = seg_waves(n) workgroups walk the active cuts
+// that ct_heads listed (walk_seg), each taking every nseg-th of them.
 __global__ __launch_bounds__(64) void ct_walk_kernel(CtBatch b, CtTable t, const RecSrc wrec,
                                                      const uint32_t *heads, const uint32_t *ctl, uint32_t *cursor,
                                                      const uint32_t *skeys, uint32_t sentinel, SegRec *seg,
-                                                     HeadExit *hx, const uint32_t *cuts) {
-  const uint32_t nseg = seg_waves(b.n);
+                                                     HeadExit *hx, const uint32_t *cuts, uint32_t nseg) {
   if (blockIdx.x < nseg) {
     const uint32_t na = ctl[kCtlSegN];
     for (uint32_t i = blockIdx.x; i < na; i += nseg) {
@@ -2012,7 +2005,13 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
   }
   asm volatile("" ::"v"(dep));
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&ctl[kCtlEvDone], 1u) == gridDim.x - 1;
+  // the arrival orders this workgroup's histogram merges before it and the last
+  // arriver's reads after it (acquire-release at agent scope: one ordering
+  // operation per workgroup, where a __threadfence in every wave cost 9-23 us a
+  // pass; returning device atomics completing at L2 alone is a gfx950 property,
+  // not a guarantee of the memory model)
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&ctl[kCtlEvDone], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
   if (p == 0) {                                        // the last workgroup: evict at all, and from which bit
@@ -2317,10 +2316,6 @@ struct CtScratch {
   ct_u32x4 *ox = nullptr;     // the four stage-A outcomes per packet (batches with four labels)
   uint64_t ox_cap = 0;
   RadixScratch rx;            // the (key bucket, index) sort (radix.hip)
-#if PCN_CT_ROCPRIM
-  void *rp_temp = nullptr;
-  size_t rp_bytes = 0;
-#endif
   // ct_advance_carry: 1 + the batch's last port-writing frame
   unsigned long long *zfound = nullptr;
 };
@@ -2489,7 +2484,7 @@ int ct_advance_carry(const CtBatch &b, CtScratch &s, uint32_t *carry, int num_cu
 
 int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream) {
   if (b.n == 0) return hipSuccess;
-  if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);   // hipCUB item counts are int
+  if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);   // 32-bit item indices (radix.hip)
   hipStream_t st = static_cast<hipStream_t>(stream);
   // key buckets: 2^kbits >= n (a 2^24 batch sorts 24-bit keys in three 8-bit
   // passes; 2^kbits >= 2n gave 25 bits and a 9-bit first pass, +20 us, for half
@@ -2531,28 +2526,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   CT_CHECK(hipGetLastError());
   // (ct_heads advances the carry from ct_prep's published groups)
   // the sort (radix.hip; s.keys is its ping-pong buffer from here on)
-#if PCN_CT_ROCPRIM
-  {
-    using Cfg = rocprim::radix_sort_config<
-        rocprim::default_config, rocprim::default_config,
-        rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 9,
-                                            rocprim::block_radix_rank_algorithm::match>>;
-    size_t need = 0;
-    auto sort = [&](void *tmp, size_t &bytes) {
-      return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, s.keys, s.keys2, rocprim::counting_iterator<uint32_t>(0u),
-                                            s.idx2, static_cast<unsigned int>(b.n), 0u, kbits, st);
-    };
-    CT_CHECK(sort(nullptr, need));
-    if (s.rp_bytes < need) {
-      if (s.rp_temp) CT_CHECK(hipFree(s.rp_temp));
-      CT_CHECK(hipMalloc(&s.rp_temp, need));
-      s.rp_bytes = need;
-    }
-    CT_CHECK(sort(s.rp_temp, need));
-  }
-#else
   CT_CHECK(radix_sort_pairs(s.rx, s.keys, s.keys2, s.idx2, b.n, kbits, num_cus, st));
-#endif
   const RecSrc src{s.brec, s.idx2, s.keys2, s.ox, b.nlab == 4 ? 1u : 0u};
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;
@@ -2563,12 +2537,13 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   // (the walk plan is computed on the device from ct_heads' counts, in the walk
   // itself: no read-back, the stream stays asynchronous)
   // the cuts of long runs, then the plan's upper bound
-  const unsigned wgrid = static_cast<unsigned>(seg_waves(b.n) + b.n / 64 + kRunClasses + 1);
+  const uint32_t nseg = seg_waves(b.n, num_cus);
+  const unsigned wgrid = static_cast<unsigned>(nseg + b.n / 64 + kRunClasses + 1);
   hipLaunchKernelGGL(ct_walk_kernel, dim3(wgrid), dim3(64), 0, st, b, t, src, s.heads, s.ctl, s.cursor,
-                     s.keys2, sentinel, s.seg, s.hx, s.cuts);
+                     s.keys2, sentinel, s.seg, s.hx, s.cuts, nseg);
   CT_CHECK(hipGetLastError());
   if (kSeg) {
-    hipLaunchKernelGGL(ct_seg_fix_kernel, dim3(seg_waves(b.n)), dim3(64), 0, st, b, t, src, s.keys2, s.seg, s.hx,
+    hipLaunchKernelGGL(ct_seg_fix_kernel, dim3(nseg), dim3(64), 0, st, b, t, src, s.keys2, s.seg, s.hx,
                        s.cursor, s.ctl, s.cuts);
     CT_CHECK(hipGetLastError());
   }

@@ -376,10 +376,12 @@ int fold_all_copies(void *c, void *stream) {
 
 // Bookkeeping of the launches into the packed copies, in two halves around a
 // launch on stream s.  Before it (register_pack_stream): s joins the known
-// streams, and when it is a second stream every earlier stream that has no
-// event yet gets one now, at the end of what it has queued -- so a fold inside
-// this very launch (launch_classify, cb->fold) already waits for their work,
-// and no stream handle is ever used after the launch that introduced it.
+// streams, and when that makes two or more, every other known stream records
+// its event now, at the end of what it has queued (an event recorded earlier
+// may predate batches queued while it was the only stream: once the other
+// streams are released, note_pack_stream records nothing) -- so a fold inside
+// this very launch (launch_classify, cb->fold) waits for all their work, and no
+// stream handle is ever used after the launch that introduced it.
 // After it (note_pack_stream): once two streams are known, the launch leaves
 // an event behind on s.  With one stream neither records anything.
 void register_pack_stream(pcn_ipt *ctx, hipStream_t s) {
@@ -388,8 +390,8 @@ void register_pack_stream(pcn_ipt *ctx, hipStream_t s) {
   v.emplace_back(s, nullptr);
   if (v.size() < 2) return;
   for (auto &se : v) {
-    if (se.first == s || se.second) continue;
-    hip_check(hipEventCreateWithFlags(&se.second, hipEventDisableTiming), "hipEventCreate");
+    if (se.first == s) continue;
+    if (!se.second) hip_check(hipEventCreateWithFlags(&se.second, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventRecord(se.second, se.first), "hipEventRecord(pack)");
   }
 }
@@ -1644,6 +1646,12 @@ int pcn_ipt_release_stream(pcn_ipt *ctx, void *stream) {
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     if (it->second) hip_check(hipEventDestroy(it->second), "hipEventDestroy");
     v.erase(it);
+    // a lone stream records no events (note_pack_stream): drop the one it
+    // holds, so no later fold trusts an event older than its last batches
+    if (v.size() == 1 && v[0].second) {
+      hip_check(hipEventDestroy(v[0].second), "hipEventDestroy");
+      v[0].second = nullptr;
+    }
     return 0;
   });
 }

@@ -217,6 +217,37 @@ def config_frames(cfg, n, rs=None, seed=None):
     return build_frames(*cols, frame_len=64)
 
 
+def spread_frames(frames64, n, stride, out=None, fix_lengths=True):
+    """Fixed-size frames of `stride` bytes (>= 64) on the device from n 64-byte
+    frames (a uint8 torch tensor of n*64 bytes, on the device): each frame's first
+    64 bytes copied to i*stride, the rest zero (payload).  fix_lengths rewrites the
+    IPv4 total length (and, for UDP, the UDP length) of untagged IPv4 frames for
+    a frame of `stride` bytes.  `out` (>= n*stride bytes) is reused when given.
+    The frame-size sweep's layout (bench.py frame_sizes, tests): the classify
+    kernel reads only a frame's first 48-52 bytes (Iptables_Parser_dp.c:126-143),
+    so a larger frame changes the access pattern, not what is read."""
+    import torch
+    if stride < 64:
+        raise ValueError("stride must be >= 64")
+    buf = (torch.empty(n * stride, dtype=torch.uint8, device=frames64.device) if out is None
+           else out[: n * stride])
+    v = buf.view(n, stride)
+    if stride > 64:
+        v[:, 64:].zero_()
+    src = frames64[: n * 64].view(n, 64)
+    v[:, :64] = src
+    if fix_lengths:
+        ipv4 = (src[:, 12] == 8) & (src[:, 13] == 0)
+        tot, ul = stride - 14, stride - 34
+
+        def put16(col, val, mask):
+            v[:, col] = torch.where(mask, torch.full_like(src[:, col], (val >> 8) & 255), src[:, col])
+            v[:, col + 1] = torch.where(mask, torch.full_like(src[:, col], val & 255), src[:, col + 1])
+        put16(16, tot, ipv4)
+        put16(38, ul, ipv4 & (src[:, 23] == UDP))
+    return buf
+
+
 def imix_frames(rs, n, seed, *, vlan_frac=0.3, ipv6_frac=0.3, align=1):
     """Config 5: IMIX 7:4:1 of 64/576/1500-byte frames packed back to back, with
     802.1Q-tagged and IPv6 frames mixed in.  align=64 starts every frame at a

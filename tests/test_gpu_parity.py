@@ -223,6 +223,42 @@ def test_full_size_headline_config3(dev):
     assert_jit_used(ipt, 1)
 
 
+@pytest.mark.parametrize("stride,log2n", [(1500, 24), (1536, 22), (1024, 22), (576, 22), (256, 22), (128, 22),
+                                          (1500, 16), (1501, 16)],
+                         ids=["1500-full", "1536", "1024", "576", "256", "128", "1500-small", "1501-odd"])
+def test_frame_size_sweep_parity(dev, stride, log2n):
+    """The north_star frame sizes (bench.py frame_sizes): config 3's rules over
+    fixed-size frames of `stride` bytes (packet_len = stride), 1500 B at the full
+    2^24 batch (25 GB of frames in HBM).  16-byte multiples run the fixed-stride
+    path, 1500 / 1501 the generic gather (a window at any byte offset).  A quarter
+    of the batch is edge-case frames (fuzz_frames: odd ethertypes, VLAN / IPv6,
+    ICMP types, GRE, odd protocols), the rest the bench's TCP/UDP mix.  The oracle
+    reads each frame's first 128 bytes (the parse reads at most 76: an ICMP
+    error's quoted header) with packet_len = stride.  Bit-exact verdicts, rule ids
+    and counters (bytes = pkts * stride), through the chain program."""
+    rs = synth.config_rules(3)
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
+    n = 1 << log2n
+    hdr = synth.config_frames(3, n, rs, seed=stride)
+    rng = np.random.default_rng(stride)
+    m = n // 4
+    fz, _ = synth.fuzz_frames(m, stride, rs, stride=64)
+    hdr[rng.choice(n, m, replace=False)] = fz.reshape(m, 64)
+    buf = synth.spread_frames(torch.from_numpy(hdr.reshape(-1)).to(dev), n, stride)
+    del hdr
+    w = min(stride, 128)
+    host = buf.view(n, stride)[:, :w].cpu().numpy().reshape(-1)
+    for _ in range(2):                 # twice: the counters add up over launches
+        v_o, r_o = o.classify(host, n=n, stride=w, fixed_len=stride, nthreads=NTHREADS)
+        v_g, r_g = ipt.classify(buf, n=n, stride=stride, fixed_len=stride)
+        torch.cuda.synchronize()
+        assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
+    assert_counters(o, ipt, chains=(1,), n=len(rs.rules()))
+    assert_jit_used(ipt, 1)
+    del buf
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("hook", [0, 1], ids=["xdp", "tc"])
 def test_full_size_config5(dev, hook):
     """Config 5 at its bench size (2^22 IMIX frames packed back to back, 10k
@@ -438,6 +474,46 @@ def test_stream_of_a_closed_ring_is_never_touched(dev, monkeypatch):
         torch.cuda.synchronize()
         assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
     ipt.release_stream(side.cuda_stream)
+    assert_counters(o, ipt, chains=(1,), n=len(rs.rules()))
+
+
+def test_fold_waits_for_a_stream_that_was_alone(dev, monkeypatch):
+    """A user stream U, then a two-stream ring (U + A + B known: events recorded),
+    the ring closed (A, B released: U alone records nothing), more batches on U,
+    then a new stream whose launches fold before every launch (test limit): the fold
+    must wait for U's later batches, not for U's event from before the ring closed.
+    Counters equal the oracle's."""
+    monkeypatch.setenv("PCN_IPT_DEBUG_PACK_MAX_PKTS", str(1 << 13))
+    rs = synth.config_rules(2)
+    o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
+    n = 1 << 16
+    user = torch.cuda.Stream()
+    batches = [synth.config_frames(2, n, rs, seed=20 + k).reshape(-1) for k in range(3)]
+    dbatches = [torch.from_numpy(f).to(dev) for f in batches]
+    torch.cuda.synchronize()
+    ipt.classify(dbatches[0], n=n, stream=user.cuda_stream, rule_ids=False)
+    o.classify(batches[0], n=n, nthreads=NTHREADS)
+    ring = ipt.ring(slots=2, slot_frames=1 << 14, slot_bytes=(1 << 14) * 64, streams=2)
+    for k in range(4):
+        slot, frames, _, _, _ = ring.acquire()
+        f = synth.config_frames(2, 1 << 14, rs, seed=40 + k).reshape(-1)
+        frames[:f.size] = f
+        ring.submit(slot, 1 << 14)
+        o.classify(f, n=1 << 14, nthreads=NTHREADS)
+        done, _, _ = ring.complete()
+        ring.release(done)
+    ring.close()
+    for k in (1, 2):       # U alone again: several batches queued back to back
+        for _ in range(4):
+            ipt.classify(dbatches[k], n=n, stream=user.cuda_stream, rule_ids=False)
+            o.classify(batches[k], n=n, nthreads=NTHREADS)
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        ipt.classify(dbatches[0], n=n, stream=side.cuda_stream, rule_ids=False)
+        o.classify(batches[0], n=n, nthreads=NTHREADS)
+    torch.cuda.synchronize()
+    ipt.release_stream(side.cuda_stream)
+    ipt.release_stream(user.cuda_stream)
     assert_counters(o, ipt, chains=(1,), n=len(rs.rules()))
 
 

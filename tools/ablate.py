@@ -42,6 +42,10 @@ def child(lib, hit, log2n, iters, cfg, jit):
         cols = synth.make_headers(rs, n, synth.CONFIG_SEEDS[3], hit_frac=hit,
                                   protos=(6, 17) if cfg == 3 else (17,))
         frames = torch.from_numpy(synth.build_frames(*cols).reshape(-1)).cuda()
+        stride = int(os.environ.get("FRAME_STRIDE", "64"))   # the frame-size sweep (bench.py frame_sizes)
+        if stride != 64:
+            frames = synth.spread_frames(frames, n, stride)
+            kw = dict(stride=stride, fixed_len=stride)
     v = torch.empty(n, dtype=torch.uint8, device="cuda")
     # clock settle (as bench.py): untimed launches for SETTLE seconds (default 0.5)
     import time
@@ -62,7 +66,7 @@ def child(lib, hit, log2n, iters, cfg, jit):
     info = fw.info()
     print(json.dumps({"lib": os.path.basename(lib or "product"), "jit": ipt.jit_info()["launches_jit"] > 0,
                       "cfg": cfg, "log2n": log2n, "image_bytes": info["table_bytes"], "slots_info": info,
-                      "defs": os.environ.get("PCN_IPT_JIT_DEFS", ""),
+                      "defs": os.environ.get("PCN_IPT_JIT_DEFS", ""), "stride": kw.get("stride", 64),
                       "knobs": {k[14:]: v for k, v in os.environ.items() if k.startswith("PCN_IPT_DEBUG_")},
                       "hit": hit, "ms": ms,
                       "gpkt_s": n / ms / 1e6, "frac": 64 * n / (ms * 1e-3) / 8e12}))

@@ -114,3 +114,23 @@ pmcct() {
   done
   rm -rf "$O/$name"
 }
+
+# Counter calibration of one tools/gather_calib pattern: its own timing line, then a
+# FETCH_SIZE pass and a TCC_EA0_RDREQ split pass, each summarised over the pattern's
+# kernel (calib_*): calib <name> <pattern> <log2n> <kernel>  -> $O/calib_<name>{.log,_fetch.json,_rdreq.json}
+calib() {
+  local name=$1 pat=$2 log2n=$3 kern=$4
+  run calib_$name 120 "$R/tools/gather_calib" "$pat" "$log2n" 10
+  local k=0
+  for grp in "FETCH_SIZE" "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum"; do
+    k=$((k + 1))
+    mkdir -p "$O/calib_$name/p$k"
+    ( cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv \
+        -d "$O/calib_$name/p$k" -o run -- "$R/tools/gather_calib" "$pat" "$log2n" 4 > "$O/calib_$name/p$k.log" 2>&1 )
+    local rc=$?
+    echo "== calib $name pass $k rc=$rc"
+    case $rc in 0) ;; *) tail -5 "$O/calib_$name/p$k.log"; exit $rc ;; esac
+  done
+  python3 "$R/tools/pmc_summary.py" "$O/calib_$name" --kernel "$kern" --frames $((1 << log2n)) \
+    --out "$O/calib_${name}.json" > /dev/null && rm -rf "$O/calib_$name"
+}
