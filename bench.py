@@ -257,9 +257,10 @@ def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3, stride=64, fra
             frames[r * stride:(r + q) * stride] = frames_host[lo * stride:(lo + q) * stride]
         ring.release(slot)
     nsub = max(1, n // chunk)
-    best = 0.0
+    best, best_st, best_el = 0.0, None, 0.0
     for _ in range(reps):
         submitted = completed = 0
+        ring.stats(reset=True)
         t0 = time.perf_counter()
         while completed < nsub:
             while submitted < nsub:
@@ -274,9 +275,24 @@ def e2e_rate(ipt, frames_host, n, chunk=1 << 21, slots=4, reps=3, stride=64, fra
             slot = ring.complete(wait=True)[0]
             ring.release(slot)
             completed += 1
-        best = max(best, nsub * chunk / (time.perf_counter() - t0) / 1e6)
+        el = time.perf_counter() - t0
+        rate = nsub * chunk / el / 1e6
+        if rate > best:
+            best, best_st, best_el = rate, ring.stats(), el
     ring.close()
-    return best
+    st = best_st
+    sub = max(1, st["submits"])
+    info = {"mpkt_s": round(best, 2),
+            "h2d_gb_s": round(st["h2d_bytes"] / best_el / 1e9, 2),
+            "d2h_gb_s": round(st["d2h_bytes"] / best_el / 1e9, 2),
+            "submit_ms_per_chunk": round(st["submit_ns"] / sub / 1e6, 4),
+            "submit_share_of_wall": round(st["submit_ns"] / 1e9 / best_el, 3)}
+    if zero_copy:
+        info["pcie_read_gb_s"] = round(st["zc_bytes"] / best_el / 1e9, 2)
+    if host_pack:
+        info["pack_ms_per_chunk"] = round(st["pack_ns"] / sub / 1e6, 4)
+        info["pack_share_of_wall"] = round(st["pack_ns"] / 1e9 / best_el, 3)
+    return info
 
 
 def e2e_legs(ipt, frames_host, n, rs, log):
@@ -288,20 +304,35 @@ def e2e_legs(ipt, frames_host, n, rs, log):
     threads = host_cores()[0]
     legs = (("whole_frames", 0, False, False), ("header_only_48", 48, False, False), ("zero_copy", 0, True, False),
             ("header_pack_48", 48, False, True))
+    detail = {}
     for name, hb, zc, hp in legs:
-        out[name] = round(e2e_rate(ipt, frames_host, n, hdr_bytes=hb, zero_copy=zc, host_pack=hp,
-                                   pack_threads=min(threads, 16)), 2)
-        log(f"[bench] e2e 64B {name}: {out[name]} Mpkt/s")
+        detail[name] = e2e_rate(ipt, frames_host, n, hdr_bytes=hb, zero_copy=zc, host_pack=hp,
+                                pack_threads=min(threads, 16))
+        out[name] = detail[name]["mpkt_s"]
+        log(f"[bench] e2e 64B {name}: {detail[name]}")
     out["pack_threads"] = min(threads, 16)
+    out["legs"] = detail
+    out["pcie_h2d_ceiling_gb_s"] = pcie_h2d_ceiling()
     m = 1 << 16
     cols = synth.make_headers(rs, m, synth.CONFIG_SEEDS[3] + 1)
     big = synth.build_frames(*cols, frame_len=1536).reshape(-1)
     out["frames_1500"] = {}
     for name, hb, zc in (("whole_frames", 0, False), ("header_only_64", 64, False), ("zero_copy", 0, True)):
-        out["frames_1500"][name] = round(e2e_rate(ipt, big, 1 << 20, chunk=m, stride=1536, frame_len=1500,
-                                                  hdr_bytes=hb, zero_copy=zc), 2)
-        log(f"[bench] e2e 1500B {name}: {out['frames_1500'][name]} Mpkt/s")
+        d = e2e_rate(ipt, big, 1 << 20, chunk=m, stride=1536, frame_len=1500, hdr_bytes=hb, zero_copy=zc)
+        out["frames_1500"][name] = d["mpkt_s"]
+        out["frames_1500"].setdefault("legs", {})[name] = d
+        log(f"[bench] e2e 1500B {name}: {d}")
     out["kept"] = max((k for k, _, _, _ in legs), key=lambda k: out[k])
+    # what bounds the kept leg: its PCIe bytes against the copy ceiling, its host submit
+    # (pack) time against the wall time
+    kd = detail[out["kept"]]
+    pcie = kd.get("h2d_gb_s", 0) + kd.get("pcie_read_gb_s", 0)
+    host = kd.get("pack_share_of_wall", kd.get("submit_share_of_wall", 0))
+    out["bound"] = (f"PCIe: {pcie} GB/s in against a {out['pcie_h2d_ceiling_gb_s']} GB/s pinned-copy ceiling"
+                    if pcie >= 0.8 * out["pcie_h2d_ceiling_gb_s"] else
+                    f"host: the submits' {'pack' if 'pack_share_of_wall' in kd else 'host'} time is "
+                    f"{host:.0%} of the wall time" if host >= 0.8 else
+                    f"neither saturated: PCIe {pcie} GB/s of {out['pcie_h2d_ceiling_gb_s']}, host {host:.0%}")
     out["value"] = out[out["kept"]]
     out["unit"] = "Mpkt/s"
     out["what"] = ("host ingest ring (pcn_ipt_ring): pinned slots -> H2D -> classify -> D2H verdicts, 4 slots x 2^21 "
@@ -312,6 +343,26 @@ def e2e_legs(ipt, frames_host, n, rs, log):
                    "one contiguous 48-byte-stride copy; the pack is inside the timed loop); frames_1500: 4 slots x "
                    "2^16 1500-byte frames at a 1536-byte stride, the first three")
     return out
+
+
+def pcie_h2d_ceiling(mb=256, streams=4, reps=5):
+    """Pinned host -> device copy rate (GB/s) with `streams` copies of mb MB in flight:
+    the PCIe ceiling the e2e legs are set against (the DMA engines of one GPU)."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = [torch.empty(mb << 20, dtype=torch.uint8).pin_memory() for _ in range(streams)]
+    dst = [torch.empty(mb << 20, dtype=torch.uint8, device=dev) for _ in range(streams)]
+    ss = [torch.cuda.Stream(dev) for _ in range(streams)]
+    best = 0.0
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s, a, b in zip(ss, src, dst):
+            with torch.cuda.stream(s):
+                b.copy_(a, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, streams * (mb << 20) / (time.perf_counter() - t0) / 1e9)
+    return round(best, 2)
 
 
 def gather_ceiling(frames, offsets, lens, n, s_ptr, kern_ms):

@@ -211,6 +211,8 @@ typedef struct {
   uint64_t launches_jit;      /* ... that ran a chain program                  */
   uint32_t programs_ready;    /* chain programs compiled                       */
   uint32_t programs_failed;   /* compiles or module loads that failed          */
+  uint64_t launches_split;    /* chain-program launches split into a gather kernel and a rule kernel
+                                 (offsets / lens batches of a chain whose image exceeds LDS) */
 } pcn_ipt_jit_info;
 int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out);
 /* Test hook: the number of guard words past the classify kernel's stale-port
@@ -243,6 +245,12 @@ int pcn_ipt_debug_sort_pairs(pcn_ipt *ctx, const uint32_t *keys, uint64_t n, uin
  * device (works with device = -1).  On failure the compiler log is in
  * pcn_ipt_last_error(). */
 int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain);
+/* The same for the launch shape of `shape` (fixed stride or offsets / lens,
+ * side inputs, hook, direction, batch size; its buffers are never read): e.g.
+ * an IMIX batch, whose chain program differs from the usual one (and, for a
+ * chain whose image exceeds LDS, is a split program: a gather kernel and a
+ * rule kernel).  Blocking; 0 or a negative errno. */
+int pcn_ipt_chain_program_compile_for(pcn_ipt *ctx, int chain, const pcn_ipt_batch *shape);
 /* Resources of the chain program a chain's launches last asked for (or, before
  * any launch, of its usual launch shape, as pcn_ipt_chain_program_compile plans
  * it), read from the code object's metadata: what a measurement of that
@@ -333,6 +341,20 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *ring, uint32_t slot, const pcn_ipt_ring_ba
 int pcn_ipt_ring_complete(pcn_ipt_ring *ring, int wait, uint32_t *slot, uint64_t *n, const uint8_t **verdicts,
                           const int32_t **rule_ids);
 int pcn_ipt_ring_release(pcn_ipt_ring *ring, uint32_t slot);
+/* What the ring's submits moved and what their host side cost, since creation
+ * or the last reset: the bound of an end-to-end rate (host pack threads or the
+ * PCIe copy) is read from these.  No reference counterpart (the reference's
+ * packets never leave the kernel's RX path); measurement only. */
+typedef struct {
+  uint64_t submits;       /* batches submitted */
+  uint64_t frames;        /* frames submitted */
+  uint64_t h2d_bytes;     /* bytes queued host -> device (frames or header rows, offsets / lens / in_port) */
+  uint64_t d2h_bytes;     /* bytes queued device -> host (verdicts, rule ids) */
+  uint64_t zc_bytes;      /* zero copy: header bytes the kernel reads over PCIe (the 64-byte sector of each frame) */
+  uint64_t pack_ns;       /* PCN_IPT_RING_HOST_PACK: wall time of the packs (all pack threads together) */
+  uint64_t submit_ns;     /* wall time inside pcn_ipt_ring_submit, pack included */
+} pcn_ipt_ring_stats;
+int pcn_ipt_ring_get_stats(pcn_ipt_ring *ring, pcn_ipt_ring_stats *out, int reset);
 
 /* ---- counters ---------------------------------------------------------- */
 /* Per-rule pkts/bytes (ActionLookup pkts_/bytes_<CHAIN>) and default counters

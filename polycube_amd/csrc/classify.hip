@@ -838,8 +838,18 @@ __device__ __forceinline__ DevChain chain_desc(const LaunchArgs &a) {
   }
 }
 
-template <bool FIXED, bool LDS, int CH, int NS, bool JIT>
+// SPLIT (chain programs of split launches, pcn_ipt.cpp): 0 = the one fused
+// kernel; 1 = the gather kernel: every step up to the rule stage (parse, TC
+// untag, chain select, ICMP checks, labels), with no chain image in LDS and
+// two workgroups per CU, writing the fields the rule stage reads for each
+// frame that reaches it (LaunchArgs::split_rec) and finishing the others;
+// 2 = the rule kernel: those fields read back coalesced, the image in LDS, the
+// rule stage, verdicts and counters of those frames.  The gather's HBM latency
+// is then hidden by occupancy, and the rule stage's LDS / L2 chains by a
+// kernel that waits on nothing else.
+template <bool FIXED, bool LDS, int CH, int NS, bool JIT, int SPLIT = 0>
 __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
+  static_assert(SPLIT == 0 || !FIXED, "split launches are offsets / lens (IMIX) batches");
   const DevChain run_ch = chain_desc<JIT, CH>(a);   // the chain that runs rules (CH < 3)
   const unsigned long long clk0 = a.dbg_clk ? __builtin_amdgcn_s_memrealtime() : 0ull;
   unsigned long long clk1 = 0, clk2 = 0;
@@ -951,7 +961,11 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   constexpr int PF = FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
   Stage st[PF];
   auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
-    if (FIXED && PCN_HDR_LDS) {
+    if constexpr (SPLIT == 2) {                  // the gather kernel's fields for frame j, coalesced
+      const uint64_t jf = j < a.n ? j : last;
+      x.g[0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.split_rec) + jf);
+      x.L = has_lens ? a.lens[jf] : a.fixed_len;
+    } else if (FIXED && PCN_HDR_LDS) {
       uint64_t group = j - lane;                 // wave-uniform
       group = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(group >> 32))) << 32) |
               __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(group));
@@ -1028,9 +1042,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     }
     const uint64_t jc = j < a.n ? j : last;
     x.port = kLoadPort ? a.in_port[jc & a.in_port_mask] : 0u;
-    x.ct = kLoadCt ? a.ct_status[jc & a.ct_mask] : 0u;
+    x.ct = kLoadCt && SPLIT != 2 ? a.ct_status[jc & a.ct_mask] : 0u;   // (the rule kernel: in the record)
   };
-  if (!FIXED && PCN_GEN_QUAD && PCN_OFF_AHEAD && has_off) {
+  if (SPLIT != 2 && !FIXED && PCN_GEN_QUAD && PCN_OFF_AHEAD && has_off) {
 #pragma unroll
     for (int d = 0; d < PF; ++d) {
       const uint64_t j = first + d * step;
@@ -1054,11 +1068,13 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // PF): the loop is unrolled PF times so no stage is
   // ever copied (a register move of an in-flight load waits for it).
   auto process = [&](const uint64_t i, Stage &cur) {
-    const bool valid = i < a.n;
+    bool valid = i < a.n;
     // Pin every prefetched dword (used or not) until here, so no register the
     // load writes is recycled mid-iteration (a WAW hazard costs a vmcnt wait).
     Hdr h;
-    if (FIXED && !PCN_HDR_LDS) {
+    if constexpr (SPLIT == 2) {
+      asm volatile("" : "+v"(cur.g[0]));
+    } else if (FIXED && !PCN_HDR_LDS) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
 #pragma unroll
@@ -1145,7 +1161,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
     uint32_t L = FIXED ? a.fixed_len : cur.L;
     const uint32_t cur_port = cur.port, cur_ct = cur.ct;
-    constexpr bool kLate = PCN_PF_LATE && !FIXED && JIT && kJitChain.lay.part_dense;
+    constexpr bool kLate = SPLIT != 1 && PCN_PF_LATE && !FIXED && JIT && kJitChain.lay.part_dense;
     if (!kLate) prefetch(cur, i + PF * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
@@ -1153,6 +1169,24 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     int32_t chain = -1;     // chain whose rules must run (-1: decided already)
     Parsed p{};
     uint32_t port = 0;
+    uint32_t untag = 0;     // SPLIT 1: kSplitUntag once the outer VLAN tag is stripped
+    if constexpr (SPLIT == 2) {
+      // the gather kernel's fields (SPLIT 1 below): only frames that reach the
+      // rule stage are this kernel's
+      const u32x4 r = cur.g[0];
+      const uint32_t meta = r.w >> 24;
+      valid = valid && (meta & kSplitNeed);
+      p.saddr = r.x;
+      p.daddr = r.y;
+      p.sport = r.z & 0xffffu;
+      p.dport = r.z >> 16;
+      p.proto = r.w & 0xffu;
+      p.flags = (r.w >> 8) & 0xffu;
+      p.ct = (r.w >> 16) & 0xffu;
+      port = a.has_in_port ? cur_port : const_port;
+      if (meta & kSplitUntag) L -= 4;
+      chain = valid ? static_cast<int32_t>(meta & 3u) : -1;
+    } else {
     // Wave fast path: when every lane holds a plain IPv4 TCP/UDP frame long
     // enough for its L4 header (fixed stride: XDP, one length) and the launch
     // has a chain every such frame selects, the Parser / ChainSelector /
@@ -1193,6 +1227,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
 #pragma unroll
           for (int k = 3; k < 12; ++k) h.w[k] = h.w[k + 1];
           L -= 4;
+          untag = kSplitUntag;
         }
       }
       // ---- Parser_dp.c:94-153 ----
@@ -1324,12 +1359,30 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         if (done) chain = -1;
       }
     }
+    }  // SPLIT != 2
     // ---- rule chains ----
     // CH < 3: only chain CH can reach the rule stage in this launch (the host
     // picks the variant), so its descriptor is a constant-index kernarg load
     // that stays in SGPRs.  CH == 3: ingress with both INPUT and FORWARD rules.
     if (PCN_ABLATE == 1) { verdict = chain >= 0 ? 1u : verdict; chain = -1; }
-    if (CH < 3) {
+    bool wr = valid;        // this kernel writes the frame's verdict (and counts it)
+    if constexpr (SPLIT == 1) {
+      // the rule stage runs in the rule kernel: its fields, for every frame
+      // (kSplitNeed marks those it runs), one coalesced 16-byte store
+      if (valid) {
+        const uint32_t meta = (chain >= 0 ? kSplitNeed | static_cast<uint32_t>(chain) : 0u) | untag;
+        u32x4 r;
+        r.x = p.saddr;
+        r.y = p.daddr;
+        r.z = p.sport | (p.dport << 16);
+        r.w = (p.proto & 0xffu) | (p.flags & 0xffu) << 8 | (p.ct & 0xffu) << 16 | meta << 24;
+        __builtin_nontemporal_store(r, reinterpret_cast<u32x4 *>(a.split_rec) + i);
+      }
+      if (chain >= 0) {
+        wr = false;
+        chain = -1;
+      }
+    } else if (CH < 3) {
       run_chain<LDS, NS, kDealW, JIT && PCN_MERGE_BLOCKS>(run_ch, chain >= 0, p, port, ws, a.wave_bytes, verdict, rid,
                                                           wide);
       if (chain >= 0) cchain = chain;
@@ -1346,7 +1399,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       }
     }
     if (kLate) prefetch(cur, i + PF * step);
-    if (valid) {
+    if (wr) {
       a.verdicts[i] = static_cast<uint8_t>(verdict);
       if (a.rule_ids) a.rule_ids[i] = rid;
     }
@@ -1527,9 +1580,22 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(const LaunchArgs a) {
 #ifndef PCN_WAVES_PER_SIMD
 #define PCN_WAVES_PER_SIMD 1   // >= 8: two 1024-thread workgroups per CU (<= 64 VGPRs)
 #endif
+#if defined(PCN_JIT_SPLIT) && PCN_JIT_SPLIT
+// A split launch's two kernels (classify_body SPLIT): the gather kernel under
+// the program's usual name, in PCN_SPLIT_G_BLOCK-thread workgroups, as many
+// per CU as its registers allow (no chain image in LDS: ~75 VGPRs, 6 waves
+// per SIMD), then the rule kernel.
+extern "C" __global__ __launch_bounds__(PCN_SPLIT_G_BLOCK) void pcn_classify_jit(const LaunchArgs a) {
+  classify_body<PCN_JIT_FIXED, false, PCN_JIT_CH, PCN_JIT_NS, true, 1>(a);
+}
+extern "C" __global__ __launch_bounds__(kBlock, PCN_WAVES_PER_SIMD) void pcn_split_rules(const LaunchArgs a) {
+  classify_body<PCN_JIT_FIXED, PCN_JIT_LDS, PCN_JIT_CH, PCN_JIT_NS, true, 2>(a);
+}
+#else
 extern "C" __global__ __launch_bounds__(kBlock, PCN_WAVES_PER_SIMD) void pcn_classify_jit(const LaunchArgs a) {
   classify_body<PCN_JIT_FIXED, PCN_JIT_LDS, PCN_JIT_CH, PCN_JIT_NS, true>(a);
 }
+#endif
 #else
 namespace {
 
@@ -1556,8 +1622,13 @@ void launch_ns(const LaunchArgs &a, int ch, int, unsigned grid, size_t lds, hipS
 // reach the rule stage (0..2) or 3 for INPUT+FORWARD.  `jit` (a hipFunction_t
 // or null) is the chain program compiled for exactly this launch shape
 // (jit.cpp); null runs the generic variant.  Returns a hipError_t.
+//
+// Split launches (jit2 = the program's rule kernel, ga = the gather kernel's
+// arguments: its own LDS layout, no chain image): each launch chunk runs the
+// gather kernel (`jit`, ga_wg workgroups per CU) and then the rule kernel over
+// the records it left in a.split_rec (indexed from the chunk's first frame).
 int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream,
-                    CopyBound *cb) {
+                    CopyBound *cb, void *jit2, const LaunchArgs *ga, unsigned ga_wg) {
   if (a.n == 0) return hipSuccess;
   const size_t lds = a.lds_bytes;
   const bool in_lds = a.lds_images_bytes > 0;
@@ -1583,6 +1654,9 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
   // (each copy takes the flushes of `wpc` workgroups).
   const uint64_t max_len = a.lens ? 65535u : (a.fixed_len ? a.fixed_len : 1u);
   const uint64_t wpc = (grid + uint64_t(a.ctr_rep_mask)) / (uint64_t(a.ctr_rep_mask) + 1);
+  const bool split = jit && jit2 && ga;
+  const uint64_t gwant = (a.n + PCN_SPLIT_G_BLOCK - 1) / PCN_SPLIT_G_BLOCK;
+  const unsigned ggrid = split ? static_cast<unsigned>(std::min<uint64_t>(gwant, uint64_t(num_cus) * ga_wg)) : 0u;
   // (a workgroup takes whole kBlock-frame rows of the grid stride)
   uint64_t per_block = 0xFFFFFFFFull / max_len;
   if (cb && a.ctr_pack_off) {
@@ -1598,7 +1672,8 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
       // the most any one copy takes from this launch; fold first if the copies
       // could overflow (cb->fold resets the bound)
       const uint64_t fw = (c.n + uint64_t(grid) * kBlock - 1) / (uint64_t(grid) * kBlock) * kBlock;
-      const uint64_t pk = wpc * fw, by = pk * max_len;
+      // (a split launch's two kernels each add at most that much into a copy)
+      const uint64_t pk = wpc * fw * (split ? 2 : 1), by = pk * max_len;
       if (cb->pkts + pk > cb->max_pkts || cb->bytes + by > cb->max_bytes) {
         const int e = cb->fold(cb->ctx, static_cast<void *>(stream));
         if (e != hipSuccess) return e;
@@ -1620,6 +1695,28 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
       if (a.has_ct) c.ct_status = a.ct_status + base;
       c.verdicts = a.verdicts + base;
       if (a.rule_ids) c.rule_ids = a.rule_ids + base;
+    }
+    if (split) {
+      LaunchArgs g = *ga;            // the chunk's frames, the gather kernel's LDS layout
+      g.n = c.n;
+      g.frames = c.frames;
+      g.frames_bytes = c.frames_bytes;
+      g.offsets = c.offsets;
+      g.lens = c.lens;
+      g.in_port = c.in_port;
+      g.ct_status = c.ct_status;
+      g.verdicts = c.verdicts;
+      g.rule_ids = c.rule_ids;
+      size_t sz = sizeof(LaunchArgs);
+      void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+      hipError_t e = hipModuleLaunchKernel(static_cast<hipFunction_t>(jit), ggrid, 1, 1, PCN_SPLIT_G_BLOCK, 1, 1,
+                                           static_cast<unsigned>(g.lds_bytes), stream, nullptr, extra);
+      if (e != hipSuccess) return static_cast<int>(e);
+      void *extra2[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &c, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+      e = hipModuleLaunchKernel(static_cast<hipFunction_t>(jit2), grid, 1, 1, kBlock, 1, 1, static_cast<unsigned>(lds),
+                                stream, nullptr, extra2);
+      if (e != hipSuccess) return static_cast<int>(e);
+      continue;
     }
     if (jit) {
       size_t sz = sizeof(LaunchArgs);

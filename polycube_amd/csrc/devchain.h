@@ -47,6 +47,8 @@
                                     // reused as the candidate-stage scratch
 #define PCN_WAVE_SCRATCH_BYTES 1280 // the candidate-stage scratch alone: the whole region of a launch
                                     // without the fixed-stride header transpose
+#define PCN_SPLIT_G_BLOCK 256       // a split launch's gather kernel: workgroup size (threads), several
+                                    // workgroups per CU as its registers allow (no chain image in LDS)
 #define PCN_DEAL2_WAVE_BYTES 2304   // the scratch of a 128-candidate deal window (classify.hip PCN_DEAL2):
                                     // chain programs of chains with 2+ summary blocks
 
@@ -216,7 +218,14 @@ struct LaunchArgs {
   // workgroup b stores s_memrealtime (100 MHz) at its start, after its prologue,
   // after its last frame and after its counter flush into dbg_clk[4 b .. 4 b + 3]
   unsigned long long *dbg_clk;   // null: not recorded
+  // Split launches (classify.hip SPLIT, pcn_ipt.cpp): the gather kernel writes
+  // each frame's rule-stage fields here (16 B a frame, kSplitNeed in the top
+  // byte when the frame runs rules) and the rule kernel reads them back.
+  uint32_t *split_rec;           // [n][4] u32; null: one fused kernel
 };
+// split_rec word 3: proto | flags << 8 | ct << 16 | meta << 24, meta = chain (2 bits)
+// | outer VLAN tag stripped (bit 2: the rule kernel's length is lens - 4) | kSplitNeed
+constexpr uint32_t kSplitNeed = 0x80u, kSplitUntag = 0x04u;
 
 // Packed counter pair: packets in bits 38-63, bytes in bits 0-37.
 constexpr uint32_t kCtrPackShift = 38;

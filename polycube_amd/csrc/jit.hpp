@@ -34,6 +34,7 @@ struct JitShape {
   bool shallow = false;   // fixed stride, at most 8 frames per lane: header prefetch depth 1
   bool deal2 = false;     // two candidates per worker lane (a chain of 2+ summary blocks; the launch
                           // sized the wave region for the 128-candidate window)
+  bool split = false;     // a split launch: gather kernel + rule kernel (classify.hip SPLIT)
 };
 
 // Source of the generated "pcn_jit_spec.h" for one chain descriptor (its
@@ -60,7 +61,8 @@ class JitCache {
   void request(const std::string &spec, bool blocking);
   // The kernel (hipFunction_t) for `spec` on the current device, or null when
   // it is absent, still compiling or failed.  Loads the module on first use.
-  void *function(const std::string &spec, int device);
+  // which = 1: a split program's second kernel (pcn_split_rules), null otherwise.
+  void *function(const std::string &spec, int device, int which = 0);
   // Compiled successfully (false while compiling or after a failure).
   bool ready(const std::string &spec) const;
   // 1 and *out filled when compiled, 0 while compiling or never requested, -1 failed.
@@ -75,7 +77,10 @@ class JitCache {
     // empty vector: compile failed; the last byte says whether the counted asm
     // header loads were kept (1) or the program was rebuilt without (0)
     std::shared_future<std::vector<char>> code;
-    std::map<int, std::pair<void *, void *>> loaded;   // device -> (hipModule_t, hipFunction_t)
+    struct Loaded {
+      void *mod = nullptr, *fn = nullptr, *fn2 = nullptr;   // hipModule_t, pcn_classify_jit, pcn_split_rules
+    };
+    std::map<int, Loaded> loaded;   // by device
     bool bad = false;
   };
   mutable std::mutex mu_;

@@ -29,7 +29,7 @@
 
 namespace pcn {
 int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus, void *jit, hipStream_t stream,
-                    CopyBound *cb);
+                    CopyBound *cb, void *jit2 = nullptr, const LaunchArgs *ga = nullptr, unsigned ga_wg = 0);
 int launch_sum_ranks(const unsigned long long *in, unsigned long long *out, uint64_t count, int nranks,
                      hipStream_t stream);
 int launch_fold_reps(unsigned long long *ctr, uint64_t pairs, uint64_t pack_off, uint64_t stride, uint32_t reps,
@@ -109,6 +109,28 @@ bool multi_block_deal2() {
   static const bool v = [] {
     const char *e = std::getenv("PCN_IPT_DEBUG_DEAL2_MULTI");
     return !(e && *e == '0');
+  }();
+  return v;
+}
+
+// Split launches (classify.hip SPLIT): offsets / lens batches of a chain whose
+// image does not fit LDS (dense PART: config 5) run a gather kernel of
+// PCN_SPLIT_G_BLOCK-thread workgroups, several per CU, and then the rule
+// kernel over its records.  PCN_IPT_DEBUG_SPLIT=0: one fused kernel (A/B);
+// PCN_IPT_DEBUG_SPLIT_WG: the gather kernel's workgroups per CU (default 6:
+// its ~75 VGPRs allow 6 waves per SIMD).
+int split_mode() {
+  static const int v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_SPLIT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+unsigned split_gather_wg() {
+  static const unsigned v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_SPLIT_WG");
+    const long x = e ? std::strtol(e, nullptr, 10) : 6;
+    return x >= 1 && x <= 32 ? static_cast<unsigned>(x) : 6u;
   }();
   return v;
 }
@@ -282,6 +304,10 @@ struct pcn_ipt {
   // PCN_IPT_DEBUG_CLOCKS=1: per-workgroup clocks of the last classify launch
   unsigned long long *d_dbg_clk = nullptr;
   uint32_t dbg_grid = 0;
+  // split launches: the gather kernel's records (16 B a frame), grown to the largest batch
+  uint32_t *d_split_rec = nullptr;
+  uint64_t split_cap = 0;
+  uint64_t launches_split = 0;
 };
 
 namespace pcn {
@@ -798,6 +824,7 @@ void pcn_ipt_destroy(pcn_ipt *ctx) {
     if (ctx->ev_ct) (void)hipEventDestroy(ctx->ev_ct);
     if (ctx->h_deal_stats) (void)hipHostFree(ctx->h_deal_stats);
     if (ctx->d_dbg_clk) (void)hipFree(ctx->d_dbg_clk);
+    if (ctx->d_split_rec) (void)hipFree(ctx->d_split_rec);
     for (auto &se : ctx->pack_streams)
       if (se.second) (void)hipEventDestroy(se.second);
     for (void *p : {static_cast<void *>(ctx->hz[0].d_tab), static_cast<void *>(ctx->hz[0].d_ctr),
@@ -1275,7 +1302,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     // slot count of the chain program (the generic kernel always runs 6)
     const int ns = ch < 3 ? static_cast<int>(a.ch[ch].lay.nslots) : 6;
     // chain program for this launch shape (jit.hpp), when enabled and ready
-    void *fn = nullptr;
+    void *fn = nullptr, *fn2 = nullptr;
     if (plan) plan->clear();
     if (ch < 3 && (reach_fw || reach_in || reach_out) && (ctx->cfg.jit >= 0 || plan)) {
       ChainState &cs = ctx->chains[ch];
@@ -1287,6 +1314,8 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0) |
                      (a.horus_fields ? 16 : 0) | (a.offsets ? 32 : 0) | (a.lens ? 64 : 0);
       shape.deal2 = deal2;
+      shape.split = !fixed && !sa && !a.has_stale && !a.horus_fields && a.ch[ch].lay.part_dense && split_mode() &&
+                    !debug_clocks();
       {
         const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((b->n + PCN_BLOCK - 1) / PCN_BLOCK,
                                                                        uint64_t(classify_grid_cus(ctx->num_cus))));
@@ -1300,7 +1329,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
           shape.fixed != cs.jit_shape.fixed ||
           shape.lds != cs.jit_shape.lds || shape.ch != cs.jit_shape.ch || shape.ns != cs.jit_shape.ns ||
           shape.inputs != cs.jit_shape.inputs || shape.shallow != cs.jit_shape.shallow ||
-          shape.deal2 != cs.jit_shape.deal2) {
+          shape.deal2 != cs.jit_shape.deal2 || shape.split != cs.jit_shape.split) {
         cs.jit_desc = key;
         cs.jit_shape = shape;
         cs.jit_spec = jit_spec(key, shape);
@@ -1311,6 +1340,11 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       }
       ctx->jit.request(cs.jit_spec, ctx->cfg.jit == 1);
       fn = ctx->jit.function(cs.jit_spec, ctx->cfg.device);
+      if (fn && shape.split) {
+        // a split program's first kernel is its gather kernel: it never runs alone
+        fn2 = ctx->jit.function(cs.jit_spec, ctx->cfg.device, 1);
+        if (!fn2) fn = nullptr;
+      }
       cs.last_spec = fn ? cs.jit_spec : std::string();
       // the generic kernel deals 64 a pass: give the 128-item region back
       if (!fn && deal2) {
@@ -1365,8 +1399,42 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
                                                                uint64_t(classify_grid_cus(ctx->num_cus))));
       if (ctx->dbg_grid > kDbgClkGrid) a.dbg_clk = nullptr;
     }
+    LaunchArgs ga{};
+    if (fn2) {
+      // the gather kernel's records, and its own LDS layout: the default bins
+      // (it counts the frames it finishes), localip and the per-wave regions
+      // of the quad gather; no chain image, no rule bins
+      if (ctx->split_cap < b->n) {
+        if (ctx->d_split_rec) hip_check(hipFree(ctx->d_split_rec), "hipFree(split records)");
+        ctx->d_split_rec = nullptr;
+        ctx->split_cap = 0;
+        hip_check(hipMalloc(&ctx->d_split_rec, b->n * 16), "hipMalloc(split records)");
+        ctx->split_cap = b->n;
+      }
+      a.split_rec = ctx->d_split_rec;
+      ga = a;
+      ga.nbins = 3;
+      ga.hz_bins = -1;
+      for (int c = 0; c < 3; ++c) {
+        ga.ch[c].lds_bins = -1;
+        ga.ch[c].lds_nrules = 0;
+        ga.ch[c].lds_image = 0;
+        ga.ch[c].lds_limit = 0;
+      }
+      ga.lds_images_bytes = 0;
+      ga.bins_offset = kLdsDescBytes;
+      ga.lds_localip = ga.bins_offset + (8 * ga.nbins + 15) / 16 * 16;
+      ga.lds_stats = (ga.lds_localip + ga.nlocal * 4 + 15) / 16 * 16;
+      ga.lds_scratch = ga.lds_stats + 16;
+      ga.wave_bytes = wave_region_bytes(false, false);
+      ga.lds_bytes = ga.lds_scratch + (PCN_SPLIT_G_BLOCK / 64) * ga.wave_bytes;
+      ga.deal_stats = nullptr;
+      ga.dbg_clk = nullptr;
+      ++ctx->launches_split;
+    }
     if (!sa) register_pack_stream(ctx, hs);
-    int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, hs, sa ? nullptr : &ctx->pack);
+    int rc = launch_classify(a, fixed, ch, ns, classify_grid_cus(ctx->num_cus), fn, hs, sa ? nullptr : &ctx->pack,
+                             fn2, fn2 ? &ga : nullptr, split_gather_wg());
     if (!rc && !sa) note_pack_stream(ctx, hs);
     if (rc != hipSuccess) return fail(-EIO, std::string("classify launch: ") + hipGetErrorString(hipError_t(rc)));
     return 0;
@@ -1531,6 +1599,7 @@ int pcn_ipt_get_jit_info(pcn_ipt *ctx, pcn_ipt_jit_info *out) {
     out->launches_jit = ctx->launches_jit;
     out->programs_ready = static_cast<uint32_t>(ctx->jit.compiled());
     out->programs_failed = static_cast<uint32_t>(ctx->jit.failed());
+    out->launches_split = ctx->launches_split;
     return 0;
   });
 }
@@ -1561,6 +1630,27 @@ int usual_spec(pcn_ipt *ctx, int chain, std::string &spec) {
     return 0;
 }
 }  // namespace
+
+int pcn_ipt_chain_program_compile_for(pcn_ipt *ctx, int chain, const pcn_ipt_batch *shape) {
+  return guarded(ctx, [&] {
+    if (!valid_chain(chain)) return fail(-EINVAL, "bad chain");
+    if (!shape) return fail(-EINVAL, "null shape");
+    if (ctx->chains[chain].info.nrules == 0) return fail(-ENOENT, "chain has no rules");
+    // a plan reads no buffer: any non-null address stands in for the batch's own
+    pcn_ipt_batch b = *shape;
+    uint8_t *const never_read = reinterpret_cast<uint8_t *>(uintptr_t(1) << 12);
+    if (!b.frames) b.frames = never_read;
+    if (!b.verdicts) b.verdicts = never_read;
+    if (!b.n) b.n = uint64_t(1) << 20;
+    if (!b.offsets && !b.frames_bytes) b.frames_bytes = b.n * uint64_t(b.stride ? b.stride : 64);
+    std::string spec;
+    if (int rc = launch_batch(ctx, &b, nullptr, nullptr, nullptr, nullptr, nullptr, &spec)) return rc;
+    if (spec.empty()) return fail(-ENOENT, "no chain program runs this chain's rules in that launch");
+    ctx->jit.request(spec, true);
+    if (!ctx->jit.ready(spec)) return fail(-EIO, "chain program compile failed: " + ctx->jit.last_log());
+    return 0;
+  });
+}
 
 int pcn_ipt_chain_program_compile(pcn_ipt *ctx, int chain) {
   return guarded(ctx, [&] {

@@ -14,6 +14,7 @@
 #include <condition_variable>
 #include <cerrno>
 #include <cstring>
+#include <chrono>
 #include <deque>
 #include <functional>
 #include <memory>
@@ -142,6 +143,7 @@ struct pcn_ipt_ring {
   std::deque<uint32_t> inflight;   // submission order
   std::mutex mu;
   std::unique_ptr<PackPool> pack;  // PCN_IPT_RING_HOST_PACK
+  pcn_ipt_ring_stats stats{};      // under mu
 };
 
 namespace {
@@ -283,6 +285,8 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
       return ring_fail(-EINVAL, "hdr_bytes must be a multiple of 16, <= stride and >= " + std::to_string(need));
   }
   if (hipSetDevice(r->device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
+  const auto t_submit = std::chrono::steady_clock::now();
+  uint64_t pack_ns = 0;
   hipStream_t st = r->streams[slot % r->streams.size()];
   const size_t n = b->n;
   // PCIe in: frames (or their first hb bytes: a strided copy, hb-byte rows
@@ -311,10 +315,13 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
     // the slot is the producer's (kFilling): the consumer's complete / release
     // need not wait for the pack
     l.unlock();
+    const auto t_pack = std::chrono::steady_clock::now();
     r->pack->run([&](unsigned k) {
       const size_t lo = k * per, hi = std::min<size_t>(n, lo + per);
       for (size_t i = lo; i < hi; ++i) std::memcpy(dst + i * hb, src + i * stride, hb);
     }, parts);
+    pack_ns = static_cast<uint64_t>(
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_pack).count());
     l.lock();
     ok = hipMemcpyAsync(s.d_frames, s.h_pack, n * hb, hipMemcpyHostToDevice, st) == hipSuccess;
   } else if (!zc) {
@@ -360,6 +367,24 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   s.n = n;
   s.state = kInFlight;
   r->inflight.push_back(slot);
+  pcn_ipt_ring_stats &rs = r->stats;
+  rs.submits += 1;
+  rs.frames += n;
+  const uint64_t arrays = (b->use_offsets ? 4 : 0) + (b->use_lens ? 2 : 0) + (b->use_in_port ? 2 : 0);
+  if (zc) rs.zc_bytes += n * (64 + arrays);
+  else rs.h2d_bytes += (hb ? n * hb : bytes) + n * arrays;
+  rs.d2h_bytes += n * (s.d_rule_ids ? 5 : 1);
+  rs.pack_ns += pack_ns;
+  rs.submit_ns += static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_submit).count());
+  return 0;
+}
+
+int pcn_ipt_ring_get_stats(pcn_ipt_ring *r, pcn_ipt_ring_stats *out, int reset) {
+  if (!r || !out) return ring_fail(-EINVAL, "null argument");
+  std::lock_guard<std::mutex> l(r->mu);
+  *out = r->stats;
+  if (reset) r->stats = pcn_ipt_ring_stats{};
   return 0;
 }
 

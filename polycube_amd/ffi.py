@@ -51,7 +51,7 @@ class Tables(C.Structure):
 
 class JitInfo(C.Structure):
     _fields_ = [("launches_generic", C.c_uint64), ("launches_jit", C.c_uint64),
-                ("programs_ready", C.c_uint32), ("programs_failed", C.c_uint32)]
+                ("programs_ready", C.c_uint32), ("programs_failed", C.c_uint32), ("launches_split", C.c_uint64)]
 
 
 class RingConfig(C.Structure):
@@ -62,6 +62,11 @@ class RingConfig(C.Structure):
 class RingSlot(C.Structure):
     _fields_ = [("slot", C.c_uint32), ("frames", C.POINTER(C.c_uint8)), ("offsets", C.POINTER(C.c_uint32)),
                 ("lens", C.POINTER(C.c_uint16)), ("in_port", C.POINTER(C.c_uint16))]
+
+
+class RingStats(C.Structure):
+    _fields_ = [("submits", C.c_uint64), ("frames", C.c_uint64), ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64),
+                ("zc_bytes", C.c_uint64), ("pack_ns", C.c_uint64), ("submit_ns", C.c_uint64)]
 
 
 class RingBatch(C.Structure):
@@ -133,6 +138,7 @@ SIGNATURES = {
     "pcn_ipt_debug_stale_canary": (C.c_int, [C.c_void_p]),
     "pcn_ipt_debug_ct_walk_passes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "pcn_ipt_chain_program_compile": (C.c_int, [C.c_void_p, C.c_int]),
+    "pcn_ipt_chain_program_compile_for": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(Batch)]),
     "pcn_ipt_get_program_info": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ProgramInfo)]),
     "pcn_ipt_embedded_source": (C.c_char_p, [C.c_int]),
     "pcn_ipt_build_sha256": (C.c_char_p, []),
@@ -153,6 +159,7 @@ SIGNATURES = {
     "pcn_ipt_ring_complete": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
                                         C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.POINTER(C.c_int32))]),
     "pcn_ipt_ring_release": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "pcn_ipt_ring_get_stats": (C.c_int, [C.c_void_p, C.POINTER(RingStats), C.c_int]),
     "pcn_ipt_set_horus": (C.c_int, [C.c_void_p, C.c_int]),
     "pcn_ipt_get_horus_info": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(HorusInfo)]),
     "pcn_ipt_read_horus_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),

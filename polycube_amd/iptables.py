@@ -182,9 +182,27 @@ class Chain:
         _check(ffi.lib().pcn_ipt_get_program_info(self._h(), self.id, C.byref(out)))
         return {k: getattr(out, k) for k, _ in ffi.ProgramInfo._fields_}
 
-    def compile_program(self):
-        """Compile this chain's chain program now (pcn_ipt_chain_program_compile)."""
-        _check(ffi.lib().pcn_ipt_chain_program_compile(self._h(), self.id))
+    def compile_program(self, n=None, offsets=False, lens=False, stride=64, fixed_len=64, in_port=False,
+                        ct_status=False, direction=None, hook=XDP):
+        """Compile this chain's chain program now: for its usual launch shape
+        (pcn_ipt_chain_program_compile), or, given any shape argument, for the launch
+        shape of such a batch (pcn_ipt_chain_program_compile_for; IMIX: offsets=lens=True)."""
+        if n is None and not (offsets or lens or in_port or ct_status or hook or direction is not None
+                              or stride != 64 or fixed_len != 64):
+            _check(ffi.lib().pcn_ipt_chain_program_compile(self._h(), self.id))
+            return
+        fake = 1 << 12      # never read: a plan reads no buffer
+        b = ffi.Batch()
+        b.n = n or (1 << 20)
+        b.offsets = fake if offsets else None
+        b.lens = fake if lens else None
+        b.stride, b.fixed_len = stride, fixed_len
+        b.in_port = fake if in_port else None
+        b.ct_status = fake if ct_status else None
+        b.const_in_port = 1
+        b.direction = (EGRESS if self.id == 2 else INGRESS) if direction is None else direction
+        b.hook = hook
+        _check(ffi.lib().pcn_ipt_chain_program_compile_for(self._h(), self.id, C.byref(b)))
 
     def export_map(self, field, cap=70000):
         nrw = ffi.lib().pcn_ipt_chain_nrw(self._h(), self.id)
@@ -507,3 +525,10 @@ class IngestRing:
 
     def release(self, slot):
         _check(ffi.lib().pcn_ipt_ring_release(self._h, slot))
+
+    def stats(self, reset=False):
+        """pcn_ipt_ring_get_stats: what the submits moved over PCIe and what their host side
+        (pack, submit) cost since creation or the last reset."""
+        st = ffi.RingStats()
+        _check(ffi.lib().pcn_ipt_ring_get_stats(self._h, C.byref(st), int(reset)))
+        return {k: getattr(st, k) for k, _ in ffi.RingStats._fields_}

@@ -166,6 +166,43 @@ def test_fuzz_parity(dev, seed, jit):
     assert_counters(o, ipt)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_split_launch_edge_frames(dev, seed):
+    """Split launches (a gather kernel, then a rule kernel over its 16-byte records:
+    offsets / lens batches of a chain whose image exceeds LDS) on edge-case frames:
+    config 5's 10k rules in FORWARD and 3-6k in OUTPUT, INPUT empty (localip steers
+    a share of the ingress frames to its default and of the egress frames to
+    OUTPUT), short / odd frames, VLAN and IPv6, random in_port and ct_status arrays
+    (odd seeds), both directions, the TC hook on seeds 2-3.  Bit-exact against the
+    oracle: verdicts, rule ids and every counter."""
+    rng = np.random.default_rng(seed)
+    rs = synth.config_rules(5)
+    rules = rs.rules()
+    big = dict(max_rules=16384, max_counted_rules=10000, max_action_rules=10000)
+    localip = [ip_nbo(f"10.0.{k}.{k}") for k in range(40)]
+    o, ipt = make_pair({1: rules, 2: rules[: 3000 + 1000 * seed]}, {0: "ACCEPT", 1: "DROP", 2: "ACCEPT"}, localip,
+                       jit=1, **big)
+    n = 1 << 18
+    frames, lens = synth.fuzz_frames(n, 100 + seed, rs, stride=96)
+    f = frames.reshape(n, 96).copy()
+    ips = rng.choice(np.array([(10 << 24) | (k << 16) | k for k in range(40)], np.uint32), size=n)
+    be = np.stack([(ips >> 24) & 255, (ips >> 16) & 255, (ips >> 8) & 255, ips & 255], axis=1).astype(np.uint8)
+    for col in (26, 30):                 # local sources (OUTPUT) and destinations (INPUT)
+        loc = rng.random(n) < 0.2
+        f[loc, col:col + 4] = be[loc]
+    offsets = (np.arange(n, dtype=np.uint64) * 96).astype(np.uint32)
+    in_port = rng.choice(np.array([0, 1, 2, 3, 7, 0xFFFF], np.uint16), size=n) if seed % 2 else None
+    ct = rng.integers(0, 4, size=n).astype(np.uint8) if seed % 2 else None
+    hook = 1 if seed >= 2 else 0
+    for direction in (0, 1):
+        res = run_both(o, ipt, dev, f.reshape(-1), n, stride=96, offsets=offsets, lens=lens, in_port=in_port,
+                       direction=direction, ct=ct, hook=hook)
+        assert_same(*res)
+    assert_counters(o, ipt, n=10000)
+    info = ipt.jit_info()
+    assert info["launches_split"] >= 1 and info["programs_failed"] == 0, info
+
+
 @JIT
 @pytest.mark.parametrize("hook", [0, 1], ids=["xdp", "tc"])
 @pytest.mark.parametrize("align", [1, 64], ids=["packed", "aligned"])
@@ -274,6 +311,7 @@ def test_full_size_config5(dev, hook):
         assert_same(*run_both(o, ipt, dev, buf, n, offsets=offsets, lens=lens, hook=hook))
     assert_counters(o, ipt, n=10000)
     assert_jit_used(ipt, 1)
+    assert ipt.jit_info()["launches_split"] == 2      # the gather kernel + rule kernel launches
 
 
 def test_table_level_boundary(dev):
