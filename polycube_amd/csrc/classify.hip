@@ -132,6 +132,15 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 #ifndef PCN_OFF_AHEAD
 #define PCN_OFF_AHEAD 1
 #endif
+// Split launches (SPLIT 2, the rule kernel): records in flight per lane, and
+// whether the next record is fetched after the rule stage (as the fused
+// kernel does for dense PART) rather than before it.
+#ifndef PCN_SPLIT_R_PF
+#define PCN_SPLIT_R_PF 2
+#endif
+#ifndef PCN_SPLIT_R_LATE
+#define PCN_SPLIT_R_LATE 0
+#endif
 // Tuning switches (tools/ablate.py builds experiment variants with -D...).
 
 namespace pcn {
@@ -958,7 +967,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   const bool has_off = JIT ? (kJitInputs & 32) != 0 : a.offsets != nullptr;
   const bool has_lens = JIT ? (kJitInputs & 64) != 0 : a.lens != nullptr;
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
-  constexpr int PF = FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
+  // (a split launch's rule kernel: its 16-byte records, PCN_SPLIT_R_PF ahead)
+  constexpr int PF = SPLIT == 2 ? PCN_SPLIT_R_PF : FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
   Stage st[PF];
   auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
     if constexpr (SPLIT == 2) {                  // the gather kernel's fields for frame j, coalesced
@@ -1161,7 +1171,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     asm volatile("" : "+v"(cur.port), "+v"(cur.ct));
     uint32_t L = FIXED ? a.fixed_len : cur.L;
     const uint32_t cur_port = cur.port, cur_ct = cur.ct;
-    constexpr bool kLate = SPLIT != 1 && PCN_PF_LATE && !FIXED && JIT && kJitChain.lay.part_dense;
+    constexpr bool kLate = (SPLIT == 0 || (SPLIT == 2 && PCN_SPLIT_R_LATE)) && PCN_PF_LATE && !FIXED && JIT &&
+                           kJitChain.lay.part_dense;
     if (!kLate) prefetch(cur, i + PF * step);
     uint32_t verdict = PCN_IPT_DROP;
     int32_t rid = PCN_IPT_RID_NOCHAIN;
