@@ -433,6 +433,30 @@ def ct_rate(ipt, rs, n, dev, steps=5, warmup=2, flows=1 << 16, seed=0xC7):
                                                            "share_ms": round(share_ms, 3)}
 
 
+def ct_single_flow(ipt, rs, n, dev, steps=3):
+    """The stateful leg's worst case for the walk: the whole batch one TCP connection
+    (handshake, data, close; no noise, no ICMP), so every segment of its one run is
+    walked speculatively and chained by ct_seg_fix.  ms per batch."""
+    import torch
+
+    from polycube_amd import synth
+    f, _ = synth.flow_traffic(n, 1, 0xC7, stride=64, rs=rs, p_noise=0.0, p_icmp=0.0, p_err=0.0)
+    frames = torch.from_numpy(f).to(dev)
+    verdicts = torch.empty(n, dtype=torch.uint8, device=dev)
+    ipt.ct_enable(20)
+    ipt.ct_set_time(1_700_000_000 * 10**9)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ipt.classify(frames, n=n, verdicts=verdicts, stream=stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ipt.classify(frames, n=n, verdicts=verdicts, stream=stream)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    ipt.ct_disable()
+    return ms
+
+
 def fw_rate(rules, frames, n, dev, s_ptr, jit, steps=20, horus=False, settle=0.5):
     """The headline rules in a pcn-firewall INGRESS chain (conntrack OFF), same
     resident frames: time per pcn_ipt_classify call (one HIP event pair around
@@ -528,9 +552,12 @@ def frame_size_sweep(ipt, rules, frames, n, dev, stream, log, steps=20, sizes=FR
     pair around `steps` launches).  The roofline is the 64-byte header sector per frame
     (the Parser reads bytes 0..47, Iptables_Parser_dp.c:126-143): `frac` = 64 B x n /
     time / peak.  `lines_128b` is the count of 128-byte lines a frame's 48-byte window
-    touches (1500 B: 48 of every 128 windows cross into a second line), the L2's request
-    unit; `traffic` the PMC HBM bytes per frame where profiles/pmc_traffic.json
-    holds an entry for this build.  Each size's first 2^16 frames are checked against
+    touches (1500 B: 48 of every 128 windows cross into a second line): every L2 fill is a
+    128-byte request, so a frame at a stride of 128 B or more moves at least one whole line
+    (tools/gather_calib.hip: TCC_EA0_RDREQ = the lines touched), and
+    `line_frac` = lines x 128 B x n / time / peak is the roofline of that access pattern;
+    `traffic` the PMC HBM bytes per frame where profiles/pmc_traffic.json holds an entry
+    for this build.  Each size's first 2^16 frames are checked against
     the oracle (verdicts and rule ids)."""
     import torch
 
@@ -559,6 +586,7 @@ def frame_size_sweep(ipt, rules, frames, n, dev, stream, log, steps=20, sizes=FR
         traffic, note = load_traffic(3, 0, n, key=None if size == 64 else f"config3_stride{size}")
         out[str(size)] = {"kernel_ms": round(ms, 4), "mpkt_s": round(n / ms / 1e3, 1),
                           "frac": round(BYTES_PER_PKT * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "line_frac": round(lines * 128 * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                           "frame_gb_s": round(size * n / (ms * 1e-3) / 1e9, 1),
                           "lines_128b_per_frame": round(lines, 4),
                           "line_gb_s": round(lines * 128 * n / (ms * 1e-3) / 1e9, 1),
@@ -989,7 +1017,11 @@ def main():
                             "miss drops (the tail call into the deleted ConntrackLabel)"}}
         if world == 1 and not args.no_ct and cfg == 3:
             rate, ms, live, shard = ct_rate(ipt, rs, n, dev)
+            one_ms = ct_single_flow(ipt, rs, n, dev)
             line["stateful_conntrack"] = {
+                "single_flow_ms": round(one_ms, 3),
+                "single_flow_what": ct_single_flow.__doc__.split("\n", 1)[0] + " " +
+                                    ct_single_flow.__doc__.split("\n", 1)[1].strip(),
                 "value": round(rate, 2), "unit": "Mpkt/s", "ms_per_step": round(ms, 3),
                 "flow_split_8": dict(shard, what="pcn_ipt_flow_split of the whole batch for rank 0 of 8 (split_ms, "
                                                  "incl. its count read-back), then rank 0's owned frames through "
