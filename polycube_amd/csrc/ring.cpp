@@ -9,6 +9,7 @@
 // per submit, pipelined over HIP streams so the PCIe copies in and out overlap
 // the classify kernels of other slots.
 #include <hip/hip_runtime.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -132,6 +133,39 @@ int device_of(const pcn_ipt *ctx);
 
 namespace {
 int ring_fail(int code, const std::string &msg) { return pcn::fail(code, msg); }
+}  // namespace
+
+namespace {
+// Copy `rows` rows of hb bytes from a stride-byte source into contiguous rows
+// (the host pack).  The common widths copy with a compile-time size, so each
+// row is a few 16-byte moves instead of a memcpy call (a 48-byte call per
+// frame held 16 threads at ~3.7 GB/s each, 74 % of the e2e leg's wall time).
+// The rows go out with streaming stores: the packed buffer is read only by
+// the DMA engine, so its lines need not be fetched into the cache first (a
+// plain store reads each destination line before writing it).
+template <size_t W>
+void pack_fixed(uint8_t *dst, const uint8_t *src, size_t rows, size_t stride) {
+  static_assert(W % 16 == 0, "16-byte rows");
+  if (reinterpret_cast<uintptr_t>(dst) % 16) {
+    for (size_t i = 0; i < rows; ++i) std::memcpy(dst + i * W, src + i * stride, W);
+    return;
+  }
+  for (size_t i = 0; i < rows; ++i) {
+    const __m128i *s = reinterpret_cast<const __m128i *>(src + i * stride);
+    __m128i *d = reinterpret_cast<__m128i *>(dst + i * W);
+    for (size_t q = 0; q < W / 16; ++q) _mm_stream_si128(d + q, _mm_loadu_si128(s + q));
+  }
+  _mm_sfence();
+}
+void pack_rows(uint8_t *dst, const uint8_t *src, size_t rows, size_t hb, size_t stride) {
+  switch (hb) {
+    case 48: pack_fixed<48>(dst, src, rows, stride); return;
+    case 64: pack_fixed<64>(dst, src, rows, stride); return;
+    case 80: pack_fixed<80>(dst, src, rows, stride); return;
+    default:
+      for (size_t i = 0; i < rows; ++i) std::memcpy(dst + i * hb, src + i * stride, hb);
+  }
+}
 }  // namespace
 
 struct pcn_ipt_ring {
@@ -318,7 +352,7 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
     const auto t_pack = std::chrono::steady_clock::now();
     r->pack->run([&](unsigned k) {
       const size_t lo = k * per, hi = std::min<size_t>(n, lo + per);
-      for (size_t i = lo; i < hi; ++i) std::memcpy(dst + i * hb, src + i * stride, hb);
+      pack_rows(dst + lo * hb, src + lo * stride, hi - lo, hb, stride);
     }, parts);
     pack_ns = static_cast<uint64_t>(
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_pack).count());
