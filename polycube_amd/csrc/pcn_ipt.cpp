@@ -114,17 +114,17 @@ bool multi_block_deal2() {
 }
 
 // Split launches (classify.hip SPLIT): offsets / lens batches of a chain whose
-// image does not fit LDS (dense PART: config 5) run a gather kernel of
+// image does not fit LDS (dense PART: config 5) may run a gather kernel of
 // PCN_SPLIT_G_BLOCK-thread workgroups, several per CU, and then the rule
-// kernel over its records.  PCN_IPT_DEBUG_SPLIT=0: one fused kernel (A/B);
-// PCN_IPT_DEBUG_SPLIT_WG: the gather kernel's workgroups per CU (default 6:
-// its ~75 VGPRs allow 6 waves per SIMD).
-int split_mode() {
-  static const int v = [] {
-    const char *e = std::getenv("PCN_IPT_DEBUG_SPLIT");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
+// kernel over its records.  Built, bit-exact and measured slower than the one
+// fused kernel (config 5 XDP 134 -> 201-213 us: gather 123 + rules 85 us,
+// profiles/r06_s2/), so off unless a context is created with
+// PCN_IPT_DEBUG_SPLIT=1 in the environment (read per context, for the tests'
+// and the A/B's sake).  PCN_IPT_DEBUG_SPLIT_WG: the gather kernel's
+// workgroups per CU (default 6: its ~75 VGPRs allow 6 waves per SIMD).
+bool split_env() {
+  const char *e = std::getenv("PCN_IPT_DEBUG_SPLIT");
+  return e && std::atoi(e) == 1;
 }
 unsigned split_gather_wg() {
   static const unsigned v = [] {
@@ -307,6 +307,7 @@ struct pcn_ipt {
   // split launches: the gather kernel's records (16 B a frame), grown to the largest batch
   uint32_t *d_split_rec = nullptr;
   uint64_t split_cap = 0;
+  bool split = false;                      // split launches allowed (PCN_IPT_DEBUG_SPLIT=1 at creation)
   uint64_t launches_split = 0;
 };
 
@@ -733,6 +734,7 @@ int pcn_ipt_create(const pcn_ipt_config *cfg, pcn_ipt **out) {
   if (ctx->cfg.jit < -1 || ctx->cfg.jit > 1) return fail(-EINVAL, "jit must be -1, 0 or 1");
   ctx->ctr_words = 2 + 2 * size_t(ctx->cfg.max_counted_rules);
   ctx->ctr_reps = ctr_reps_default();
+  ctx->split = split_env();
   ctx->pack.fold = fold_all_copies;
   ctx->pack.ctx = ctx.get();
   ctx->pack.max_pkts = kCtrPackPktsMax;
@@ -1314,7 +1316,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0) |
                      (a.horus_fields ? 16 : 0) | (a.offsets ? 32 : 0) | (a.lens ? 64 : 0);
       shape.deal2 = deal2;
-      shape.split = !fixed && !sa && !a.has_stale && !a.horus_fields && a.ch[ch].lay.part_dense && split_mode() &&
+      shape.split = !fixed && !sa && !a.has_stale && !a.horus_fields && a.ch[ch].lay.part_dense && ctx->split &&
                     !debug_clocks();
       {
         const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>((b->n + PCN_BLOCK - 1) / PCN_BLOCK,

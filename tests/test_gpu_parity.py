@@ -169,7 +169,8 @@ def test_fuzz_parity(dev, seed, jit):
 @pytest.mark.parametrize("seed", range(4))
 def test_split_launch_edge_frames(dev, seed):
     """Split launches (a gather kernel, then a rule kernel over its 16-byte records:
-    offsets / lens batches of a chain whose image exceeds LDS) on edge-case frames:
+    offsets / lens batches of a chain whose image exceeds LDS; opt-in, measured slower
+    than the fused kernel) on edge-case frames:
     config 5's 10k rules in FORWARD and 3-6k in OUTPUT, INPUT empty (localip steers
     a share of the ingress frames to its default and of the egress frames to
     OUTPUT), short / odd frames, VLAN and IPv6, random in_port and ct_status arrays
@@ -180,8 +181,12 @@ def test_split_launch_edge_frames(dev, seed):
     rules = rs.rules()
     big = dict(max_rules=16384, max_counted_rules=10000, max_action_rules=10000)
     localip = [ip_nbo(f"10.0.{k}.{k}") for k in range(40)]
-    o, ipt = make_pair({1: rules, 2: rules[: 3000 + 1000 * seed]}, {0: "ACCEPT", 1: "DROP", 2: "ACCEPT"}, localip,
-                       jit=1, **big)
+    os.environ["PCN_IPT_DEBUG_SPLIT"] = "1"      # read when the context is created (off by default)
+    try:
+        o, ipt = make_pair({1: rules, 2: rules[: 3000 + 1000 * seed]}, {0: "ACCEPT", 1: "DROP", 2: "ACCEPT"},
+                           localip, jit=1, **big)
+    finally:
+        del os.environ["PCN_IPT_DEBUG_SPLIT"]
     n = 1 << 18
     frames, lens = synth.fuzz_frames(n, 100 + seed, rs, stride=96)
     f = frames.reshape(n, 96).copy()
@@ -311,7 +316,6 @@ def test_full_size_config5(dev, hook):
         assert_same(*run_both(o, ipt, dev, buf, n, offsets=offsets, lens=lens, hook=hook))
     assert_counters(o, ipt, n=10000)
     assert_jit_used(ipt, 1)
-    assert ipt.jit_info()["launches_split"] == 2      # the gather kernel + rule kernel launches
 
 
 def test_table_level_boundary(dev):
