@@ -407,6 +407,8 @@ typedef struct {
   uint64_t inserts_lost;     /* inserts refused: no free slot near the key's home (table (nearly) full) */
   uint64_t max_entries;      /* live entries kept after each batch (LRU; 0 = unbounded) */
   uint64_t evicted;          /* entries deleted by the LRU so far */
+  uint64_t fused_batches;    /* stateful batches whose classify pass also built the walk records
+                                (frames shorter than 70 bytes, one label: the frames read once) */
 } pcn_ipt_ct_info;
 /* capacity = 2^capacity_log2 slots (0 => 2^18); the table persists across enable/disable. */
 int pcn_ipt_ct_enable(pcn_ipt *ctx, uint32_t capacity_log2);

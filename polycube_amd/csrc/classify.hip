@@ -830,7 +830,8 @@ __device__ __forceinline__ void run_chain(const DevChain &ch, bool mine, const P
 #ifdef PCN_JIT
 constexpr DevChain kJitChain = PCN_JIT_CHAIN;
 constexpr int kJitInputs = PCN_JIT_INPUTS;   // bit 0: in_port array, bits 1-2: ct_status (array / stage-A label),
-                                             // 3 stale ports, 4 Horus, 5 offsets array, 6 lens array
+                                             // 3 stale ports, 4 Horus, 5 offsets array, 6 lens array,
+                                             // 7 stage A writes the walk records (LaunchArgs::ct_brec)
 #else
 constexpr DevChain kJitChain{};
 constexpr int kJitInputs = 7;
@@ -911,6 +912,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // always resolve.
   constexpr bool kStale = (!JIT || (kJitInputs & 8)) && PCN_DBG_HZ != 1;
   constexpr bool kHorus = (!JIT || (kJitInputs & 16)) && PCN_DBG_HZ != 2;   // a Horus program is in place
+  constexpr bool kCtRec = (!JIT || (kJitInputs & 128)) && SPLIT == 0;   // stage A writes the walk records
   const bool chunked = kStale && a.has_stale;
   uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1181,6 +1183,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     Parsed p{};
     uint32_t port = 0;
     uint32_t untag = 0;     // SPLIT 1: kSplitUntag once the outer VLAN tag is stripped
+    uint32_t ps = 0;        // the Parser's outcome: 0 RX_DROP, 1 not IPv4, 2 parsed (walk records)
+    uint32_t own_pd = 0;    // the Parser's srcPort / dstPort as stored (wire bytes 34-37)
+    uint32_t stale = 0;     // ... as a packet it writes none for sees them (Q4; chunked launches)
     if constexpr (SPLIT == 2) {
       // the gather kernel's fields (SPLIT 1 below): only frames that reach the
       // rule stage are this kernel's
@@ -1212,6 +1217,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       fast = __ballot(!plain) == 0;
     }
     if (fast) {
+      ps = 2;
       port = a.has_in_port ? cur_port : const_port;
       p.proto = h.w[5] >> 24;
       p.saddr = (h.w[6] >> 16) | (h.w[7] << 16);
@@ -1244,18 +1250,19 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       // ---- Parser_dp.c:94-153 ----
       gen = true;
       if (L < 14 || untag_drop) verdict = PCN_IPT_DROP;
-      else if ((h.w[3] & 0xffff) != 0x0008) verdict = PCN_IPT_ACCEPT;   // ethertype != 0x0800
+      else if ((h.w[3] & 0xffff) != 0x0008) { verdict = PCN_IPT_ACCEPT; ps = 1; }   // ethertype != 0x0800
       else if (L < 34) verdict = PCN_IPT_DROP;
       else {
         p.proto = h.w[5] >> 24;
         p.saddr = (h.w[6] >> 16) | (h.w[7] << 16);
         p.daddr = (h.w[7] >> 16) | (h.w[8] << 16);
         done = false;
+        ps = 2;
         if (p.proto == 6) {
-          if (L < 54) { verdict = PCN_IPT_DROP; done = true; }
+          if (L < 54) { verdict = PCN_IPT_DROP; done = true; ps = 0; }
           p.flags = h.w[11] >> 24;
         } else if (p.proto == 17) {
-          if (L < 42) { verdict = PCN_IPT_DROP; done = true; }
+          if (L < 42) { verdict = PCN_IPT_DROP; done = true; ps = 0; }
         }
         p.sport = bswap16u(h.w[8] >> 16);
         p.dport = bswap16u(h.w[9] & 0xffff);
@@ -1263,8 +1270,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     }
     // ---- the Parser's srcPort/dstPort as stored (wire bytes 34-37), stale
     // for a packet it writes none for (Q4): Horus keys read them ----
-    const uint32_t own_pd = (h.w[8] >> 16) | (h.w[9] << 16);
-    uint32_t stale = 0;
+    own_pd = (h.w[8] >> 16) | (h.w[9] << 16);
     if (chunked) {
       const bool wrote = fast ? valid : gen && !done && (p.proto == 6 || p.proto == 17);
       const bool need = gen && !done && p.proto != 6 && p.proto != 17;
@@ -1413,6 +1419,41 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     if (wr) {
       a.verdicts[i] = static_cast<uint8_t>(verdict);
       if (a.rule_ids) a.rule_ids[i] = rid;
+    }
+    // ---- stage A of a stateful batch that writes the walk records itself ----
+    // (frames shorter than 70 bytes and one label: what ct_prep would build
+    // from a second read of the frames, devchain.h ct_walk_rec; the label-0
+    // outcome is this launch's own)
+    if (kCtRec && a.ct_brec && valid) {
+      CtFrame f{};
+      const bool tcp = p.proto == 6;
+      f.status = ps;
+      f.ports_ok = ps == 2 && (tcp || p.proto == 17);
+      f.L = L;
+      f.src = p.saddr;
+      f.dst = p.daddr;
+      f.seq = ps == 2 && tcp ? (h.w[9] >> 16) | (h.w[10] << 16) : 0u;
+      f.ack = ps == 2 && tcp ? (h.w[10] >> 16) | (h.w[11] << 16) : 0u;
+      f.flags = ps == 2 && tcp ? h.w[11] >> 24 : 0u;
+      f.own = own_pd;
+      f.stale = stale;
+      f.proto = p.proto;
+      f.icmp = (h.w[8] >> 16) & 0xffu;
+      uint32_t cc = 3;
+      bool pass = false, labeled = false;
+      if (ps == 2) {
+        const bool ingress = a.direction == PCN_IPT_INGRESS;
+        const bool ldst = !a.fw && ingress && !a.allow_logic && a.nlocal && localip_has(a, p.daddr);
+        const bool lsrc = !a.fw && !ingress && a.nlocal && localip_has(a, p.saddr);
+        ct_select(false, false, a.fw != 0, ingress, a.allow_logic != 0, ldst, lsrc, a.empty_mask, a.drop_mask, cc, pass,
+                  labeled);
+      }
+      const CtWalkOut wo = ct_walk_rec(f, cc, pass, labeled, rid * 2 | static_cast<int32_t>(verdict), a.ct_sentinel);
+      u32x4 *d = reinterpret_cast<u32x4 *>(a.ct_brec) + 2 * i;
+      d[0] = u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]};
+      d[1] = u32x4{wo.w[4], wo.w[5], wo.w[6], wo.w[7]};
+      a.ct_keys[i] = wo.key;
+      a.ct_lcs[i] = wo.lcs;
     }
     // ---- counters ----
     if (PCN_ABLATE == 4) return;
@@ -1702,6 +1743,11 @@ int launch_classify(const LaunchArgs &a, bool fixed, int ch, int ns, int num_cus
       if (!a.offsets) { c.frames = a.frames + base * a.stride; c.frames_bytes = a.frames_bytes - base * a.stride; }
       else c.offsets = a.offsets + base;
       if (a.lens) c.lens = a.lens + base;
+      if (a.ct_brec) {
+        c.ct_brec = a.ct_brec + base * 8;
+        c.ct_keys = a.ct_keys + base;
+        c.ct_lcs = a.ct_lcs + base;
+      }
       if (a.has_in_port) c.in_port = a.in_port + base;
       if (a.has_ct) c.ct_status = a.ct_status + base;
       c.verdicts = a.verdicts + base;

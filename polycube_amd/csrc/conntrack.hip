@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "conntrack.hpp"
+#include "devchain.h"
 #include "radix.hpp"
 #include "pcn_ipt.h"
 
@@ -36,6 +37,9 @@ namespace pcn {
 namespace {
 
 enum : uint8_t { K_NONE = 0, K_INV, K_TCP, K_UDP, K_ECHO, K_REPLY, K_ERR, K_HARD };
+static_assert(K_INV == kCtKInv && K_TCP == kCtKTcp && K_UDP == kCtKUdp && K_ECHO == kCtKEcho &&
+                  K_REPLY == kCtKReply && K_ERR == kCtKErr && K_HARD == kCtKHard,
+              "record kinds as devchain.h numbers them");
 enum { ST_NEW = 0, ST_EST, ST_REL, ST_INV, ST_SYN_SENT, ST_SYN_RECV, ST_FIN_WAIT_1, ST_FIN_WAIT_2, ST_LAST_ACK,
        ST_TIME_WAIT };
 constexpr uint8_t FIN = 0x01, SYN = 0x02, RST = 0x04, ACK = 0x10;
@@ -161,11 +165,7 @@ __device__ __forceinline__ bool localip_has(const CtBatch &b, uint32_t ip) {
 }
 
 __device__ __forceinline__ uint64_t key_hash(uint32_t src, uint32_t dst, uint8_t proto, uint16_t sp, uint16_t dp) {
-  uint64_t h = ((uint64_t(src) << 32) | dst) * 0x9E3779B97F4A7C15ull;
-  h ^= ((uint64_t(proto) << 32) | (uint64_t(sp) << 16) | dp) * 0xC2B2AE3D27D4EB4Full;
-  h ^= h >> 29;
-  h *= 0xBF58476D1CE4E5B9ull;
-  return h ^ (h >> 32);
+  return ct_key_hash(src, dst, proto, sp, dp);     // devchain.h (the classify kernel's stage A uses it too)
 }
 
 // A packet's walk record in HBM (32 B), written by ct_prep in batch order and
@@ -419,90 +419,52 @@ __global__ __launch_bounds__(kPrepBlock) PCN_CT_PREP_ATTR void ct_prep_kernel(Ct
     }
     PackedRec pr;
     if (valid) {
-      CtRec r{};
-      r.len = static_cast<uint16_t>(p.L);
-      r.kind = K_NONE;
+      // the record (devchain.h ct_walk_rec: the classify kernel's stage A
+      // builds the same one when it writes the records itself)
       uint32_t chain = 3;
-      bool pass = false;
+      bool pass = false, labeled = false;
       if (p.status == 2) {
-        bool labeled = true;
         // a Horus hit (stage A found it: the same for every label) skips the
         // ChainSelector / ChainForwarder: DROP is final, ACCEPT is PASS_LABELING
         // (Horus_dp.c:150-160; Firewall_Horus_dp.c:151-161), or final for a
-        // pcn-firewall program built with conntrack off (:162-164)
+        // pcn-firewall program built with conntrack off (:162-164).
+        // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder; an empty
+        // chain goes to DefaultAction after labelling, which stage A resolved.
         const bool horus = rid0 <= PCN_IPT_RID_HORUS0;
-        if (horus) {
-          if (ver0 == PCN_IPT_ACCEPT && !b.horus_final) pass = true;
-          else labeled = false;
-        } else if (b.fw) {
-          // pcn-firewall: Parser -> ConntrackLabel -> ChainForwarder
-          // (Firewall_ChainForwarder_dp.c:20-42).  An empty chain goes to
-          // DefaultAction after labelling, which stage A already resolved.
-          chain = b.direction == PCN_IPT_INGRESS ? PCN_IPT_FORWARD : PCN_IPT_OUTPUT;
-        } else if (b.direction == PCN_IPT_INGRESS) {
-          if (b.allow_logic) pass = true;
-          else chain = (b.nlocal && localip_has(b, p.dst)) ? PCN_IPT_INPUT : PCN_IPT_FORWARD;
-        } else if (b.nlocal && localip_has(b, p.src)) {
-          chain = PCN_IPT_OUTPUT;
-        } else {
-          labeled = false;                                   // egress PASS, no labeling
-        }
-        if (!b.fw && labeled && chain < 3 && ((b.empty_mask >> chain) & 1)) {
-          if ((b.drop_mask >> chain) & 1) labeled = false;  // DROP_NO_LABELING (default counters)
-          else pass = true;                                  // PASS_LABELING
-        }
-        if (labeled) {
-          // the shared `packet` struct: ports stale for anything but TCP/UDP (Q4)
-          const uint32_t ports = p.ports_ok ? own : stale;
-          const uint16_t sp = static_cast<uint16_t>(ports & 0xffff), dp = static_cast<uint16_t>(ports >> 16);
-          // ConntrackLabel_dp.c:200-228
-          uint8_t ipRev, portRev;
-          if (p.src <= p.dst) { r.src = p.src; r.dst = p.dst; ipRev = 0; }
-          else { r.src = p.dst; r.dst = p.src; ipRev = 1; }
-          if (sp < dp) { r.sport = sp; r.dport = dp; portRev = 0; }
-          else if (sp > dp) { r.sport = dp; r.dport = sp; portRev = 1; }
-          else { r.sport = sp; r.dport = dp; portRev = ipRev; }
-          r.proto = p.proto;
-          r.rev = static_cast<uint8_t>(ipRev | (portRev << 1));
-          r.seq = p.seq;
-          r.ack = p.ack;
-          r.flags = p.flags;
-          r.icmp = p.icmp;
-          if (p.proto == 6) r.kind = K_TCP;
-          else if (p.proto == 17) r.kind = K_UDP;
-          else if (p.proto == 1) {
-            if (p.L < 42) r.kind = K_NONE;                   // RX_DROP (:441-443)
-            else if (p.icmp == 8) r.kind = K_ECHO;
-            else if (p.icmp == 0) r.kind = p.L >= 70 ? K_HARD : K_REPLY;
-            else if (p.icmp >= 13 && p.icmp <= 18) r.kind = K_INV;
-            else if (p.L < 70) r.kind = K_NONE;              // RX_DROP (:486-505)
-            else r.kind = K_ERR;
-            if (r.kind == K_ERR || r.kind == K_HARD) {      // the quoted header's key (:491-529)
-              const uint32_t qs = p.isrc <= p.idst ? p.isrc : p.idst, qd = p.isrc <= p.idst ? p.idst : p.isrc;
-              const uint16_t qa = p.isport <= p.idport ? p.isport : p.idport;
-              const uint16_t qb = p.isport <= p.idport ? p.idport : p.isport;
-              if (r.kind == K_ERR) {
-                r.src = qs; r.dst = qd; r.sport = qa; r.dport = qb; r.proto = p.iproto;
-              } else {
-                r.seq = qs; r.ack = qd; r.flags = p.iproto; r.iports = uint32_t(qa) | (uint32_t(qb) << 16);
-              }
-            }
-          } else {
-            r.kind = K_INV;                                  // :562-566
-          }
-        }
+        const bool ingress = b.direction == PCN_IPT_INGRESS;
+        const bool local_dst = !b.fw && ingress && !b.allow_logic && b.nlocal && localip_has(b, p.dst);
+        const bool local_src = !b.fw && !ingress && b.nlocal && localip_has(b, p.src);
+        ct_select(horus, ver0 == PCN_IPT_ACCEPT && !b.horus_final, b.fw, ingress, b.allow_logic, local_dst, local_src,
+                  b.empty_mask, b.drop_mask, chain, pass, labeled);
       }
-      r.cinfo = static_cast<uint8_t>((chain & 3) | (pass ? 4 : 0));
-      const bool member = r.kind >= K_TCP && r.kind <= K_ERR;
-      const uint32_t key = member ? static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel)
-                                  : sentinel;
-      keys[i] = key;
-      lcs[i] = uint32_t(r.len) | uint32_t(r.cinfo) << 16;   // what ct_count reads (not the 64-byte record)
+      CtFrame f;
+      f.status = static_cast<uint32_t>(p.status);
+      f.ports_ok = p.ports_ok;
+      f.L = p.L;
+      f.src = p.src;
+      f.dst = p.dst;
+      f.seq = p.seq;
+      f.ack = p.ack;
+      f.own = own;
+      f.stale = stale;
+      f.proto = p.proto;
+      f.flags = p.flags;
+      f.icmp = p.icmp;
+      f.isrc = p.isrc;
+      f.idst = p.idst;
+      f.iproto = p.iproto;
+      f.isport = p.isport;
+      f.idport = p.idport;
       const int32_t o0 = b.nlab ? (rid0 * 2) | ver0 : 0;   // pack_outcome(b, 0, i)
-      pr = pack_rec(r, o0);
+      const CtWalkOut wo = ct_walk_rec(f, chain, pass, labeled, o0, sentinel);
+      const bool member = wo.kind >= K_TCP && wo.kind <= K_ERR;
+      keys[i] = wo.key;
+      lcs[i] = wo.lcs;                                  // what ct_count reads (not the 64-byte record)
       if (b.nlab == 4)
         ox[i] = ct_u32x4{static_cast<uint32_t>(o0), static_cast<uint32_t>(pack_outcome(b, 1, i)),
                          static_cast<uint32_t>(pack_outcome(b, 2, i)), static_cast<uint32_t>(pack_outcome(b, 3, i))};
+      static_assert(sizeof(PackedRec) == sizeof(wo.w), "the walk record is 8 words");
+      __builtin_memcpy(&pr, wo.w, sizeof(pr));
 #if PCN_CT_PREP_LDS
       if (fast) {                                       // this lane's record into its LDS row
         union {
@@ -518,13 +480,13 @@ __global__ __launch_bounds__(kPrepBlock) PCN_CT_PREP_ATTR void ct_prep_kernel(Ct
 #else
       store_prec(&brec[i], pr);
 #endif
-      if (r.kind == K_HARD) hard_list[atomicAdd(hard_cnt, 1u)] = static_cast<uint32_t>(i);
+      if (wo.kind == K_HARD) hard_list[atomicAdd(hard_cnt, 1u)] = static_cast<uint32_t>(i);
       // every packet's outcome as far as it is known here, coalesced: final for
       // those with no table access (label INVALID for K_INV, else any label);
       // the label-0 one for the rest, which the walk overwrites only where it
       // differs (put_outcome)
       // (one label: stage A wrote its outcomes into the final arrays themselves)
-      const bool l3 = !member && r.kind == K_INV && !pass && b.nlab == 4;
+      const bool l3 = !member && wo.kind == K_INV && !pass && b.nlab == 4;
       if (!a0_final) {
         b.verdicts[i] = l3 ? b.a_verdict[3 * b.n + i] : ver0;
         b.rule_ids[i] = l3 ? b.a_rid[3 * b.n + i] : rid0;
@@ -984,7 +946,7 @@ __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const
          w += uint64_t(gridDim.x) * blockDim.x)
       bm[w] = 0;
   __shared__ uint32_t cnt[kRunClasses], base[kRunClasses];
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
+  if (desc && blockIdx.x == 0 && threadIdx.x < 64) {   // (null: stage A advanced it)
     const uint32_t c = ports_lookback(desc, (n + 63) / 64, carry);
     if (threadIdx.x == 0) *carry = c;
   }
@@ -2542,19 +2504,34 @@ int ct_advance_carry(const CtBatch &b, CtScratch &s, uint32_t *carry, int num_cu
   return hipSuccess;
 }
 
-int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream) {
-  if (b.n == 0) return hipSuccess;
-  if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);   // 32-bit item indices (radix.hip)
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  // key buckets: 2^kbits >= n (a 2^24 batch sorts 24-bit keys in three 8-bit
-  // passes; 2^kbits >= 2n gave 25 bits and a 9-bit first pass, +20 us, for half
-  // the bucket collisions between connections, which the walk takes in passes)
+// key buckets: 2^kbits >= n (a 2^24 batch sorts 24-bit keys in three 8-bit
+// passes; 2^kbits >= 2n gave 25 bits and a 9-bit first pass, +20 us, for half
+// the bucket collisions between connections, which the walk takes in passes)
 #ifndef PCN_CT_KEY_SLACK
 #define PCN_CT_KEY_SLACK 1
 #endif
+static uint32_t key_bits(uint64_t n) {
   uint32_t kbits = 8;
-  while (kbits < 30 && (uint64_t(1) << kbits) < PCN_CT_KEY_SLACK * b.n) ++kbits;
-  kbits = std::min(kbits, debug_key_bits());
+  while (kbits < 30 && (uint64_t(1) << kbits) < PCN_CT_KEY_SLACK * n) ++kbits;
+  return std::min(kbits, debug_key_bits());
+}
+
+int ct_prep_buffers(CtScratch &s, uint64_t n, uint32_t **brec, uint32_t **keys, uint32_t **lcs, uint32_t *sentinel) {
+  if (n == 0 || n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);
+  const uint32_t kbits = key_bits(n);
+  CT_CHECK(grow(s, n, kbits, false));
+  *brec = reinterpret_cast<uint32_t *>(s.brec);
+  *keys = s.keys;
+  *lcs = s.lcs;
+  *sentinel = (1u << kbits) - 1;
+  return hipSuccess;
+}
+
+int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream, bool prepped) {
+  if (b.n == 0) return hipSuccess;
+  if (b.n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);   // 32-bit item indices (radix.hip)
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint32_t kbits = key_bits(b.n);
   const uint32_t sentinel = (1u << kbits) - 1;
   CT_CHECK(grow(s, b.n, kbits, b.nlab == 4));
   const unsigned blk = 256, grid = grid_for(b.n, blk, num_cus);
@@ -2570,11 +2547,13 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
     CT_CHECK(hipMemsetAsync(s.bm, 0, s.bm_bytes, st));
   }
   s.dirty = true;
-  const uint32_t pchunk = prep_chunk(b.n, num_cus);
-  const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
-  hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.ox, s.lcs, s.keys, kbits,
-                     s.ctl + kCtlHard, s.hard_list, s.pdesc, s.ctl + kCtlChunk, pchunk);
-  CT_CHECK(hipGetLastError());
+  if (!prepped) {
+    const uint32_t pchunk = prep_chunk(b.n, num_cus);
+    const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));
+    hipLaunchKernelGGL(ct_prep_kernel, dim3(pgrid), dim3(kPrepBlock), 0, st, b, t.carry, s.brec, s.ox, s.lcs, s.keys,
+                       kbits, s.ctl + kCtlHard, s.hard_list, s.pdesc, s.ctl + kCtlChunk, pchunk);
+    CT_CHECK(hipGetLastError());
+  }
   // long echo replies join their own key's run unless their quoted key's
   // bucket is in the batch (each kernel returns at once without replies)
   const uint64_t bm_words = (uint64_t(1) << kbits) / 32;
@@ -2591,7 +2570,7 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   const uint32_t hper = heads_per(b.n, num_cus);
   const uint64_t htile = uint64_t(hper) * kHeadsBlock;
   hipLaunchKernelGGL(ct_heads_kernel, dim3(static_cast<unsigned>((b.n + htile - 1) / htile)), dim3(kHeadsBlock), 0, st,
-                     b.n, s.keys2, s.heads, s.ctl + kCtlClass, sentinel, hper, s.pdesc, t.carry, s.cuts,
+                     b.n, s.keys2, s.heads, s.ctl + kCtlClass, sentinel, hper, prepped ? nullptr : s.pdesc, t.carry, s.cuts,
                      s.ctl + kCtlSegN, s.ctl + kCtlHard, s.bm, bm_words);
   CT_CHECK(hipGetLastError());
   // (the walk plan is computed on the device from ct_heads' counts, in the walk

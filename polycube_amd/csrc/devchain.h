@@ -222,6 +222,14 @@ struct LaunchArgs {
   // each frame's rule-stage fields here (16 B a frame, kSplitNeed in the top
   // byte when the frame runs rules) and the rule kernel reads them back.
   uint32_t *split_rec;           // [n][4] u32; null: one fused kernel
+  // Stage A of a stateful batch that also writes the walk records (pcn_ipt.cpp
+  // ct_fused_prep; conntrack.hip then skips ct_prep): per frame its 32-byte
+  // record (CtWalkOut::w), its key bucket and its {len, cinfo} word.  Null
+  // otherwise.  Launches with these set track the stale ports (has_stale).
+  uint32_t *ct_brec;             // [n][8] u32
+  uint32_t *ct_keys;             // [n]
+  uint32_t *ct_lcs;              // [n]
+  uint32_t ct_sentinel;          // the key bucket of packets without one (2^kbits - 1)
 };
 // split_rec word 3: proto | flags << 8 | ct << 16 | meta << 24, meta = chain (2 bits)
 // | outer VLAN tag stripped (bit 2: the rule kernel's length is lens - 4) | kSplitNeed
@@ -241,6 +249,142 @@ struct CopyBound {
   int (*fold)(void *ctx, void *stream);   // stream: a hipStream_t
   void *ctx;
 };
+
+// ---- conntrack walk records -------------------------------------------
+// The record of a packet in the stateful pipeline (conntrack.hip): built by
+// ct_prep, or -- in a batch whose frames are all shorter than 70 bytes, so no
+// ICMP header quotes another, and with one label -- by the classify kernel's
+// stage-A launch itself, which then is the batch's only pass over the frames.
+// Both go through the two functions below, restated from
+// Iptables_ChainSelector_dp.c:131-298 (Firewall_ChainForwarder_dp.c:20-42) and
+// Iptables_ConntrackLabel_dp.c:190-531.
+// Record kinds (conntrack.hip K_*): the same numbering.
+constexpr uint32_t kCtKNone = 0, kCtKInv = 1, kCtKTcp = 2, kCtKUdp = 3, kCtKEcho = 4, kCtKReply = 5, kCtKErr = 6,
+                   kCtKHard = 7;
+
+// What a record is built from: the Parser's fields as conntrack.hip's parse
+// reads them (multi-byte fields are little-endian loads of network-order bytes).
+struct CtFrame {
+  uint32_t status;               // 0 RX_DROP in the parser, 1 not IPv4 (pass), 2 IPv4 parsed
+  uint32_t ports_ok;             // the Parser wrote srcPort / dstPort (TCP / UDP)
+  uint32_t L, src, dst, seq, ack;
+  uint32_t own, stale;           // wire bytes 34-37 of this frame; the shared struct's ports (Q4)
+  uint32_t proto, flags, icmp;
+  uint32_t isrc, idst, iproto, isport, idport;   // the quoted header (ICMP errors, long echo replies)
+};
+
+// ChainSelector (pcn-iptables) / ChainForwarder (pcn-firewall) as the
+// conntrack labels see it: the chain a labelled packet's rules come from (3:
+// none), PASS_LABELING, or no labelling at all.  horus: stage A found a Horus
+// hit (DROP: final; ACCEPT: PASS_LABELING unless horus_final).
+PCN_HD inline void ct_select(bool horus, bool horus_pass, bool fw, bool ingress, bool allow_logic, bool local_dst,
+                             bool local_src, uint32_t empty_mask, uint32_t drop_mask, uint32_t &chain, bool &pass,
+                             bool &labeled) {
+  chain = 3;
+  pass = false;
+  labeled = true;
+  if (horus) {
+    if (horus_pass) pass = true;
+    else labeled = false;
+  } else if (fw) {
+    chain = ingress ? 1u : 2u;                     // INGRESS / EGRESS in the FORWARD / OUTPUT slots
+  } else if (ingress) {
+    if (allow_logic) pass = true;
+    else chain = local_dst ? 0u : 1u;              // INPUT / FORWARD
+  } else if (local_src) {
+    chain = 2u;                                    // OUTPUT
+  } else {
+    labeled = false;                               // egress PASS, no labelling
+  }
+  if (!fw && labeled && chain < 3 && ((empty_mask >> chain) & 1)) {
+    if ((drop_mask >> chain) & 1) labeled = false; // DROP_NO_LABELING (default counters)
+    else pass = true;                              // PASS_LABELING
+  }
+}
+
+PCN_HD inline uint64_t ct_key_hash(uint32_t src, uint32_t dst, uint32_t proto, uint32_t sp, uint32_t dp) {
+  uint64_t h = ((uint64_t(src) << 32) | dst) * 0x9E3779B97F4A7C15ull;
+  h ^= ((uint64_t(proto) << 32) | (uint64_t(sp) << 16) | dp) * 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 32);
+}
+
+// The 32-byte walk record (conntrack.hip PackedRec: src, dst, sport | dport
+// << 16, seq, ack, iports, proto | flags << 8 | kind << 16 | (rev | cinfo <<
+// 2) << 24, o0), its key bucket (sentinel: no table access) and the {len,
+// cinfo} word ct_count reads.  The key orders the addresses and ports
+// (ConntrackLabel_dp.c:200-228); an ICMP packet's ports are the stale ones
+// (Q4); an ICMP error keys on the header it quotes, a long echo reply keeps
+// that header's key for its ICMP_MISS lookup (:491-529).
+struct CtWalkOut {
+  uint32_t w[8];
+  uint32_t key, lcs;
+  uint32_t kind;
+};
+PCN_HD inline CtWalkOut ct_walk_rec(const CtFrame &p, uint32_t chain, bool pass, bool labeled, int32_t o0,
+                                    uint32_t sentinel) {
+  CtWalkOut o{};
+  uint32_t src = 0, dst = 0, sport = 0, dport = 0, seq = 0, ack = 0, iports = 0, proto = 0, flags = 0, rev = 0;
+  uint32_t kind = kCtKNone;
+  if (p.status != 2) {
+    chain = 3;
+    pass = false;
+    labeled = false;
+  }
+  if (labeled) {
+    const uint32_t ports = p.ports_ok ? p.own : p.stale;
+    const uint32_t sp = ports & 0xffffu, dp = ports >> 16;
+    uint32_t ipRev, portRev;
+    if (p.src <= p.dst) { src = p.src; dst = p.dst; ipRev = 0; }
+    else { src = p.dst; dst = p.src; ipRev = 1; }
+    if (sp < dp) { sport = sp; dport = dp; portRev = 0; }
+    else if (sp > dp) { sport = dp; dport = sp; portRev = 1; }
+    else { sport = sp; dport = dp; portRev = ipRev; }
+    proto = p.proto;
+    rev = ipRev | (portRev << 1);
+    seq = p.seq;
+    ack = p.ack;
+    flags = p.flags;
+    if (p.proto == 6) kind = kCtKTcp;
+    else if (p.proto == 17) kind = kCtKUdp;
+    else if (p.proto == 1) {
+      if (p.L < 42) kind = kCtKNone;                 // RX_DROP (:441-443)
+      else if (p.icmp == 8) kind = kCtKEcho;
+      else if (p.icmp == 0) kind = p.L >= 70 ? kCtKHard : kCtKReply;
+      else if (p.icmp >= 13 && p.icmp <= 18) kind = kCtKInv;
+      else if (p.L < 70) kind = kCtKNone;            // RX_DROP (:486-505)
+      else kind = kCtKErr;
+      if (kind == kCtKErr || kind == kCtKHard) {    // the quoted header's key
+        const uint32_t qs = p.isrc <= p.idst ? p.isrc : p.idst, qd = p.isrc <= p.idst ? p.idst : p.isrc;
+        const uint32_t qa = p.isport <= p.idport ? p.isport : p.idport;
+        const uint32_t qb = p.isport <= p.idport ? p.idport : p.isport;
+        if (kind == kCtKErr) {
+          src = qs; dst = qd; sport = qa; dport = qb; proto = p.iproto;
+        } else {
+          seq = qs; ack = qd; flags = p.iproto; iports = qa | (qb << 16);
+        }
+      }
+    } else {
+      kind = kCtKInv;                                // :562-566
+    }
+  }
+  const uint32_t cinfo = (chain & 3u) | (pass ? 4u : 0u);
+  const bool member = kind >= kCtKTcp && kind <= kCtKErr;
+  o.key = member ? static_cast<uint32_t>(ct_key_hash(src, dst, proto & 0xffu, sport & 0xffffu, dport & 0xffffu) % sentinel)
+                 : sentinel;
+  o.lcs = (p.L & 0xffffu) | cinfo << 16;
+  o.w[0] = src;
+  o.w[1] = dst;
+  o.w[2] = (sport & 0xffffu) | (dport & 0xffffu) << 16;
+  o.w[3] = seq;
+  o.w[4] = ack;
+  o.w[5] = iports;
+  o.w[6] = (proto & 0xffu) | (flags & 0xffu) << 8 | kind << 16 | (rev | cinfo << 2) << 24;
+  o.w[7] = static_cast<uint32_t>(o0);
+  o.kind = kind;
+  return o;
+}
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)
 #define PCN_FW_LAUNCH_CT_OFF 1     // DISABLED: no ConntrackLabel stage

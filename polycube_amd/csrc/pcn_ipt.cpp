@@ -122,6 +122,16 @@ bool multi_block_deal2() {
 // PCN_IPT_DEBUG_SPLIT=1 in the environment (read per context, for the tests'
 // and the A/B's sake).  PCN_IPT_DEBUG_SPLIT_WG: the gather kernel's
 // workgroups per CU (default 6: its ~75 VGPRs allow 6 waves per SIMD).
+// PCN_IPT_DEBUG_CT_FUSED=0: stateful batches always run ct_prep (A/B of the
+// stage A that writes the walk records)
+bool ct_fused_prep() {
+  static const bool v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_CT_FUSED");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 bool split_env() {
   const char *e = std::getenv("PCN_IPT_DEBUG_SPLIT");
   return e && std::atoi(e) == 1;
@@ -308,6 +318,7 @@ struct pcn_ipt {
   uint32_t *d_split_rec = nullptr;
   uint64_t split_cap = 0;
   bool split = false;                      // split launches allowed (PCN_IPT_DEBUG_SPLIT=1 at creation)
+  uint64_t ct_fused_batches = 0;           // stateful batches whose stage A wrote the walk records
   uint64_t launches_split = 0;
 };
 
@@ -1062,6 +1073,10 @@ struct StageA {
   const uint8_t *ct;
   uint8_t *verdicts;
   int32_t *rule_ids;
+  // non-null: this stage A also writes the walk records (conntrack.hpp
+  // ct_prep_buffers), so ct_run skips ct_prep
+  uint32_t *brec = nullptr, *keys = nullptr, *lcs = nullptr;
+  uint32_t sentinel = 0;
 };
 
 // carry_out (stateless batches that track the stale ports): when the kernel
@@ -1246,6 +1261,51 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     // outcome, and stage A's counters went to discarded scratch (their LDS adds,
     // ballots and the flush into one block were pure cost)
     if (sa && !debug_stage_a_counts()) a.count_mask = 0;
+    // The Parser's stale ports (Q4) computed in the kernel (has_stale): one
+    // word per 64-frame group of the batch, a start counter, the carry in and
+    // (on the batch's last launch) out.
+    auto track_stale = [&]() {
+      if (plan) {
+        a.has_stale = 1;
+        return;
+      }
+      // the key reads ports: stale ones (Q4) computed in the kernel
+      // one word per 64-frame group of the batch (+1 for the look-back from
+      // the end); the kernel publishes only groups that hold frames
+      const size_t groups = b->n / 64 + 1;
+      if (ctx->stale_groups < groups) {
+        if (ctx->d_stale_desc) hip_check(hipFree(ctx->d_stale_desc), "hipFree");
+        ctx->d_stale_desc = nullptr;
+        // + kStaleCanary guard words past the groups (pcn_ipt_debug_stale_canary)
+        hip_check(hipMalloc(&ctx->d_stale_desc, (groups + kStaleCanary) * 8), "hipMalloc(stale groups)");
+        hip_check(hipMemset(ctx->d_stale_desc, 0, groups * 8), "hipMemset(stale groups)");
+        hip_check(hipMemset(ctx->d_stale_desc + groups, kStaleCanaryByte, kStaleCanary * 8), "hipMemset(canary)");
+        ctx->stale_groups = groups;
+        ctx->stale_epoch = 0;
+      }
+      if (debug_stale_canary() && groups < ctx->stale_groups)
+        // test hook: guard every word past this batch's groups, not only those
+        // past the largest batch so far
+        hip_check(hipMemsetAsync(ctx->d_stale_desc + groups, kStaleCanaryByte, (ctx->stale_groups - groups) * 8,
+                                 static_cast<hipStream_t>(stream)), "hipMemset(canary)");
+      ctx->stale_guard_from = debug_stale_canary() ? groups : ctx->stale_groups;
+      if (!ctx->d_chunk_ctr) {   // zero from here on: each launch's last workgroup resets it
+        hip_check(hipMalloc(&ctx->d_chunk_ctr, 64), "hipMalloc(chunk counter)");
+        hip_check(hipMemset(ctx->d_chunk_ctr, 0, 64), "hipMemset(chunk counter)");
+      }
+      if (++ctx->stale_epoch >= (1u << 24)) {       // words of an old epoch must never match
+        hip_check(hipMemsetAsync(ctx->d_stale_desc, 0, ctx->stale_groups * 8, static_cast<hipStream_t>(stream)),
+                  "hipMemset(stale groups)");
+        ctx->stale_epoch = 1;
+      }
+      a.has_stale = 1;
+      a.stale_desc = ctx->d_stale_desc;
+      a.stale_carry = carry;
+      a.chunk_ctr = ctx->d_chunk_ctr;
+      a.stale_epoch = ctx->stale_epoch;
+      a.carry_out = carry_out;
+      if (carried) *carried = carry_out != nullptr;
+    };
     // Horus: the program the batch's Parser calls, while one is in place
     if (const HorusProg *hz = horus_of_batch(ctx, b->direction)) {
       a.horus = hz->d_tab;
@@ -1260,46 +1320,16 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
         if (ctx->fw_ct_mode == PCN_FW_CT_DISABLED) a.horus_flags |= kHzMissDrops;   // :170-174
       }
       a.fast_chain = -1;                               // the lookup lives in the general path
-      if (plan && carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) {
-        a.has_stale = 1;
-      } else if (carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) {
-        // the key reads ports: stale ones (Q4) computed in the kernel
-        // one word per 64-frame group of the batch (+1 for the look-back from
-        // the end); the kernel publishes only groups that hold frames
-        const size_t groups = b->n / 64 + 1;
-        if (ctx->stale_groups < groups) {
-          if (ctx->d_stale_desc) hip_check(hipFree(ctx->d_stale_desc), "hipFree");
-          ctx->d_stale_desc = nullptr;
-          // + kStaleCanary guard words past the groups (pcn_ipt_debug_stale_canary)
-          hip_check(hipMalloc(&ctx->d_stale_desc, (groups + kStaleCanary) * 8), "hipMalloc(stale groups)");
-          hip_check(hipMemset(ctx->d_stale_desc, 0, groups * 8), "hipMemset(stale groups)");
-          hip_check(hipMemset(ctx->d_stale_desc + groups, kStaleCanaryByte, kStaleCanary * 8), "hipMemset(canary)");
-          ctx->stale_groups = groups;
-          ctx->stale_epoch = 0;
-        }
-        if (debug_stale_canary() && groups < ctx->stale_groups)
-          // test hook: guard every word past this batch's groups, not only those
-          // past the largest batch so far
-          hip_check(hipMemsetAsync(ctx->d_stale_desc + groups, kStaleCanaryByte, (ctx->stale_groups - groups) * 8,
-                                   static_cast<hipStream_t>(stream)), "hipMemset(canary)");
-        ctx->stale_guard_from = debug_stale_canary() ? groups : ctx->stale_groups;
-        if (!ctx->d_chunk_ctr) {   // zero from here on: each launch's last workgroup resets it
-          hip_check(hipMalloc(&ctx->d_chunk_ctr, 64), "hipMalloc(chunk counter)");
-          hip_check(hipMemset(ctx->d_chunk_ctr, 0, 64), "hipMemset(chunk counter)");
-        }
-        if (++ctx->stale_epoch >= (1u << 24)) {       // words of an old epoch must never match
-          hip_check(hipMemsetAsync(ctx->d_stale_desc, 0, ctx->stale_groups * 8, static_cast<hipStream_t>(stream)),
-                    "hipMemset(stale groups)");
-          ctx->stale_epoch = 1;
-        }
-        a.has_stale = 1;
-        a.stale_desc = ctx->d_stale_desc;
-        a.stale_carry = carry;
-        a.chunk_ctr = ctx->d_chunk_ctr;
-        a.stale_epoch = ctx->stale_epoch;
-        a.carry_out = carry_out;
-        if (carried) *carried = carry_out != nullptr;
-      }
+      if (carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) track_stale();
+    }
+    // stage A of a stateful batch that writes the walk records (ct_fused_prep):
+    // its records need every frame's stale ports too
+    if (sa && sa->brec) {
+      a.ct_brec = sa->brec;
+      a.ct_keys = sa->keys;
+      a.ct_lcs = sa->lcs;
+      a.ct_sentinel = sa->sentinel;
+      if (!a.has_stale) track_stale();
     }
     // slot count of the chain program (the generic kernel always runs 6)
     const int ns = ch < 3 ? static_cast<int>(a.ch[ch].lay.nslots) : 6;
@@ -1314,7 +1344,7 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       shape.ch = ch;
       shape.ns = ns;
       shape.inputs = (a.has_in_port ? 1 : 0) | (a.has_ct && !sa ? 2 : 0) | (sa ? 4 : 0) | (a.has_stale ? 8 : 0) |
-                     (a.horus_fields ? 16 : 0) | (a.offsets ? 32 : 0) | (a.lens ? 64 : 0);
+                     (a.horus_fields ? 16 : 0) | (a.offsets ? 32 : 0) | (a.lens ? 64 : 0) | (a.ct_brec ? 128 : 0);
       shape.deal2 = deal2;
       shape.split = !fixed && !sa && !a.has_stale && !a.horus_fields && a.ch[ch].lay.part_dense && ctx->split &&
                     !debug_clocks();
@@ -1573,9 +1603,21 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
       a_rid = rids;
       a_v = b->verdicts;
     }
+    // Frames shorter than 70 bytes (no ICMP header can quote another) with
+    // one label and no Horus program: stage A builds the walk records, key
+    // buckets and {len, cinfo} words itself (devchain.h ct_walk_rec) and
+    // advances the carry, and ct_run skips ct_prep -- the batch's frames are
+    // read once instead of twice (PCN_IPT_DEBUG_CT_FUSED=0: ct_prep, A/B).
+    const bool fused = nlab == 1 && !hz && !b->offsets && !b->lens && b->fixed_len < 70 &&
+                       b->hook == PCN_IPT_HOOK_XDP && n < 0x7FFFFFFFull && ct_fused_prep();
+    if (!ctx->cts) ctx->cts = ct_scratch_new();
     for (uint32_t l = 0; l < nlab; ++l) {
       StageA sa{ctx->d_labels + l, a_v + l * n, a_rid + l * n};
-      int rc = launch_batch(ctx, b, stream, &sa, stale);
+      if (fused) {
+        const int e = ct_prep_buffers(*ctx->cts, n, &sa.brec, &sa.keys, &sa.lcs, &sa.sentinel);
+        if (e != hipSuccess) return fail(-EIO, std::string("conntrack buffers: ") + hipGetErrorString(hipError_t(e)));
+      }
+      int rc = fused ? launch_batch(ctx, b, stream, &sa, carry, carry) : launch_batch(ctx, b, stream, &sa, stale);
       if (rc) return rc;
     }
     // pcn-firewall AUTOMATIC: ESTABLISHED packets are accepted before the chain
@@ -1588,8 +1630,9 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     cb.a_verdict = a_v;
     cb.a_rid = a_rid;
     cb.rule_ids = rids;
-    const int e = ct_run(cb, ctx->ct, *ctx->cts, ctx->num_cus, st);
+    const int e = ct_run(cb, ctx->ct, *ctx->cts, ctx->num_cus, st, fused);
     if (e != hipSuccess) return fail(-EIO, std::string("conntrack: ") + hipGetErrorString(hipError_t(e)));
+    if (fused) ++ctx->ct_fused_batches;
     return mark();
   });
 }
@@ -2164,6 +2207,7 @@ int pcn_ipt_ct_get_info(pcn_ipt *ctx, pcn_ipt_ct_info *out) {
       hip_check(hipMemcpy(st, ctx->ct.stats, 16, hipMemcpyDeviceToHost), "hipMemcpy(conntrack stats)");
       out->inserts_lost = st[0];
       out->evicted = st[1];
+      out->fused_batches = ctx->ct_fused_batches;
     }
     out->max_entries = ctx->ct.max_entries;
     return 0;

@@ -84,7 +84,8 @@ class ChainInfo(C.Structure):
 
 class CtInfo(C.Structure):
     _fields_ = [("enabled", C.c_uint32), ("capacity_log2", C.c_uint32), ("now", C.c_uint64),
-                ("inserts_lost", C.c_uint64), ("max_entries", C.c_uint64), ("evicted", C.c_uint64)]
+                ("inserts_lost", C.c_uint64), ("max_entries", C.c_uint64), ("evicted", C.c_uint64),
+                ("fused_batches", C.c_uint64)]
 
 
 class CommInfo(C.Structure):

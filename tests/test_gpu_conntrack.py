@@ -215,6 +215,54 @@ def test_stateless_accept_established_with_given_labels(dev):
     assert st[0][1] == int((r_o == -3).sum())
 
 
+@pytest.mark.parametrize("setup", ["forward", "local_in_out", "allow_logic", "empty_input_drop"])
+def test_stage_a_builds_the_walk_records(dev, setup):
+    """Batches of 64-byte frames with one label: the classify pass (stage A) builds
+    the walk records, key buckets and {len, cinfo} words itself (devchain.h
+    ct_walk_rec) and advances the stale-port carry, so ct_prep never runs and the
+    frames are read once.  ICMP-heavy traffic (each echo keys on the stale ports of
+    the last TCP/UDP frame before it, Q4, across 64-frame groups and batches), odd
+    batch sizes, noise, both directions, and chain selections: FORWARD only; local
+    addresses (INPUT / OUTPUT); allow logic (all PASS_LABELING); an empty INPUT
+    chain with DROP (DROP_NO_LABELING).  Bit-exact against the oracle: verdicts,
+    rule ids, counters and the whole table, and every batch took the fused path."""
+    from test_gpu_parity import ip_nbo
+    rs = synth.config_rules(3)
+    rules = rs.rules()
+    localip, chains, defaults = (), {1: rules}, {1: "DROP"}
+    if setup == "local_in_out":
+        localip = [ip_nbo(f"10.0.{k}.{k}") for k in range(40)]
+        chains = {0: rules[:300], 1: rules[300:], 2: rules[::3]}
+        defaults = {0: "ACCEPT", 1: "DROP", 2: "DROP"}
+    elif setup == "allow_logic":
+        chains, defaults = {2: rules[:100]}, {0: "ACCEPT", 1: "ACCEPT", 2: "ACCEPT"}
+    elif setup == "empty_input_drop":
+        localip = [ip_nbo(f"10.0.{k}.{k}") for k in range(40)]
+        chains, defaults = {1: rules}, {0: "DROP", 1: "ACCEPT"}
+    o, ipt = ct_pair(chains, defaults, localip, cap_log2=18, jit=1)
+    rng = np.random.default_rng(7)
+    n = 1 << 18
+    f, _ = synth.flow_traffic(n, 3000, 11, stride=64, rs=rs, p_icmp=0.3, p_noise=0.1, p_err=0.05)
+    fr = f.reshape(n, 64)
+    if localip:
+        ips = rng.choice(np.array([(10 << 24) | (k << 16) | k for k in range(40)], np.uint32), size=n)
+        be = np.stack([(ips >> 24) & 255, (ips >> 16) & 255, (ips >> 8) & 255, ips & 255], axis=1).astype(np.uint8)
+        for col in (26, 30):
+            loc = rng.random(n) < 0.15
+            fr[loc, col:col + 4] = be[loc]
+    cuts = [0, 1, 64, 129, 1000, 1 << 16, (1 << 16) + 7, n]
+    nb = 0
+    for direction in (0, 1):
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, fr[lo:hi].reshape(-1), hi - lo, stride=64, direction=direction)
+            assert_same(v_o, r_o, v_g, r_g)
+            nb += 1
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert_ae(o, ipt)
+    assert ipt.ct_info()["fused_batches"] == nb, ipt.ct_info()
+
+
 def test_headline_size_flows_parity(dev):
     """2^22 packets of 2^16 interleaved flows, 64-byte frames, config-3 rules."""
     rs = synth.config_rules(3)
