@@ -117,6 +117,9 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 // records written with buffer stores every wave issues, so the hand-counted
 // header wait knows how many stores are younger than the loads it waits for.
 // (0: plain conditional stores, and a wait that also drains the next frame's loads)
+#ifndef PCN_DBG_CTREC
+#define PCN_DBG_CTREC 0  // measurement only: 1 = stage A builds the walk records but stores none, 2 = builds none
+#endif
 #ifndef PCN_STORE_COUNT
 #define PCN_STORE_COUNT 0
 #endif
@@ -1514,7 +1517,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // (frames shorter than 70 bytes and one label: what ct_prep would build
     // from a second read of the frames, devchain.h ct_walk_rec; the label-0
     // outcome is this launch's own)
-    if (kCtRec && (kCount || (a.ct_brec && valid))) {
+    if (kCtRec && PCN_DBG_CTREC != 2 && (kCount || (a.ct_brec && valid))) {
       CtFrame f{};
       const bool tcp = p.proto == 6;
       f.status = ps;
@@ -1539,7 +1542,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
                   labeled);
       }
       const CtWalkOut wo = ct_walk_rec(f, cc, pass, labeled, rid * 2 | static_cast<int32_t>(verdict), a.ct_sentinel);
-      if constexpr (kCount) {
+      if (PCN_DBG_CTREC == 1 && wo.key != 0x9E3779B9u) {
+        // measurement only: the record built, not stored (wrong results)
+      } else if constexpr (kCount) {
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]}, rs_v, static_cast<int>(32 * lane), 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{wo.w[4], wo.w[5], wo.w[6], wo.w[7]}, rs_v, static_cast<int>(32 * lane + 16),
                                                0, 0);
