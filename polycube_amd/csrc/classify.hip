@@ -120,6 +120,9 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 #ifndef PCN_DBG_CTREC
 #define PCN_DBG_CTREC 0  // measurement only: 1 = stage A builds the walk records but stores none, 2 = builds none
 #endif
+#ifndef PCN_CTREC_LDS
+#define PCN_CTREC_LDS 0  // stage A's walk records through the wave's LDS region, stored 1 KB per instruction
+#endif
 #ifndef PCN_STORE_COUNT
 #define PCN_STORE_COUNT 0
 #endif
@@ -1517,6 +1520,28 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // (frames shorter than 70 bytes and one label: what ct_prep would build
     // from a second read of the frames, devchain.h ct_walk_rec; the label-0
     // outcome is this launch's own)
+    // Its stale ports (Q4) without waiting on another workgroup: the group's
+    // ports word published, the ports of an earlier TCP / UDP frame of the
+    // group taken from it, and the lanes with none before them marked for
+    // conntrack.hip ct_stale_fix (uniform control flow: ballots over the wave)
+    bool ct_early = false;   // no TCP / UDP frame before this one in its group
+    uint64_t ct_g = 0;       // the group (uniform)
+    if (kCtRec && a.ct_pdesc) {
+      const bool wrote = valid && ps == 2 && (p.proto == 6 || p.proto == 17);
+      const uint64_t wm = __ballot(wrote);
+      const uint32_t last_pd = __shfl(own_pd, wm ? 63 - __builtin_clzll(wm) : 0);
+      const uint64_t g0 = (a.gbase + i) >> 6;
+      ct_g = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g0 >> 32))) << 32) |
+             static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g0)));
+      if (lane == 0 && valid)
+        a.ct_pdesc[ct_g] = ct_ports_word(wm ? kCtPortsLocal : kCtPortsNone, last_pd);
+      const uint64_t before = wm & ((1ull << lane) - 1);
+      stale = __shfl(own_pd, before ? 63 - __builtin_clzll(before) : 0);
+      ct_early = !before;
+    }
+    bool ct_fix = false;     // this lane's record waits for the ports before its group
+    constexpr bool kRecLds = PCN_CTREC_LDS && !kCount && PCN_DBG_CTREC == 0;
+    u32x4 rec0 = {}, rec1 = {};   // kRecLds: the record, stored after the block by the whole wave
     if (kCtRec && PCN_DBG_CTREC != 2 && (kCount || (a.ct_brec && valid))) {
       CtFrame f{};
       const bool tcp = p.proto == 6;
@@ -1541,6 +1566,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         ct_select(false, false, a.fw != 0, ingress, a.allow_logic != 0, ldst, lsrc, a.empty_mask, a.drop_mask, cc, pass,
                   labeled);
       }
+      ct_fix = valid && labeled && ps == 2 && !f.ports_ok && ct_early;
       const CtWalkOut wo = ct_walk_rec(f, cc, pass, labeled, rid * 2 | static_cast<int32_t>(verdict), a.ct_sentinel);
       if (PCN_DBG_CTREC == 1 && wo.key != 0x9E3779B9u) {
         // measurement only: the record built, not stored (wrong results)
@@ -1552,6 +1578,11 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         __builtin_amdgcn_raw_buffer_store_b32(
             wo.lcs, __builtin_amdgcn_make_buffer_rsrc(a.ct_lcs + wb, 0, static_cast<int>(a.ct_brec ? 4 * nv : 0u), 0x00020000),
             static_cast<int>(4 * lane), 0, 0);
+      } else if constexpr (kRecLds) {
+        rec0 = u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]};
+        rec1 = u32x4{wo.w[4], wo.w[5], wo.w[6], wo.w[7]};
+        a.ct_keys[i] = wo.key;
+        a.ct_lcs[i] = wo.lcs;
       } else {
         u32x4 *d = reinterpret_cast<u32x4 *>(a.ct_brec) + 2 * i;
         d[0] = u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]};
@@ -1559,6 +1590,31 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
         a.ct_keys[i] = wo.key;
         a.ct_lcs[i] = wo.lcs;
       }
+    }
+    if (kCtRec && kRecLds && a.ct_brec) {
+      // The wave's 64 records (2 KB) through its LDS region, free after the rule
+      // stage, so each store instruction writes 1 KB of contiguous records
+      // instead of 64 16-byte pieces at a 32-byte stride.
+      const uint64_t wb0 = i - lane;
+      const uint64_t wb = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb0 >> 32))) << 32) |
+                          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb0)));
+      asm volatile("" ::: "memory");   // the region held the rule stage's WaveScratch
+      hbuf[2 * lane] = rec0;
+      hbuf[2 * lane + 1] = rec1;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const u32x4 c0 = hbuf[lane], c1 = hbuf[64 + lane];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      u32x4 *d = reinterpret_cast<u32x4 *>(a.ct_brec + 8 * wb);
+      if (wb + (lane >> 1) < a.n) d[lane] = c0;
+      if (wb + 32 + (lane >> 1) < a.n) d[64 + lane] = c1;
+    }
+    if (kCtRec && a.ct_pdesc) {
+      const uint64_t fm = __ballot(ct_fix);
+      if (lane == 0 && valid) a.ct_fixm[ct_g] = fm;
     }
     // ---- counters ----
     if (PCN_ABLATE == 4) return;

@@ -266,6 +266,11 @@ __host__ __device__ inline uint32_t prep_chunk(uint64_t n, int num_cus) {
   return static_cast<uint32_t>(c < 512 ? 512 : c > kPrepChunk ? kPrepChunk : c);
 }
 constexpr unsigned long long kStLocal = 1, kStIncl = 2, kStNone = 3;
+static_assert(kStLocal == kCtPortsLocal && kStNone == kCtPortsNone, "devchain.h ct_ports_word: the same states");
+// ct_stale_agg / ct_stale_fix: 1024 groups a workgroup, 4 a thread
+constexpr uint32_t kStaleScanBlock = 256, kStaleScanPer = 4;
+constexpr uint64_t kStaleScanGroups = uint64_t(kStaleScanBlock) * kStaleScanPer;
+
 __device__ __forceinline__ unsigned long long ports_word(unsigned long long st, uint32_t ports) {
   return (1ull << 40) | (st << 32) | ports;
 }
@@ -2139,7 +2144,7 @@ __device__ __forceinline__ void set_bit(uint32_t *bm, uint32_t k) {
 }
 
 __device__ __forceinline__ uint32_t own_bucket(const CtRec &r, uint32_t sentinel) {
-  return static_cast<uint32_t>(key_hash(r.src, r.dst, r.proto, r.sport, r.dport) % sentinel);
+  return ct_bucket(key_hash(r.src, r.dst, r.proto, r.sport, r.dport), sentinel);
 }
 
 __global__ void ct_hbits_set_kernel(uint64_t n, const uint32_t *ctl, const uint32_t *keys, const uint32_t *hard_list,
@@ -2162,8 +2167,8 @@ __global__ void ct_hard_split_kernel(uint32_t *ctl, const uint32_t *hard_list, c
   for (uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; h < nh; h += stp) {
     const uint32_t i = hard_list[h];
     const CtRec r = ct_rec(load_prec(&brec[i]));
-    const uint32_t qb = static_cast<uint32_t>(
-        key_hash(r.seq, r.ack, r.flags, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16)) %
+    const uint32_t qb = ct_bucket(
+        key_hash(r.seq, r.ack, r.flags, static_cast<uint16_t>(r.iports & 0xffff), static_cast<uint16_t>(r.iports >> 16)),
         sentinel);
     if ((bm[qb >> 5] >> (qb & 31)) & 1) {
       th_list[atomicAdd(&ctl[kCtlTh], 1u)] = i;
@@ -2340,6 +2345,10 @@ struct CtScratch {
   RadixScratch rx;            // the (key bucket, index) sort (radix.hip)
   // ct_advance_carry: 1 + the batch's last port-writing frame
   unsigned long long *zfound = nullptr;
+  // a stage A that wrote the walk records: per group the lanes to complete
+  // (ct_stale_fix), per 1024 groups the last ports word (ct_stale_agg)
+  unsigned long long *fixm = nullptr;
+  unsigned long long *sagg = nullptr;
 };
 
 CtScratch *ct_scratch_new() { return new CtScratch(); }
@@ -2353,7 +2362,7 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->heads),
                   static_cast<void *>(s->zfound), static_cast<void *>(s->th_list), static_cast<void *>(s->bm),
                   static_cast<void *>(s->evh), static_cast<void *>(s->seg), static_cast<void *>(s->hx),
-                  static_cast<void *>(s->cuts)})
+                  static_cast<void *>(s->cuts), static_cast<void *>(s->fixm), static_cast<void *>(s->sagg)})
     if (p) (void)hipFree(p);
   radix_free(s->rx);
   delete s;
@@ -2421,6 +2430,10 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4) {
     CT_CHECK(hipMemset(s.pdesc, 0, (n / 64 + 2) * 8));
     if (s.brec) CT_CHECK(hipFree(s.brec));
     CT_CHECK(hipMalloc(&s.brec, n * sizeof(PackedRec)));
+    if (s.fixm) CT_CHECK(hipFree(s.fixm));
+    if (s.sagg) CT_CHECK(hipFree(s.sagg));
+    CT_CHECK(hipMalloc(&s.fixm, (n / 64 + 2) * 8));
+    CT_CHECK(hipMalloc(&s.sagg, (n / 64 / kStaleScanGroups + 3) * 8));
     if (kSeg) {
       if (s.seg) CT_CHECK(hipFree(s.seg));
       if (s.hx) CT_CHECK(hipFree(s.hx));
@@ -2447,6 +2460,100 @@ static int grow(CtScratch &s, uint64_t n, uint32_t kbits, bool lab4) {
     s.bm_bytes = bmb;
   }
   return hipSuccess;
+}
+
+// The stale ports of a stage A that wrote the walk records (LaunchArgs::ct_pdesc):
+// each 64-frame group published its ports word, Local (the ports of its last
+// TCP / UDP frame) or None, and the lanes whose records were built without the
+// ports the groups before it leave (fixm).  ct_stale_agg gives every run of
+// kStaleScanGroups groups the last Local word in it; ct_stale_fix scans each run
+// (the last Local word before it from the aggregates, else the batch's carry),
+// completes the marked records (devchain.h ct_rec_restale) and advances the
+// carry.  No workgroup waits on another, and an all-ICMP batch costs one pass.
+
+__global__ __launch_bounds__(kStaleScanBlock) void ct_stale_agg_kernel(const unsigned long long *pdesc, uint64_t ngroups,
+                                                                      unsigned long long *agg, const uint32_t *carry,
+                                                                      uint32_t nblk) {
+  __shared__ int best;
+  if (threadIdx.x == 0) best = -1;
+  __syncthreads();
+  const uint64_t g0 = blockIdx.x * kStaleScanGroups + uint64_t(threadIdx.x) * kStaleScanPer;
+  unsigned long long d[kStaleScanPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kStaleScanPer; ++k) d[k] = g0 + k < ngroups ? pdesc[g0 + k] : 0ull;
+  int pos = -1;
+  uint32_t ports = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kStaleScanPer; ++k)
+    if (((d[k] >> 32) & 3) == kStLocal) {
+      pos = static_cast<int>(threadIdx.x * kStaleScanPer + k);
+      ports = static_cast<uint32_t>(d[k]);
+    }
+  if (pos >= 0) atomicMax(&best, pos);
+  __syncthreads();
+  if (pos >= 0 && pos == best) agg[blockIdx.x] = ct_ports_word(kCtPortsLocal, ports);
+  if (threadIdx.x == 0 && best < 0) agg[blockIdx.x] = ct_ports_word(kCtPortsNone, 0);
+  if (blockIdx.x == 0 && threadIdx.x == 0) agg[nblk] = *carry;   // ct_stale_fix writes the new carry
+}
+
+__global__ __launch_bounds__(kStaleScanBlock) void ct_stale_fix_kernel(const unsigned long long *pdesc,
+                                                                      const unsigned long long *fixm, uint64_t ngroups,
+                                                                      const unsigned long long *agg, uint32_t nblk,
+                                                                      uint32_t *carry, PackedRec *brec, uint32_t *keys,
+                                                                      uint32_t sentinel, uint64_t n) {
+  __shared__ unsigned long long sv[kStaleScanBlock];
+  __shared__ uint32_t cin;
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  if (t < 64) {   // the ports before this run: the last Local aggregate before it, else the carry
+    uint32_t c = static_cast<uint32_t>(agg[nblk]);
+    for (int64_t j0 = static_cast<int64_t>(blockIdx.x) - 1; j0 >= 0; j0 -= 64) {
+      const int64_t j = j0 - static_cast<int64_t>(lane);
+      const unsigned long long a = j >= 0 ? agg[j] : 0ull;
+      const uint64_t m = __ballot(j >= 0 && ((a >> 32) & 3) == kStLocal);
+      if (m) {   // the lowest lane is the latest run
+        c = __shfl(static_cast<uint32_t>(a), __builtin_ctzll(m));
+        break;
+      }
+    }
+    if (t == 0) cin = c;
+  }
+  const uint64_t g0 = blockIdx.x * kStaleScanGroups + uint64_t(t) * kStaleScanPer;
+  unsigned long long d[kStaleScanPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kStaleScanPer; ++k) d[k] = g0 + k < ngroups ? pdesc[g0 + k] : 0ull;
+  unsigned long long last = 0;   // this thread's last Local word (0: none)
+#pragma unroll
+  for (uint32_t k = 0; k < kStaleScanPer; ++k)
+    if (((d[k] >> 32) & 3) == kStLocal) last = d[k];
+  sv[t] = last;
+  __syncthreads();
+  // inclusive scan over the threads, the latest Local word winning
+  for (uint32_t off = 1; off < kStaleScanBlock; off <<= 1) {
+    const unsigned long long v = sv[t], u = t >= off ? sv[t - off] : 0ull;
+    __syncthreads();
+    if (!v && u) sv[t] = u;
+    __syncthreads();
+  }
+  const unsigned long long pre = t ? sv[t - 1] : 0ull;
+  uint32_t run = pre ? static_cast<uint32_t>(pre) : cin;
+  unsigned long long fm[kStaleScanPer];   // (all loaded before the first is used)
+#pragma unroll
+  for (uint32_t k = 0; k < kStaleScanPer; ++k) fm[k] = g0 + k < ngroups ? fixm[g0 + k] : 0ull;
+#pragma unroll
+  for (uint32_t k = 0; k < kStaleScanPer; ++k) {
+    const uint64_t g = g0 + k;
+    for (unsigned long long m = fm[k]; m; m &= m - 1) {
+      const uint64_t f = g * 64 + static_cast<uint64_t>(__builtin_ctzll(m));
+      if (f >= n) break;
+      PackedRec r = load_prec(&brec[f]);
+      if (((r.pfk >> 16) & 0xffu) == kCtKErr) continue;   // keys on the quoted header (no stale ports)
+      keys[f] = ct_rec_restale(r.src, r.dst, r.ports, r.pfk, run, sentinel);
+      brec[f].ports = r.ports;
+      brec[f].pfk = r.pfk;
+    }
+    if (((d[k] >> 32) & 3) == kStLocal) run = static_cast<uint32_t>(d[k]);
+  }
+  if (blockIdx.x == nblk - 1 && t == kStaleScanBlock - 1) *carry = run;   // the ports the batch leaves
 }
 
 // The carry alone: the ports of the batch's last frame that wrote them.
@@ -2516,7 +2623,8 @@ static uint32_t key_bits(uint64_t n) {
   return std::min(kbits, debug_key_bits());
 }
 
-int ct_prep_buffers(CtScratch &s, uint64_t n, uint32_t **brec, uint32_t **keys, uint32_t **lcs, uint32_t *sentinel) {
+int ct_prep_buffers(CtScratch &s, uint64_t n, uint32_t **brec, uint32_t **keys, uint32_t **lcs, uint32_t *sentinel,
+                    unsigned long long **pdesc, unsigned long long **fixm) {
   if (n == 0 || n >= 0x7FFFFFFFull) return int(hipErrorInvalidValue);
   const uint32_t kbits = key_bits(n);
   CT_CHECK(grow(s, n, kbits, false));
@@ -2524,6 +2632,8 @@ int ct_prep_buffers(CtScratch &s, uint64_t n, uint32_t **brec, uint32_t **keys, 
   *keys = s.keys;
   *lcs = s.lcs;
   *sentinel = (1u << kbits) - 1;
+  *pdesc = s.pdesc;
+  *fixm = s.fixm;
   return hipSuccess;
 }
 
@@ -2541,12 +2651,25 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   // ctl's first kCtlZero words and the ports descriptors are zero: from their
   // allocation, then from the previous batch's ct_count; only a batch that
   // returned early with an error leaves them to memsets here
+  // (a prepped batch's stage A has written every group's ports word already)
   if (s.dirty) {
     CT_CHECK(hipMemsetAsync(s.ctl, 0, kCtlZero * 4, st));
-    CT_CHECK(hipMemsetAsync(s.pdesc, 0, (s.cap / 64 + 2) * 8, st));
+    if (!prepped) CT_CHECK(hipMemsetAsync(s.pdesc, 0, (s.cap / 64 + 2) * 8, st));
     CT_CHECK(hipMemsetAsync(s.bm, 0, s.bm_bytes, st));
   }
   s.dirty = true;
+  if (prepped) {
+    // the records stage A built before the ports the earlier groups leave were
+    // known, completed; the carry advanced
+    const uint64_t ngroups = (b.n + 63) / 64;
+    const uint32_t nblk = static_cast<uint32_t>((ngroups + kStaleScanGroups - 1) / kStaleScanGroups);
+    hipLaunchKernelGGL(ct_stale_agg_kernel, dim3(nblk), dim3(kStaleScanBlock), 0, st, s.pdesc, ngroups, s.sagg, t.carry,
+                       nblk);
+    CT_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(ct_stale_fix_kernel, dim3(nblk), dim3(kStaleScanBlock), 0, st, s.pdesc, s.fixm, ngroups, s.sagg,
+                       nblk, t.carry, s.brec, s.keys, sentinel, b.n);
+    CT_CHECK(hipGetLastError());
+  }
   if (!prepped) {
     const uint32_t pchunk = prep_chunk(b.n, num_cus);
     const unsigned pgrid = static_cast<unsigned>(std::min<uint64_t>(uint64_t(num_cus) * 8, (b.n + pchunk - 1) / pchunk));

@@ -88,14 +88,18 @@ void ct_scratch_free(CtScratch *s);
 // Stages B-E for one batch whose stage-A outcomes are in b.a_*.  Synchronises
 // the stream once when the batch holds long echo replies.  Returns a hipError_t.
 // prepped: stage A already wrote the walk records, key buckets and {len, cinfo}
-// words (into ct_prep_buffers') and advanced the carry, so ct_prep and the
-// carry look-back are skipped: the frames are read once per batch.
+// words (into ct_prep_buffers') and published each 64-frame group's ports word
+// and the lanes whose records wait for the ports before their group, so ct_prep
+// is skipped (the frames are read once per batch): ct_stale_agg / ct_stale_fix
+// complete those records and advance the carry.
 int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream, bool prepped = false);
 
 // The buffers a stage A that writes the walk records fills for an n-packet
 // batch (grown as needed): 8 u32 per record, the key bucket and the {len,
-// cinfo} word per packet, and the bucket of packets without a key.
-int ct_prep_buffers(CtScratch &s, uint64_t n, uint32_t **brec, uint32_t **keys, uint32_t **lcs, uint32_t *sentinel);
+// cinfo} word per packet, the bucket of packets without a key, and per 64-frame
+// group the ports word and the lanes to complete (LaunchArgs::ct_pdesc / ct_fixm).
+int ct_prep_buffers(CtScratch &s, uint64_t n, uint32_t **brec, uint32_t **keys, uint32_t **lcs, uint32_t *sentinel,
+                    unsigned long long **pdesc, unsigned long long **fixm);
 
 // Stateless batches (labels given per packet) on chains with accept-established
 // on: move rule-0 hits to the accept-established path (rule id -3 and its

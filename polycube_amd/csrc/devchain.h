@@ -225,11 +225,19 @@ struct LaunchArgs {
   // Stage A of a stateful batch that also writes the walk records (pcn_ipt.cpp
   // ct_fused_prep; conntrack.hip then skips ct_prep): per frame its 32-byte
   // record (CtWalkOut::w), its key bucket and its {len, cinfo} word.  Null
-  // otherwise.  Launches with these set track the stale ports (has_stale).
+  // otherwise.
   uint32_t *ct_brec;             // [n][8] u32
   uint32_t *ct_keys;             // [n]
   uint32_t *ct_lcs;              // [n]
   uint32_t ct_sentinel;          // the key bucket of packets without one (2^kbits - 1)
+  // ... and its stale ports without waiting on other workgroups: every 64-frame
+  // group publishes its ports word (ct_ports_word: its last TCP / UDP frame's
+  // ports, or none) and a mask of the lanes whose record was built before the
+  // ports the earlier groups leave are known (labelled, no ports of their own,
+  // no TCP / UDP frame before them in the group); conntrack.hip ct_stale_fix
+  // completes those records once every group has published.
+  unsigned long long *ct_pdesc;  // [n / 64 + 1]
+  unsigned long long *ct_fixm;   // [n / 64 + 1]
 };
 // split_rec word 3: proto | flags << 8 | ct << 16 | meta << 24, meta = chain (2 bits)
 // | outer VLAN tag stripped (bit 2: the rule kernel's length is lens - 4) | kSplitNeed
@@ -310,6 +318,15 @@ PCN_HD inline uint64_t ct_key_hash(uint32_t src, uint32_t dst, uint32_t proto, u
   return h ^ (h >> 32);
 }
 
+// The key bucket of a key hash: h % sentinel, sentinel = 2^kbits - 1 (kbits >= 8,
+// conntrack.hip key_bits), by folding (2^kbits = 1 mod sentinel) instead of a
+// 64-bit division.
+PCN_HD inline uint32_t ct_bucket(uint64_t h, uint32_t sentinel) {
+  const uint32_t k = 32 - __builtin_clz(sentinel);   // sentinel = 2^k - 1
+  while (h > sentinel) h = (h & sentinel) + (h >> k);
+  return h == sentinel ? 0u : static_cast<uint32_t>(h);
+}
+
 // The 32-byte walk record (conntrack.hip PackedRec: src, dst, sport | dport
 // << 16, seq, ack, iports, proto | flags << 8 | kind << 16 | (rev | cinfo <<
 // 2) << 24, o0), its key bucket (sentinel: no table access) and the {len,
@@ -371,7 +388,7 @@ PCN_HD inline CtWalkOut ct_walk_rec(const CtFrame &p, uint32_t chain, bool pass,
   }
   const uint32_t cinfo = (chain & 3u) | (pass ? 4u : 0u);
   const bool member = kind >= kCtKTcp && kind <= kCtKErr;
-  o.key = member ? static_cast<uint32_t>(ct_key_hash(src, dst, proto & 0xffu, sport & 0xffffu, dport & 0xffffu) % sentinel)
+  o.key = member ? ct_bucket(ct_key_hash(src, dst, proto & 0xffu, sport & 0xffffu, dport & 0xffffu), sentinel)
                  : sentinel;
   o.lcs = (p.L & 0xffffu) | cinfo << 16;
   o.w[0] = src;
@@ -384,6 +401,32 @@ PCN_HD inline CtWalkOut ct_walk_rec(const CtFrame &p, uint32_t chain, bool pass,
   o.w[7] = static_cast<uint32_t>(o0);
   o.kind = kind;
   return o;
+}
+
+// The same record once the stale ports (Q4) it was built with are known to be
+// `stale` (a labelled record of a frame whose Parser wrote no ports: its
+// kind is not kCtKErr, which keys on the quoted header): the ports word, the
+// rev bits of pfk and the key bucket, as ct_walk_rec computes them.
+PCN_HD inline uint32_t ct_rec_restale(uint32_t src, uint32_t dst, uint32_t &ports, uint32_t &pfk, uint32_t stale,
+                                      uint32_t sentinel) {
+  const uint32_t sp = stale & 0xffffu, dp = stale >> 16;
+  const uint32_t ipRev = (pfk >> 24) & 1u;
+  uint32_t sport, dport, portRev;
+  if (sp < dp) { sport = sp; dport = dp; portRev = 0; }
+  else if (sp > dp) { sport = dp; dport = sp; portRev = 1; }
+  else { sport = sp; dport = dp; portRev = ipRev; }
+  ports = sport | dport << 16;
+  pfk = (pfk & ~(3u << 24)) | (ipRev | portRev << 1) << 24;
+  const uint32_t kind = (pfk >> 16) & 0xffu, proto = pfk & 0xffu;
+  const bool member = kind >= kCtKTcp && kind <= kCtKErr;
+  return member ? ct_bucket(ct_key_hash(src, dst, proto, sport, dport), sentinel) : sentinel;
+}
+
+// Ports words per 64-frame group (conntrack.hip ports_word): bit 40 published,
+// bits 32-33 the state, bits 0-31 the ports of the group's last TCP / UDP frame.
+constexpr unsigned long long kCtPortsLocal = 1, kCtPortsNone = 3;
+PCN_HD inline unsigned long long ct_ports_word(unsigned long long st, uint32_t ports) {
+  return (1ull << 40) | (st << 32) | ports;
 }
 
 // LaunchArgs::fw: pcn-firewall dispatch with its conntrack mode (defines.h:56-58)

@@ -1077,6 +1077,7 @@ struct StageA {
   // ct_prep_buffers), so ct_run skips ct_prep
   uint32_t *brec = nullptr, *keys = nullptr, *lcs = nullptr;
   uint32_t sentinel = 0;
+  unsigned long long *pdesc = nullptr, *fixm = nullptr;   // the stale ports, completed by ct_stale_fix
 };
 
 // carry_out (stateless batches that track the stale ports): when the kernel
@@ -1323,13 +1324,16 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
       if (carry && (hz->fields & (PCN_IPT_HZ_SRCPORT | PCN_IPT_HZ_DSTPORT))) track_stale();
     }
     // stage A of a stateful batch that writes the walk records (ct_fused_prep):
-    // its records need every frame's stale ports too
+    // its records need every frame's stale ports too -- published per group and
+    // completed after the launch (conntrack.hip ct_stale_fix), so no workgroup
+    // waits on another's groups
     if (sa && sa->brec) {
       a.ct_brec = sa->brec;
       a.ct_keys = sa->keys;
       a.ct_lcs = sa->lcs;
       a.ct_sentinel = sa->sentinel;
-      if (!a.has_stale) track_stale();
+      a.ct_pdesc = sa->pdesc;
+      a.ct_fixm = sa->fixm;
     }
     // slot count of the chain program (the generic kernel always runs 6)
     const int ns = ch < 3 ? static_cast<int>(a.ch[ch].lay.nslots) : 6;
@@ -1605,19 +1609,20 @@ int pcn_ipt_classify(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream) {
     }
     // Frames shorter than 70 bytes (no ICMP header can quote another) with
     // one label and no Horus program: stage A builds the walk records, key
-    // buckets and {len, cinfo} words itself (devchain.h ct_walk_rec) and
-    // advances the carry, and ct_run skips ct_prep -- the batch's frames are
-    // read once instead of twice (PCN_IPT_DEBUG_CT_FUSED=0: ct_prep, A/B).
+    // buckets and {len, cinfo} words itself (devchain.h ct_walk_rec), and ct_run
+    // skips ct_prep (its ct_stale_fix completes the stale ports and advances the
+    // carry) -- the batch's frames are read once instead of twice
+    // (PCN_IPT_DEBUG_CT_FUSED=0: ct_prep, A/B).
     const bool fused = nlab == 1 && !hz && !b->offsets && !b->lens && b->fixed_len < 70 &&
                        b->hook == PCN_IPT_HOOK_XDP && n < 0x7FFFFFFFull && ct_fused_prep();
     if (!ctx->cts) ctx->cts = ct_scratch_new();
     for (uint32_t l = 0; l < nlab; ++l) {
       StageA sa{ctx->d_labels + l, a_v + l * n, a_rid + l * n};
       if (fused) {
-        const int e = ct_prep_buffers(*ctx->cts, n, &sa.brec, &sa.keys, &sa.lcs, &sa.sentinel);
+        const int e = ct_prep_buffers(*ctx->cts, n, &sa.brec, &sa.keys, &sa.lcs, &sa.sentinel, &sa.pdesc, &sa.fixm);
         if (e != hipSuccess) return fail(-EIO, std::string("conntrack buffers: ") + hipGetErrorString(hipError_t(e)));
       }
-      int rc = fused ? launch_batch(ctx, b, stream, &sa, carry, carry) : launch_batch(ctx, b, stream, &sa, stale);
+      int rc = launch_batch(ctx, b, stream, &sa, fused ? nullptr : stale);
       if (rc) return rc;
     }
     // pcn-firewall AUTOMATIC: ESTABLISHED packets are accepted before the chain

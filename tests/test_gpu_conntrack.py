@@ -263,6 +263,36 @@ def test_stage_a_builds_the_walk_records(dev, setup):
     assert ipt.ct_info()["fused_batches"] == nb, ipt.ct_info()
 
 
+def test_stage_a_stale_ports_across_icmp_only_stretches(dev):
+    """The fused stage A's stale ports (Q4) where whole runs of 64-frame groups hold
+    no TCP/UDP frame: every ICMP frame there keys on the ports of the last TCP/UDP
+    frame before the stretch, in this batch or (a batch that starts with the stretch,
+    and an all-ICMP batch) in an earlier one -- what conntrack.hip ct_stale_agg /
+    ct_stale_fix resolve after the launch, across its 4096-group runs.  Bit-exact
+    against the oracle, tables and counters included, every batch on the fused path."""
+    rs = synth.config_rules(3)
+    rules = rs.rules()
+    o, ipt = ct_pair({1: rules}, {1: "DROP"}, cap_log2=18, jit=1)
+    mixed, _ = synth.flow_traffic(1 << 18, 2000, 21, stride=64, rs=rs, p_icmp=0.3, p_noise=0.05, p_err=0.05)
+    icmp, _ = synth.flow_traffic(1 << 19, 3000, 22, stride=64, rs=rs, p_icmp=1.0, p_noise=0.0, p_err=0.0)
+    mixed, icmp = mixed.reshape(-1, 64), icmp.reshape(-1, 64)
+    assert set(np.unique(icmp[:, 23])) == {1}, "the stretch is all ICMP"
+    batches = [
+        np.concatenate([mixed[:5000], icmp[:300000], mixed[5000:5100]]),   # > 4096 ICMP-only groups mid-batch
+        icmp[300000:400001],                                              # a batch of ICMP only: the carry
+        np.concatenate([icmp[400001:400100], mixed[5100:90000]]),          # starts with the stretch
+        mixed[90000:90037],
+    ]
+    nb = 0
+    for fr in batches:
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, np.ascontiguousarray(fr).reshape(-1), len(fr), stride=64)
+        assert_same(v_o, r_o, v_g, r_g)
+        nb += 1
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert ipt.ct_info()["fused_batches"] == nb, ipt.ct_info()
+
+
 def test_headline_size_flows_parity(dev):
     """2^22 packets of 2^16 interleaved flows, 64-byte frames, config-3 rules."""
     rs = synth.config_rules(3)
