@@ -2679,13 +2679,17 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   }
   // long echo replies join their own key's run unless their quoted key's
   // bucket is in the batch (each kernel returns at once without replies)
+  // (a prepped batch has none: its frames are shorter than 70 bytes, and
+  // neither these two kernels nor ct_tail are launched for it)
   const uint64_t bm_words = (uint64_t(1) << kbits) / 32;
-  hipLaunchKernelGGL(ct_hbits_set_kernel, dim3(grid), dim3(blk), 0, st, b.n, s.ctl, s.keys, s.hard_list, s.brec, s.bm,
-                     sentinel);
-  CT_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(ct_hard_split_kernel, dim3(grid), dim3(blk), 0, st, s.ctl, s.hard_list, s.brec, s.keys, s.bm,
-                     sentinel, s.th_list);
-  CT_CHECK(hipGetLastError());
+  if (!prepped) {
+    hipLaunchKernelGGL(ct_hbits_set_kernel, dim3(grid), dim3(blk), 0, st, b.n, s.ctl, s.keys, s.hard_list, s.brec, s.bm,
+                       sentinel);
+    CT_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(ct_hard_split_kernel, dim3(grid), dim3(blk), 0, st, s.ctl, s.hard_list, s.brec, s.keys, s.bm,
+                       sentinel, s.th_list);
+    CT_CHECK(hipGetLastError());
+  }
   // (ct_heads advances the carry from ct_prep's published groups)
   // the sort (radix.hip; s.keys is its ping-pong buffer from here on)
   CT_CHECK(radix_sort_pairs(s.rx, s.keys, s.keys2, s.idx2, b.n, kbits, num_cus, st));
@@ -2709,9 +2713,11 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
                        s.cursor, s.ctl, s.cuts);
     CT_CHECK(hipGetLastError());
   }
-  hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.heads, s.ctl, s.th_list,
-                     s.cursor);
-  CT_CHECK(hipGetLastError());
+  if (!prepped) {   // (the long echo replies the walk cannot take: none in a prepped batch)
+    hipLaunchKernelGGL(ct_tail_kernel, dim3(1), dim3(64), 0, st, b, t, src, s.brec, s.heads, s.ctl, s.th_list,
+                       s.cursor);
+    CT_CHECK(hipGetLastError());
+  }
   if (t.max_entries) {                         // LRU down to max_entries (no read-back either)
     const uint64_t cap = uint64_t(1) << t.cap_log2;
     // few workgroups: each one's merge and finish atomics land on the same few
