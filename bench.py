@@ -590,7 +590,7 @@ def frame_size_sweep(ipt, rules, frames, n, dev, stream, log, steps=20, sizes=FR
                           "frame_gb_s": round(size * n / (ms * 1e-3) / 1e9, 1),
                           "lines_128b_per_frame": round(lines, 4),
                           "line_gb_s": round(lines * 128 * n / (ms * 1e-3) / 1e9, 1),
-                          "path": "fixed-stride" if size % 16 == 0 else "generic gather (any byte offset)",
+                          "path": "fixed-stride" if size % 4 == 0 else "generic gather (any byte offset)",
                           "traffic_bytes_per_frame": None if traffic is None else round(traffic / n, 2),
                           "traffic_from": note, "parity_sample_vs_oracle": ok}
         log(f"[bench] frame size {size}: {out[str(size)]}")

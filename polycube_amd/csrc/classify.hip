@@ -1156,8 +1156,10 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     // Pin every prefetched dword (used or not) until here, so no register the
     // load writes is recycled mid-iteration (a WAW hazard costs a vmcnt wait).
     Hdr h;
+    u32x4 srec = {};   // SPLIT 2: this frame's record, taken before the stage is refilled
     if constexpr (SPLIT == 2) {
       asm volatile("" : "+v"(cur.g[0]));
+      srec = cur.g[0];
     } else if (FIXED && !PCN_HDR_LDS) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
@@ -1263,7 +1265,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     if constexpr (SPLIT == 2) {
       // the gather kernel's fields (SPLIT 1 below): only frames that reach the
       // rule stage are this kernel's
-      const u32x4 r = cur.g[0];
+      const u32x4 r = srec;
       const uint32_t meta = r.w >> 24;
       valid = valid && (meta & kSplitNeed);
       p.saddr = r.x;

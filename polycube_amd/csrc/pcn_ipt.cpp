@@ -145,6 +145,16 @@ unsigned split_gather_wg() {
   return v;
 }
 
+// PCN_IPT_DEBUG_FIXED_ALIGN=16: fixed-stride batches only at 16-byte strides (A/B of the
+// dword-aligned fixed path; 4 otherwise)
+uint32_t fixed_align() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_FIXED_ALIGN");
+    return e && std::strtol(e, nullptr, 10) == 16 ? 16u : 4u;
+  }();
+  return v;
+}
+
 // PCN_IPT_DEBUG_SHALLOW=0: keep prefetch depth 2 for launches of few frames
 // per lane (A/B of JitShape::shallow)
 bool shallow_prefetch() {
@@ -1136,10 +1146,14 @@ int launch_batch(pcn_ipt *ctx, const pcn_ipt_batch *b, void *stream, const Stage
     auto runs = [&](int c) {
       return any_rules && (ch < 3 ? c == ch : (c == PCN_IPT_FORWARD || c == PCN_IPT_INPUT));
     };
-    // fixed-stride fast path: 16-byte aligned 48-byte header windows inside the buffer
+    // fixed-stride fast path: 48-byte header windows inside the buffer, each read as
+    // three 16-byte loads from the frame's start, which need dword alignment only
+    // (a 1500-byte stride: 172 B of lines a frame, against the generic gather's 16-byte
+    // aligned 64-byte span; PCN_IPT_DEBUG_FIXED_ALIGN=16 restores the 16-byte rule, A/B)
     // (TC frames may carry a VLAN tag: the 52-byte window of the generic path)
-    bool fixed = b->hook == PCN_IPT_HOOK_XDP && !b->offsets && !b->lens && b->stride % 16 == 0 && b->stride >= 48 &&
-                 (reinterpret_cast<uintptr_t>(b->frames) % 16) == 0 &&
+    const uint32_t falign = fixed_align();
+    bool fixed = b->hook == PCN_IPT_HOOK_XDP && !b->offsets && !b->lens && b->stride % falign == 0 && b->stride >= 48 &&
+                 (reinterpret_cast<uintptr_t>(b->frames) % falign) == 0 &&
                  (b->n - 1) * uint64_t(b->stride) + 48 <= b->frames_bytes;
     // LDS plan (every field below): a chain program of a chain with 2+ summary
     // blocks deals 128 candidates a pass (jit.cpp) and needs the larger wave
