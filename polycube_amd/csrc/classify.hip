@@ -106,26 +106,6 @@ __device__ __forceinline__ T hdr_load(const T *p) {
 #ifndef PCN_STAGE_FAST
 #define PCN_STAGE_FAST 1 // prologue: first headers in flight during the image stage, staging loads batched
 #endif
-// Chain programs (one rule chain): the running chain's image loads are issued
-// before the first header loads and only they are waited for before the LDS
-// stores, so the first headers stay in flight through the staging (vmcnt is in
-// order: staging loads issued after the headers waited for them too).
-#ifndef PCN_STAGE_EARLY
-#define PCN_STAGE_EARLY 0
-#endif
-// Fixed-stride chain programs: verdicts, rule ids and (stateful stage A) walk
-// records written with buffer stores every wave issues, so the hand-counted
-// header wait knows how many stores are younger than the loads it waits for.
-// (0: plain conditional stores, and a wait that also drains the next frame's loads)
-#ifndef PCN_DBG_CTREC
-#define PCN_DBG_CTREC 0  // measurement only: 1 = stage A builds the walk records but stores none, 2 = builds none
-#endif
-#ifndef PCN_CTREC_LDS
-#define PCN_CTREC_LDS 0  // stage A's walk records through the wave's LDS region, stored 1 KB per instruction
-#endif
-#ifndef PCN_STORE_COUNT
-#define PCN_STORE_COUNT 0
-#endif
 // Offsets / lengths batches (IMIX): a wave's 64 scattered headers are fetched
 // four lanes to a frame, one 16-byte chunk each from the frame's 16-byte
 // aligned start, so one load instruction reads 16 frames' contiguous bytes
@@ -892,51 +872,12 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   // (The first frames' headers are already in flight: the prefetch below is
   // issued before this when PCN_STAGE_FAST.)  Every load of a pass is issued
   // before its stores, so a 128 KB image costs one L2 round trip, not eight.
-  constexpr bool kEarly = PCN_STAGE_EARLY && PCN_STAGE_FAST && LDS && JIT && CH < 3 && SPLIT != 2;
-  constexpr uint32_t kEarlyU = 10;   // 160 KB / (1024 threads x 16 B): the whole image in one pass
-  u32x4 er[kEarlyU];
-  auto stage_early_load = [&]() {   // the running chain's image into registers (clamped: no branch)
-    if (!run_ch.lds_limit) return;
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(run_ch.image);
-    const uint32_t n16 = run_ch.lds_limit / 16;
-#pragma unroll
-    for (uint32_t u = 0; u < kEarlyU; ++u) {
-      const uint32_t k = threadIdx.x + u * kBlock;
-      const u32x4 *p = src + (k < n16 ? k : n16 - 1);
-      // (asm on the asm-header path: counted by hand with those loads; no nt
-      // hint, every CU of the XCD reads the same image from L2)
-      if (FIXED && PCN_HDR_ASM) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(er[u]) : "v"(p));
-      else er[u] = *p;
-    }
-  };
-  auto stage_early_store = [&]() {
-    if (!run_ch.lds_limit) return;
-    if constexpr (FIXED && PCN_HDR_ASM) {
-      // the 3 * PF header chunk loads issued after the image's stay in flight
-      constexpr int PFH = PCN_PREFETCH_FIXED;
-      static_assert(PFH == 1 || PFH == 2 || PFH == 3, "counted image waits for PF 1..3");
-#define PCN_ER_OPS "+v"(er[0]), "+v"(er[1]), "+v"(er[2]), "+v"(er[3]), "+v"(er[4]), "+v"(er[5]), "+v"(er[6]), \
-                   "+v"(er[7]), "+v"(er[8]), "+v"(er[9])
-      if constexpr (PFH == 1) asm volatile("s_waitcnt vmcnt(3)" : PCN_ER_OPS);
-      else if constexpr (PFH == 2) asm volatile("s_waitcnt vmcnt(6)" : PCN_ER_OPS);
-      else asm volatile("s_waitcnt vmcnt(9)" : PCN_ER_OPS);
-#undef PCN_ER_OPS
-    }
-    u32x4 *dst = reinterpret_cast<u32x4 *>(pcn_smem + run_ch.lds_image);
-    const uint32_t n16 = run_ch.lds_limit / 16;
-#pragma unroll
-    for (uint32_t u = 0; u < kEarlyU; ++u) {
-      const uint32_t k = threadIdx.x + u * kBlock;
-      if (k < n16) dst[k] = er[u];
-    }
-  };
   auto stage_images = [&]() {
     if (!LDS) return;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const DevChain &ch = c == CH ? run_ch : a.ch[c];
       if (!ch.lds_limit) continue;
-      if (kEarly && c == CH) continue;   // staged by stage_early_*
       const u32x4 *src = reinterpret_cast<const u32x4 *>(ch.image);
       u32x4 *dst = reinterpret_cast<u32x4 *>(pcn_smem + ch.lds_image);
       const uint32_t n16 = ch.lds_limit / 16;
@@ -1030,11 +971,6 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
   u32x4 *hbuf = reinterpret_cast<u32x4 *>(pcn_smem + a.lds_scratch + (threadIdx.x >> 6) * a.wave_bytes);
   // (a split launch's rule kernel: its 16-byte records, PCN_SPLIT_R_PF ahead)
   constexpr int PF = SPLIT == 2 ? PCN_SPLIT_R_PF : FIXED ? PCN_PREFETCH_FIXED : PCN_PREFETCH_GENERIC;
-  // counted output stores (see the stores after the rule stage): the fixed
-  // path's asm header loads are waited for by hand, and the stores of the
-  // PF frames issued since a stage's loads are younger than them
-  constexpr bool kCount = PCN_STORE_COUNT && FIXED && PCN_HDR_LDS && PCN_HDR_ASM && SPLIT == 0 && !kLoadPort && !kLoadCt;
-  constexpr int kStoresPerFrame = kCount ? (kCtRec ? 6 : 2) : 0;
   Stage st[PF];
   auto prefetch = [&](Stage &x, uint64_t j) {   // j: this lane's frame index
     if constexpr (SPLIT == 2) {                  // the gather kernel's fields for frame j, coalesced
@@ -1127,16 +1063,8 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       st[d].offn = a.offsets[j < a.n ? j : last];
     }
   }
-  if constexpr (kEarly) stage_early_load();   // after the offsets: the header loads wait for those only
 #pragma unroll
   for (int d = 0; d < PF; ++d) prefetch(st[d], first + d * step);
-  if constexpr (kEarly) stage_early_store();
-  if constexpr (kCount) {
-    // the stores of the PF frames "before" the first: discarded (no records), counted
-    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(a.verdicts, 0, 0, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < PF * kStoresPerFrame; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 256 * k, 0, 0);   // (apart: never merged)
-  }
   if (PCN_STAGE_FAST) stage_images();
   // pkts[nbins], then (variable lengths only) bytes[nbins]; with a fixed
   // length every bin's bytes are pkts * len at the flush
@@ -1170,11 +1098,9 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
     } else if (FIXED) {
       if (PCN_HDR_ASM) {
         static_assert(PF == 1 || PF == 2 || PF == 3, "counted header waits for PF 1..3");
-        // younger than this stage's loads: the later stages' loads and the
-        // stores of the PF frames since (kCount; fewer without it: a wait too deep)
-        constexpr int kYounger = 3 * (PF - 1) + PF * kStoresPerFrame;
-        static_assert(kYounger <= 63, "vmcnt is 6 bits");
-        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(cur.c[0]), "+v"(cur.c[1]), "+v"(cur.c[2]) : "i"(kYounger));
+        if constexpr (PF == 1) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cur.c[0]), "+v"(cur.c[1]), "+v"(cur.c[2]));
+        else if constexpr (PF == 2) asm volatile("s_waitcnt vmcnt(3)" : "+v"(cur.c[0]), "+v"(cur.c[1]), "+v"(cur.c[2]));
+        else asm volatile("s_waitcnt vmcnt(6)" : "+v"(cur.c[0]), "+v"(cur.c[1]), "+v"(cur.c[2]));
       } else {
 #pragma unroll
         for (int q = 0; q < 3; ++q) asm volatile("" : "+v"(cur.c[q]));
@@ -1492,29 +1418,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       }
     }
     if (kLate) prefetch(cur, i + PF * step);
-    // Counted stores (kCount): the wave's outputs go out as buffer stores bounded
-    // by the batch end, issued by every wave whatever its lanes (out-of-range
-    // lanes and absent arrays write nothing), so the header wait above can
-    // count them (kStoresPerFrame each) and keep the next frames in flight.
-    __amdgpu_buffer_rsrc_t rs_v, rs_r;
-    uint32_t nv = 0;
-    uint64_t wb = 0;   // the wave's first frame (uniform)
-    if constexpr (kCount) {
-      const uint64_t wb0 = i - lane;
-      wb = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb0 >> 32))) << 32) |
-           static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb0)));
-      nv = a.n > wb ? (a.n - wb < 64 ? static_cast<uint32_t>(a.n - wb) : 64u) : 0u;
-      rs_v = __builtin_amdgcn_make_buffer_rsrc(a.verdicts + wb, 0, static_cast<int>(nv), 0x00020000);
-      rs_r = __builtin_amdgcn_make_buffer_rsrc(a.rule_ids ? static_cast<void *>(a.rule_ids + wb) : static_cast<void *>(a.verdicts),
-                                               0, a.rule_ids ? static_cast<int>(4 * nv) : 0, 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(verdict), rs_v, static_cast<int>(lane), 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(rid), rs_r, static_cast<int>(4 * lane), 0, 0);
-      if constexpr (kCtRec) {
-        const uint32_t nb = a.ct_brec ? nv : 0u;   // (always set with kCtRec: inputs bit 128)
-        rs_v = __builtin_amdgcn_make_buffer_rsrc(a.ct_brec + 8 * wb, 0, static_cast<int>(32 * nb), 0x00020000);
-        rs_r = __builtin_amdgcn_make_buffer_rsrc(a.ct_keys + wb, 0, static_cast<int>(4 * nb), 0x00020000);
-      }
-    } else if (wr) {
+    if (wr) {
       a.verdicts[i] = static_cast<uint8_t>(verdict);
       if (a.rule_ids) a.rule_ids[i] = rid;
     }
@@ -1542,9 +1446,7 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       ct_early = !before;
     }
     bool ct_fix = false;     // this lane's record waits for the ports before its group
-    constexpr bool kRecLds = PCN_CTREC_LDS && !kCount && PCN_DBG_CTREC == 0;
-    u32x4 rec0 = {}, rec1 = {};   // kRecLds: the record, stored after the block by the whole wave
-    if (kCtRec && PCN_DBG_CTREC != 2 && (kCount || (a.ct_brec && valid))) {
+    if (kCtRec && a.ct_brec && valid) {
       CtFrame f{};
       const bool tcp = p.proto == 6;
       f.status = ps;
@@ -1570,49 +1472,11 @@ __device__ __forceinline__ void classify_body(const LaunchArgs &a) {
       }
       ct_fix = valid && labeled && ps == 2 && !f.ports_ok && ct_early;
       const CtWalkOut wo = ct_walk_rec(f, cc, pass, labeled, rid * 2 | static_cast<int32_t>(verdict), a.ct_sentinel);
-      if (PCN_DBG_CTREC == 1 && wo.key != 0x9E3779B9u) {
-        // measurement only: the record built, not stored (wrong results)
-      } else if constexpr (kCount) {
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]}, rs_v, static_cast<int>(32 * lane), 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{wo.w[4], wo.w[5], wo.w[6], wo.w[7]}, rs_v, static_cast<int>(32 * lane + 16),
-                                               0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(wo.key, rs_r, static_cast<int>(4 * lane), 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(
-            wo.lcs, __builtin_amdgcn_make_buffer_rsrc(a.ct_lcs + wb, 0, static_cast<int>(a.ct_brec ? 4 * nv : 0u), 0x00020000),
-            static_cast<int>(4 * lane), 0, 0);
-      } else if constexpr (kRecLds) {
-        rec0 = u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]};
-        rec1 = u32x4{wo.w[4], wo.w[5], wo.w[6], wo.w[7]};
-        a.ct_keys[i] = wo.key;
-        a.ct_lcs[i] = wo.lcs;
-      } else {
-        u32x4 *d = reinterpret_cast<u32x4 *>(a.ct_brec) + 2 * i;
-        d[0] = u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]};
-        d[1] = u32x4{wo.w[4], wo.w[5], wo.w[6], wo.w[7]};
-        a.ct_keys[i] = wo.key;
-        a.ct_lcs[i] = wo.lcs;
-      }
-    }
-    if (kCtRec && kRecLds && a.ct_brec) {
-      // The wave's 64 records (2 KB) through its LDS region, free after the rule
-      // stage, so each store instruction writes 1 KB of contiguous records
-      // instead of 64 16-byte pieces at a 32-byte stride.
-      const uint64_t wb0 = i - lane;
-      const uint64_t wb = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb0 >> 32))) << 32) |
-                          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(wb0)));
-      asm volatile("" ::: "memory");   // the region held the rule stage's WaveScratch
-      hbuf[2 * lane] = rec0;
-      hbuf[2 * lane + 1] = rec1;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const u32x4 c0 = hbuf[lane], c1 = hbuf[64 + lane];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      u32x4 *d = reinterpret_cast<u32x4 *>(a.ct_brec + 8 * wb);
-      if (wb + (lane >> 1) < a.n) d[lane] = c0;
-      if (wb + 32 + (lane >> 1) < a.n) d[64 + lane] = c1;
+      u32x4 *d = reinterpret_cast<u32x4 *>(a.ct_brec) + 2 * i;
+      d[0] = u32x4{wo.w[0], wo.w[1], wo.w[2], wo.w[3]};
+      d[1] = u32x4{wo.w[4], wo.w[5], wo.w[6], wo.w[7]};
+      a.ct_keys[i] = wo.key;
+      a.ct_lcs[i] = wo.lcs;
     }
     if (kCtRec && a.ct_pdesc) {
       const uint64_t fm = __ballot(ct_fix);
