@@ -162,7 +162,12 @@ int main(int argc, char **argv) {
     const uint32_t stride = static_cast<uint32_t>(std::atoi(pat.c_str() + 7));
     if (stride < 48 || stride % 4) { std::fprintf(stderr, "stride must be >= 48 and a multiple of 4\n"); return 2; }
     const uint64_t bytes = n * stride;
-    CK(hipMalloc(&f, bytes + 64));
+    // CALIB_ALLOC=uc / fg: the frames in uncached / fine-grained device memory (whether the
+    // L2 then fetches less than a 128-byte line for a 48-byte window)
+    const char *al = std::getenv("CALIB_ALLOC");
+    if (al && std::string(al) == "uc") CK(hipExtMallocWithFlags(reinterpret_cast<void **>(&f), bytes + 64, hipDeviceMallocUncached));
+    else if (al && std::string(al) == "fg") CK(hipExtMallocWithFlags(reinterpret_cast<void **>(&f), bytes + 64, hipDeviceMallocFinegrained));
+    else CK(hipMalloc(&f, bytes + 64));
     CK(hipMemset(f, 5, bytes + 64));
     std::vector<uint64_t> s(n);
     for (uint64_t i = 0; i < n; ++i) s[i] = i * stride;
