@@ -263,6 +263,26 @@ def test_stage_a_builds_the_walk_records(dev, setup):
     assert ipt.ct_info()["fused_batches"] == nb, ipt.ct_info()
 
 
+def test_stage_a_records_from_the_generic_kernel(dev):
+    """The fused stage A through the generic classify kernel (no chain program: jit
+    -1), which carries the same record building and stale-port publication: ICMP-heavy
+    64-byte frames over ragged batches, bit-exact against the oracle, tables included."""
+    rs = synth.config_rules(3)
+    rules = rs.rules()
+    o, ipt = ct_pair({1: rules}, {1: "DROP"}, cap_log2=18, jit=-1)
+    n = 1 << 16
+    f, _ = synth.flow_traffic(n, 1500, 31, stride=64, rs=rs, p_icmp=0.4, p_noise=0.1, p_err=0.05)
+    fr = f.reshape(n, 64)
+    cuts = [0, 63, 64, 4100, 30001, n]
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        v_o, r_o, v_g, r_g = run_ct(o, ipt, dev, fr[lo:hi].reshape(-1), hi - lo, stride=64)
+        assert_same(v_o, r_o, v_g, r_g)
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+    assert ipt.ct_info()["fused_batches"] == len(cuts) - 1, ipt.ct_info()
+    assert ipt.jit_info()["launches_jit"] == 0, ipt.jit_info()
+
+
 def test_stage_a_stale_ports_across_icmp_only_stretches(dev):
     """The fused stage A's stale ports (Q4) where whole runs of 64-frame groups hold
     no TCP/UDP frame: every ICMP frame there keys on the ports of the last TCP/UDP
