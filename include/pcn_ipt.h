@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PCN_IPT_ABI_VERSION 9
+#define PCN_IPT_ABI_VERSION 10
 
 /* Chains and directions (ChainNameEnum; ProgramType INGRESS/EGRESS). */
 enum { PCN_IPT_INPUT = 0, PCN_IPT_FORWARD = 1, PCN_IPT_OUTPUT = 2, PCN_IPT_NCHAINS = 3 };
@@ -318,7 +318,13 @@ typedef struct {
   uint64_t frames_bytes;  /* bytes to copy (0 => n * stride) */
   uint32_t stride;
   uint32_t fixed_len;
-  uint8_t use_offsets, use_lens, use_in_port, reserved;
+  uint8_t use_offsets, use_lens, use_in_port;
+  /* With hdr_bytes: the bytes at the front of each frame that stay on the host,
+   * 0 or 12 -- the Ethernet addresses, which no stage of the path reads (the
+   * Parser starts at h_proto, Iptables_Parser_dp.c:94-108).  Each frame then
+   * crosses PCIe as hdr_bytes - 12 bytes (36 at the XDP hook).  Not with the
+   * connection table on. */
+  uint8_t hdr_skip;
   uint16_t const_in_port;
   uint16_t direction;     /* PCN_IPT_INGRESS / PCN_IPT_EGRESS */
   uint16_t hook;          /* PCN_IPT_HOOK_XDP / PCN_IPT_HOOK_TC */

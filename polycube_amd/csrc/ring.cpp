@@ -157,15 +157,40 @@ void pack_fixed(uint8_t *dst, const uint8_t *src, size_t rows, size_t stride) {
   }
   _mm_sfence();
 }
+// Rows of W bytes, W a multiple of 4 but not of 16 (the windows without their
+// 12 Ethernet-address bytes, hdr_skip): four rows are a whole number of 16-byte
+// stores, assembled in registers (compile-time copies) and streamed out.
+template <size_t W>
+void pack_fixed4(uint8_t *dst, const uint8_t *src, size_t rows, size_t stride) {
+  static_assert(W % 4 == 0 && (4 * W) % 16 == 0, "four rows: whole 16-byte stores");
+  size_t i = 0;
+  if (reinterpret_cast<uintptr_t>(dst) % 16 == 0) {
+    alignas(16) uint8_t buf[4 * W];
+    for (; i + 4 <= rows; i += 4) {
+      for (size_t r = 0; r < 4; ++r) std::memcpy(buf + r * W, src + (i + r) * stride, W);
+      __m128i *d = reinterpret_cast<__m128i *>(dst + i * W);
+      for (size_t q = 0; q < 4 * W / 16; ++q) _mm_stream_si128(d + q, _mm_load_si128(reinterpret_cast<const __m128i *>(buf) + q));
+    }
+    _mm_sfence();
+  }
+  for (; i < rows; ++i) std::memcpy(dst + i * W, src + i * stride, W);
+}
 void pack_rows(uint8_t *dst, const uint8_t *src, size_t rows, size_t hb, size_t stride) {
   switch (hb) {
     case 48: pack_fixed<48>(dst, src, rows, stride); return;
     case 64: pack_fixed<64>(dst, src, rows, stride); return;
     case 80: pack_fixed<80>(dst, src, rows, stride); return;
+    case 36: pack_fixed4<36>(dst, src, rows, stride); return;
+    case 52: pack_fixed4<52>(dst, src, rows, stride); return;
     default:
       for (size_t i = 0; i < rows; ++i) std::memcpy(dst + i * hb, src + i * stride, hb);
   }
 }
+// hdr_skip: the device rows start kSkipPad bytes into the slot's frame buffer, so
+// frame i's (unused) first bytes, read by the classify kernel's header window
+// from before row i, stay inside the buffer (and a generic-path gather's 16-byte
+// aligned start, up to 15 bytes earlier still)
+constexpr size_t kSkipPad = 32;
 }  // namespace
 
 struct pcn_ipt_ring {
@@ -308,8 +333,11 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   const uint64_t bytes = b->frames_bytes ? b->frames_bytes : b->n * uint64_t(b->stride);
   if (bytes > r->cfg.slot_bytes) return ring_fail(-EINVAL, "frame bytes exceed the slot");
   const uint32_t hb = b->hdr_bytes;
+  const uint32_t skip = b->hdr_skip;
   const bool zc = r->cfg.flags & PCN_IPT_RING_ZERO_COPY;
   if (hb && zc) return ring_fail(-EINVAL, "hdr_bytes with a zero-copy ring (the kernel reads only the headers anyway)");
+  if (skip && !hb) return ring_fail(-EINVAL, "hdr_skip needs a header-only transfer (hdr_bytes)");
+  if (skip != 0 && skip != 12) return ring_fail(-EINVAL, "hdr_skip must be 0 or 12 (the Ethernet addresses)");
   if (hb) {
     pcn_ipt_ct_info ci{};
     const bool ct = pcn_ipt_ct_get_info(r->ctx, &ci) == 0 && ci.enabled;
@@ -317,7 +345,12 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
     if (b->use_offsets) return ring_fail(-EINVAL, "a header-only transfer needs a fixed stride");
     if (hb % 16 || hb > b->stride || hb < need)
       return ring_fail(-EINVAL, "hdr_bytes must be a multiple of 16, <= stride and >= " + std::to_string(need));
+    if (skip && ct) return ring_fail(-EINVAL, "hdr_skip with the connection table on");
+    if (skip && kSkipPad + b->n * uint64_t(hb - skip) > r->cfg.slot_bytes)
+      return ring_fail(-EINVAL, "hdr_skip: the packed rows exceed the slot");
   }
+  const uint32_t rw = hb - skip;   // bytes of a frame that cross PCIe (header-only transfers)
+  uint8_t *const d_rows = s.d_frames + (skip ? kSkipPad : 0);
   if (hipSetDevice(r->device) != hipSuccess) return ring_fail(-ENODEV, "hipSetDevice failed");
   const auto t_submit = std::chrono::steady_clock::now();
   uint64_t pack_ns = 0;
@@ -329,7 +362,7 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   if (hb && r->pack && n) {
     // host pack: the windows into contiguous pinned rows (the slot's last
     // copy out of them was queued on this slot's stream: wait for it first)
-    if (s.pack_cap < n * hb) {
+    if (s.pack_cap < n * rw) {
       if (hipStreamSynchronize(st) != hipSuccess) return ring_fail(-EIO, "hipStreamSynchronize failed");
       if (s.h_pack) (void)hipHostFree(s.h_pack);
       s.h_pack = nullptr;
@@ -341,25 +374,25 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
     } else if (hipEventSynchronize(s.done) != hipSuccess) {   // (a released slot: its copies are done already)
       return ring_fail(-EIO, "hipEventSynchronize failed");
     }
-    const uint8_t *src = s.h_frames;
+    const uint8_t *src = s.h_frames + skip;
     uint8_t *dst = s.h_pack;
     const uint32_t stride = b->stride;
     const unsigned parts = r->cfg.pack_threads * 4;
-    const size_t per = (n + parts - 1) / parts;
+    const size_t per = ((n + parts - 1) / parts + 3) / 4 * 4;   // (whole groups of four rows)
     // the slot is the producer's (kFilling): the consumer's complete / release
     // need not wait for the pack
     l.unlock();
     const auto t_pack = std::chrono::steady_clock::now();
     r->pack->run([&](unsigned k) {
-      const size_t lo = k * per, hi = std::min<size_t>(n, lo + per);
-      pack_rows(dst + lo * hb, src + lo * stride, hi - lo, hb, stride);
+      const size_t lo = std::min<size_t>(n, k * per), hi = std::min<size_t>(n, lo + per);
+      pack_rows(dst + lo * rw, src + lo * stride, hi - lo, rw, stride);
     }, parts);
     pack_ns = static_cast<uint64_t>(
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_pack).count());
     l.lock();
-    ok = hipMemcpyAsync(s.d_frames, s.h_pack, n * hb, hipMemcpyHostToDevice, st) == hipSuccess;
+    ok = hipMemcpyAsync(d_rows, s.h_pack, n * rw, hipMemcpyHostToDevice, st) == hipSuccess;
   } else if (!zc) {
-    ok = hb ? hipMemcpy2DAsync(s.d_frames, hb, s.h_frames, b->stride, hb, n, hipMemcpyHostToDevice, st) == hipSuccess
+    ok = hb ? hipMemcpy2DAsync(d_rows, rw, s.h_frames + skip, b->stride, rw, n, hipMemcpyHostToDevice, st) == hipSuccess
             : hipMemcpyAsync(s.d_frames, s.h_frames, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
   }
   if (!zc) {   // the per-frame arrays the batch uses
@@ -376,11 +409,12 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   };
   if (!ok) return quiesce(-EIO, "hipMemcpyAsync (H2D) failed");
   pcn_ipt_batch batch{};
-  batch.frames = zc ? s.z_frames : s.d_frames;
-  batch.frames_bytes = hb ? n * hb : bytes;
+  // (hdr_skip: frame i starts 12 bytes before its row, in the previous row or the pad)
+  batch.frames = zc ? s.z_frames : d_rows - skip;
+  batch.frames_bytes = hb ? skip + n * rw : bytes;
   batch.offsets = b->use_offsets ? (zc ? s.z_offsets : s.d_offsets) : nullptr;
   batch.lens = b->use_lens ? (zc ? s.z_lens : s.d_lens) : nullptr;
-  batch.stride = hb ? hb : b->stride;
+  batch.stride = hb ? rw : b->stride;
   batch.fixed_len = b->fixed_len;
   batch.in_port = b->use_in_port ? (zc ? s.z_in_port : s.d_in_port) : nullptr;
   batch.const_in_port = b->const_in_port;
@@ -406,7 +440,7 @@ int pcn_ipt_ring_submit(pcn_ipt_ring *r, uint32_t slot, const pcn_ipt_ring_batch
   rs.frames += n;
   const uint64_t arrays = (b->use_offsets ? 4 : 0) + (b->use_lens ? 2 : 0) + (b->use_in_port ? 2 : 0);
   if (zc) rs.zc_bytes += n * (64 + arrays);
-  else rs.h2d_bytes += (hb ? n * hb : bytes) + n * arrays;
+  else rs.h2d_bytes += (hb ? n * rw : bytes) + n * arrays;
   rs.d2h_bytes += n * (s.d_rule_ids ? 5 : 1);
   rs.pack_ns += pack_ns;
   rs.submit_ns += static_cast<uint64_t>(

@@ -72,7 +72,7 @@ class RingStats(C.Structure):
 class RingBatch(C.Structure):
     _fields_ = [("n", C.c_uint64), ("frames_bytes", C.c_uint64), ("stride", C.c_uint32), ("fixed_len", C.c_uint32),
                 ("use_offsets", C.c_uint8), ("use_lens", C.c_uint8), ("use_in_port", C.c_uint8),
-                ("reserved", C.c_uint8), ("const_in_port", C.c_uint16), ("direction", C.c_uint16),
+                ("hdr_skip", C.c_uint8), ("const_in_port", C.c_uint16), ("direction", C.c_uint16),
                 ("hook", C.c_uint16), ("hdr_bytes", C.c_uint16)]
 
 
@@ -107,7 +107,7 @@ class ProgramInfo(C.Structure):
 
 
 # name -> (restype, argtypes); every symbol declared in include/pcn_ipt.h
-ABI_VERSION = 9            # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
+ABI_VERSION = 10           # PCN_IPT_ABI_VERSION of include/pcn_ipt.h this binding mirrors
 
 SIGNATURES = {
     "pcn_ipt_abi_version": (C.c_int, []),

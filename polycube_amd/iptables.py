@@ -503,9 +503,10 @@ class IngestRing:
                 np.ctypeslib.as_array(s.in_port, (f,)))
 
     def submit(self, slot, n, *, frames_bytes=0, stride=64, fixed_len=64, offsets=False, lens=False,
-               in_port=False, const_in_port=1, direction=INGRESS, hook=XDP, hdr_bytes=0):
-        """hdr_bytes: copy only each frame's first hdr_bytes over PCIe (pcn_ipt_ring_batch.hdr_bytes)."""
-        b = ffi.RingBatch(n, frames_bytes, stride, fixed_len, int(offsets), int(lens), int(in_port), 0,
+               in_port=False, const_in_port=1, direction=INGRESS, hook=XDP, hdr_bytes=0, hdr_skip=0):
+        """hdr_bytes: copy only each frame's first hdr_bytes over PCIe (pcn_ipt_ring_batch.hdr_bytes);
+        hdr_skip: of those, leave the first hdr_skip (0 or 12: the Ethernet addresses) on the host."""
+        b = ffi.RingBatch(n, frames_bytes, stride, fixed_len, int(offsets), int(lens), int(in_port), hdr_skip,
                           const_in_port, direction, hook, hdr_bytes)
         _check(ffi.lib().pcn_ipt_ring_submit(self._h, slot, C.byref(b)))
 

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert ffi.lib().pcn_ipt_abi_version() == ffi.ABI_VERSION == 9
+    assert ffi.lib().pcn_ipt_abi_version() == ffi.ABI_VERSION == 10
 
 
 def test_classify_fails_loudly_without_device():

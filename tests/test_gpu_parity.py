@@ -618,15 +618,19 @@ def test_ingest_ring_parity(dev, zero_copy):
     assert_counters(o, ipt)
 
 
+@pytest.mark.parametrize("skip", [0, 12], ids=["whole_window", "no_mac"])
 @pytest.mark.parametrize("pack", [False, True], ids=["strided", "host_pack"])
 @pytest.mark.parametrize("hook,hdr", [(0, 48), (1, 64)], ids=["xdp48", "tc64"])
-def test_ingest_ring_header_only(dev, hook, hdr, pack):
+def test_ingest_ring_header_only(dev, hook, hdr, pack, skip):
     """pcn_ipt_ring_batch.hdr_bytes: only each frame's first hdr bytes cross
     PCIe (a strided copy, packed on the device) while the lengths still come
     from fixed_len / lens: equal to the oracle on the whole frames.  64-byte
     frames at a 64-byte stride (the bench's slots, the fixed-stride kernel),
     fuzz frames (every protocol, edge lengths) at a 96-byte stride and up to
-    1536-byte frames; too few header bytes and offsets batches are refused."""
+    1536-byte frames; too few header bytes and offsets batches are refused.
+    hdr_skip 12: the Ethernet addresses stay on the host too (36 / 52 bytes a
+    frame cross PCIe; the device rows sit at a 36 / 52-byte stride, each frame
+    starting 12 bytes before its row), with the same verdicts."""
     from polycube_amd import IptablesError
     rs = synth.config_rules(3)
     o, ipt = make_pair({1: rs.rules()}, {1: "DROP"}, jit=1)
@@ -644,14 +648,15 @@ def test_ingest_ring_header_only(dev, hook, hdr, pack):
             lens[:n] = ln
             kw = dict(lens=True)
         frames[:f.size] = f
-        ring.submit(slot, n, stride=stride, fixed_len=stride, hook=hook, hdr_bytes=hdr, **kw)
+        ring.submit(slot, n, stride=stride, fixed_len=stride, hook=hook, hdr_bytes=hdr, hdr_skip=skip, **kw)
         v_o, r_o = o.classify(f, n=n, lens=ln, stride=stride, fixed_len=stride, hook=hook, nthreads=NTHREADS)
         done, v, r = ring.complete()
         assert done == slot
         assert_same(v_o, r_o, v.copy(), r.copy())
         ring.release(done)
     slot = ring.acquire()[0]
-    for bad in (dict(hdr_bytes=hdr - 16), dict(hdr_bytes=hdr + 8), dict(hdr_bytes=hdr, offsets=True)):
+    for bad in (dict(hdr_bytes=hdr - 16), dict(hdr_bytes=hdr + 8), dict(hdr_bytes=hdr, offsets=True),
+                dict(hdr_skip=12), dict(hdr_bytes=hdr, hdr_skip=4)):
         with pytest.raises(IptablesError) as e:
             ring.submit(slot, 16, stride=128, fixed_len=128, hook=hook, **bad)
         assert e.value.code == -22
