@@ -95,7 +95,8 @@ def trial(seed, torch, dev):
         ch.default = d
         ch.apply_rules()
         nrules[c] = len(rules)
-    stride = int(rng.choice([64, 96, 128]))
+    # (68, 100, 1500: strides the fixed-stride path takes with dword-aligned loads)
+    stride = int(rng.choice([64, 96, 128, 68, 100, 1500]))
     n = int(rng.integers(1, 1 << 15))
     frames, lens = synth.fuzz_frames(n, seed, synth.make_rules(64, seed, protos=(6, 17, 1)), stride=stride)
     frames = frames.reshape(-1)
