@@ -2191,17 +2191,45 @@ static_assert(kCountChunk * 65535 < (1ull << 40) && kCountChunk < (1ull << 24), 
 // 93 us; 256 of them 29 us).
 inline uint64_t count_chunk(uint64_t n, int num_cus) {
   constexpr uint64_t q = 4 * kCountBlock;
-  const uint64_t c = (n / uint64_t(num_cus) + q - 1) / q * q;   // (two per CU measured slower: 29 -> 36 us)
+  const uint64_t c = (n / uint64_t(num_cus) + q - 1) / q * q;   // (two per CU measured slower: 29 -> 36 us; 33 -> 38 in r06_s19)
   return c < q ? q : c > kCountChunk ? kCountChunk : c;
 }
 
+// bin k of ct_count's 4 x (2 + kLdsRules): per chain c < 3 the default (0),
+// accept-established (1) and rule bins (2..); group 3 the Horus rule ids
+__device__ __forceinline__ void ct_count_add(const CtBatch &b, uint32_t k, unsigned long long pk,
+                                             unsigned long long by) {
+  constexpr uint32_t per = 2 + kLdsRules;
+  const uint32_t c = k / per, bin = k % per;
+  unsigned long long *dp, *db;
+  if (c == 3) { dp = &b.horus_ctr[2 * (bin - 2)]; db = &b.horus_ctr[2 * (bin - 2) + 1]; }
+  else if (bin == 0) { dp = &b.ctr[c][0]; db = &b.ctr[c][1]; }
+  else if (bin == 1) { dp = &b.ae_ctr[2 * c]; db = &b.ae_ctr[2 * c + 1]; }
+  else { dp = &b.ctr[c][2 + 2 * (bin - 2)]; db = &b.ctr[c][3 + 2 * (bin - 2)]; }
+  atomicAdd(dp, pk);
+  atomicAdd(db, by);
+}
+
 #ifndef PCN_CT_COUNT_U
-#define PCN_CT_COUNT_U 16
+#define PCN_CT_COUNT_U 8   // (16: 37.0 us a 2^24 batch against 33.4, profiles/r06_s19/)
 #endif
+template <class T>
+__device__ __forceinline__ T sel3(uint32_t c, T a, T b, T d) {
+  return c == 0 ? a : c == 1 ? b : d;
+}
 // It also leaves the next batch's control words and ports descriptors zeroed
 // (ctl[0, kCtlZero), pdesc[0, ngroups)): two memsets a batch were a launch each.
-__global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk, uint32_t *ctl,
-                                unsigned long long *pdesc, uint64_t ngroups) {
+// The workgroup's bins go out as one row of `part` (ct_count_reduce_kernel sums
+// the rows and adds each counter once): adding them to the counters here, two
+// device-scope atomics per non-zero bin from every workgroup, landed ~500 K
+// atomics a 2^24 batch on ~2 K addresses, serialised where they meet.  (part
+// null: the atomics, PCN_IPT_DEBUG_CT_COUNT_ATOMIC=1, for the A/B.)
+// VEC: rule ids and {len, cinfo} words read 16 bytes (four packets) a load
+// (both arrays 16-byte aligned; a chunk is a multiple of 4096 packets).
+template <bool VEC>
+__global__ __launch_bounds__(kCountBlock) void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk,
+                                                               uint32_t *ctl, unsigned long long *pdesc,
+                                                               uint64_t ngroups, unsigned long long *part) {
   constexpr uint32_t per = 2 + kLdsRules;
   for (uint64_t g = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; g < ngroups; g += uint64_t(gridDim.x) * blockDim.x)
     pdesc[g] = 0;
@@ -2217,56 +2245,107 @@ __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk, 
   // The default rule's packets (half of them on the bench traffic) go to one
   // bin per chain: as LDS atomics, 32 lanes of an instruction on one address
   // serialised.  A lane sums them in registers instead (packed as the bins).
-  unsigned long long dflt[3] = {0, 0, 0};
-  // packets per thread whose loads are in flight together (4: a thread's 64
-  // packets of a 2^24 batch took 16 dependent round trips)
-  constexpr uint32_t U = PCN_CT_COUNT_U;
-  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
-    int32_t rids[U];
-    uint32_t lcv[U];
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const uint64_t i = i0 + u * blockDim.x;
-      rids[u] = i < hi ? b.rule_ids[i] : PCN_IPT_RID_NOCHAIN;
-      lcv[u] = i < hi ? lcs[i] : 3u << 16;
+  unsigned long long dflt0 = 0, dflt1 = 0, dflt2 = 0;
+  // (b.ncounted[c] or b.ctr[c] indexed by a lane's chain is a vector load from
+  // the kernel arguments, or from a private copy of them, whose wait, vmcnt(0),
+  // drained every load in flight: they are kept in scalars, made opaque so the
+  // compiler cannot fold the selects back into an indexed load)
+  auto sreg = [](auto x) {
+    asm volatile("" : "+s"(x));
+    return x;
+  };
+  const uint32_t nc0 = sreg(b.ncounted[0]), nc1 = sreg(b.ncounted[1]), nc2 = sreg(b.ncounted[2]);
+  unsigned long long *const ctr0 = sreg(b.ctr[0]), *const ctr1 = sreg(b.ctr[1]), *const ctr2 = sreg(b.ctr[2]);
+  unsigned long long *const hctr = b.horus_ctr;
+  // One packet's bin by selects, one branch for the LDS atomic and one for the
+  // rare global counters (rule or Horus ids >= kLdsRules): the branch per case
+  // made the kernel instruction-bound (63 us a 2^24 batch, 31 of them the loads).
+  // Horus ids: Horus_dp.c:80-90, counted at the lookup, whatever the chain.
+  // (values selected by sel3: `c == 0 ? x : ...` of lvalues is a select between
+  // their addresses, which put them in scratch)
+  auto count1 = [&](int32_t rid, uint32_t lc) {
+    const uint32_t len = lc & 0xffff, c = (lc >> 16) & 3;
+    const unsigned long long v = (1ull << 40) | len;
+    const bool hor = rid <= PCN_IPT_RID_HORUS0;
+    const uint32_t hid = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
+    const bool chain = !hor && c != 3;
+    const bool rule = chain && rid >= 0 && static_cast<uint32_t>(rid) < sel3(c, nc0, nc1, nc2);
+    const bool hc = hor && hctr != nullptr;
+    const bool dfl = chain && rid == PCN_IPT_RID_DEFAULT;
+    dflt0 += dfl && c == 0 ? v : 0ull;
+    dflt1 += dfl && c == 1 ? v : 0ull;
+    dflt2 += dfl && c == 2 ? v : 0ull;
+    const uint32_t id = hc ? hid : static_cast<uint32_t>(rid);
+    if ((hc || rule) && id >= kLdsRules) {
+      unsigned long long *const cr =
+          hc ? hctr + 2 * uint64_t(id) : sel3(c, ctr0, ctr1, ctr2) + 2 + 2 * uint64_t(id);
+      atomicAdd(cr, 1ull);
+      atomicAdd(cr + 1, static_cast<unsigned long long>(len));
     }
+    const bool lds = (hc || rule) ? id < kLdsRules : chain && rid == -3;
+    const uint32_t bin = hc ? 3 * per + 2 + id : rule ? c * per + 2 + id : c * per + 1;
+    if (lds) atomicAdd(&bins[bin], v);
+  };
+  // U packets per thread whose loads are in flight together (4: a thread's 64
+  // packets of a 2^24 batch took 16 dependent round trips): unconditional, the
+  // index clamped to the chunk's last (a conditional load merges into a phi the
+  // compiler resolves with an immediate wait); lanes past it are masked where
+  // the packets are counted.  (The next round's loads issued before a round is
+  // counted measured slower, 35.1 against 33.4 us: r06_s19.)
+  constexpr uint32_t U = PCN_CT_COUNT_U;
+  if constexpr (VEC) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    constexpr uint32_t V = U / 4;
+    const u32x4 *const rv = reinterpret_cast<const u32x4 *>(b.rule_ids);
+    const u32x4 *const lv = reinterpret_cast<const u32x4 *>(lcs);
+    const uint64_t lo4 = lo / 4, hi4 = hi / 4;          // lo is a multiple of 4
+    const uint64_t step = uint64_t(V) * blockDim.x;
+    auto load = [&](u32x4 *r, u32x4 *l, uint64_t q0) {
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const int32_t rid = rids[u];
-      const uint32_t lc = lcv[u], len = lc & 0xffff, cinfo = lc >> 16;
-      if (rid <= PCN_IPT_RID_HORUS0) {                  // Horus_dp.c:80-90, counted at the lookup
-        if (!b.horus_ctr) continue;
-        const uint32_t id = static_cast<uint32_t>(PCN_IPT_RID_HORUS0 - rid);
-        if (id >= kLdsRules) {
-          atomicAdd(&b.horus_ctr[2 * id], 1ull);
-          atomicAdd(&b.horus_ctr[2 * id + 1], static_cast<unsigned long long>(len));
-        } else {
-          atomicAdd(&bins[3 * per + 2 + id], (1ull << 40) | len);
-        }
-        continue;
+      for (uint32_t u = 0; u < V; ++u) {
+        const uint64_t q = q0 + u * blockDim.x;
+        const uint64_t j = q < hi4 ? q : hi4 - 1;
+        r[u] = rv[j];
+        l[u] = lv[j];
       }
-      const uint32_t c = cinfo & 3;
-      if (c == 3) continue;
-      uint32_t bin;
-      if (rid >= 0) {
-        if (uint32_t(rid) >= b.ncounted[c]) continue;
-        if (uint32_t(rid) >= kLdsRules) {
-          atomicAdd(&b.ctr[c][2 + 2 * uint64_t(rid)], 1ull);
-          atomicAdd(&b.ctr[c][3 + 2 * uint64_t(rid)], static_cast<unsigned long long>(len));
-          continue;
-        }
-        bin = 2 + uint32_t(rid);
-      } else if (rid == PCN_IPT_RID_DEFAULT) {
-        dflt[c] += (1ull << 40) | len;               // (c < 3)
-        continue;
-      } else if (rid == -3) {
-        bin = 1;
-      } else {
-        continue;
+    };
+    for (uint64_t q0 = lo4 + threadIdx.x; q0 < hi4; q0 += step) {
+      u32x4 r[V], l[V];
+      load(r, l, q0);
+#pragma unroll
+      for (uint32_t u = 0; u < V; ++u) {
+        if (q0 + u * blockDim.x >= hi4) continue;
+        count1(static_cast<int32_t>(r[u].x), l[u].x);
+        count1(static_cast<int32_t>(r[u].y), l[u].y);
+        count1(static_cast<int32_t>(r[u].z), l[u].z);
+        count1(static_cast<int32_t>(r[u].w), l[u].w);
       }
-      atomicAdd(&bins[c * per + bin], (1ull << 40) | len);
+    }
+    if (threadIdx.x < hi - hi4 * 4) {                   // the last 0-3 packets of an unaligned end
+      const uint64_t i = hi4 * 4 + threadIdx.x;
+      count1(b.rule_ids[i], lcs[i]);
+    }
+  } else {
+    const uint64_t step = uint64_t(U) * blockDim.x;
+    auto load = [&](int32_t *r, uint32_t *l, uint64_t i0) {
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint64_t i = i0 + u * blockDim.x;
+        const uint64_t j = i < hi ? i : hi - 1;
+        r[u] = b.rule_ids[j];
+        l[u] = lcs[j];
+      }
+    };
+    for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += step) {
+      int32_t rids[U];
+      uint32_t lcv[U];
+      load(rids, lcv, i0);
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u)
+        if (i0 + u * blockDim.x < hi) count1(rids[u], lcv[u]);
     }
   }
+  const unsigned long long dflt[3] = {dflt0, dflt1, dflt2};
   // the default bins, summed over the wave: one LDS atomic per wave and chain
 #pragma unroll
   for (uint32_t c = 0; c < 3; ++c) {
@@ -2276,18 +2355,56 @@ __global__ void ct_count_kernel(CtBatch b, const uint32_t *lcs, uint64_t chunk, 
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(&bins[c * per], v);
   }
   __syncthreads();
+  if (part) {
+    unsigned long long *const row = part + uint64_t(blockIdx.x) * (4 * per);
+    for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) row[k] = bins[k];
+    return;
+  }
   for (uint32_t k = threadIdx.x; k < 4 * per; k += blockDim.x) {
     const unsigned long long v = bins[k];
-    if (!v) continue;
-    const uint32_t c = k / per, bin = k % per;
-    unsigned long long *dp, *db;
-    if (c == 3) { dp = &b.horus_ctr[2 * (bin - 2)]; db = &b.horus_ctr[2 * (bin - 2) + 1]; }
-    else if (bin == 0) { dp = &b.ctr[c][0]; db = &b.ctr[c][1]; }
-    else if (bin == 1) { dp = &b.ae_ctr[2 * c]; db = &b.ae_ctr[2 * c + 1]; }
-    else { dp = &b.ctr[c][2 + 2 * (bin - 2)]; db = &b.ctr[c][3 + 2 * (bin - 2)]; }
-    atomicAdd(dp, v >> 40);
-    atomicAdd(db, v & ((1ull << 40) - 1));
+    if (v) ct_count_add(b, k, v >> 40, v & ((1ull << 40) - 1));
   }
+}
+
+// Per bin (64 a workgroup, lane = bin) the sum of the ct_count rows: 16 waves
+// take every 16th row, their sums meet in LDS, and each non-zero bin is added
+// to its counters once.
+constexpr uint32_t kCountRedWaves = 16;
+__global__ __launch_bounds__(64 * kCountRedWaves) void ct_count_reduce_kernel(CtBatch b,
+                                                                               const unsigned long long *part,
+                                                                               uint32_t rows) {
+  constexpr uint32_t per = 2 + kLdsRules, nbins = 4 * per;
+  constexpr uint32_t R = 8;   // rows whose loads are in flight together
+  __shared__ unsigned long long sp[kCountRedWaves][64], sb[kCountRedWaves][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t k = blockIdx.x * 64 + lane;
+  unsigned long long p = 0, by = 0;
+  if (k < nbins) {
+    for (uint32_t r0 = w; r0 < rows; r0 += R * kCountRedWaves) {
+      unsigned long long v[R];
+#pragma unroll
+      for (uint32_t j = 0; j < R; ++j) {
+        const uint32_t r = r0 + j * kCountRedWaves;
+        v[j] = part[uint64_t(r < rows ? r : w) * nbins + k];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < R; ++j) {
+        if (r0 + j * kCountRedWaves >= rows) continue;
+        p += v[j] >> 40;
+        by += v[j] & ((1ull << 40) - 1);
+      }
+    }
+  }
+  sp[w][lane] = p;
+  sb[w][lane] = by;
+  __syncthreads();
+  if (w || k >= nbins) return;
+#pragma unroll
+  for (uint32_t x = 1; x < kCountRedWaves; ++x) {
+    p += sp[x][lane];
+    by += sb[x][lane];
+  }
+  if (p) ct_count_add(b, k, p, by);
 }
 
 // Stateless accept-established: rule 0 of an AE chain is exactly
@@ -2349,6 +2466,8 @@ struct CtScratch {
   // (ct_stale_fix), per 1024 groups the last ports word (ct_stale_agg)
   unsigned long long *fixm = nullptr;
   unsigned long long *sagg = nullptr;
+  unsigned long long *cpart = nullptr;    // ct_count: a row of bins per workgroup
+  uint64_t cpart_rows = 0;
 };
 
 CtScratch *ct_scratch_new() { return new CtScratch(); }
@@ -2362,7 +2481,8 @@ void ct_scratch_free(CtScratch *s) {
                   static_cast<void *>(s->heads),
                   static_cast<void *>(s->zfound), static_cast<void *>(s->th_list), static_cast<void *>(s->bm),
                   static_cast<void *>(s->evh), static_cast<void *>(s->seg), static_cast<void *>(s->hx),
-                  static_cast<void *>(s->cuts), static_cast<void *>(s->fixm), static_cast<void *>(s->sagg)})
+                  static_cast<void *>(s->cuts), static_cast<void *>(s->fixm), static_cast<void *>(s->sagg),
+                  static_cast<void *>(s->cpart)})
     if (p) (void)hipFree(p);
   radix_free(s->rx);
   delete s;
@@ -2734,9 +2854,27 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
   ++t.seq;                                     // the next batch's touch stamps are newer
   const uint64_t cchunk = count_chunk(b.n, num_cus);
   const unsigned cgrid = static_cast<unsigned>((b.n + cchunk - 1) / cchunk);
-  hipLaunchKernelGGL(ct_count_kernel, dim3(cgrid), dim3(kCountBlock), 0, st, b, s.lcs, cchunk, s.ctl, s.pdesc,
-                     b.n / 64 + 1);
+  static const bool count_atomic = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_CT_COUNT_ATOMIC");
+    return e && e[0] == '1';
+  }();
+  constexpr uint32_t kCountBins = 4 * (2 + kLdsRules);
+  if (!count_atomic && s.cpart_rows < cgrid) {
+    if (s.cpart) CT_CHECK(hipFree(s.cpart));
+    s.cpart = nullptr;
+    s.cpart_rows = 0;
+    CT_CHECK(hipMalloc(&s.cpart, uint64_t(cgrid) * kCountBins * 8));
+    s.cpart_rows = cgrid;
+  }
+  const bool cvec = (reinterpret_cast<uintptr_t>(b.rule_ids) | reinterpret_cast<uintptr_t>(s.lcs)) % 16 == 0;
+  hipLaunchKernelGGL(cvec ? ct_count_kernel<true> : ct_count_kernel<false>, dim3(cgrid), dim3(kCountBlock), 0, st, b,
+                     s.lcs, cchunk, s.ctl, s.pdesc, b.n / 64 + 1, count_atomic ? nullptr : s.cpart);
   CT_CHECK(hipGetLastError());
+  if (!count_atomic) {
+    hipLaunchKernelGGL(ct_count_reduce_kernel, dim3((kCountBins + 63) / 64), dim3(64 * kCountRedWaves), 0, st, b,
+                       s.cpart, cgrid);
+    CT_CHECK(hipGetLastError());
+  }
   s.dirty = false;
   return hipSuccess;
 }

@@ -115,6 +115,31 @@ def test_flow_traffic_parity_across_batches(dev, jit, mode):
     assert ipt.ct_info()["inserts_lost"] == 0
 
 
+@pytest.mark.parametrize("offset", [0, 1])
+def test_counters_of_a_10k_rule_chain_with_rule_ids_at_any_alignment(dev, offset):
+    """ct_count over the final rule ids: rule ids above the 1024 LDS bins (global
+    counters), ragged batch ends (the 16-byte loads' tail), and a caller's rule-id
+    buffer 4 bytes off 16-byte alignment (the 4-byte-load kernel)."""
+    rs = synth.config_rules(5)
+    rules = rs.rules()
+    o, ipt = ct_pair({1: rules}, {1: "DROP"}, jit=1, max_rules=16384, max_counted_rules=10000,
+                     max_action_rules=10000)
+    f, lens = synth.flow_traffic(30000, 2000, 11, rs=rs, lens_mode="mixed")
+    for lo, hi in ((0, 9001), (9001, 9003), (9003, 30000)):
+        n = hi - lo
+        buf = torch.empty(n + 4, dtype=torch.int32, device=dev)
+        rid = buf[offset:offset + n]
+        assert (rid.data_ptr() % 16 != 0) == (offset != 0)
+        v_o, r_o = o.classify(f[lo * 128:hi * 128], n=n, lens=lens[lo:hi], stride=128, fixed_len=128)
+        v_g, r_g = ipt.classify(t(dev, f[lo * 128:hi * 128]), n=n, lens=t(dev, lens[lo:hi], np.int16), stride=128,
+                                fixed_len=128, rule_ids=rid)
+        torch.cuda.synchronize()
+        assert_same(v_o, r_o, v_g.cpu().numpy(), r_g.cpu().numpy())
+    assert (r_o >= 1024).any()
+    assert_tables(o, ipt)
+    assert_counters(o, ipt, n=len(rules) + 1)
+
+
 @pytest.mark.parametrize("mode", ["plain", "ct_rules"])
 def test_fixed_stride_64_with_lengths(dev, mode):
     """ct_prep's coalesced path (frames at a 64-byte stride, windows and walk records
