@@ -1,15 +1,16 @@
 // radix.hip — the stateful pipeline's sort (radix.hpp): stable LSD radix sort
 // of (key bucket, batch index) pairs, hand-written for gfx950, reduce-then-scan.
 //
-// Each digit pass (9 / 8 / 8 bits of a 25-bit key) splits its input into one
-// contiguous super-tile per workgroup (a whole number of 8192-item sub-tiles,
-// one workgroup of 1024 threads per CU), and runs three kernels over the same
-// split:
-// 1. radix_up_kernel: the super-tile's count of every digit (LDS adds; the
-//    all-ones digit -- the batch's "no table" bucket, often most keys --
-//    wave-aggregated), cnt[b][512];
+// Each digit pass (8 / 8 / 8 bits of a 2^24 batch's 24-bit key; up to 9 bits a
+// pass) splits its input into one contiguous super-tile per CU (a whole
+// number of 8192-item sub-tiles), and runs three kernels over the same split:
+// 1. radix_up_kernel: each half super-tile's count of every digit (two
+//    workgroups a super-tile, two per CU, so one's loads overlap the other's
+//    LDS adds: 31 -> 26 us a pass; the all-ones digit -- the batch's "no
+//    table" bucket, often most keys -- wave-aggregated), cnt[row][512];
 // 2. radix_colscan_kernel: per digit the exclusive prefix over super-tiles,
-//    pre[b][d], and the digit's total, tot[d];
+//    pre[b][d], and the digit's total, tot[d] (16 digits a workgroup, the rows
+//    in 64 slices: 5 us at 512 rows);
 // 3. radix_pass_kernel: the digits' global starts (an exclusive scan of tot),
 //    then the super-tile's sub-tiles in order: each ranked wave by wave and
 //    slot by slot in input order (lanes of one digit matched with `bits`
@@ -30,6 +31,7 @@
 #include "radix.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pcn {
 namespace {
@@ -86,6 +88,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *wtot) 
   return before + inc - x;
 }
 
+// SUB workgroups share a super-tile, each counting 1 / SUB of it into a row of
+// its own (cnt[b * SUB + part]; the column scan sums them): two per CU overlap
+// one's loads with the other's LDS atomics.
+template <uint32_t U, uint32_t SUB>
 __global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, uint64_t n, uint32_t shift,
                                                                uint32_t bits, uint64_t per, uint32_t *cnt,
                                                                uint32_t runs) {
@@ -94,7 +100,9 @@ __global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, 
   const uint32_t dmask = (1u << bits) - 1;
   if (tid < kRMaxBins) h[tid] = 0;
   __syncthreads();
-  const uint64_t lo = uint64_t(blockIdx.x) * per, hi = lo + per < n ? lo + per : n;
+  const uint64_t sper = per / SUB;   // (per: a multiple of 8192)
+  const uint64_t lo = uint64_t(blockIdx.x / SUB) * per + (blockIdx.x % SUB) * sper;
+  const uint64_t hi = lo + sper < n ? lo + sper : n > lo ? n : lo;   // (a part past the end: empty)
   // Lanes of one digit add together, by their leader: the all-ones digit (the
   // "no table" bucket) and, in the last pass (`runs`), the first other lane's
   // digit; the rest lane by lane.  The last pass reads keys sorted by every
@@ -119,8 +127,7 @@ __global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, 
     if (v && dk != dmask && dk != d0) atomicAdd(&h[dk], 1u);
   };
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  constexpr uint32_t U = 16;   // 16-byte loads in flight per thread
-  // lo is a multiple of 8192: 16-byte aligned.  The whole 16-byte vectors
+  // U 16-byte loads in flight per thread; lo is a multiple of 4096: 16-byte aligned.  The whole 16-byte vectors
   // [lo, hi4) are read with unconditional loads (the index clamped, the lanes
   // past the range masked): a conditional load merges into a phi the compiler
   // resolves with an immediate vmcnt(0), one round trip per load.  The last
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, 
       add(k4[u].w, v);
     }
   };
-  // A round is 16 loads per thread, all in flight together (256 KB a CU:
+  // A round is U loads per thread, all in flight together (256 KB a CU:
   // a 2^24-key batch is one round per workgroup).  Double-buffered rounds
   // measured no better: the compiler drains the loads a loop carries at the
   // loop head anyway.
@@ -163,28 +170,61 @@ __global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, 
   if (tid < kRMaxBins) cnt[uint64_t(blockIdx.x) * kRMaxBins + tid] = h[tid];
 }
 
-// 64 digits a workgroup (lane = digit), wave w a contiguous range of super-tiles
+static uint32_t up_sub() {   // PCN_IPT_DEBUG_RADIX_UP_SUB=1|2: workgroups per super-tile in the up-sweep (A/B)
+  static const uint32_t v = [] {
+    const char *e = std::getenv("PCN_IPT_DEBUG_RADIX_UP_SUB");
+    return e && e[0] == '1' ? 1u : 2u;
+  }();
+  return v;
+}
+
+// 16 digits a workgroup; the rows (sub per super-tile) in 64 slices, lane l of
+// wave w taking digit l % 16 of slice 4w + l / 16: each slice's sum, their
+// exclusive prefix in LDS, then each slice's rows again with the running
+// prefix (pre is written per super-tile, at its first row).  The rows of a
+// slice are read R at a time, their loads in flight together (unconditional,
+// the row clamped and masked).  (64 digits a workgroup over 16 wave-slices,
+// one round trip per row: 7.5 us a scan at 256 rows, 12.4 at 512.)
+constexpr uint32_t kScanDigits = 16, kScanSlices = kRBlock / kScanDigits;   // 64
 __global__ __launch_bounds__(kRBlock) void radix_colscan_kernel(const uint32_t *cnt, uint32_t *pre, uint32_t *tot,
-                                                                 uint32_t groups, uint32_t nb) {
-  __shared__ uint32_t part[kRWaves][64];
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t d = blockIdx.x * 64 + lane;
-  const uint32_t per = (groups + kRWaves - 1) / kRWaves;
-  const uint32_t lo = w * per, hi = lo + per < groups ? lo + per : groups;
+                                                                 uint32_t groups, uint32_t nb, uint32_t sub) {
+  __shared__ uint32_t part[kScanSlices][kScanDigits];
+  const uint32_t dl = threadIdx.x % kScanDigits, sl = threadIdx.x / kScanDigits;
+  const uint32_t d = blockIdx.x * kScanDigits + dl;
+  const uint32_t rps = (groups + kScanSlices - 1) / kScanSlices;
+  const uint32_t lo = sl * rps < groups ? sl * rps : groups, hi = lo + rps < groups ? lo + rps : groups;
+  constexpr uint32_t R = 8;
+  const uint32_t dd = d < nb ? d : 0;
+  auto chunk = [&](uint32_t *x, uint32_t b0) {
+#pragma unroll
+    for (uint32_t j = 0; j < R; ++j) {
+      const uint32_t b = b0 + j < hi ? b0 + j : hi - 1;
+      x[j] = cnt[uint64_t(b) * kRMaxBins + dd];
+    }
+  };
   uint32_t sum = 0;
-  if (d < nb)
-    for (uint32_t b = lo; b < hi; ++b) sum += cnt[uint64_t(b) * kRMaxBins + d];
-  part[w][lane] = sum;
+  for (uint32_t b0 = lo; b0 < hi; b0 += R) {
+    uint32_t x[R];
+    chunk(x, b0);
+#pragma unroll
+    for (uint32_t j = 0; j < R; ++j) sum += b0 + j < hi ? x[j] : 0u;
+  }
+  part[sl][dl] = sum;
   __syncthreads();
   uint32_t run = 0;
-  for (uint32_t k = 0; k < w; ++k) run += part[k][lane];
-  if (d < nb && w == kRWaves - 1) tot[d] = run + sum;
-  if (d < nb)
-    for (uint32_t b = lo; b < hi; ++b) {
-      const uint32_t x = cnt[uint64_t(b) * kRMaxBins + d];
-      pre[uint64_t(b) * kRMaxBins + d] = run;
-      run += x;
+  for (uint32_t k = 0; k < sl; ++k) run += part[k][dl];
+  if (d < nb && sl == kScanSlices - 1) tot[d] = run + sum;
+  for (uint32_t b0 = lo; b0 < hi; b0 += R) {
+    uint32_t x[R];
+    chunk(x, b0);
+#pragma unroll
+    for (uint32_t j = 0; j < R; ++j) {
+      const uint32_t b = b0 + j;
+      if (b >= hi) break;
+      if (d < nb && b % sub == 0) pre[uint64_t(b / sub) * kRMaxBins + d] = run;
+      run += x[j];
     }
+  }
 }
 
 // 4 waves per SIMD.  A sub-tile's values and the next sub-tile's keys are
@@ -370,19 +410,28 @@ int radix_sort_pairs(RadixScratch &s, uint32_t *keys_in, uint32_t *keys_out, uin
   const uint64_t subs = (n + kRTile - 1) / kRTile;
   const uint64_t per = (subs + g0 - 1) / g0 * kRTile;
   const uint32_t groups = static_cast<uint32_t>((n + per - 1) / per);
+  constexpr uint32_t kMaxSub = 2;
+  const uint32_t sub = up_sub();
   if (s.seg_groups < groups) {
     if (s.seg) RX_CHECK(hipFree(s.seg));
     s.seg = nullptr;
-    RX_CHECK(hipMalloc(&s.seg, (2 * uint64_t(groups) + 1) * kRMaxBins * 4));
+    RX_CHECK(hipMalloc(&s.seg, ((kMaxSub + 1) * uint64_t(groups) + 1) * kRMaxBins * 4));
     s.seg_groups = groups;
   }
-  uint32_t *const cnt = s.seg, *const pre = cnt + uint64_t(groups) * kRMaxBins, *const tot = pre + uint64_t(groups) * kRMaxBins;
+  uint32_t *const cnt = s.seg, *const pre = cnt + uint64_t(groups) * kMaxSub * kRMaxBins;
+  uint32_t *const tot = pre + uint64_t(groups) * kRMaxBins;
   for (uint32_t p = 0; p < dg.npass; ++p) {
     const uint32_t nb = 1u << dg.bits[p];
-    hipLaunchKernelGGL(radix_up_kernel, dim3(groups), dim3(kRBlock), 0, st, kin[p], n, dg.shift[p], dg.bits[p], per,
-                       cnt, p > 0 && p + 1 == dg.npass ? 1u : 0u);
+    const uint32_t runs = p > 0 && p + 1 == dg.npass ? 1u : 0u;
+    if (sub == 2)
+      hipLaunchKernelGGL((radix_up_kernel<8, 2>), dim3(2 * groups), dim3(kRBlock), 0, st, kin[p], n, dg.shift[p],
+                         dg.bits[p], per, cnt, runs);
+    else
+      hipLaunchKernelGGL((radix_up_kernel<16, 1>), dim3(groups), dim3(kRBlock), 0, st, kin[p], n, dg.shift[p],
+                         dg.bits[p], per, cnt, runs);
     RX_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(radix_colscan_kernel, dim3((nb + 63) / 64), dim3(kRBlock), 0, st, cnt, pre, tot, groups, nb);
+    hipLaunchKernelGGL(radix_colscan_kernel, dim3((nb + kScanDigits - 1) / kScanDigits), dim3(kRBlock), 0, st, cnt,
+                       pre, tot, sub * groups, nb, sub);
     RX_CHECK(hipGetLastError());
     if (vin[p])
       hipLaunchKernelGGL(radix_pass_kernel<true>, dim3(groups), dim3(kRBlock), kPassLds, st, kin[p], vin[p], kout[p],
