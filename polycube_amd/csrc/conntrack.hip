@@ -2095,11 +2095,12 @@ __global__ __launch_bounds__(kEvBlock) void ct_ev_pass_kernel(CtTable t, uint32_
 
 // Delete the live entries whose stamp is at most the chosen one (exactly the
 // oldest live - max_entries), count them, and clear the histograms.
-__global__ __launch_bounds__(256) void ct_ev_evict_kernel(CtTable t, const uint32_t *ctl, uint32_t *hist) {
+constexpr uint32_t kEvictBlock = 1024;
+__global__ __launch_bounds__(kEvictBlock) void ct_ev_evict_kernel(CtTable t, const uint32_t *ctl, uint32_t *hist) {
   const uint64_t stp = uint64_t(gridDim.x) * blockDim.x;
   const uint64_t g = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   for (uint64_t k = g; k < uint64_t(kEvPasses) * kEvBins; k += stp) hist[k] = 0;
-  if (!ctl[kCtlEvict]) return;
+  if (!ctl[kCtlEvict]) return;                       // (uniform: every thread returns)
   const uint64_t cut = *reinterpret_cast<const unsigned long long *>(ctl + kCtlEvPrefix);
   const uint64_t cap = uint64_t(1) << t.cap_log2;
   uint32_t n = 0;
@@ -2123,11 +2124,21 @@ __global__ __launch_bounds__(256) void ct_ev_evict_kernel(CtTable t, const uint3
       ++n;
     }
   }
-  // one atomic per wave on the one counter (one per thread with a deletion
-  // serialised there: ~200 K of them when a batch overflows the table)
+  // one atomic per workgroup on the one counter: device-scope atomics on one
+  // address serialise (~7 ns apiece), and one per wave -- 4,096 waves of a
+  // 2^20-slot table, nearly all deleting on the bench traffic -- was 30 us of
+  // the kernel's 30 (one per thread with a deletion: ~200 K of them)
+  __shared__ uint32_t wn[kEvictBlock / 64];
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o);
-  if ((threadIdx.x & 63) == 0 && n) atomicAdd(&t.stats[1], static_cast<unsigned long long>(n));
+  if ((threadIdx.x & 63) == 0) wn[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kEvictBlock / 64; ++w) tot += wn[w];
+    if (tot) atomicAdd(&t.stats[1], static_cast<unsigned long long>(tot));
+  }
 }
 
 // Long echo replies (K_HARD) into the walk: a reply joins its own key's run
@@ -2847,8 +2858,9 @@ int ct_run(const CtBatch &b, CtTable &t, CtScratch &s, int num_cus, void *stream
       hipLaunchKernelGGL(ct_ev_pass_kernel, dim3(pgrid2), dim3(kEvBlock), 0, st, t, s.ctl, s.evh, p);
       CT_CHECK(hipGetLastError());
     }
-    const unsigned egrid = static_cast<unsigned>(std::min<uint64_t>(cap / 256 + 1, uint64_t(num_cus) * 4));
-    hipLaunchKernelGGL(ct_ev_evict_kernel, dim3(egrid), dim3(256), 0, st, t, s.ctl, s.evh);
+    // one workgroup per CU (a 2^20-slot table: 4 stamps a thread, one round)
+    const unsigned egrid = static_cast<unsigned>(std::min<uint64_t>(cap / kEvictBlock + 1, uint64_t(num_cus)));
+    hipLaunchKernelGGL(ct_ev_evict_kernel, dim3(egrid), dim3(kEvictBlock), 0, st, t, s.ctl, s.evh);
     CT_CHECK(hipGetLastError());
   }
   ++t.seq;                                     // the next batch's touch stamps are newer
