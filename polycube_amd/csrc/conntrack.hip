@@ -2961,8 +2961,12 @@ __device__ __forceinline__ uint32_t flow_owner_core(const CtBatch &b, uint64_t i
     return at + 4 <= b.frames_bytes ? *reinterpret_cast<const uint32_t *>(b.frames + at) : 0u;
   };
   uint32_t s = 0;
+  // (vec: word k or k + 1 of h12 chosen by value -- h12[k + s] indexed by the
+  // run-time shift, or a select of the two elements as lvalues, put the whole
+  // array in scratch: 400 bytes a lane in flow_count)
   auto W = [&](uint32_t k) {
-    if (vec && k + s < 12) return h12[k + s];
+    if (vec && k + 1 < 12) return sel3(s, h12[k], h12[k + 1], h12[k + 1]);
+    if (vec && k + s < 12) return h12[11];
     return __builtin_amdgcn_alignbyte(D(k + s + 1), D(k + s), sh);
   };
   if (L < 14) return 0;
