@@ -48,6 +48,9 @@ constexpr uint32_t kPassLds = kRWaves * kRMaxBins * 4 + (2 * kRMaxBins + kRWaves
 static_assert(kRMaxBins <= kRBlock, "one thread per digit");
 
 constexpr uint32_t kRMaxPass = 4;                  // keys of up to 36 bits
+#ifndef PCN_RADIX_UNI_ROUNDS
+#define PCN_RADIX_UNI_ROUNDS 4   // the up-sweep's last pass: equal-digit vectors aggregated (0: off, A/B)
+#endif
 
 struct Digits {
   uint32_t npass;
@@ -142,10 +145,29 @@ __global__ __launch_bounds__(kRBlock) void radix_up_kernel(const uint32_t *kin, 
       k4[u] = kv[q < hi4 ? q : hi4 - 1];
     }
   };
+  // The last pass (`runs`): a lane's four keys are mostly one digit (a run),
+  // and so are most lanes of a wave: the lanes whose four digits are equal add
+  // 4 x their count once per distinct digit (up to kUniRounds digits a vector
+  // slot; lanes left over, and the others, key by key as before).
+  constexpr int kUniRounds = PCN_RADIX_UNI_ROUNDS;
   auto count = [&](const u32x4 *k4, uint64_t base) {
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      const bool v = base + u * kRBlock + tid < hi4;
+      bool v = base + u * kRBlock + tid < hi4;
+      if (kUniRounds > 0 && runs) {
+        const uint32_t dx = (k4[u].x >> shift) & dmask;
+        const bool uni = v && dx == ((k4[u].y >> shift) & dmask) && dx == ((k4[u].z >> shift) & dmask) &&
+                         dx == ((k4[u].w >> shift) & dmask);
+        uint64_t left = __ballot(uni);
+        for (int it = 0; it < kUniRounds && left; ++it) {   // (wave-uniform)
+          const uint32_t l0 = static_cast<uint32_t>(__builtin_ctzll(left));
+          const uint32_t d0 = static_cast<uint32_t>(__shfl(static_cast<int>(dx), static_cast<int>(l0)));
+          const uint64_t m0 = __ballot(uni && dx == d0);
+          if (lane == l0) atomicAdd(&h[d0], 4u * static_cast<uint32_t>(__builtin_popcountll(m0)));
+          left &= ~m0;
+        }
+        v = v && (!uni || ((left >> lane) & 1));
+      }
       add(k4[u].x, v);
       add(k4[u].y, v);
       add(k4[u].z, v);
