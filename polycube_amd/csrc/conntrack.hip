@@ -996,9 +996,15 @@ __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const
     if (lo + r >= n || k == sentinel || km == k) return kRunClasses;
     return kl == k ? 0 : k63 == k ? 1 : k7 == k ? 2 : k1 == k ? 3 : 4;   // more than kLongRun / 63 / 7 / 1 packets
   };
+  // each position's class (3 bits) kept for the second pass, which re-read
+  // the six keys of every position from LDS
   uint32_t mine[kRunClasses] = {};
-  for (uint32_t j = 0; j < per; ++j) {
+  uint64_t cls = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kHeadsPer; ++j) {
+    if (j >= per) break;
     const uint32_t c = run_class_lds(j * kHeadsBlock + threadIdx.x);
+    cls |= uint64_t(c) << (3 * j);
 #pragma unroll
     for (uint32_t k = 0; k < kRunClasses; ++k) mine[k] += c == k;
   }
@@ -1012,10 +1018,12 @@ __global__ __launch_bounds__(kHeadsBlock) void ct_heads_kernel(uint64_t n, const
   }
   __syncthreads();
   const uint32_t lane = __lane_id();
-  for (uint32_t it = 0; it < per; ++it) {
+#pragma unroll
+  for (uint32_t it = 0; it < kHeadsPer; ++it) {
+    if (it >= per) break;                            // (per: uniform)
     const uint32_t r = it * kHeadsBlock + threadIdx.x;
     const uint64_t q = lo + r;
-    const uint32_t c = run_class_lds(r);
+    const uint32_t c = static_cast<uint32_t>(cls >> (3 * it)) & 7u;
 #pragma unroll
     for (uint32_t k = 0; k < kRunClasses; ++k) {
       const uint64_t m = __ballot(c == k);
